@@ -1,0 +1,262 @@
+"""ORACLE (test infrastructure only) -- CPU restatements of the reference hot path.
+
+Importable ONLY from ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg.  The product (``tianshou-fork_amd/tianshou_amd``) never imports it;
+it is the checker the HIP path is compared against.
+
+Pinned against the reference's own outputs: ``tests/golden/*`` were recorded from
+/root/reference by ``tools/gen_goldens.py`` and ``tests/test_oracle.py`` checks every
+function here against them (bit-exact for index math and the GAE f64 results).
+
+Each function cites the reference code it restates.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+def lib():
+    """liboracle.so (plain C, built by oracle/Makefile)."""
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            import subprocess
+            subprocess.run(["make", "-C", _HERE], check=True, capture_output=True)
+        L = ctypes.CDLL(path)
+        for name, vt in (("oracle_gae_f32vals", ctypes.c_void_p),
+                         ("oracle_gae_f64vals", ctypes.c_void_p)):
+            fn = getattr(L, name)
+            fn.restype = None
+            fn.argtypes = [vt, vt, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                           ctypes.c_double, ctypes.c_double, ctypes.c_void_p]
+        _LIB = L
+    return _LIB
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+# ---------------------------------------------------------------------------------------
+# GAE: tianshou/policy/base.py:337-384 (compute_episodic_return) + :453-497 (_gae_return)
+# ---------------------------------------------------------------------------------------
+def gae_return(v_s, v_next_masked, rew, end_flag, gamma, gae_lambda):
+    """_gae_return restated (base.py:453-497). f32 values -> NEP-50 f32 product path."""
+    n = len(rew)
+    rew = np.ascontiguousarray(rew, np.float64)
+    end = np.ascontiguousarray(end_flag, np.uint8)
+    out = np.zeros(n, np.float64)
+    if v_s.dtype == np.float32 and v_next_masked.dtype == np.float32:
+        lib().oracle_gae_f32vals(_ptr(np.ascontiguousarray(v_s)),
+                                 _ptr(np.ascontiguousarray(v_next_masked)), _ptr(rew),
+                                 _ptr(end), n, float(gamma), float(gae_lambda), _ptr(out))
+    else:
+        lib().oracle_gae_f64vals(_ptr(np.ascontiguousarray(v_s, np.float64)),
+                                 _ptr(np.ascontiguousarray(v_next_masked, np.float64)),
+                                 _ptr(rew), _ptr(end), n, float(gamma), float(gae_lambda),
+                                 _ptr(out))
+    return out
+
+
+def compute_episodic_return(rew, terminated, truncated, indices, unfinished, v_s_=None,
+                            v_s=None, gamma=0.99, gae_lambda=0.95):
+    """BasePolicy.compute_episodic_return restated (base.py:337-384).
+
+    ``terminated`` doubles as the value mask (base.py:317-335: ~buffer.terminated[indices],
+    and batch = buffer[indices]).  Returns (returns f64, advantage f64).
+    """
+    rew = np.asarray(rew)
+    terminated = np.asarray(terminated).astype(bool)
+    if v_s_ is None:
+        assert np.isclose(gae_lambda, 1.0)
+        v_s_ = np.zeros_like(rew)
+    else:
+        v_s_ = np.asarray(v_s_).flatten()
+        v_s_ = v_s_ * ~terminated          # dtype kept: f32 stays f32 (NEP 50)
+    v_s = np.roll(v_s_, 1) if v_s is None else np.asarray(v_s).flatten()
+    end_flag = np.logical_or(terminated, np.asarray(truncated).astype(bool))
+    end_flag[np.isin(indices, unfinished)] = True
+    if v_s.dtype != v_s_.dtype:
+        v_s, v_s_ = v_s.astype(np.float64), v_s_.astype(np.float64)
+    adv = gae_return(v_s, v_s_, rew, end_flag, gamma, gae_lambda)
+    returns = adv + v_s
+    return returns, adv
+
+
+# ---------------------------------------------------------------------------------------
+# VectorReplayBuffer index math: tianshou/data/buffer/vecbuf.py:33-37,
+# manager.py:54-192,259-297, base.py:140-214,276-305
+# ---------------------------------------------------------------------------------------
+class VecBufferIndex:
+    """Vectorised restatement of ReplayBufferManager's index bookkeeping (no per-env loop;
+    buffer_ids within one add are unique, as in every reference call site)."""
+
+    def __init__(self, total_size, buffer_num):
+        assert buffer_num > 0
+        self.num = buffer_num
+        self.size = int(np.ceil(total_size / buffer_num))        # vecbuf.py:35
+        self.maxsize = self.size * buffer_num
+        self.offset = np.arange(buffer_num, dtype=np.int64) * self.size
+        self.done = np.zeros(self.maxsize, bool)
+        self.rew = np.zeros(self.maxsize, np.float64)
+        self.ep_rew = np.zeros(buffer_num, np.float64)
+        self.ep_len = np.zeros(buffer_num, np.int64)
+        self.ep_idx = np.zeros(buffer_num, np.int64)
+        self.reset(False)
+
+    def reset(self, keep_statistics=False):                     # manager.py:54-58
+        self.index = np.zeros(self.num, np.int64)
+        self.sizes = np.zeros(self.num, np.int64)
+        self.last_index = self.offset.copy()
+        if not keep_statistics:
+            self.ep_rew[:] = 0.0
+            self.ep_len[:] = 0
+            self.ep_idx[:] = 0
+
+    def __len__(self):
+        return int(self.sizes.sum())
+
+    def add(self, rew, terminated, truncated, buffer_ids=None):  # manager.py:104-161
+        ids = np.arange(self.num) if buffer_ids is None else np.asarray(buffer_ids, np.int64)
+        rew = np.asarray(rew)
+        done = np.logical_or(terminated, truncated).astype(bool)
+        ptr = self.index[ids].copy()                             # base.py:202
+        self.sizes[ids] = np.minimum(self.sizes[ids] + 1, self.size)
+        self.index[ids] = (ptr + 1) % self.size
+        self.ep_rew[ids] += rew
+        self.ep_len[ids] += 1
+        out_rew = np.where(done, self.ep_rew[ids], self.ep_rew[ids] * 0.0)
+        out_len = np.where(done, self.ep_len[ids], 0)
+        out_idx = self.ep_idx[ids] + self.offset[ids]
+        d = ids[done]
+        self.ep_rew[d] = 0.0
+        self.ep_len[d] = 0
+        self.ep_idx[d] = self.index[d]
+        gptr = ptr + self.offset[ids]
+        self.last_index[ids] = gptr
+        self.done[gptr] = done
+        self.rew[gptr] = rew
+        return gptr, out_rew, out_len, out_idx
+
+    def sample_indices0(self):                                   # manager.py:177-192
+        parts = []
+        for b in range(self.num):
+            parts.append(np.concatenate([np.arange(self.index[b], self.sizes[b]),
+                                         np.arange(self.index[b])]) + self.offset[b])
+        return np.concatenate(parts).astype(np.int64)
+
+    def unfinished_index(self):                                  # manager.py:68-74
+        out = []
+        for b in range(self.num):
+            if self.sizes[b]:
+                last = (self.index[b] - 1) % self.sizes[b] + self.offset[b]
+                if not self.done[last]:
+                    out.append(last)
+        return np.array(out, np.int64)
+
+    def _seg(self, index):
+        index = np.asarray(index, np.int64) % self.maxsize
+        b = index // self.size
+        start = self.offset[b]
+        cur = np.maximum(1, self.sizes[b])
+        return index, b, start, cur
+
+    def prev(self, index):                                       # manager.py:259-277
+        index, b, start, cur = self._seg(index)
+        sub = (index - start - 1) % cur
+        end = self.done[sub + start] | (sub + start == self.last_index[b])
+        return (sub + end) % cur + start
+
+    def next(self, index):                                       # manager.py:280-297
+        index, b, start, cur = self._seg(index)
+        end = self.done[index] | (index == self.last_index[b])
+        return (index - start + 1 - end) % cur + start
+
+
+# ---------------------------------------------------------------------------------------
+# RunningMeanStd: tianshou/utils/statistics.py:69-114
+# ---------------------------------------------------------------------------------------
+class RMS:
+    def __init__(self, eps=np.finfo(np.float32).eps.item(), clip_max=10.0):
+        self.mean, self.var, self.count = 0.0, 1.0, 0
+        self.eps, self.clip_max = eps, clip_max
+
+    def update(self, x):
+        bm, bv, bc = np.mean(x, axis=0), np.var(x, axis=0), len(x)
+        delta = bm - self.mean
+        tot = self.count + bc
+        new_mean = self.mean + delta * bc / tot
+        m2 = self.var * self.count + bv * bc + delta ** 2 * self.count * bc / tot
+        self.mean, self.var, self.count = new_mean, m2 / tot, tot
+
+    def norm(self, x):
+        y = (x - self.mean) / np.sqrt(self.var + self.eps)
+        return np.clip(y, -self.clip_max, self.clip_max) if self.clip_max else y
+
+
+# ---------------------------------------------------------------------------------------
+# Batch.split: tianshou/data/batch.py:896-912
+# ---------------------------------------------------------------------------------------
+def split_parts(n, size, shuffle=True, merge_last=False):
+    if size == -1:
+        size = n
+    assert 1 <= size
+    idx = np.random.permutation(n) if shuffle else np.arange(n)
+    merge_last = merge_last and n % size > 0
+    parts = []
+    for s in range(0, n, size):
+        if merge_last and s + size + size >= n:
+            parts.append(idx[s:])
+            break
+        parts.append(idx[s:s + size])
+    return parts
+
+
+# ---------------------------------------------------------------------------------------
+# PPO minibatch loss (tianshou/policy/modelfree/ppo.py:106-151), Gaussian
+# Independent(Normal(mu, exp(sigma_param)), 1) (utils/models.py:96-97,
+# utils/net/continuous.py:229-235).  torch fp32 on CPU = the fp32 reference the fused
+# HIP loss kernel is checked against.
+# ---------------------------------------------------------------------------------------
+def ppo_gaussian_loss_torch(mu, sigma_param, value, act, logp_old, adv, returns, v_s,
+                            eps_clip=0.2, dual_clip=None, value_clip=False, norm_adv=True,
+                            vf_coef=0.5, ent_coef=0.01, eps=1e-8):
+    """Returns (loss, clip_loss, vf_loss, ent_loss, grads{mu, sigma_param, value})."""
+    import torch
+    from torch.distributions import Independent, Normal
+    mu = mu.detach().clone().requires_grad_(True)
+    sp = sigma_param.detach().clone().requires_grad_(True)
+    value = value.detach().clone().requires_grad_(True)
+    shape = [1] * mu.dim()
+    shape[1] = -1
+    sigma = (sp.view(shape) + torch.zeros_like(mu)).exp()
+    dist = Independent(Normal(mu, sigma), 1)
+    if norm_adv:
+        adv = (adv - adv.mean()) / (adv.std() + eps)
+    ratio = (dist.log_prob(act) - logp_old).exp().float()
+    ratio = ratio.reshape(ratio.size(0), -1).transpose(0, 1)
+    surr1 = ratio * adv
+    surr2 = ratio.clamp(1.0 - eps_clip, 1.0 + eps_clip) * adv
+    if dual_clip:
+        clip1 = torch.min(surr1, surr2)
+        clip2 = torch.max(clip1, dual_clip * adv)
+        clip_loss = -torch.where(adv < 0, clip2, clip1).mean()
+    else:
+        clip_loss = -torch.min(surr1, surr2).mean()
+    if value_clip:
+        v_clip = v_s + (value - v_s).clamp(-eps_clip, eps_clip)
+        vf1 = (returns - value).pow(2)
+        vf2 = (returns - v_clip).pow(2)
+        vf_loss = torch.max(vf1, vf2).mean()
+    else:
+        vf_loss = (returns - value).pow(2).mean()
+    ent_loss = dist.entropy().mean()
+    loss = clip_loss + vf_coef * vf_loss - ent_coef * ent_loss
+    loss.backward()
+    return (loss.detach(), clip_loss.detach(), vf_loss.detach(), ent_loss.detach(),
+            dict(mu=mu.grad, sigma_param=sp.grad, value=value.grad))

@@ -1,0 +1,158 @@
+"""Pin the CPU oracle to the reference's own outputs (tests/golden, made by
+tools/gen_goldens.py from /root/reference).  CPU only."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref, synth_env
+
+
+def _load(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name))
+
+
+def test_gae_known_answers(golden_dir):
+    """test/base/test_returns.py:22-112 vectors, bit-exact in f64."""
+    z = _load(golden_dir, "returns_known.npz")
+    for c in range(int(z["ncases"])):
+        p = f"c{c}_"
+        v = z[p + "v_next"] if bool(z[p + "has_v"]) else None
+        ret, adv = ref.compute_episodic_return(
+            z[p + "rew"], z[p + "term"], z[p + "trunc"], z[p + "indices"], z[p + "unfinished"],
+            v, None, float(z[p + "gamma"]), float(z[p + "lam"]))
+        assert np.array_equal(ret, z[p + "returns"]), c
+        assert np.array_equal(adv, z[p + "adv"]), c
+
+
+@pytest.mark.parametrize("tag", ["full", "wrap", "part"])
+def test_gae_random_bitexact(golden_dir, tag):
+    z = _load(golden_dir, "gae_random.npz")
+    p = tag + "_"
+    ret, adv = ref.compute_episodic_return(
+        z[p + "rew"], z[p + "term"], z[p + "trunc"], z[p + "indices"], z[p + "unfinished"],
+        z[p + "v_s_"], z[p + "v_s"], 0.99, 0.95)
+    assert np.array_equal(adv, z[p + "adv"])
+    assert np.array_equal(ret, z[p + "returns"])
+    s = np.float64(z[p + "scale"])
+    ret, adv = ref.compute_episodic_return(
+        z[p + "rew"], z[p + "term"], z[p + "trunc"], z[p + "indices"], z[p + "unfinished"],
+        z[p + "v_s_"] * s, z[p + "v_s"] * s, 0.99, 0.95)
+    assert np.array_equal(adv, z[p + "adv_scaled"])
+    assert np.array_equal(ret, z[p + "returns_scaled"])
+
+
+@pytest.mark.parametrize("name", ["manager", "ragged"])
+def test_buffer_index_math(golden_dir, name):
+    """test/base/test_buffer.py:701-901 sequence + ragged random trace, bit-exact."""
+    with open(os.path.join(golden_dir, "buffer_traces.json")) as f:
+        tr = json.load(f)[name]
+    buf = ref.VecBufferIndex(tr["total"], tr["num"])
+    allidx = np.arange(buf.maxsize)
+    for step in tr["trace"]:
+        if step["op"] == "add":
+            d = step["data"]
+            ptr, ep_rew, ep_len, ep_idx = buf.add(np.asarray(d["rew"], float),
+                                                  np.asarray(d["terminated"]),
+                                                  np.asarray(d["truncated"]), step["ids"])
+            assert ptr.tolist() == step["ptr"]
+            assert ep_rew.tolist() == step["ep_rew"]
+            assert ep_len.tolist() == step["ep_len"]
+            assert ep_idx.tolist() == step["ep_idx"]
+        else:
+            buf.reset(step["keep"])
+        st = step["state"]
+        assert buf.sample_indices0().tolist() == st["sample0"]
+        assert buf.prev(allidx).tolist() == st["prev"]
+        assert buf.next(allidx).tolist() == st["next"]
+        assert buf.unfinished_index().tolist() == st["unfinished"]
+        assert len(buf) == st["len"]
+        assert buf.last_index.tolist() == st["last_index"]
+        assert buf.sizes.tolist() == st["lengths"]
+        if st["done"]:
+            assert buf.done.astype(int).tolist() == st["done"]
+
+
+def test_split_table(golden_dir):
+    with open(os.path.join(golden_dir, "split.json")) as f:
+        g = json.load(f)
+    for c in g["cases"]:
+        if c["seed"] is not None:
+            np.random.seed(c["seed"])
+        parts = ref.split_parts(c["n"], c["size"], c["shuffle"], c["merge_last"])
+        assert [p.tolist() for p in parts] == c["parts"], c
+    np.random.seed(3)
+    big = np.random.permutation(1 << 16)
+    assert big[:64].tolist() == g["perm_seed3_n65536_head"]
+    assert int((big * np.arange(1 << 16)).sum()) == g["perm_seed3_n65536_wsum"]
+
+
+def test_rms(golden_dir):
+    z = _load(golden_dir, "rms.npz")
+    r = ref.RMS()
+    for i in range(int(z["n"])):
+        r.update(z[f"x{i}"])
+        assert np.array_equal(np.asarray(r.mean), z[f"mean{i}"])
+        assert np.array_equal(np.asarray(r.var), z[f"var{i}"])
+        assert r.count == int(z[f"count{i}"])
+        assert np.array_equal(r.norm(z[f"x{i}"]), z[f"norm{i}"])
+
+
+def test_synth_env_through_reference_collector(golden_dir):
+    """The synthetic env restated in NumPy reproduces what the reference Collector stored
+    (rew / flags exactly; obs after the reference's own VectorEnvNormObs)."""
+    z = _load(golden_dir, "collector.npz")
+    E, D, L, T = (int(z[k]) for k in ("E", "D", "L", "T"))
+    env = synth_env.SynthVecEnvNP(E, (D,), int(z["A"]), L)
+    rms = ref.RMS()
+    obs = env.reset()
+    rms.update(obs)
+    obs = rms.norm(obs)
+    store = {k: np.zeros((E, T) + s, dt) for k, s, dt in
+             (("obs", (D,), np.float32), ("obs_next", (D,), np.float32),
+              ("rew", (), np.float64), ("term", (), bool), ("trunc", (), bool))}
+    for t in range(T):
+        nxt, rew, term, trunc = env.step()
+        rms.update(nxt)
+        nxt = rms.norm(nxt)
+        store["obs"][:, t], store["obs_next"][:, t] = obs, nxt
+        store["rew"][:, t], store["term"][:, t], store["trunc"][:, t] = rew, term, trunc
+        done = np.flatnonzero(term | trunc)
+        obs = nxt.copy()
+        if len(done):
+            r = env.reset(done)
+            rms.update(r)
+            obs[done] = rms.norm(r)
+    assert np.array_equal(store["rew"].reshape(-1), z["c1_buf_rew"])
+    assert np.array_equal(store["term"].reshape(-1), z["c1_buf_terminated"])
+    assert np.array_equal(store["trunc"].reshape(-1), z["c1_buf_truncated"])
+    assert np.array_equal(store["obs"].reshape(-1, D), z["c1_buf_obs"])
+    assert np.array_equal(store["obs_next"].reshape(-1, D), z["c1_buf_obs_next"])
+    assert np.array_equal(np.asarray(rms.mean), z["c1_rms_mean"])
+    assert rms.count == int(z["c1_rms_count"])
+
+
+def test_ppo_loss_oracle_matches_reference_grads(golden_dir):
+    """One full-batch PPO minibatch through the torch-fp32 loss restatement reproduces the
+    reference's recorded gradients (wrt the actor head/critic head outputs are implied by
+    the parameter grads; here we check the loss values via a tiny re-run of the nets)."""
+    z = _load(golden_dir, "ppo_learn.npz")
+    cfg = json.loads(str(z["base_cfg"]))
+    assert cfg["n"] == cfg["batch_size"] and cfg["repeat"] == 1
+    from tianshou_amd.utils.net import build_actor_critic_from_state
+    actor, critic = build_actor_critic_from_state(
+        {k[len("base_init_"):]: torch.as_tensor(z[k]) for k in z.files
+         if k.startswith("base_init_")}, device="cpu")
+    obs = torch.as_tensor(z["base_obs"])
+    (mu, _), _ = actor(obs)
+    value = critic(obs).flatten()
+    loss, clip, vf, ent, g = ref.ppo_gaussian_loss_torch(
+        mu, actor.sigma_param.detach().flatten(), value, torch.as_tensor(z["base_act"]),
+        torch.as_tensor(z["base_logp_old"]), torch.as_tensor(z["base_adv"]),
+        torch.as_tensor(z["base_returns"]), torch.as_tensor(z["base_v_s"]),
+        vf_coef=0.25, ent_coef=0.0)
+    np.testing.assert_allclose(float(clip), float(z["base_loss_clip"][0]), rtol=1e-5)
+    np.testing.assert_allclose(float(vf), float(z["base_loss_vf"][0]), rtol=1e-5)
+    np.testing.assert_allclose(float(ent), float(z["base_loss_ent"][0]), rtol=1e-5)

@@ -1,0 +1,454 @@
+"""Generate golden vectors by running the REFERENCE (tianshou 0.5.1 at /root/reference).
+
+Runs only in the build container (the reference does not exist on the GPU box).  It imports
+the reference through ``tools/refstubs.py`` (third-party stubs, numba.njit = identity) and
+writes small fixtures under ``tests/golden/``.  The fixtures are data (inputs + the
+reference's outputs); no reference source is copied.
+
+    python tools/gen_goldens.py            # regenerate everything
+
+Each section names the reference code path it records.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+OUT = os.path.join(ROOT, "tests", "golden")
+sys.path.insert(0, HERE)
+sys.path.insert(0, ROOT)
+
+import refstubs  # noqa: E402
+
+refstubs.import_reference()
+
+import gymnasium as gym  # noqa: E402  (stub)
+from tianshou.data import Batch, ReplayBuffer, VectorReplayBuffer, Collector  # noqa: E402
+from tianshou.env import DummyVectorEnv, VectorEnvNormObs  # noqa: E402
+from tianshou.policy import BasePolicy, PPOPolicy  # noqa: E402
+from tianshou.utils import RunningMeanStd  # noqa: E402
+from tianshou.utils.models import (  # noqa: E402
+    fixed_std_normal, get_actor_critic, init_and_get_optim)
+
+from oracle import synth_env  # noqa: E402
+
+
+def _save(name, **arrays):
+    path = os.path.join(OUT, name)
+    np.savez_compressed(path, **arrays)
+    print("wrote", path, sum(np.asarray(a).nbytes for a in arrays.values()), "bytes raw")
+
+
+# --------------------------------------------------------------------------------------
+# 1. test/base/test_returns.py:22-112 known-answer cases through
+#    BasePolicy.compute_episodic_return (tianshou/policy/base.py:337-384)
+# --------------------------------------------------------------------------------------
+def gen_returns_known():
+    fn = BasePolicy.compute_episodic_return
+    cases = [
+        dict(terminated=[1, 0, 0, 1, 0, 0, 0, 1.], truncated=[0, 0, 0, 0, 0, 1, 0, 0],
+             rew=[0, 1, 2, 3, 4, 5, 6, 7.], v=None, gamma=.1, lam=1.0),
+        dict(terminated=[0, 1, 0, 1, 0, 1, 0.], truncated=[0, 0, 0, 0, 0, 0, 0.],
+             rew=[7, 6, 1, 2, 3, 4, 5.], v=None, gamma=.1, lam=1.0),
+        dict(terminated=[0, 1, 0, 1, 0, 0, 1.], truncated=[0, 0, 0, 0, 0, 0, 0],
+             rew=[7, 6, 1, 2, 3, 4, 5.], v=None, gamma=.1, lam=1.0),
+        dict(terminated=[0, 0, 0, 1., 0, 0, 0, 1, 0, 0, 0, 1],
+             truncated=[0] * 12,
+             rew=[101, 102, 103., 200, 104, 105, 106, 201, 107, 108, 109, 202],
+             v=[2., 3., 4, -1, 5., 6., 7, -2, 8., 9., 10, -3], gamma=0.99, lam=0.95),
+        dict(terminated=[0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1],
+             truncated=[0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0, 0],
+             rew=[101, 102, 103., 200, 104, 105, 106, 201, 107, 108, 109, 202],
+             v=[2., 3., 4, -1, 5., 6., 7, -2, 8., 9., 10, -3], gamma=0.99, lam=0.95),
+    ]
+    out = {}
+    for c, case in enumerate(cases):
+        buf = ReplayBuffer(20)
+        batch = Batch(terminated=np.array(case["terminated"]),
+                      truncated=np.array(case["truncated"]),
+                      rew=np.array(case["rew"]))
+        for b in batch:
+            b.obs = b.act = 1
+            buf.add(b)
+        idx = buf.sample_indices(0)
+        if case["v"] is None:
+            ret, adv = fn(batch, buf, idx, gamma=case["gamma"], gae_lambda=case["lam"])
+            v = np.zeros(len(idx))
+        else:
+            v = np.array(case["v"])
+            ret, adv = fn(batch, buf, idx, v, gamma=case["gamma"], gae_lambda=case["lam"])
+        p = f"c{c}_"
+        out[p + "rew"] = batch.rew.astype(np.float64)
+        out[p + "term"] = batch.terminated.astype(bool)
+        out[p + "trunc"] = batch.truncated.astype(bool)
+        out[p + "v_next"] = v.astype(np.float64)  # passed as v_s_ ; v_s = roll(v_s_, 1)
+        out[p + "has_v"] = np.array(case["v"] is not None)
+        out[p + "gamma"] = np.array(case["gamma"])
+        out[p + "lam"] = np.array(case["lam"])
+        out[p + "indices"] = idx
+        out[p + "unfinished"] = buf.unfinished_index()
+        out[p + "returns"] = ret
+        out[p + "adv"] = adv
+    out["ncases"] = np.array(len(cases))
+    _save("returns_known.npz", **out)
+
+
+# --------------------------------------------------------------------------------------
+# 2. Random GAE through VectorReplayBuffer.sample(0) + compute_episodic_return.
+#    Records the A5-bits semantics (f32 values -> NEP50 f32 product) and the rew_norm
+#    f64-scaled-values variant (tianshou/policy/modelfree/a2c.py:98-100).
+# --------------------------------------------------------------------------------------
+def _fill_vecbuf(env_num, size_per_env, steps, rng, p_term, trunc_every):
+    buf = VectorReplayBuffer(env_num * size_per_env, env_num)
+    ids = np.arange(env_num)
+    for t in range(steps):
+        rew = rng.random(env_num)
+        term = rng.random(env_num) < p_term
+        trunc = ((t + 1) % trunc_every == 0) & ~term
+        if t == steps - 1:
+            term[0], trunc[0] = True, False
+            if env_num > 1:
+                term[1], trunc[1] = False, True
+        buf.add(Batch(obs=np.zeros(env_num), act=np.zeros(env_num), rew=rew,
+                      terminated=term, truncated=trunc), buffer_ids=ids)
+    return buf
+
+
+def gen_gae_random():
+    out = {}
+    specs = {
+        "full": (32, 2048, 2048, 0.01, 1000),   # on-policy: buffer exactly full
+        "wrap": (16, 100, 250, 0.05, 37),       # ring wrapped: rotated sample order
+        "part": (8, 64, 40, 0.05, 17),          # partially filled: ragged offsets
+    }
+    for tag, (env_num, size, steps, p_term, trunc_every) in specs.items():
+        rng = np.random.default_rng(1234 + len(tag))
+        buf = _fill_vecbuf(env_num, size, steps, rng, p_term, trunc_every)
+        batch, idx = buf.sample(0)
+        n = len(idx)
+        v_s = rng.standard_normal(n).astype(np.float32)
+        v_s_ = rng.standard_normal(n).astype(np.float32)
+        ret, adv = BasePolicy.compute_episodic_return(batch, buf, idx, v_s_, v_s, 0.99, 0.95)
+        scale = np.sqrt(2.5 + 1e-8)
+        ret64, adv64 = BasePolicy.compute_episodic_return(
+            batch, buf, idx, v_s_ * scale, v_s * scale, 0.99, 0.95)
+        p = tag + "_"
+        out[p + "env_num"] = np.array(env_num)
+        out[p + "size"] = np.array(size)
+        out[p + "steps"] = np.array(steps)
+        out[p + "indices"] = idx
+        out[p + "unfinished"] = buf.unfinished_index()
+        out[p + "rew"] = batch.rew
+        out[p + "term"] = batch.terminated
+        out[p + "trunc"] = batch.truncated
+        out[p + "v_s"] = v_s
+        out[p + "v_s_"] = v_s_
+        out[p + "returns"] = ret
+        out[p + "adv"] = adv
+        out[p + "scale"] = np.array(scale)
+        out[p + "returns_scaled"] = ret64
+        out[p + "adv_scaled"] = adv64
+        # the full storage too (for device-side runs straight off the buffer layout)
+        out[p + "store_rew"] = buf.rew
+        out[p + "store_term"] = buf.terminated
+        out[p + "store_trunc"] = buf.truncated
+    _save("gae_random.npz", **out)
+
+
+# --------------------------------------------------------------------------------------
+# 3. VectorReplayBuffer index math: test/base/test_buffer.py:701-901 op sequence plus a
+#    random ragged trace (subsets of buffer_ids, wrap-around).  Records
+#    add() -> (ptr, ep_rew, ep_len, ep_idx) and sample_indices(0)/prev/next/
+#    unfinished_index/len/done after every op (tianshou/data/buffer/manager.py).
+# --------------------------------------------------------------------------------------
+def _snapshot(buf):
+    allidx = np.arange(buf.maxsize)
+    return dict(
+        sample0=buf.sample_indices(0).tolist(),
+        prev=buf.prev(allidx).tolist(),
+        next=buf.next(allidx).tolist(),
+        unfinished=buf.unfinished_index().tolist(),
+        len=int(len(buf)),
+        done=buf.done.astype(int).tolist() if not buf._meta.is_empty() else [],
+        last_index=np.asarray(buf.last_index).tolist(),
+        lengths=np.asarray(buf._lengths).tolist(),
+    )
+
+
+def _trace(total, num, ops):
+    buf = VectorReplayBuffer(total, num)
+    rec = []
+    for op in ops:
+        if op[0] == "add":
+            _, data, ids = op
+            ptr, ep_rew, ep_len, ep_idx = buf.add(Batch(**data), buffer_ids=ids)
+            rec.append(dict(op="add", data={k: np.asarray(v).tolist() for k, v in data.items()},
+                            ids=list(map(int, ids)), ptr=ptr.tolist(), ep_rew=ep_rew.tolist(),
+                            ep_len=ep_len.tolist(), ep_idx=ep_idx.tolist(), state=_snapshot(buf)))
+        elif op[0] == "reset":
+            buf.reset(keep_statistics=op[1])
+            rec.append(dict(op="reset", keep=op[1], state=_snapshot(buf)))
+    return dict(total=total, num=num, trace=rec)
+
+
+def gen_buffer_traces():
+    d = np.array([0, 0, 0, 0])
+    ops = [
+        ("add", dict(obs=[1, 2, 3], act=[1, 2, 3], rew=[1, 2, 3], terminated=[0, 0, 1],
+                     truncated=[0, 0, 0]), [0, 1, 2]),
+        ("add", dict(obs=[4], act=[4], rew=[4], terminated=[1], truncated=[0]), [3]),
+        ("add", dict(obs=d, act=d, rew=d, terminated=d, truncated=d), [0, 1, 2, 3]),
+        ("add", dict(obs=d, act=d, rew=d, terminated=1 - d, truncated=d), [0, 1, 2, 3]),
+        ("add", dict(obs=d, act=d, rew=d, terminated=d, truncated=d), [0, 1, 2, 3]),
+        ("add", dict(obs=d, act=d, rew=d, terminated=[0, 1, 0, 1], truncated=d), [0, 1, 2, 3]),
+        ("add", dict(obs=[1], act=[1], rew=[1], terminated=[1], truncated=[0]), [2]),
+    ]
+    traces = {"manager": _trace(20, 4, ops)}
+    rng = np.random.default_rng(7)
+    ops = []
+    num, per = 6, 7
+    for step in range(60):
+        k = int(rng.integers(1, num + 1))
+        ids = np.sort(rng.choice(num, size=k, replace=False))
+        rew = np.round(rng.random(k) * 8) / 4.0
+        term = (rng.random(k) < 0.15).astype(int)
+        trunc = ((rng.random(k) < 0.1) & (term == 0)).astype(int)
+        obs = rng.integers(0, 100, k)
+        ops.append(("add", dict(obs=obs, act=obs, rew=rew, terminated=term, truncated=trunc),
+                    ids))
+        if step == 30:
+            ops.append(("reset", True))
+        if step == 45:
+            ops.append(("reset", False))
+    traces["ragged"] = _trace(num * per, num, ops)
+    with open(os.path.join(OUT, "buffer_traces.json"), "w") as f:
+        json.dump(traces, f)
+    print("wrote buffer_traces.json")
+
+
+# --------------------------------------------------------------------------------------
+# 4. Batch.split (tianshou/data/batch.py:896-912): test/base/test_batch.py:76-93 table plus
+#    seeded shuffles (global legacy np.random state).
+# --------------------------------------------------------------------------------------
+def gen_split():
+    rec = []
+    for n in (10, 7, 8, 9, 33, 64, 70):
+        for size in (1, 3, 5, 7, 10, 15, 16, 100):
+            for merge_last in (False, True):
+                for shuffle, seed in ((False, None), (True, 0), (True, 7)):
+                    if seed is not None:
+                        np.random.seed(seed)
+                    b = Batch(a=np.arange(n))
+                    parts = [x.a.tolist() for x in b.split(size, shuffle=shuffle,
+                                                           merge_last=merge_last)]
+                    rec.append(dict(n=n, size=size, merge_last=merge_last, shuffle=shuffle,
+                                    seed=seed, parts=parts))
+    np.random.seed(3)
+    big = np.random.permutation(1 << 16)
+    with open(os.path.join(OUT, "split.json"), "w") as f:
+        json.dump(dict(cases=rec, perm_seed3_n65536_head=big[:64].tolist(),
+                       perm_seed3_n65536_wsum=int((big * np.arange(1 << 16)).sum())), f)
+    print("wrote split.json")
+
+
+# --------------------------------------------------------------------------------------
+# 5. RunningMeanStd (tianshou/utils/statistics.py:69-114), incl. the reset-subset updates
+#    VectorEnvNormObs does (tianshou/env/venv_wrappers.py:77-99).
+# --------------------------------------------------------------------------------------
+def gen_rms():
+    rng = np.random.default_rng(11)
+    rms = RunningMeanStd()
+    out = {}
+    sizes = [5, 3, 1, 8, 2, 64, 1]
+    for i, sz in enumerate(sizes):
+        x = (rng.standard_normal((sz, 6)) * (1 + i) + i).astype(np.float32)
+        rms.update(x)
+        out[f"x{i}"] = x
+        out[f"mean{i}"] = np.asarray(rms.mean)
+        out[f"var{i}"] = np.asarray(rms.var)
+        out[f"count{i}"] = np.array(rms.count)
+        out[f"norm{i}"] = rms.norm(x)
+    out["n"] = np.array(len(sizes))
+    _save("rms.npz", **out)
+
+
+# --------------------------------------------------------------------------------------
+# 6. PPOPolicy.learn on fixed weights (tianshou/policy/modelfree/ppo.py:99-162): losses,
+#    post-step parameters and (single-minibatch case) gradients.
+# --------------------------------------------------------------------------------------
+def _make_policy(obs_dim, act_dim, seed, **kw):
+    torch.manual_seed(seed)
+    actor, critic = get_actor_critic((obs_dim,), (64, 64), (act_dim,), "cpu")
+    optim = init_and_get_optim(actor, critic, 3e-4)
+    space = gym.spaces.Box(-1.0, 1.0, (act_dim,))
+    args = dict(discount_factor=0.99, gae_lambda=0.95, max_grad_norm=0.5, vf_coef=0.25,
+                ent_coef=0.0, reward_normalization=False, advantage_normalization=True,
+                recompute_advantage=False, eps_clip=0.2, value_clip=False, dual_clip=None,
+                action_bound_method="clip", action_scaling=True)
+    args.update(kw)
+    policy = PPOPolicy(actor, critic, optim, dist_fn=fixed_std_normal, action_space=space,
+                       **args)
+    return policy
+
+
+def _sd_arrays(prefix, module):
+    return {prefix + k: v.detach().numpy().copy() for k, v in module.state_dict().items()}
+
+
+def gen_ppo():
+    out = {}
+    variants = {
+        "base": dict(n=64, batch_size=64, repeat=1, kw={}),
+        "multi": dict(n=70, batch_size=16, repeat=2, kw={}),
+        "clips": dict(n=48, batch_size=48, repeat=1,
+                      kw=dict(dual_clip=5.0, value_clip=True, ent_coef=0.01)),
+        "nonorm": dict(n=40, batch_size=40, repeat=1,
+                       kw=dict(advantage_normalization=False, max_grad_norm=None,
+                               ent_coef=0.01)),
+    }
+    obs_dim, act_dim = 17, 6
+    for tag, v in variants.items():
+        policy = _make_policy(obs_dim, act_dim, seed=5, **v["kw"])
+        rng = np.random.default_rng(99)
+        n = v["n"]
+        obs = rng.standard_normal((n, obs_dim)).astype(np.float32)
+        act = rng.standard_normal((n, act_dim)).astype(np.float32)
+        with torch.no_grad():
+            dist = policy(Batch(obs=obs, info={})).dist
+            logp_old = dist.log_prob(torch.as_tensor(act)).numpy()
+        logp_old = (logp_old + rng.normal(0, 0.3, n)).astype(np.float32)
+        adv = (rng.standard_normal(n) * 2 + 0.3).astype(np.float32)
+        ret = rng.standard_normal(n).astype(np.float32)
+        v_s = (ret + rng.normal(0, 0.3, n)).astype(np.float32)
+        p = tag + "_"
+        out.update(_sd_arrays(p + "init_", policy))
+        batch = Batch(obs=obs, act=torch.as_tensor(act), logp_old=torch.as_tensor(logp_old),
+                      adv=torch.as_tensor(adv), returns=torch.as_tensor(ret),
+                      v_s=torch.as_tensor(v_s), info={})
+        np.random.seed(21)
+        res = policy.learn(batch, batch_size=v["batch_size"], repeat=v["repeat"])
+        for k in ("loss", "loss/clip", "loss/vf", "loss/ent"):
+            out[p + k.replace("/", "_")] = np.array(res[k])
+        out.update(_sd_arrays(p + "final_", policy))
+        grads = {p + "grad_" + name: prm.grad.detach().numpy().copy()
+                 for name, prm in policy.named_parameters() if prm.grad is not None}
+        out.update(grads)
+        out[p + "obs"], out[p + "act"], out[p + "logp_old"] = obs, act, logp_old
+        out[p + "adv"], out[p + "returns"], out[p + "v_s"] = adv, ret, v_s
+        out[p + "cfg"] = np.array(json.dumps(dict(n=n, batch_size=v["batch_size"],
+                                                   repeat=v["repeat"], **v["kw"])))
+    _save("ppo_learn.npz", **out)
+
+
+# --------------------------------------------------------------------------------------
+# 7. Collector + VectorEnvNormObs + VectorReplayBuffer + PPO process_fn/learn on the
+#    synthetic env (tianshou/data/collector.py:184-402, policy/modelfree/ppo.py:87-162).
+# --------------------------------------------------------------------------------------
+class SynthGymEnv(gym.Env):
+    """One env of oracle.synth_env, exposed through the reference's gym surface."""
+
+    def __init__(self, e, obs_dim, act_dim, ep_len, seed=0):
+        self.observation_space = gym.spaces.Box(-np.inf, np.inf, (obs_dim,), np.float32)
+        self.action_space = gym.spaces.Box(-1.0, 1.0, (act_dim,), np.float32)
+        self.e, self.obs_dim, self.ep_len, self.seed_ = e, obs_dim, ep_len, seed
+        self.j, self.t = -1, 0
+
+    def _obs(self):
+        k = synth_env.key(self.seed_, np.array([self.e]), np.array([self.j]),
+                          np.array([self.t]))
+        return synth_env.box_obs(k, self.obs_dim)[0]
+
+    def reset(self, seed=None, options=None):
+        self.j += 1
+        self.t = self.e % self.ep_len if self.j == 0 else 0
+        return self._obs(), {}
+
+    def step(self, action):
+        self.t += 1
+        k = synth_env.key(self.seed_, np.array([self.e]), np.array([self.j]),
+                          np.array([self.t]))
+        rew = float(synth_env.reward(k)[0])
+        done = self.t >= self.ep_len
+        return self._obs(), rew, bool(done and self.e % 2 == 0), \
+            bool(done and self.e % 2 == 1), {}
+
+
+def _buf_arrays(prefix, buf):
+    out = {}
+    for k in ("obs", "obs_next", "act", "rew", "terminated", "truncated", "done"):
+        out[prefix + k] = np.array(buf._meta[k], copy=True)
+    out[prefix + "env_id"] = np.array(buf._meta.info.env_id, copy=True)
+    return out
+
+
+def _stats_arrays(prefix, res):
+    return {prefix + k.replace("/", "_"): np.asarray(v) for k, v in res.items()}
+
+
+def gen_collector():
+    E, D, A, L, T = 8, 5, 2, 7, 20
+    out = dict(E=np.array(E), D=np.array(D), A=np.array(A), L=np.array(L), T=np.array(T))
+    venv = VectorEnvNormObs(DummyVectorEnv(
+        [lambda e=e: SynthGymEnv(e, D, A, L) for e in range(E)]))
+    policy = _make_policy(D, A, seed=3, reward_normalization=True, ent_coef=0.0)
+    out.update(_sd_arrays("init_", policy))
+    buf = VectorReplayBuffer(E * T, E)
+    torch.manual_seed(0)
+    np.random.seed(0)
+    c = Collector(policy, venv, buf)
+    res1 = c.collect(n_step=E * T)
+    out.update(_stats_arrays("c1_", res1))
+    out.update(_buf_arrays("c1_buf_", buf))
+    rms = venv.get_obs_rms()
+    out["c1_rms_mean"], out["c1_rms_var"], out["c1_rms_count"] = \
+        np.asarray(rms.mean), np.asarray(rms.var), np.array(rms.count)
+    out["c1_data_obs"] = np.asarray(c.data.obs)
+    # update: sample(0) -> process_fn (critic, GAE w/ rew_norm, logp_old) -> learn
+    batch, idx = buf.sample(0)
+    out["c1_indices"] = idx
+    batch = policy.process_fn(batch, buf, idx)
+    for k in ("v_s", "returns", "adv", "logp_old"):
+        out["pf_" + k] = batch[k].detach().numpy()
+    out["pf_ret_rms_mean"] = np.asarray(policy.ret_rms.mean)
+    out["pf_ret_rms_var"] = np.asarray(policy.ret_rms.var)
+    out["pf_ret_rms_count"] = np.asarray(policy.ret_rms.count)
+    np.random.seed(5)
+    res = policy.learn(batch, batch_size=E * T // 4, repeat=2)
+    for k in ("loss", "loss/clip", "loss/vf", "loss/ent"):
+        out["learn_" + k.replace("/", "_")] = np.array(res[k])
+    out.update(_sd_arrays("final_", policy))
+    # second collect after reset_buffer(keep_statistics=True) (trainer/base.py:563)
+    c.reset_buffer(keep_statistics=True)
+    res2 = c.collect(n_step=E * T // 2)
+    out.update(_stats_arrays("c2_", res2))
+    out.update(_buf_arrays("c2_buf_", buf))
+    rms = venv.get_obs_rms()
+    out["c2_rms_mean"], out["c2_rms_var"], out["c2_rms_count"] = \
+        np.asarray(rms.mean), np.asarray(rms.var), np.array(rms.count)
+    # n_episode collection on a fresh collector (surplus-env removal path)
+    venv3 = VectorEnvNormObs(DummyVectorEnv(
+        [lambda e=e: SynthGymEnv(e, D, A, L) for e in range(E)]))
+    buf3 = VectorReplayBuffer(E * T, E)
+    c3 = Collector(policy, venv3, buf3)
+    res3 = c3.collect(n_episode=11)
+    out.update(_stats_arrays("c3_", res3))
+    out.update(_buf_arrays("c3_buf_", buf3))
+    out["c3_lengths"] = np.asarray(buf3._lengths)
+    out["c3_last_index"] = np.asarray(buf3.last_index)
+    rms = venv3.get_obs_rms()
+    out["c3_rms_mean"], out["c3_rms_var"], out["c3_rms_count"] = \
+        np.asarray(rms.mean), np.asarray(rms.var), np.array(rms.count)
+    _save("collector.npz", **out)
+
+
+if __name__ == "__main__":
+    os.makedirs(OUT, exist_ok=True)
+    which = sys.argv[1:] or ["returns", "gae", "buffer", "split", "rms", "ppo", "collector"]
+    table = dict(returns=gen_returns_known, gae=gen_gae_random, buffer=gen_buffer_traces,
+                 split=gen_split, rms=gen_rms, ppo=gen_ppo, collector=gen_collector)
+    for w in which:
+        table[w]()
