@@ -1,0 +1,198 @@
+"""Headline benchmark: env-steps/s through Collector.collect + GAE + PPOPolicy.learn
+(BASELINE.json metric), config "Synthetic Box(obs=376, act=17), 4096 envs x 2048 steps".
+
+A "step" is one on-policy iteration of the reference trainer (trainer/base.py:552-563):
+    collect(n_step=envs*T) -> policy.update(0, buffer, batch_size=envs*T/32, repeat=4)
+    -> reset_buffer(keep_statistics=True)
+with SURVEY.md §8d's pinned hyper-parameters (Tanh 64-64 actor/critic, Adam 3e-4, gamma .99,
+lambda .95, eps_clip .2, vf_coef .25, ent_coef 0, max_grad_norm .5, rew_norm on,
+norm_adv on, VectorEnvNormObs on, 32 minibatches, repeat 4).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+
+Multi-GPU = env sharding (weak scaling: every rank runs envs x T of its own), RCCL
+all-reduce of gradients / advantage moments / ret_rms partials.  Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "tianshou-fork_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+GAE_BYTES_PER_TRANSITION = 26  # rew f64 8 + v_s 4 + v_s_ 4 + term 1 + trunc 1 + adv 4 + ret 4
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--envs", type=int, default=4096)
+    ap.add_argument("--T", type=int, default=2048)
+    ap.add_argument("--obs", type=int, default=376)
+    ap.add_argument("--act", type=int, default=17)
+    ap.add_argument("--repeat", type=int, default=4)
+    ap.add_argument("--minibatches", type=int, default=32)
+    ap.add_argument("--ep-len", type=int, default=1000)
+    ap.add_argument("--perm", choices=["numpy", "device"], default="device")
+    ap.add_argument("--cpu-steps", type=int, default=48,
+                    help="T' of the bounded CPU-baseline sample (envs x T')")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+class GaeTimer:
+    """HIP-event timing of every tsrl_gae launch (on the stream it is launched on)."""
+
+    def __init__(self):
+        self.events = []
+        self.n = 0
+        self.on = False
+
+    def __call__(self, phase, n):
+        if not self.on:
+            return
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(torch.cuda.current_stream())
+        if phase == "start":
+            self.events.append([ev, None])
+            self.n = n
+        else:
+            self.events[-1][1] = ev
+
+    def mean_ms(self):
+        ts = [a.elapsed_time(b) for a, b in self.events if b is not None]
+        return float(np.mean(ts)) if ts else float("nan")
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    from tianshou_amd.data import Collector, VectorReplayBuffer
+    from tianshou_amd.env import SyntheticVectorEnv, VectorEnvNormObs
+    from tianshou_amd.policy import PPOPolicy, base as pbase
+    from tianshou_amd.utils.models import fixed_std_normal, get_actor_critic, init_and_get_optim
+
+    torch.manual_seed(rank)
+    np.random.seed(rank)
+    E, T, D, A = args.envs, args.T, args.obs, args.act
+    n = E * T
+    env = VectorEnvNormObs(SyntheticVectorEnv(E, (D,), A, ep_len=args.ep_len, seed=rank,
+                                              device=dev))
+    actor, critic = get_actor_critic((D,), (64, 64), (A,), dev)
+    optim = init_and_get_optim(actor, critic, 3e-4)
+    policy = PPOPolicy(actor, critic, optim, fixed_std_normal, action_space=env.action_space,
+                       discount_factor=0.99, gae_lambda=0.95, max_grad_norm=0.5, vf_coef=0.25,
+                       ent_coef=0.0, reward_normalization=True, advantage_normalization=True,
+                       recompute_advantage=False, eps_clip=0.2, value_clip=False,
+                       dual_clip=None, action_bound_method="clip",
+                       perm_device=(args.perm == "device")).to(dev)
+    buf = VectorReplayBuffer(n, E, device=dev)
+    coll = Collector(policy, env, buf)
+    timer = GaeTimer()
+    pbase.GAE_HOOK = timer
+    phase = {"collect": 0.0, "update": 0.0}
+
+    def iteration():
+        t0 = time.perf_counter()
+        coll.collect(n_step=n)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        policy.update(0, buf, batch_size=n // args.minibatches, repeat=args.repeat)
+        coll.reset_buffer(keep_statistics=True)
+        torch.cuda.synchronize()
+        phase["collect"] += t1 - t0
+        phase["update"] += time.perf_counter() - t1
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        iteration()
+    phase.update(collect=0.0, update=0.0)
+    timer.on = True
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        iteration()
+        if rank == 0:
+            print(f"# iter {i} collect {phase['collect'] / (i + 1):.3f}s "
+                  f"update {phase['update'] / (i + 1):.3f}s", file=sys.stderr, flush=True)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    timer.on = False
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    total_steps = n * world * args.steps
+    value = total_steps / elapsed
+    gae_ms = timer.mean_ms()
+    gae_bytes = GAE_BYTES_PER_TRANSITION * n
+    achieved = gae_bytes / (gae_ms * 1e-3) / 1e9
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            from oracle import cpu_port
+            threads = min(16, os.cpu_count() or 1)
+            v, dt = cpu_port.run_iteration(E, args.cpu_steps, D, A, repeat=args.repeat,
+                                           minibatches=args.minibatches, ep_len=args.ep_len,
+                                           threads=threads)
+            cpu = {"value": v, "unit": "env-steps/s", "cores": threads, "kind": "port",
+                   "sample": f"one iteration of {E} envs x {args.cpu_steps} steps "
+                             f"(Box {D}/{A}), build CPU restatement "
+                             f"(oracle/cpu_port.py: NumPy env+obs-norm+buffer, C GAE, "
+                             f"torch-CPU PPO), {dt:.1f}s"}
+        line = {
+            "metric": "env-steps/sec through collect+GAE+PPO.learn",
+            "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f32 (GAE scan f64)", "data": "synthetic",
+            "config": {"workload": f"Synthetic Box(obs={D}, act={A}), {E} envs x {T} steps "
+                                   f"per GPU, GAE+PPO (repeat {args.repeat}, "
+                                   f"{args.minibatches} minibatches)",
+                       "envs_per_gpu": E, "steps_per_env": T, "global_batch": n * world,
+                       "minibatch": n // args.minibatches * world,
+                       "parallelism": f"env-sharded dp{world}",
+                       "permutation": args.perm,
+                       "collect_s": phase["collect"] / args.steps,
+                       "update_s": phase["update"] / args.steps},
+            "roofline": {"kernel": "tsrl_gae (gae_rows_kernel)", "bound": "hbm",
+                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "launch_us": gae_ms * 1e3,
+                         "bytes_per_launch": gae_bytes},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

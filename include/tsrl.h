@@ -1,0 +1,202 @@
+/*
+ * libtsrl -- C ABI of the MI355X (gfx950) on-policy hot path:
+ * rollout storage (VectorReplayBuffer), GAE reverse scan, PPO clipped-surrogate loss.
+ *
+ * The reference (tianshou 0.5.1) is pure Python; its "operators" for this path are the
+ * Python methods listed against each entry point below.  tianshou_amd (the host package
+ * under tianshou-fork_amd/) binds these symbols with ctypes and keeps the reference's
+ * class API on top.
+ *
+ * Conventions
+ *   - Every pointer is a DEVICE pointer owned by the caller (PyTorch allocates).  Kernels
+ *     never allocate; scratch comes from a caller buffer sized by *_workspace_bytes().
+ *   - `stream` is a hipStream_t passed as void*; every call is stream-ordered and
+ *     asynchronous; no call synchronises the device or the host.
+ *   - Return value: 0 on success, otherwise a hipError_t code; tsrl_last_error() returns
+ *     a thread-local message.  Argument errors return hipErrorInvalidValue (1).
+ *   - No global mutable state; calls are reentrant.
+ */
+#ifndef TSRL_H_
+#define TSRL_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Library identification / errors. */
+const char* tsrl_version(void);
+const char* tsrl_last_error(void);
+
+/* ---------------------------------------------------------------------------------
+ * GAE reverse scan.
+ * Replaces BasePolicy.compute_episodic_return (tianshou/policy/base.py:337-384) and the
+ * numba kernel _gae_return (tianshou/policy/base.py:453-497), with the value handling of
+ * A2CPolicy._compute_returns (tianshou/policy/modelfree/a2c.py:83-117).
+ *
+ *   v_next_masked = v_s_ * !terminated                 (value_mask, base.py:317-335)
+ *   end_i   = terminated_i | truncated_i | end_extra_i | ((i+1) % row_len == 0)
+ *   delta_i = rew_i + v_next_masked_i * gamma - v_s_i  (f32 product when value_scale==NULL,
+ *             f64 with v = (double)v * (*value_scale) otherwise: the rew_norm path)
+ *   adv_i   = delta_i + (1 - end_i) * gamma * lambda * adv_{i+1}   (f64, no FMA)
+ *   ret_i   = adv_i + v_s_i ;  ret_i /= *value_scale in rew_norm mode (a2c.py:110-111)
+ *
+ * row_len > 0 declares that every row_len-th element closes an episode segment (the
+ * VectorReplayBuffer sample(0) layout: each env's segment ends at its unfinished/last
+ * index, manager.py:68-74); the scan then runs independent row ranges in one pass.
+ * row_len == 0 runs the general 3-phase scan (needs workspace).
+ * Any of adv_out/ret_out/adv64_out/ret64_out may be NULL.  ret_partials (nullable,
+ * rew_norm only) receives per-workgroup (count, mean, M2) of the UNNORMALISED f64 returns
+ * for tsrl_ret_rms_update (RunningMeanStd.update, tianshou/utils/statistics.py:93-114).
+ * ------------------------------------------------------------------------------- */
+int64_t tsrl_gae_workspace_bytes(int64_t n, int64_t row_len);
+int64_t tsrl_gae_num_partials(int64_t n, int64_t row_len);
+int tsrl_gae(const float* v_s, const float* v_s_next, const double* rew,
+             const uint8_t* terminated, const uint8_t* truncated, const uint8_t* end_extra,
+             int64_t n, int64_t row_len, const double* value_scale, double gamma,
+             double gae_lambda, float* adv_out, float* ret_out, double* adv64_out,
+             double* ret64_out, double* ret_partials, void* workspace,
+             int64_t workspace_bytes, void* stream);
+
+/* Same scan with f64 value inputs and f64 outputs only (the public
+ * compute_episodic_return on NumPy f64 values, base.py:337-384). */
+int tsrl_gae_f64v(const double* v_s, const double* v_s_next, const double* rew,
+                  const uint8_t* terminated, const uint8_t* truncated, const uint8_t* end_extra,
+                  int64_t n, int64_t row_len, double gamma, double gae_lambda,
+                  double* adv64_out, double* ret64_out, void* workspace,
+                  int64_t workspace_bytes, void* stream);
+
+/* Merge (count, mean, M2) partials into a RunningMeanStd held on device as
+ * double rms[3] = {mean, var, count}  (statistics.py:93-114, Chan parallel merge). */
+int tsrl_ret_rms_update(const double* partials, int64_t nparts, double* rms, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * Device synthetic vector env (oracle/synth_env.py restates it).
+ * Stands behind BaseVectorEnv.step/reset (tianshou/env/venvs.py:260-381).
+ * Rows r < k act on env ids[r] (ids NULL -> env r).  step() writes raw obs rows,
+ * rew (f64), terminated/truncated (u8), and per-block column partial sums
+ * (sum, sumsq as f64, layout [nblk][dim][2]) for the VectorEnvNormObs update;
+ * reset() does the same for rows with mask[r] != 0 only (mask NULL -> all rows).
+ * ------------------------------------------------------------------------------- */
+int64_t tsrl_env_num_partials(int64_t k);
+int tsrl_synth_box_step(const int64_t* ids, int64_t k, int64_t dim, uint64_t seed,
+                        int64_t ep_len, int64_t* ep_j, int64_t* ep_t, float* obs_out,
+                        double* rew_out, uint8_t* term_out, uint8_t* trunc_out,
+                        double* col_partials, void* stream);
+int tsrl_synth_box_reset(const int64_t* ids, const uint8_t* mask, int64_t k, int64_t dim,
+                         uint64_t seed, int64_t ep_len, int64_t* ep_j, int64_t* ep_t,
+                         float* obs_out, double* col_partials, void* stream);
+int tsrl_synth_u8_step(const int64_t* ids, int64_t k, int64_t obs_bytes, uint64_t seed,
+                       int64_t ep_len, int64_t* ep_j, int64_t* ep_t, uint8_t* obs_out,
+                       double* rew_out, uint8_t* term_out, uint8_t* trunc_out, void* stream);
+int tsrl_synth_u8_reset(const int64_t* ids, const uint8_t* mask, int64_t k,
+                        int64_t obs_bytes, uint64_t seed, int64_t ep_len, int64_t* ep_j,
+                        int64_t* ep_t, uint8_t* obs_out, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * Observation RunningMeanStd (VectorEnvNormObs, tianshou/env/venv_wrappers.py:65-112;
+ * RunningMeanStd, tianshou/utils/statistics.py:69-114).
+ * rms_merge folds column partials of a batch of `count` rows (count = number of mask
+ * bytes set, or k when mask == NULL; zero rows -> no update) into mean/var (f32 [dim])
+ * and *count (f64 scalar on device).  rms_norm_rows writes
+ * clip((x - mean) / sqrt(var + eps), +-clip) for rows with mask[r] (all when NULL).
+ * ------------------------------------------------------------------------------- */
+int tsrl_rms_merge(const double* col_partials, int64_t nblk, int64_t dim,
+                   const uint8_t* mask, int64_t k, float* mean, float* var, double* count,
+                   void* stream);
+int tsrl_rms_norm_rows(const float* x, const uint8_t* mask, int64_t k, int64_t dim,
+                       const float* mean, const float* var, float eps, float clip,
+                       float* out, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * VectorReplayBuffer add for one vector step (ReplayBufferManager.add,
+ * tianshou/data/buffer/manager.py:104-161 + ReplayBuffer._add_index, base.py:195-214).
+ * Row r (env b = ids ? ids[r] : r) goes to storage row ptr[r] (or offset[b] + uniform_rel
+ * when ptr is NULL: every env at the same ring position); every pointer except the
+ * episode-statistics ones may be NULL (that key is then not written).
+ *   obs_dst[ptr]      <- obs_src[r]                       (row_bytes_obs bytes)
+ *   obs_next_dst[ptr] <- norm(obs_next_src[r]) or copy    (norm when mean != NULL)
+ *   cur_obs[r]        <- the same obs_next value          (Collector's data.obs = obs_next)
+ *   act_dst[ptr]      <- act_src[r]
+ *   rew/flags/env_id scalars; episode stats per env b:
+ *   ep_rew[b] += rew ; ep_len[b] += 1 ; on done record (ep_rew, ep_len, ep_idx+offset) in
+ *   out_ep_* (per row, nullable) and stat_*[ptr] (per storage row, nullable), then reset
+ *   and set ep_idx[b] = next_rel[r].
+ * ------------------------------------------------------------------------------- */
+typedef struct tsrl_add_args {
+    const int64_t* ids;      /* [k] env ids or NULL (identity) */
+    const int64_t* ptr;      /* [k] global storage rows, or NULL: offset[b] + uniform_rel */
+    const int64_t* next_rel; /* [k] sub-buffer index after the add (for ep_idx reset),
+                                or NULL: uniform_next */
+    const int64_t* offset;   /* [num_envs] sub-buffer offsets */
+    int64_t k;
+    int64_t uniform_rel;     /* every env at the same sub-buffer index (n_step collect) */
+    int64_t uniform_next;
+    /* row payloads */
+    const void* obs_src; void* obs_dst; int64_t obs_row_bytes;
+    const float* obs_next_src; float* obs_next_dst; float* cur_obs; int64_t obs_dim;
+    const float* norm_mean; const float* norm_var; float norm_eps; float norm_clip;
+    const void* obs_next_src_raw; void* obs_next_dst_raw; /* non-f32 obs_next (copy) */
+    const void* act_src; void* act_dst; int64_t act_row_bytes;
+    /* scalars */
+    const double* rew; const uint8_t* term; const uint8_t* trunc;
+    double* rew_dst; uint8_t* term_dst; uint8_t* trunc_dst; uint8_t* done_dst;
+    int64_t* env_id_dst;
+    /* episode statistics (device state, per env) */
+    double* ep_rew; int64_t* ep_len; int64_t* ep_idx;
+    double* out_ep_rew; int64_t* out_ep_len; int64_t* out_ep_idx; /* per row, nullable */
+    double* stat_rew; int64_t* stat_len; int64_t* stat_idx;       /* per storage row */
+} tsrl_add_args;
+int tsrl_buffer_add(const tsrl_add_args* a, void* stream);
+
+/* Row gather: dst[i] = src[idx[i]] for rows of row_bytes bytes (Batch.__getitem__ /
+ * ReplayBuffer.__getitem__ fancy indexing, tianshou/data/batch.py:446-460,
+ * buffer/base.py:360-389). */
+int tsrl_gather_rows(const void* src, int64_t row_bytes, const int64_t* idx, int64_t k,
+                     void* dst, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * PPO clipped surrogate + value + entropy loss, Gaussian Independent(Normal(mu, exp(s)),1)
+ * with state-independent log-std s (PPOPolicy.learn, tianshou/policy/modelfree/ppo.py:
+ * 106-151; ActorProb, utils/net/continuous.py:218-235; fixed_std_normal,
+ * utils/models.py:96-97).  Minibatch rows come from the full-batch arrays through idx
+ * (idx NULL -> identity).  Gradients of the MEAN loss over `b_global` rows are written
+ * per row (grad_mu [b,A], grad_value [b]); per-block partial sums (layout
+ * [nblk][4 + A]: clip_sum, vf_sum, count, unused, dlogstd[A]) feed tsrl_reduce_partials
+ * and tsrl_ppo_gauss_finalize.
+ * ------------------------------------------------------------------------------- */
+typedef struct tsrl_ppo_params {
+    double eps_clip;        /* Python floats, rounded to f32 where torch would */
+    double dual_clip;       /* <= 0 : None */
+    double vf_coef;
+    double ent_coef;
+    double adv_eps;         /* 1e-8 (PGPolicy._eps) */
+    double b_global;        /* rows in the (global) minibatch */
+    int32_t value_clip;
+    int32_t norm_adv;
+} tsrl_ppo_params;
+
+int64_t tsrl_ppo_num_partials(int64_t b);
+int tsrl_adv_moments(const float* adv, const int64_t* idx, int64_t b, double* partials,
+                     void* stream);
+int tsrl_reduce_partials(const double* partials, int64_t nblk, int64_t width, double* out,
+                         void* stream);
+int tsrl_ppo_gauss_fwd_bwd(const float* mu, const float* log_std, const float* value,
+                           const float* act, const float* logp_old, const float* adv,
+                           const float* ret, const float* v_s, const int64_t* idx,
+                           int64_t b, int64_t act_dim, const double* adv_sums,
+                           tsrl_ppo_params p, float* grad_mu, float* grad_value,
+                           double* partials, void* stream);
+int tsrl_ppo_gauss_finalize(const double* sums, int64_t act_dim, const float* log_std,
+                            tsrl_ppo_params p, float* losses, float* grad_log_std,
+                            void* stream);
+/* log N(act | mu, exp(log_std)) summed over the action dim (Independent(...,1).log_prob),
+ * used for logp_old in PPOPolicy.process_fn (ppo.py:95-96). */
+int tsrl_gauss_logp(const float* mu, const float* log_std, const float* act, int64_t b,
+                    int64_t act_dim, float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TSRL_H_ */

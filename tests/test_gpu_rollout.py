@@ -1,0 +1,199 @@
+"""Device VectorReplayBuffer / synthetic env / VectorEnvNormObs / Collector parity with the
+reference (goldens recorded by tools/gen_goldens.py).  Index math, rewards, flags, episode
+statistics: bit-exact.  Normalised observations: allclose (obs_rms moments are accumulated
+in f64 on device vs the reference's sequential f32 NumPy sums)."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref, synth_env
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    return torch.device("cuda", 0)
+
+
+@pytest.mark.parametrize("name", ["manager", "ragged"])
+def test_buffer_trace_device(golden_dir, dev, name):
+    from tianshou_amd.data import Batch, VectorReplayBuffer
+    with open(os.path.join(golden_dir, "buffer_traces.json")) as f:
+        tr = json.load(f)[name]
+    buf = VectorReplayBuffer(tr["total"], tr["num"], device=dev)
+    allidx = np.arange(buf.maxsize)
+    for step in tr["trace"]:
+        if step["op"] == "add":
+            d = step["data"]
+            ptr, ep_rew, ep_len, ep_idx = buf.add(Batch(**d), buffer_ids=step["ids"])
+            assert ptr.tolist() == step["ptr"]
+            assert ep_rew.tolist() == step["ep_rew"]
+            assert ep_len.tolist() == step["ep_len"]
+            assert ep_idx.tolist() == step["ep_idx"]
+        else:
+            buf.reset(step["keep"])
+        st = step["state"]
+        assert buf.sample_indices(0).tolist() == st["sample0"]
+        assert buf.prev(allidx).tolist() == st["prev"]
+        assert buf.next(allidx).tolist() == st["next"]
+        assert buf.unfinished_index().tolist() == st["unfinished"]
+        assert len(buf) == st["len"]
+        if st["done"]:
+            assert buf.done.cpu().numpy().astype(int).tolist() == st["done"]
+    # sample(0) gathers every key in sample order
+    batch, idx = buf.sample(0)
+    assert torch.equal(batch.done.cpu(), buf.done.cpu()[torch.as_tensor(idx)])
+
+
+def test_gather_rows(dev):
+    from tianshou_amd.data.batch import gather_rows
+    for shape, dt in (((1000, 376), torch.float32), ((777, 4, 84, 84), torch.uint8),
+                      ((5000,), torch.float64), ((300, 17), torch.float32), ((64, 3), torch.int8)):
+        x = (torch.rand(shape, device=dev) * 100).to(dt)
+        idx = torch.randint(0, shape[0], (2 * shape[0] + 3,), device=dev)
+        assert torch.equal(gather_rows(x, idx), x[idx])
+
+
+def test_synth_env_matches_oracle(dev):
+    from tianshou_amd.env import SyntheticVectorEnv
+    E, D, L = 37, 29, 9
+    env = SyntheticVectorEnv(E, (D,), 3, ep_len=L, seed=5, device=dev)
+    o = synth_env.SynthVecEnvNP(E, (D,), 3, L, seed=5)
+    obs, _ = env.reset()
+    assert torch.equal(obs.cpu(), torch.as_tensor(o.reset()))
+    for t in range(25):
+        nxt, rew, term, trunc, _ = env.step(None)
+        n2, r2, t2, u2 = o.step()
+        assert np.array_equal(nxt.cpu().numpy(), n2)
+        assert np.array_equal(rew.cpu().numpy(), r2)
+        assert np.array_equal(term.cpu().numpy(), t2) and np.array_equal(trunc.cpu().numpy(), u2)
+        done = np.flatnonzero(t2 | u2)
+        if len(done):
+            r_obs, _ = env.reset(done)
+            assert np.array_equal(r_obs.cpu().numpy(), o.reset(done))
+    # u8 Atari-shaped frames
+    envu = SyntheticVectorEnv(3, (4, 84, 84), 6, ep_len=7, device=dev, obs_dtype=np.uint8,
+                              discrete=True)
+    ou = synth_env.SynthVecEnvNP(3, (4, 84, 84), 6, 7, u8=True)
+    assert np.array_equal(envu.reset()[0].cpu().numpy(), ou.reset())
+    assert np.array_equal(envu.step(None)[0].cpu().numpy(), ou.step()[0])
+
+
+def test_rms_kernels_vs_reference(golden_dir, dev):
+    from tianshou_amd.utils.statistics import DeviceRunningMeanStd
+    z = np.load(os.path.join(golden_dir, "rms.npz"))
+    rms = DeviceRunningMeanStd(6, dev)
+    for i in range(int(z["n"])):
+        x = torch.as_tensor(z[f"x{i}"], device=dev)
+        rms.update(x)
+        np.testing.assert_allclose(rms.mean, z[f"mean{i}"], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(rms.var, z[f"var{i}"], rtol=1e-5, atol=1e-6)
+        assert rms.count == int(z[f"count{i}"])
+        np.testing.assert_allclose(rms.norm(x).cpu().numpy(), z[f"norm{i}"], rtol=1e-4,
+                                   atol=1e-5)
+
+
+def _collector_setup(z, dev, n_envs=None):
+    from tianshou_amd.data import Collector, VectorReplayBuffer
+    from tianshou_amd.env import SyntheticVectorEnv, VectorEnvNormObs
+    from tianshou_amd.policy import PPOPolicy
+    from tianshou_amd.utils.models import fixed_std_normal, get_actor_critic, init_and_get_optim
+    E, D, A, L, T = (int(z[k]) for k in ("E", "D", "A", "L", "T"))
+    env = VectorEnvNormObs(SyntheticVectorEnv(E, (D,), A, ep_len=L, device=dev))
+    actor, critic = get_actor_critic((D,), (64, 64), (A,), dev)
+    optim = init_and_get_optim(actor, critic, 3e-4)
+    policy = PPOPolicy(actor, critic, optim, fixed_std_normal, action_space=env.action_space,
+                       discount_factor=0.99, gae_lambda=0.95, max_grad_norm=0.5, vf_coef=0.25,
+                       ent_coef=0.0, reward_normalization=True, advantage_normalization=True,
+                       eps_clip=0.2).to(dev)
+    sd = {k[len("init_"):]: torch.as_tensor(z[k]) for k in z.files if k.startswith("init_")}
+    policy.load_state_dict(sd)
+    buf = VectorReplayBuffer(E * T, E, device=dev)
+    return env, policy, buf, Collector(policy, env, buf), (E, D, A, L, T)
+
+
+def _check_buf(z, prefix, buf, D):
+    m = buf._meta
+    assert np.array_equal(m.rew.cpu().numpy(), z[prefix + "rew"])
+    assert np.array_equal(m.terminated.cpu().numpy(), z[prefix + "terminated"])
+    assert np.array_equal(m.truncated.cpu().numpy(), z[prefix + "truncated"])
+    assert np.array_equal(m.done.cpu().numpy(), z[prefix + "done"])
+    written = z[prefix + "done"] | (np.abs(z[prefix + "obs"]).sum(-1) > 0)
+    assert np.array_equal(m.info.env_id.cpu().numpy()[written], z[prefix + "env_id"][written])
+    np.testing.assert_allclose(m.obs.cpu().numpy(), z[prefix + "obs"], rtol=2e-4, atol=2e-5)
+    np.testing.assert_allclose(m.obs_next.cpu().numpy(), z[prefix + "obs_next"], rtol=2e-4,
+                               atol=2e-5)
+
+
+def _check_stats(z, prefix, res):
+    assert res["n/ep"] == int(z[prefix + "n_ep"])
+    assert res["n/st"] == int(z[prefix + "n_st"])
+    assert res["lens"].tolist() == z[prefix + "lens"].tolist()
+    assert res["idxs"].tolist() == z[prefix + "idxs"].tolist()
+    assert np.array_equal(res["rews"], z[prefix + "rews"])
+    assert res["rew"] == pytest.approx(float(z[prefix + "rew"]), rel=1e-12)
+    assert res["len_std"] == pytest.approx(float(z[prefix + "len_std"]), rel=1e-12)
+
+
+def test_collector_matches_reference(golden_dir, dev):
+    """collector.py:184-402 + VectorEnvNormObs + buffer, two n_step collects with
+    reset_buffer(keep_statistics=True) between them, and an n_episode collect."""
+    z = np.load(os.path.join(golden_dir, "collector.npz"))
+    env, policy, buf, c, (E, D, A, L, T) = _collector_setup(z, dev)
+    res1 = c.collect(n_step=E * T)
+    _check_stats(z, "c1_", res1)
+    _check_buf(z, "c1_buf_", buf, D)
+    rms = env.get_obs_rms()
+    np.testing.assert_allclose(rms.mean, z["c1_rms_mean"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(rms.var, z["c1_rms_var"], rtol=1e-5, atol=1e-6)
+    assert rms.count == int(z["c1_rms_count"])
+    np.testing.assert_allclose(c.data.obs.cpu().numpy(), z["c1_data_obs"], rtol=2e-4, atol=2e-5)
+    c.reset_buffer(keep_statistics=True)
+    res2 = c.collect(n_step=E * T // 2)
+    _check_stats(z, "c2_", res2)
+    assert rms.count == int(z["c2_rms_count"])
+    # n_episode collection on a fresh collector
+    from tianshou_amd.data import Collector, VectorReplayBuffer
+    from tianshou_amd.env import SyntheticVectorEnv, VectorEnvNormObs
+    env3 = VectorEnvNormObs(SyntheticVectorEnv(E, (D,), A, ep_len=L, device=dev))
+    buf3 = VectorReplayBuffer(E * T, E, device=dev)
+    c3 = Collector(policy, env3, buf3)
+    res3 = c3.collect(n_episode=11)
+    _check_stats(z, "c3_", res3)
+    assert buf3._lengths.tolist() == z["c3_lengths"].tolist()
+    assert buf3.last_index.tolist() == z["c3_last_index"].tolist()
+    _check_buf(z, "c3_buf_", buf3, D)
+    assert env3.get_obs_rms().count == int(z["c3_rms_count"])
+
+
+def test_process_fn_matches_reference(golden_dir, dev):
+    """PPOPolicy.process_fn on the reference's collected buffer: critic values, GAE with
+    rew_norm (f64 path), logp_old, ret_rms (ppo.py:87-97, a2c.py:83-117)."""
+    z = np.load(os.path.join(golden_dir, "collector.npz"))
+    env, policy, buf, c, (E, D, A, L, T) = _collector_setup(z, dev)
+    c.collect(n_step=E * T)  # fills ring bookkeeping; overwrite payload with the reference's
+    m = buf._meta
+    for k in ("obs", "obs_next", "act", "rew", "terminated", "truncated", "done"):
+        getattr(m, k).copy_(torch.as_tensor(z["c1_buf_" + k], device=dev))
+    batch, idx = buf.sample(0)
+    assert idx.tolist() == z["c1_indices"].tolist()
+    batch = policy.process_fn(batch, buf, idx)
+    for k in ("v_s", "logp_old"):
+        np.testing.assert_allclose(batch[k].cpu().numpy(), z["pf_" + k], rtol=1e-4, atol=1e-5)
+    for k in ("returns", "adv"):
+        np.testing.assert_allclose(batch[k].cpu().numpy(), z["pf_" + k], rtol=1e-4, atol=1e-4)
+    assert policy.ret_rms.mean == pytest.approx(float(z["pf_ret_rms_mean"]), rel=1e-5)
+    assert policy.ret_rms.var == pytest.approx(float(z["pf_ret_rms_var"]), rel=1e-5)
+    assert policy.ret_rms.count == int(z["pf_ret_rms_count"])
+    np.random.seed(5)
+    res = policy.learn(batch, batch_size=E * T // 4, repeat=2)
+    np.testing.assert_allclose(res["loss"], z["learn_loss"], rtol=2e-3, atol=2e-4)
+    sd = policy.state_dict()
+    for k in z.files:
+        if k.startswith("final_actor.") or k.startswith("final_critic."):
+            np.testing.assert_allclose(sd[k[len("final_"):]].cpu().numpy(), z[k], rtol=1e-3,
+                                       atol=1e-4)

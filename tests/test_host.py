@@ -1,0 +1,120 @@
+"""CPU-only checks of the host side: the C-ABI library loads and exports every symbol the
+header declares, the host ring arithmetic reproduces the reference buffer traces bit-exactly,
+minibatch splitting follows Batch.split, and the Batch container behaves."""
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+from tests.conftest import ROOT
+
+
+def _header_symbols():
+    with open(os.path.join(ROOT, "include", "tsrl.h")) as f:
+        txt = f.read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(tsrl_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    import ctypes
+    from tianshou_amd import _C
+    syms = _header_symbols()
+    assert len(syms) >= 20
+    lib = ctypes.CDLL(_C.LIB_PATH)
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    assert set(syms) == set(_C.EXPORTED), set(syms) ^ set(_C.EXPORTED)
+    assert _C.lib().tsrl_version().startswith(b"tsrl")
+
+
+def test_ctypes_struct_layout_matches_header(tmp_path):
+    """AddArgs / PPOParams mirror the C structs (sizes via a compiled probe)."""
+    import ctypes
+    import subprocess
+    from tianshou_amd import _C
+    src = tmp_path / "probe.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "tsrl.h"\n'
+                   'int main(){printf("%zu %zu %zu %zu\\n", sizeof(tsrl_add_args), '
+                   'sizeof(tsrl_ppo_params), offsetof(tsrl_add_args, stat_idx), '
+                   'offsetof(tsrl_ppo_params, norm_adv));}')
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)],
+                   check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()
+    assert int(out[0]) == ctypes.sizeof(_C.AddArgs)
+    assert int(out[1]) == ctypes.sizeof(_C.PPOParams)
+    assert int(out[2]) == _C.AddArgs.stat_idx.offset
+    assert int(out[3]) == _C.PPOParams.norm_adv.offset
+
+
+@pytest.mark.parametrize("name", ["manager", "ragged"])
+def test_ring_index_matches_reference(golden_dir, name):
+    from tianshou_amd.data.buffer import RingIndex
+    with open(os.path.join(golden_dir, "buffer_traces.json")) as f:
+        tr = json.load(f)[name]
+    size = int(np.ceil(tr["total"] / tr["num"]))
+    ring = RingIndex(size, tr["num"])
+    for step in tr["trace"]:
+        if step["op"] == "add":
+            ptr, _ = ring.advance(np.asarray(step["ids"], np.int64))
+            assert ptr.tolist() == step["ptr"]
+        else:
+            ring.reset()
+        st = step["state"]
+        assert ring.sample0().tolist() == st["sample0"]
+        assert ring.last_index.tolist() == st["last_index"]
+        assert ring.lengths.tolist() == st["lengths"]
+
+
+def test_ring_uniform_fast_paths():
+    from tianshou_amd.data.buffer import RingIndex
+    ring = RingIndex(16, 8)
+    for t in range(16):
+        assert ring.uniform_rel() == t
+        ptr, nxt = ring.advance(None)
+        assert ptr.tolist() == (np.arange(8) * 16 + t).tolist()
+    assert ring.is_identity()
+    assert ring.sample0().tolist() == list(range(128))
+    assert ring.chunk_layout()[0] == 16
+    ring.advance(np.array([3]))
+    assert ring.uniform_rel() is None and not ring.is_identity()
+
+
+def test_split_bounds_and_indices(golden_dir):
+    from tianshou_amd.data.batch import split_indices
+    from tianshou_amd.policy.ppo import split_bounds
+    with open(os.path.join(golden_dir, "split.json")) as f:
+        g = json.load(f)
+    for c in g["cases"]:
+        if c["seed"] is not None:
+            np.random.seed(c["seed"])
+        parts = split_indices(c["n"], c["size"], c["shuffle"], c["merge_last"])
+        assert [p.tolist() for p in parts] == c["parts"]
+        if c["merge_last"]:
+            b = split_bounds(c["n"], c["size"], True)
+            assert [e - s for s, e in b] == [len(p) for p in c["parts"]]
+
+
+def test_batch_container():
+    from tianshou_amd.data import Batch
+    b = Batch(obs=np.arange(10).reshape(5, 2), rew=np.arange(5.0), info={"env_id": np.arange(5)})
+    assert len(b) == 5
+    s = b[np.array([4, 0])]
+    assert s.obs.tolist() == [[8, 9], [0, 1]] and s.info.env_id.tolist() == [4, 0]
+    b[np.array([1])] = Batch(rew=np.array([7.0]))
+    assert b.rew[1] == 7.0
+    parts = list(b.split(2, shuffle=False, merge_last=True))
+    assert [len(p) for p in parts] == [2, 3]
+    with pytest.raises(AssertionError):
+        list(b.split(0))
+
+
+def test_product_refuses_cpu_tensors():
+    """No CPU fallback: kernels only take HIP device tensors."""
+    import torch
+    from tianshou_amd import _C
+    with pytest.raises(_C.TsrlError):
+        _C.ptr(torch.zeros(3))

@@ -1,0 +1,249 @@
+// Device synthetic vector env.  oracle/synth_env.py is the CPU restatement.
+//
+// Stands behind the BaseVectorEnv.step/reset surface (tianshou/env/venvs.py:260-381): one
+// kernel steps every env of the shard and, while the raw observation rows are still in
+// registers, accumulates the per-column (sum, sumsq) partials VectorEnvNormObs needs for its
+// RunningMeanStd update (venv_wrappers.py:93-99), so the obs rows are read once.
+#include "tsrl_common.h"
+
+namespace tsrl {
+namespace {
+
+constexpr int TPB = 256;
+constexpr int ROWS = 32;  // env rows per workgroup
+constexpr uint64_t GOLD = 0x9E3779B97F4A7C15ull;
+constexpr uint64_t REW_SALT = 0xD1B54A32D192ED03ull;
+
+__device__ __forceinline__ uint64_t env_key(uint64_t s_seed, uint64_t e, int64_t j, int64_t t) {
+    return sm64(sm64(sm64(s_seed ^ e) ^ (uint64_t)j) ^ (uint64_t)t);
+}
+
+__device__ __forceinline__ float box_val(uint64_t k, int64_t d) {
+    const uint64_t h = sm64(k + (uint64_t)d * GOLD);
+    return (float)(h >> 40) * 0x1p-23f - 1.0f;
+}
+
+struct RowState {
+    uint64_t key;
+    int active;
+};
+
+// Rows [r0, r0+ROWS): obs rows + column partials over active rows.
+__device__ void box_rows(const RowState* rs, int64_t r0, int64_t k, int64_t dim, float* obs,
+                         double* partials) {
+    const int nrows = (int)min((int64_t)ROWS, k - r0);
+    for (int64_t d = threadIdx.x; d < dim; d += TPB) {
+        double s = 0.0, ss = 0.0;
+        for (int r = 0; r < nrows; ++r) {
+            if (!rs[r].active) continue;
+            const float x = box_val(rs[r].key, d);
+            obs[(r0 + r) * dim + d] = x;
+            s += (double)x;
+            ss += (double)x * (double)x;
+        }
+        if (partials) {
+            double* pp = partials + ((int64_t)blockIdx.x * dim + d) * 2;
+            pp[0] = s;
+            pp[1] = ss;
+        }
+    }
+}
+
+__global__ __launch_bounds__(TPB) void box_step_kernel(const int64_t* ids, int64_t k,
+                                                       int64_t dim, uint64_t s_seed,
+                                                       int64_t ep_len, int64_t* ep_j,
+                                                       int64_t* ep_t, float* obs, double* rew,
+                                                       uint8_t* term, uint8_t* trunc,
+                                                       double* partials) {
+    __shared__ RowState rs[ROWS];
+    const int64_t r0 = (int64_t)blockIdx.x * ROWS;
+    if (threadIdx.x < ROWS) {
+        const int64_t r = r0 + threadIdx.x;
+        RowState st = {0ull, 0};
+        if (r < k) {
+            const int64_t e = ids ? ids[r] : r;
+            const int64_t j = ep_j[e];
+            const int64_t t = ep_t[e] + 1;
+            ep_t[e] = t;
+            st.key = env_key(s_seed, (uint64_t)e, j, t);
+            st.active = 1;
+            const uint64_t h = sm64(st.key ^ REW_SALT);
+            rew[r] = (double)(h >> 40) * 0x1p-24;
+            const bool done = t >= ep_len;
+            term[r] = (uint8_t)(done && (e % 2 == 0));
+            trunc[r] = (uint8_t)(done && (e % 2 == 1));
+        }
+        rs[threadIdx.x] = st;
+    }
+    __syncthreads();
+    box_rows(rs, r0, k, dim, obs, partials);
+}
+
+__global__ __launch_bounds__(TPB) void box_reset_kernel(const int64_t* ids, const uint8_t* mask,
+                                                        int64_t k, int64_t dim, uint64_t s_seed,
+                                                        int64_t ep_len, int64_t* ep_j,
+                                                        int64_t* ep_t, float* obs,
+                                                        double* partials) {
+    __shared__ RowState rs[ROWS];
+    const int64_t r0 = (int64_t)blockIdx.x * ROWS;
+    if (threadIdx.x < ROWS) {
+        const int64_t r = r0 + threadIdx.x;
+        RowState st = {0ull, 0};
+        if (r < k && (!mask || mask[r])) {
+            const int64_t e = ids ? ids[r] : r;
+            const int64_t j = ep_j[e] + 1;
+            const int64_t t = (j == 0) ? (e % ep_len) : 0;
+            ep_j[e] = j;
+            ep_t[e] = t;
+            st.key = env_key(s_seed, (uint64_t)e, j, t);
+            st.active = 1;
+        }
+        rs[threadIdx.x] = st;
+    }
+    __syncthreads();
+    box_rows(rs, r0, k, dim, obs, partials);
+}
+
+// u8 (Atari-shaped) observations: 4 bytes per thread-iteration, packed 32-bit stores.
+__device__ void u8_rows(const RowState* rs, int64_t r0, int64_t k, int64_t nbytes,
+                        uint8_t* obs) {
+    const int nrows = (int)min((int64_t)ROWS, k - r0);
+    const int64_t nw = nbytes / 4;
+    for (int r = 0; r < nrows; ++r) {
+        if (!rs[r].active) continue;
+        const uint64_t key = rs[r].key;
+        uint8_t* row = obs + (r0 + r) * nbytes;
+        if ((nbytes & 3) == 0 && (((uintptr_t)row) & 3) == 0) {
+            uint32_t* w = reinterpret_cast<uint32_t*>(row);
+            for (int64_t q = threadIdx.x; q < nw; q += TPB) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    v |= (uint32_t)(sm64(key + (uint64_t)(4 * q + b) * GOLD) & 0xFF) << (8 * b);
+                w[q] = v;
+            }
+        } else {
+            for (int64_t i = threadIdx.x; i < nbytes; i += TPB)
+                row[i] = (uint8_t)(sm64(key + (uint64_t)i * GOLD) & 0xFF);
+        }
+    }
+}
+
+__global__ __launch_bounds__(TPB) void u8_step_kernel(const int64_t* ids, int64_t k,
+                                                      int64_t nbytes, uint64_t s_seed,
+                                                      int64_t ep_len, int64_t* ep_j,
+                                                      int64_t* ep_t, uint8_t* obs, double* rew,
+                                                      uint8_t* term, uint8_t* trunc) {
+    __shared__ RowState rs[ROWS];
+    const int64_t r0 = (int64_t)blockIdx.x * ROWS;
+    if (threadIdx.x < ROWS) {
+        const int64_t r = r0 + threadIdx.x;
+        RowState st = {0ull, 0};
+        if (r < k) {
+            const int64_t e = ids ? ids[r] : r;
+            const int64_t j = ep_j[e];
+            const int64_t t = ep_t[e] + 1;
+            ep_t[e] = t;
+            st.key = env_key(s_seed, (uint64_t)e, j, t);
+            st.active = 1;
+            const uint64_t h = sm64(st.key ^ REW_SALT);
+            rew[r] = (double)(h >> 40) * 0x1p-24;
+            const bool done = t >= ep_len;
+            term[r] = (uint8_t)(done && (e % 2 == 0));
+            trunc[r] = (uint8_t)(done && (e % 2 == 1));
+        }
+        rs[threadIdx.x] = st;
+    }
+    __syncthreads();
+    u8_rows(rs, r0, k, nbytes, obs);
+}
+
+__global__ __launch_bounds__(TPB) void u8_reset_kernel(const int64_t* ids, const uint8_t* mask,
+                                                       int64_t k, int64_t nbytes,
+                                                       uint64_t s_seed, int64_t ep_len,
+                                                       int64_t* ep_j, int64_t* ep_t,
+                                                       uint8_t* obs) {
+    __shared__ RowState rs[ROWS];
+    const int64_t r0 = (int64_t)blockIdx.x * ROWS;
+    if (threadIdx.x < ROWS) {
+        const int64_t r = r0 + threadIdx.x;
+        RowState st = {0ull, 0};
+        if (r < k && (!mask || mask[r])) {
+            const int64_t e = ids ? ids[r] : r;
+            const int64_t j = ep_j[e] + 1;
+            const int64_t t = (j == 0) ? (e % ep_len) : 0;
+            ep_j[e] = j;
+            ep_t[e] = t;
+            st.key = env_key(s_seed, (uint64_t)e, j, t);
+            st.active = 1;
+        }
+        rs[threadIdx.x] = st;
+    }
+    __syncthreads();
+    u8_rows(rs, r0, k, nbytes, obs);
+}
+
+inline unsigned blocks_for(int64_t k) { return (unsigned)((k + ROWS - 1) / ROWS); }
+
+}  // namespace
+}  // namespace tsrl
+
+using namespace tsrl;
+
+extern "C" int64_t tsrl_env_num_partials(int64_t k) { return (k + ROWS - 1) / ROWS; }
+
+extern "C" int tsrl_synth_box_step(const int64_t* ids, int64_t k, int64_t dim, uint64_t seed,
+                                   int64_t ep_len, int64_t* ep_j, int64_t* ep_t, float* obs_out,
+                                   double* rew_out, uint8_t* term_out, uint8_t* trunc_out,
+                                   double* col_partials, void* stream) {
+    TSRL_CHECK_ARG(k >= 0 && dim > 0 && ep_len > 0, "tsrl_synth_box_step: bad sizes");
+    if (k == 0) return 0;
+    TSRL_CHECK_ARG(ep_j && ep_t && obs_out && rew_out && term_out && trunc_out,
+                   "tsrl_synth_box_step: null pointer");
+    hipLaunchKernelGGL(box_step_kernel, dim3(blocks_for(k)), dim3(TPB), 0, as_stream(stream),
+                       ids, k, dim, sm64(seed), ep_len, ep_j, ep_t, obs_out, rew_out, term_out,
+                       trunc_out, col_partials);
+    TSRL_LAUNCH_CHECK("tsrl_synth_box_step");
+    return 0;
+}
+
+extern "C" int tsrl_synth_box_reset(const int64_t* ids, const uint8_t* mask, int64_t k,
+                                    int64_t dim, uint64_t seed, int64_t ep_len, int64_t* ep_j,
+                                    int64_t* ep_t, float* obs_out, double* col_partials,
+                                    void* stream) {
+    TSRL_CHECK_ARG(k >= 0 && dim > 0 && ep_len > 0, "tsrl_synth_box_reset: bad sizes");
+    if (k == 0) return 0;
+    TSRL_CHECK_ARG(ep_j && ep_t && obs_out, "tsrl_synth_box_reset: null pointer");
+    hipLaunchKernelGGL(box_reset_kernel, dim3(blocks_for(k)), dim3(TPB), 0, as_stream(stream),
+                       ids, mask, k, dim, sm64(seed), ep_len, ep_j, ep_t, obs_out, col_partials);
+    TSRL_LAUNCH_CHECK("tsrl_synth_box_reset");
+    return 0;
+}
+
+extern "C" int tsrl_synth_u8_step(const int64_t* ids, int64_t k, int64_t obs_bytes,
+                                  uint64_t seed, int64_t ep_len, int64_t* ep_j, int64_t* ep_t,
+                                  uint8_t* obs_out, double* rew_out, uint8_t* term_out,
+                                  uint8_t* trunc_out, void* stream) {
+    TSRL_CHECK_ARG(k >= 0 && obs_bytes > 0 && ep_len > 0, "tsrl_synth_u8_step: bad sizes");
+    if (k == 0) return 0;
+    TSRL_CHECK_ARG(ep_j && ep_t && obs_out && rew_out && term_out && trunc_out,
+                   "tsrl_synth_u8_step: null pointer");
+    hipLaunchKernelGGL(u8_step_kernel, dim3(blocks_for(k)), dim3(TPB), 0, as_stream(stream), ids,
+                       k, obs_bytes, sm64(seed), ep_len, ep_j, ep_t, obs_out, rew_out, term_out,
+                       trunc_out);
+    TSRL_LAUNCH_CHECK("tsrl_synth_u8_step");
+    return 0;
+}
+
+extern "C" int tsrl_synth_u8_reset(const int64_t* ids, const uint8_t* mask, int64_t k,
+                                   int64_t obs_bytes, uint64_t seed, int64_t ep_len,
+                                   int64_t* ep_j, int64_t* ep_t, uint8_t* obs_out,
+                                   void* stream) {
+    TSRL_CHECK_ARG(k >= 0 && obs_bytes > 0 && ep_len > 0, "tsrl_synth_u8_reset: bad sizes");
+    if (k == 0) return 0;
+    TSRL_CHECK_ARG(ep_j && ep_t && obs_out, "tsrl_synth_u8_reset: null pointer");
+    hipLaunchKernelGGL(u8_reset_kernel, dim3(blocks_for(k)), dim3(TPB), 0, as_stream(stream),
+                       ids, mask, k, obs_bytes, sm64(seed), ep_len, ep_j, ep_t, obs_out);
+    TSRL_LAUNCH_CHECK("tsrl_synth_u8_reset");
+    return 0;
+}

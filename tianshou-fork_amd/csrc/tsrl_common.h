@@ -1,0 +1,54 @@
+// Shared helpers for the libtsrl HIP kernels (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdarg.h>
+
+#include "../../include/tsrl.h"
+
+namespace tsrl {
+
+constexpr int kWave = 64;
+
+// Thread-local last-error message, exposed through tsrl_last_error().
+void set_error(const char* fmt, ...);
+
+#define TSRL_CHECK_ARG(cond, ...)                                   \
+    do {                                                            \
+        if (!(cond)) {                                              \
+            ::tsrl::set_error(__VA_ARGS__);                         \
+            return (int)hipErrorInvalidValue;                       \
+        }                                                           \
+    } while (0)
+
+#define TSRL_LAUNCH_CHECK(what)                                                     \
+    do {                                                                            \
+        hipError_t _e = hipGetLastError();                                          \
+        if (_e != hipSuccess) {                                                     \
+            ::tsrl::set_error("%s: launch failed: %s", what, hipGetErrorString(_e)); \
+            return (int)_e;                                                         \
+        }                                                                           \
+    } while (0)
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+__host__ __device__ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// splitmix64 finaliser of (x + golden gamma): the counter-based hash of the synthetic env
+// (oracle/synth_env.py restates it on the CPU).
+__host__ __device__ __forceinline__ uint64_t sm64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// Wave-wide sum of a double (64 lanes, xor butterfly).
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+    return v;
+}
+
+}  // namespace tsrl

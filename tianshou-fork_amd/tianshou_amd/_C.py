@@ -1,0 +1,125 @@
+"""ctypes binding of libtsrl.so (include/tsrl.h) -- the only way this package reaches the GPU
+kernels.  There is no CPU fallback: if the library is missing, or a tensor handed to a
+kernel is not a HIP device tensor, the call raises.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libtsrl.so")
+
+_i64 = ctypes.c_int64
+_u64 = ctypes.c_uint64
+_p = ctypes.c_void_p
+_d = ctypes.c_double
+_f = ctypes.c_float
+_i32 = ctypes.c_int32
+
+
+class AddArgs(ctypes.Structure):
+    """Mirror of ``tsrl_add_args`` (field order must match include/tsrl.h)."""
+    _fields_ = [
+        ("ids", _p), ("ptr", _p), ("next_rel", _p), ("offset", _p), ("k", _i64),
+        ("uniform_rel", _i64), ("uniform_next", _i64),
+        ("obs_src", _p), ("obs_dst", _p), ("obs_row_bytes", _i64),
+        ("obs_next_src", _p), ("obs_next_dst", _p), ("cur_obs", _p), ("obs_dim", _i64),
+        ("norm_mean", _p), ("norm_var", _p), ("norm_eps", _f), ("norm_clip", _f),
+        ("obs_next_src_raw", _p), ("obs_next_dst_raw", _p),
+        ("act_src", _p), ("act_dst", _p), ("act_row_bytes", _i64),
+        ("rew", _p), ("term", _p), ("trunc", _p),
+        ("rew_dst", _p), ("term_dst", _p), ("trunc_dst", _p), ("done_dst", _p),
+        ("env_id_dst", _p),
+        ("ep_rew", _p), ("ep_len", _p), ("ep_idx", _p),
+        ("out_ep_rew", _p), ("out_ep_len", _p), ("out_ep_idx", _p),
+        ("stat_rew", _p), ("stat_len", _p), ("stat_idx", _p),
+    ]
+
+
+class PPOParams(ctypes.Structure):
+    """Mirror of ``tsrl_ppo_params``."""
+    _fields_ = [
+        ("eps_clip", _d), ("dual_clip", _d), ("vf_coef", _d), ("ent_coef", _d),
+        ("adv_eps", _d), ("b_global", _d), ("value_clip", _i32), ("norm_adv", _i32),
+    ]
+
+
+_SIGS = {
+    "tsrl_version": ([], ctypes.c_char_p),
+    "tsrl_last_error": ([], ctypes.c_char_p),
+    "tsrl_gae_workspace_bytes": ([_i64, _i64], _i64),
+    "tsrl_gae_num_partials": ([_i64, _i64], _i64),
+    "tsrl_gae": ([_p, _p, _p, _p, _p, _p, _i64, _i64, _p, _d, _d, _p, _p, _p, _p, _p, _p, _i64,
+                  _p], ctypes.c_int),
+    "tsrl_gae_f64v": ([_p, _p, _p, _p, _p, _p, _i64, _i64, _d, _d, _p, _p, _p, _i64, _p],
+                      ctypes.c_int),
+    "tsrl_ret_rms_update": ([_p, _i64, _p, _p], ctypes.c_int),
+    "tsrl_env_num_partials": ([_i64], _i64),
+    "tsrl_synth_box_step": ([_p, _i64, _i64, _u64, _i64, _p, _p, _p, _p, _p, _p, _p, _p],
+                            ctypes.c_int),
+    "tsrl_synth_box_reset": ([_p, _p, _i64, _i64, _u64, _i64, _p, _p, _p, _p, _p], ctypes.c_int),
+    "tsrl_synth_u8_step": ([_p, _i64, _i64, _u64, _i64, _p, _p, _p, _p, _p, _p, _p],
+                           ctypes.c_int),
+    "tsrl_synth_u8_reset": ([_p, _p, _i64, _i64, _u64, _i64, _p, _p, _p, _p], ctypes.c_int),
+    "tsrl_rms_merge": ([_p, _i64, _i64, _p, _i64, _p, _p, _p, _p], ctypes.c_int),
+    "tsrl_rms_norm_rows": ([_p, _p, _i64, _i64, _p, _p, _f, _f, _p, _p], ctypes.c_int),
+    "tsrl_buffer_add": ([ctypes.POINTER(AddArgs), _p], ctypes.c_int),
+    "tsrl_gather_rows": ([_p, _i64, _p, _i64, _p, _p], ctypes.c_int),
+    "tsrl_ppo_num_partials": ([_i64], _i64),
+    "tsrl_adv_moments": ([_p, _p, _i64, _p, _p], ctypes.c_int),
+    "tsrl_reduce_partials": ([_p, _i64, _i64, _p, _p], ctypes.c_int),
+    "tsrl_ppo_gauss_fwd_bwd": ([_p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _p, PPOParams,
+                                _p, _p, _p, _p], ctypes.c_int),
+    "tsrl_ppo_gauss_finalize": ([_p, _i64, _p, PPOParams, _p, _p, _p], ctypes.c_int),
+    "tsrl_gauss_logp": ([_p, _p, _p, _i64, _i64, _p, _p], ctypes.c_int),
+}
+
+EXPORTED = tuple(_SIGS)
+_LIB = None
+
+
+class TsrlError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libtsrl.so; raise ImportError (loudly) when it has not been built."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"libtsrl.so not found at {LIB_PATH}: build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (args, res) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        _LIB = L
+    return _LIB
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = lib().tsrl_last_error().decode(errors="replace")
+        raise TsrlError(f"{what or 'libtsrl'} failed (hipError {rc}): {msg}")
+
+
+def stream_ptr(device=None):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t, dtype=None):
+    """Device pointer of a contiguous HIP tensor (None -> NULL)."""
+    if t is None:
+        return None
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"expected a torch.Tensor, got {type(t)}")
+    if t.device.type != "cuda":
+        raise TsrlError(f"libtsrl kernels need HIP device tensors; got a tensor on {t.device}")
+    if dtype is not None and t.dtype != dtype:
+        raise TypeError(f"expected dtype {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError("libtsrl kernels need contiguous tensors")
+    return t.data_ptr()

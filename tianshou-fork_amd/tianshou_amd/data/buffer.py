@@ -1,0 +1,480 @@
+"""Device-resident VectorReplayBuffer / ReplayBuffer.
+
+API of tianshou/data/buffer/{base,manager,vecbuf}.py (0.5.1): ``add``, ``sample``,
+``sample_indices``, ``prev``, ``next``, ``unfinished_index``, ``reset``, ``len``,
+``__getitem__`` and attribute access to stored keys.  Layout is the reference's env-major
+one: env b owns storage rows [b*S, (b+1)*S), S = ceil(total_size / buffer_num)
+(vecbuf.py:35).  Storage lives in HBM (torch tensors on the HIP device); the per-env ring
+bookkeeping (_index, _lengths, last_index) is host NumPy, vectorised, and never needs device
+data; episode statistics (ep_rew/ep_len/ep_idx) live on device and are updated by the
+``tsrl_buffer_add`` kernel.
+"""
+from typing import Any, List, Optional, Tuple, Union
+
+import numpy as np
+import torch
+
+from tianshou_amd import _C
+from tianshou_amd.data.batch import Batch, gather_rows
+
+_RESERVED = ("obs", "act", "rew", "terminated", "truncated", "done", "obs_next", "info",
+             "policy")
+
+
+def _default_device():
+    return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
+        else torch.device("cuda")
+
+
+class RingIndex:
+    """Host-side ring arithmetic of ReplayBufferManager (manager.py:24-192, base.py:140-214)
+    for ``num`` sub-buffers of ``size`` rows.  Pure NumPy: the CPU tests exercise it
+    directly; it never touches device data."""
+
+    def __init__(self, size: int, num: int) -> None:
+        self.size = int(size)
+        self.num = int(num)
+        self.maxsize = self.size * self.num
+        self.offset = np.arange(self.num, dtype=np.int64) * self.size
+        self.reset()
+
+    def reset(self) -> None:
+        self.index = np.zeros(self.num, np.int64)
+        self.lengths = np.zeros(self.num, np.int64)
+        self.last_index = self.offset.copy()
+
+    def advance(self, ids: Optional[np.ndarray]) -> Tuple[np.ndarray, np.ndarray]:
+        """One add for envs ``ids`` (unique; None = all): returns (global ptr, next_rel)."""
+        if ids is None:
+            rel = self.index.copy()
+            self.lengths = np.minimum(self.lengths + 1, self.size)
+            self.index = (rel + 1) % self.size
+            ptr = rel + self.offset
+            self.last_index = ptr.copy()
+            return ptr, self.index.copy()
+        rel = self.index[ids]
+        self.lengths[ids] = np.minimum(self.lengths[ids] + 1, self.size)
+        self.index[ids] = (rel + 1) % self.size
+        ptr = rel + self.offset[ids]
+        self.last_index[ids] = ptr
+        return ptr, self.index[ids].copy()
+
+    def uniform_rel(self) -> Optional[int]:
+        """The common ring position when every sub-buffer is at the same index."""
+        i0 = int(self.index[0])
+        if np.all(self.index == i0) and np.all(self.lengths == self.lengths[0]):
+            return i0
+        return None
+
+    def sample0(self) -> np.ndarray:
+        """sample_indices(0): each env's rows in ring order, env-major (manager.py:177-192)."""
+        L = self.lengths
+        if self.num and np.all(L == L[0]):
+            n = int(L[0])
+            if n == 0:
+                return np.zeros(0, np.int64)
+            p = np.arange(n, dtype=np.int64)
+            rel = (self.index[:, None] + p[None, :]) % n
+            return (rel + self.offset[:, None]).reshape(-1)
+        parts = [np.concatenate([np.arange(self.index[b], L[b]), np.arange(self.index[b])])
+                 + self.offset[b] for b in range(self.num)]
+        return np.concatenate(parts).astype(np.int64)
+
+    def chunk_layout(self) -> Tuple[Optional[int], np.ndarray]:
+        """(row_len, lengths): row_len is the common per-env chunk length of sample(0) when
+        all non-empty envs have the same length (so every row_len-th sample closes an env's
+        segment), else None."""
+        nz = self.lengths[self.lengths > 0]
+        if len(nz) and np.all(nz == nz[0]):
+            return int(nz[0]), self.lengths
+        return None, self.lengths
+
+    def is_identity(self) -> bool:
+        """sample(0) == arange(maxsize): every env full and at ring position 0."""
+        return bool(np.all(self.lengths == self.size) and np.all(self.index == 0))
+
+
+class VectorReplayBuffer:
+    """VectorReplayBuffer(total_size, buffer_num) in HBM (vecbuf.py:15-37)."""
+
+    _reserved_keys = _RESERVED
+
+    def __init__(self, total_size: int, buffer_num: int, stack_num: int = 1,
+                 ignore_obs_next: bool = False, save_only_last_obs: bool = False,
+                 sample_avail: bool = False, device=None, **kwargs: Any) -> None:
+        assert buffer_num > 0
+        assert stack_num > 0, "stack_num should be greater than 0"
+        if stack_num != 1 or save_only_last_obs or sample_avail:
+            raise NotImplementedError(
+                "frame-stack sampling (stack_num>1 / save_only_last_obs / sample_avail) is "
+                "the next row of the scope table (SURVEY.md §8f item 2)")
+        self.options = dict(stack_num=stack_num, ignore_obs_next=ignore_obs_next,
+                            save_only_last_obs=save_only_last_obs, sample_avail=sample_avail)
+        self.stack_num = stack_num
+        self.buffer_num = int(buffer_num)
+        size = int(np.ceil(total_size / buffer_num))
+        self._ring = RingIndex(size, buffer_num)
+        self.maxsize = self._ring.maxsize
+        self._offset = self._ring.offset
+        self._extend_offset = np.concatenate([self._offset, [self.maxsize]])
+        self._save_obs_next = not ignore_obs_next
+        self._indices = np.arange(self.maxsize)
+        self.device = torch.device(device) if device is not None else None
+        self._meta = Batch()
+        self._dev = None  # device-side episode state, allocated with the storage
+        self._last_sample0 = None
+
+    # -- bookkeeping views ------------------------------------------------------------------
+    @property
+    def _lengths(self) -> np.ndarray:
+        return self._ring.lengths
+
+    @property
+    def last_index(self) -> np.ndarray:
+        return self._ring.last_index
+
+    @property
+    def _index_per_env(self) -> np.ndarray:
+        return self._ring.index
+
+    def __len__(self) -> int:
+        return int(self._ring.lengths.sum())
+
+    def __repr__(self) -> str:
+        return self.__class__.__name__ + repr(self._meta)[5:]
+
+    def __getattr__(self, key: str) -> Any:
+        meta = self.__dict__.get("_meta")
+        if meta is not None and key in meta.keys():
+            return meta[key]
+        raise AttributeError(key)
+
+    # -- storage ------------------------------------------------------------------------------
+    def _ensure_device(self):
+        if self.device is None:
+            self.device = _default_device()
+        return self.device
+
+    def _alloc_state(self) -> None:
+        if self._dev is not None:
+            return
+        dev = self._ensure_device()
+        n = self.buffer_num
+        self._dev = dict(
+            offset=torch.as_tensor(self._offset, device=dev),
+            ep_rew=torch.zeros(n, dtype=torch.float64, device=dev),
+            ep_len=torch.zeros(n, dtype=torch.int64, device=dev),
+            ep_idx=torch.zeros(n, dtype=torch.int64, device=dev),
+            stat_rew=torch.zeros(self.maxsize, dtype=torch.float64, device=dev),
+            stat_len=torch.zeros(self.maxsize, dtype=torch.int64, device=dev),
+            stat_idx=torch.zeros(self.maxsize, dtype=torch.int64, device=dev),
+        )
+
+    def _alloc_storage(self, obs_shape, obs_dtype, act_shape, act_dtype) -> None:
+        """First add allocates ``maxsize`` rows per key (batch.py:94-131 lazy alloc)."""
+        if not self._meta.is_empty():
+            return
+        dev = self._ensure_device()
+        self._alloc_state()
+        m = self.maxsize
+        meta = Batch(
+            obs=torch.zeros((m,) + tuple(obs_shape), dtype=obs_dtype, device=dev),
+            act=torch.zeros((m,) + tuple(act_shape), dtype=act_dtype, device=dev),
+            rew=torch.zeros(m, dtype=torch.float64, device=dev),
+            terminated=torch.zeros(m, dtype=torch.bool, device=dev),
+            truncated=torch.zeros(m, dtype=torch.bool, device=dev),
+            done=torch.zeros(m, dtype=torch.bool, device=dev),
+            info=Batch(env_id=torch.zeros(m, dtype=torch.int64, device=dev)),
+        )
+        if self._save_obs_next:
+            meta.obs_next = torch.zeros((m,) + tuple(obs_shape), dtype=obs_dtype, device=dev)
+        self._meta = meta
+
+    def reset(self, keep_statistics: bool = False) -> None:
+        """manager.py:54-58 (+ base.py:140-146 per sub-buffer)."""
+        self._ring.reset()
+        if not keep_statistics and self._dev is not None:
+            self._dev["ep_rew"].zero_()
+            self._dev["ep_len"].zero_()
+            self._dev["ep_idx"].zero_()
+
+    def set_batch(self, batch: Batch) -> None:
+        raise NotImplementedError("set_batch/update/hdf5 are out of scope (SURVEY.md §8f)")
+
+    def update(self, buffer) -> np.ndarray:
+        raise NotImplementedError  # ReplayBufferManager cannot be updated (manager.py:99-101)
+
+    # -- add ------------------------------------------------------------------------------------
+    def _to_dev(self, x, dtype=None):
+        dev = self._ensure_device()
+        if isinstance(x, torch.Tensor):
+            t = x.to(dev)
+        else:
+            t = torch.as_tensor(np.asarray(x), device=dev)
+        if dtype is not None:
+            t = t.to(dtype)
+        return t.contiguous()
+
+    def add(self, batch: Batch, buffer_ids: Optional[Union[np.ndarray, List[int]]] = None
+            ) -> Tuple[np.ndarray, np.ndarray, np.ndarray, np.ndarray]:
+        """ReplayBufferManager.add (manager.py:104-161).  Returns NumPy
+        (ptr, ep_rew, ep_len, ep_idx) like the reference (this reads back the episode stats;
+        the Collector uses the fused, sync-free ``_add_step`` instead)."""
+        for key in ("obs", "act", "rew", "terminated", "truncated"):
+            assert key in batch.keys(), f"missing key {key}"
+        ids = np.arange(self.buffer_num) if buffer_ids is None else \
+            np.asarray(buffer_ids, dtype=np.int64)
+        k = len(ids)
+        obs = self._to_dev(batch.obs)
+        act = self._to_dev(batch.act)
+        if obs.dtype == torch.float64:
+            obs = obs.float()
+        if act.dtype == torch.float64:
+            act = act.float()
+        if obs.dim() == 1:
+            obs = obs.reshape(k)
+        self._alloc_storage(obs.shape[1:], obs.dtype, act.shape[1:], act.dtype)
+        rew = self._to_dev(batch.rew, torch.float64).reshape(k)
+        term = self._to_dev(batch.terminated).reshape(k).bool()
+        trunc = self._to_dev(batch.truncated).reshape(k).bool()
+        obs_next = None
+        if self._save_obs_next and "obs_next" in batch.keys() and \
+                not (isinstance(batch.obs_next, Batch) and batch.obs_next.is_empty()):
+            obs_next = self._to_dev(batch.obs_next).to(self._meta.obs_next.dtype)
+        ptr, next_rel = self._ring.advance(ids)
+        out_rew = torch.empty(k, dtype=torch.float64, device=self.device)
+        out_len = torch.empty(k, dtype=torch.int64, device=self.device)
+        out_idx = torch.empty(k, dtype=torch.int64, device=self.device)
+        self._launch_add(
+            ids=self._to_dev(ids, torch.int64), k=k, ptr=self._to_dev(ptr, torch.int64),
+            next_rel=self._to_dev(next_rel, torch.int64), obs=obs.to(self._meta.obs.dtype),
+            act=act.to(self._meta.act.dtype), obs_next_raw=obs_next, rew=rew, term=term,
+            trunc=trunc, out=(out_rew, out_len, out_idx))
+        # extra keys (info.*, policy.*) by plain device scatter
+        for key in ("info", "policy"):
+            v = batch.get(key)
+            if isinstance(v, Batch) and not v.is_empty():
+                self._scatter_extra(key, v, ptr)
+        return ptr, out_rew.cpu().numpy(), out_len.cpu().numpy(), out_idx.cpu().numpy()
+
+    def _scatter_extra(self, key: str, value: Batch, ptr: np.ndarray) -> None:
+        dst = self._meta.get(key)
+        if dst is None or not isinstance(dst, Batch):
+            dst = Batch()
+            self._meta.__dict__[key] = dst
+        pt = torch.as_tensor(ptr, device=self.device)
+        for k, v in value.items():
+            if isinstance(v, Batch):
+                continue
+            if k == "env_id" and key == "info":
+                continue  # written by the kernel
+            t = self._to_dev(v)
+            if k not in dst.keys():
+                dst.__dict__[k] = torch.zeros((self.maxsize,) + tuple(t.shape[1:]),
+                                              dtype=t.dtype, device=self.device)
+            dst.__dict__[k][pt] = t.to(dst.__dict__[k].dtype)
+
+    def _launch_add(self, *, ids, k, ptr=None, next_rel=None, uniform_rel=0, uniform_next=0,
+                    obs=None, act=None, obs_next=None, obs_next_raw=None, cur_obs=None,
+                    norm=None, rew=None, term=None, trunc=None, out=None,
+                    stats=True) -> None:
+        """One tsrl_buffer_add launch (see include/tsrl.h)."""
+        m = self._meta
+        d = self._dev
+        a = _C.AddArgs()
+        a.ids = _C.ptr(ids)
+        a.ptr = _C.ptr(ptr)
+        a.next_rel = _C.ptr(next_rel)
+        a.offset = _C.ptr(d["offset"])
+        a.k = k
+        a.uniform_rel = uniform_rel
+        a.uniform_next = uniform_next
+        if obs is not None:
+            a.obs_src = _C.ptr(obs)
+            a.obs_dst = _C.ptr(m.obs)
+        a.obs_row_bytes = m.obs.element_size() * int(np.prod(m.obs.shape[1:]))
+        has_next = self._save_obs_next and "obs_next" in m.keys()
+        if obs_next is not None:  # f32 rows, optionally normalised in-kernel
+            a.obs_next_src = _C.ptr(obs_next)
+            a.obs_next_dst = _C.ptr(m.obs_next) if has_next else None
+            a.cur_obs = _C.ptr(cur_obs)
+            a.obs_dim = int(np.prod(m.obs.shape[1:]))
+            if norm is not None:
+                a.norm_mean = _C.ptr(norm.mean_t)
+                a.norm_var = _C.ptr(norm.var_t)
+                a.norm_eps = float(norm.eps)
+                a.norm_clip = float(norm.clip_max or 0.0)
+        if obs_next_raw is not None and has_next:
+            a.obs_next_src_raw = _C.ptr(obs_next_raw)
+            a.obs_next_dst_raw = _C.ptr(m.obs_next)
+        if act is not None:
+            a.act_src = _C.ptr(act)
+            a.act_dst = _C.ptr(m.act)
+        a.act_row_bytes = m.act.element_size() * int(np.prod(m.act.shape[1:]))
+        a.rew = _C.ptr(rew)
+        a.term = _C.ptr(term)
+        a.trunc = _C.ptr(trunc)
+        a.rew_dst = _C.ptr(m.rew)
+        a.term_dst = _C.ptr(m.terminated)
+        a.trunc_dst = _C.ptr(m.truncated)
+        a.done_dst = _C.ptr(m.done)
+        a.env_id_dst = _C.ptr(m.info.env_id)
+        a.ep_rew = _C.ptr(d["ep_rew"])
+        a.ep_len = _C.ptr(d["ep_len"])
+        a.ep_idx = _C.ptr(d["ep_idx"])
+        if out is not None:
+            a.out_ep_rew, a.out_ep_len, a.out_ep_idx = (_C.ptr(t) for t in out)
+        if stats:
+            a.stat_rew = _C.ptr(d["stat_rew"])
+            a.stat_len = _C.ptr(d["stat_len"])
+            a.stat_idx = _C.ptr(d["stat_idx"])
+        _C.check(_C.lib().tsrl_buffer_add(a, _C.stream_ptr(self.device)), "tsrl_buffer_add")
+
+    # -- sampling -------------------------------------------------------------------------------
+    def sample_indices(self, batch_size: int) -> np.ndarray:
+        """manager.py:163-192 (host RNG: the same np.random calls as the reference)."""
+        if batch_size < 0:
+            return np.array([], int)
+        if batch_size == 0:
+            idx = self._ring.sample0()
+            self._last_sample0 = idx  # lets process_fn recognise the sample(0) layout
+            return idx
+        lengths = self._ring.lengths
+        buffer_idx = np.random.choice(self.buffer_num, batch_size, p=lengths / lengths.sum())
+        sample_num = np.bincount(buffer_idx, minlength=self.buffer_num)
+        sample_num[sample_num == 0] = -1
+        parts = []
+        for b in range(self.buffer_num):
+            bsz = sample_num[b]
+            if bsz > 0:
+                parts.append(np.random.choice(lengths[b], bsz) + self._offset[b])
+            else:
+                parts.append(np.array([], int))
+        return np.concatenate(parts).astype(np.int64)
+
+    def _ring_sample0_env(self, b: int) -> np.ndarray:
+        i, L = self._ring.index[b], self._ring.lengths[b]
+        return np.concatenate([np.arange(i, L), np.arange(i)])
+
+    def sample(self, batch_size: int) -> Tuple[Batch, np.ndarray]:
+        indices = self.sample_indices(batch_size)
+        return self[indices], indices
+
+    def __getitem__(self, index) -> Batch:
+        if isinstance(index, slice):
+            indices = self.sample_indices(0) if index == slice(None) \
+                else self._indices[:len(self)][index]
+        else:
+            indices = np.asarray(index)
+        m = self._meta
+        if m.is_empty():
+            return Batch()
+        if isinstance(index, np.ndarray) and len(indices) == self.maxsize and \
+                self._ring.is_identity() and np.array_equal(indices[:1], [0]) and \
+                indices[-1] == self.maxsize - 1:
+            view = True  # sample(0) of a full on-policy buffer: storage order, no copy
+        else:
+            view = False
+        if view:
+            obs = m.obs
+            obs_next = m.obs_next if self._save_obs_next else gather_rows(m.obs, self.next(indices))
+            return Batch(obs=obs, act=m.act, rew=m.rew, terminated=m.terminated,
+                         truncated=m.truncated, done=m.done, obs_next=obs_next,
+                         info=Batch(env_id=m.info.env_id), policy=m.get("policy", Batch()))
+        it = torch.as_tensor(np.asarray(indices, np.int64).reshape(-1), device=self.device)
+        if self._save_obs_next:
+            obs_next = gather_rows(m.obs_next, it)
+        else:
+            obs_next = gather_rows(m.obs, self.next(indices))
+        info = Batch({k: gather_rows(v, it) for k, v in m.info.items()
+                      if isinstance(v, torch.Tensor)})
+        pol = m.get("policy", Batch())
+        policy = Batch({k: gather_rows(v, it) for k, v in pol.items()
+                        if isinstance(v, torch.Tensor)}) if not pol.is_empty() else Batch()
+        return Batch(obs=gather_rows(m.obs, it), act=gather_rows(m.act, it),
+                     rew=gather_rows(m.rew, it), terminated=gather_rows(m.terminated, it),
+                     truncated=gather_rows(m.truncated, it), done=gather_rows(m.done, it),
+                     obs_next=obs_next, info=info, policy=policy)
+
+    # -- episode-aware index stepping (device done flags; returns NumPy) ----------------------
+    def _done_at(self, pos: np.ndarray) -> np.ndarray:
+        if self._meta.is_empty():
+            return np.zeros(len(pos), bool)
+        t = torch.as_tensor(np.asarray(pos, np.int64), device=self.device)
+        return self._meta.done[t].cpu().numpy()
+
+    def prev(self, index) -> np.ndarray:
+        """manager.py:259-277 (_prev_index)."""
+        scalar = np.isscalar(index)
+        index = np.atleast_1d(np.asarray(index, np.int64)) % self.maxsize
+        b = index // self._ring.size
+        start = self._offset[b]
+        cur = np.maximum(1, self._ring.lengths[b])
+        sub = (index - start - 1) % cur
+        end = self._done_at(sub + start) | (sub + start == self._ring.last_index[b])
+        out = (sub + end) % cur + start
+        return out[0] if scalar else out
+
+    def next(self, index) -> np.ndarray:
+        """manager.py:280-297 (_next_index)."""
+        scalar = np.isscalar(index)
+        index = np.atleast_1d(np.asarray(index, np.int64)) % self.maxsize
+        b = index // self._ring.size
+        start = self._offset[b]
+        cur = np.maximum(1, self._ring.lengths[b])
+        end = self._done_at(index) | (index == self._ring.last_index[b])
+        out = (index - start + 1 - end) % cur + start
+        return out[0] if scalar else out
+
+    def _last_positions(self) -> np.ndarray:
+        L = self._ring.lengths
+        envs = np.flatnonzero(L > 0)
+        return (self._ring.index[envs] - 1) % L[envs] + self._offset[envs]
+
+    def unfinished_index(self) -> np.ndarray:
+        """manager.py:68-74 (+ base.py:148-151 per sub-buffer)."""
+        last = self._last_positions()
+        if len(last) == 0:
+            return np.array([], np.int64)
+        return last[~self._done_at(last)]
+
+    def _unfinished_device(self) -> torch.Tensor:
+        """Device int64 tensor of candidate positions (last rows); masked by ~done."""
+        last = torch.as_tensor(self._last_positions(), device=self.device)
+        return last[~self._meta.done[last]]
+
+
+class ReplayBuffer(VectorReplayBuffer):
+    """Single ReplayBuffer(size) (base.py:11-389): one sub-buffer; batch sampling uses
+    np.random.choice(self._size, batch_size) as base.py:285-286 does."""
+
+    def __init__(self, size: int, stack_num: int = 1, ignore_obs_next: bool = False,
+                 save_only_last_obs: bool = False, sample_avail: bool = False, device=None,
+                 **kwargs: Any) -> None:
+        super().__init__(size, 1, stack_num, ignore_obs_next, save_only_last_obs, sample_avail,
+                         device)
+
+    def add(self, batch: Batch, buffer_ids=None):
+        """base.py:216-274: a single transition (no batch dim) or a stacked one."""
+        stacked = buffer_ids is not None
+        if not stacked:
+            batch = Batch({k: (np.asarray(v)[None] if not isinstance(v, (Batch, torch.Tensor))
+                               else (v.unsqueeze(0) if isinstance(v, torch.Tensor) else v))
+                           for k, v in batch.items()})
+        ptr, r, ln, i = super().add(batch, [0])
+        return ptr, r, ln, i
+
+    @property
+    def _size(self) -> int:
+        return int(self._ring.lengths[0])
+
+    @property
+    def _index(self) -> int:
+        return int(self._ring.index[0])
+
+    def sample_indices(self, batch_size: int) -> np.ndarray:
+        if batch_size > 0:
+            return np.random.choice(self._size, batch_size)
+        if batch_size == 0:
+            return np.concatenate([np.arange(self._index, self._size), np.arange(self._index)])
+        return np.array([], int)

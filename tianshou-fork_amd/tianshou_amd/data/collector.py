@@ -1,0 +1,358 @@
+"""Collector (tianshou/data/collector.py:21-402) on device.
+
+Two paths behind the reference API:
+
+* fused (a ``DeviceVectorEnv``, optionally wrapped in ``VectorEnvNormObs``, no
+  ``preprocess_fn``): every vector step is policy forward -> map_action -> env kernel (raw obs
+  + column partials) -> obs_rms merge -> one ``tsrl_buffer_add`` launch that writes obs, act,
+  rew, flags, env_id, the NORMALISED obs_next (into the buffer and into the live obs) and the
+  episode statistics -> masked reset kernel for done envs (+ its obs_rms merge and
+  normalisation).  No host<->device synchronisation inside an n_step collect; the returned
+  statistics are gathered once at the end.
+* generic (any other env): the reference's loop, with the buffer still in HBM.
+"""
+import time
+import warnings
+from typing import Any, Callable, Dict, Optional
+
+import numpy as np
+import torch
+
+from tianshou_amd.data.batch import Batch
+from tianshou_amd.data.buffer import ReplayBuffer, VectorReplayBuffer
+from tianshou_amd.env.synthetic import DeviceVectorEnv
+from tianshou_amd.env.wrappers import VectorEnvNormObs
+
+
+def _empty_data() -> Batch:
+    return Batch(obs={}, act={}, rew={}, terminated={}, truncated={}, done={}, obs_next={},
+                 info={}, policy={})
+
+
+class Collector:
+    def __init__(self, policy, env, buffer: Optional[ReplayBuffer] = None,
+                 preprocess_fn: Optional[Callable[..., Batch]] = None,
+                 exploration_noise: bool = False) -> None:
+        self.env = env
+        self.env_num = len(env)
+        self.exploration_noise = exploration_noise
+        self.policy = policy
+        self.preprocess_fn = preprocess_fn
+        self._action_space = env.action_space
+        self._norm = env if isinstance(env, VectorEnvNormObs) else None
+        self._base = env.venv if self._norm is not None else env
+        self._fused = isinstance(self._base, DeviceVectorEnv) and preprocess_fn is None
+        self.device = getattr(self._base, "device", None)
+        self._assign_buffer(buffer)
+        self._scratch = None
+        self.reset(False)
+
+    def _assign_buffer(self, buffer) -> None:
+        if buffer is None:
+            buffer = VectorReplayBuffer(self.env_num, self.env_num, device=self.device)
+        elif type(buffer) is ReplayBuffer or (isinstance(buffer, ReplayBuffer)
+                                              and buffer.buffer_num == 1 and self.env_num > 1):
+            if self.env_num > 1:
+                raise TypeError(
+                    f"Cannot use ReplayBuffer(size={buffer.maxsize}, ...) to collect "
+                    f"{self.env_num} envs,\n\tplease use VectorReplayBuffer(total_size="
+                    f"{buffer.maxsize}, buffer_num={self.env_num}, ...) instead.")
+        else:
+            assert buffer.buffer_num >= self.env_num
+        if buffer.device is None and self.device is not None:
+            buffer.device = self.device
+        self.buffer = buffer
+
+    # -- resets ---------------------------------------------------------------------------------
+    def reset(self, reset_buffer: bool = True,
+              gym_reset_kwargs: Optional[Dict[str, Any]] = None) -> None:
+        self.data = _empty_data()
+        self.reset_env(gym_reset_kwargs)
+        if reset_buffer:
+            self.reset_buffer()
+        self.reset_stat()
+
+    def reset_stat(self) -> None:
+        self.collect_step, self.collect_episode, self.collect_time = 0, 0, 0.0
+
+    def reset_buffer(self, keep_statistics: bool = False) -> None:
+        self.buffer.reset(keep_statistics=keep_statistics)
+
+    def _alloc_scratch(self) -> None:
+        if self._scratch is not None:
+            return
+        b, N = self._base, self.env_num
+        dev = b.device
+        self._scratch = dict(
+            cur=b.alloc_obs(N) if b.u8 else torch.empty((N,) + b.obs_shape, device=dev),
+            raw=b.alloc_obs(N),
+            reset_raw=b.alloc_obs(N),
+            rew=torch.empty(N, dtype=torch.float64, device=dev),
+            term=torch.empty(N, dtype=torch.bool, device=dev),
+            trunc=torch.empty(N, dtype=torch.bool, device=dev),
+            done=torch.empty(N, dtype=torch.bool, device=dev),
+            part=b.alloc_partials(N),
+            part2=b.alloc_partials(N),
+            env_id=torch.arange(N, device=dev),
+        )
+
+    def reset_env(self, gym_reset_kwargs: Optional[Dict[str, Any]] = None) -> None:
+        if not self._fused:
+            gym_reset_kwargs = gym_reset_kwargs or {}
+            obs, info = self.env.reset(**gym_reset_kwargs)
+            if self.preprocess_fn:
+                processed = self.preprocess_fn(obs=obs, info=info,
+                                               env_id=np.arange(self.env_num))
+                obs = processed.get("obs", obs)
+                info = processed.get("info", info)
+            self.data.info = info
+            self.data.obs = obs
+            return
+        self._alloc_scratch()
+        s, b, N = self._scratch, self._base, self.env_num
+        b._reset_raw(None, None, N, s["raw"], s["part"])
+        self._finish_obs(s["raw"], s["cur"], s["part"], None, N)
+        self.data.obs = s["cur"]
+        self.data.info = Batch(env_id=s["env_id"])
+
+    def _finish_obs(self, raw, cur, partials, mask, k) -> None:
+        """obs_rms update + normalisation of (masked) raw rows into ``cur``."""
+        if self._norm is not None and not self._base.u8:
+            rms = self._norm.obs_rms
+            if self._norm.update_obs_rms:
+                rms.merge_partials(partials, self._base.nblk_for(k), mask, k)
+            rms.norm_rows(raw.reshape(k, -1), cur.reshape(k, -1), mask)
+        elif mask is None:
+            cur.copy_(raw)
+        else:
+            m = mask.view((k,) + (1,) * (raw.dim() - 1))
+            torch.where(m, raw, cur, out=cur)
+
+    # -- collect ----------------------------------------------------------------------------------
+    def collect(self, n_step: Optional[int] = None, n_episode: Optional[int] = None,
+                random: bool = False, render: Optional[float] = None, no_grad: bool = True,
+                gym_reset_kwargs: Optional[Dict[str, Any]] = None) -> Dict[str, Any]:
+        assert not self.env.is_async, "Please use AsyncCollector if using async venv."
+        if n_step is not None:
+            assert n_episode is None, (
+                f"Only one of n_step or n_episode is allowed in Collector."
+                f"collect, got n_step={n_step}, n_episode={n_episode}.")
+            assert n_step > 0
+            if not n_step % self.env_num == 0:
+                warnings.warn(
+                    f"n_step={n_step} is not a multiple of #env ({self.env_num}), "
+                    "which may cause extra transitions collected into the buffer.")
+        elif n_episode is not None:
+            assert n_episode > 0
+        else:
+            raise TypeError("Please specify at least one (either n_step or n_episode) "
+                            "in AsyncCollector.collect().")
+        start_time = time.time()
+        if self._fused:
+            step_count, episode_count, rews, lens, idxs = self._collect_fused(
+                n_step, n_episode, random, no_grad)
+        else:
+            step_count, episode_count, rews, lens, idxs = self._collect_generic(
+                n_step, n_episode, random, render, no_grad, gym_reset_kwargs)
+        self.collect_step += step_count
+        self.collect_episode += episode_count
+        self.collect_time += max(time.time() - start_time, 1e-9)
+        if n_episode:
+            self.data = _empty_data()
+            self.reset_env()
+        if episode_count > 0:
+            rew_mean, rew_std = rews.mean(), rews.std()
+            len_mean, len_std = lens.mean(), lens.std()
+        else:
+            rews, lens, idxs = np.array([]), np.array([], int), np.array([], int)
+            rew_mean = rew_std = len_mean = len_std = 0
+        return {"n/ep": episode_count, "n/st": step_count, "rews": rews, "lens": lens,
+                "idxs": idxs, "rew": rew_mean, "len": len_mean, "rew_std": rew_std,
+                "len_std": len_std}
+
+    def _policy_act(self, obs, info, random: bool, no_grad: bool, k: int):
+        if random:
+            try:
+                acts = [self._action_space[i].sample() for i in range(k)]
+            except TypeError:
+                acts = [self._action_space.sample() for _ in range(k)]
+            act = torch.as_tensor(np.asarray(acts), device=self.device)
+            if hasattr(self.policy, "map_action_inverse"):
+                act = self.policy.map_action_inverse(act)
+            return act, Batch()
+        data = Batch(obs=obs, info=info)
+        if no_grad:
+            with torch.no_grad():
+                result = self.policy(data, None)
+        else:
+            result = self.policy(data, None)
+        act = result.act
+        if self.exploration_noise:
+            act = self.policy.exploration_noise(act, data)
+        policy = result.get("policy", Batch())
+        return act, policy
+
+    def _collect_fused(self, n_step, n_episode, random, no_grad):
+        self._alloc_scratch()
+        s, b, buf = self._scratch, self._base, self.buffer
+        N = self.env_num
+        act_space = self._action_space
+        if hasattr(act_space, "n"):
+            act_shape, act_dtype = (), torch.int64
+        else:
+            act_shape, act_dtype = tuple(act_space.shape), torch.float32
+        buf._alloc_storage(b.obs_shape, b.obs_torch_dtype, act_shape, act_dtype)
+        dev = buf.device
+        # rows r < kk of the scratch arrays belong to env ready[r] (ready None: env r)
+        kk = N if n_step is not None else min(N, n_episode)
+        ready = None
+        ids_t = None
+        cur = s["cur"] if kk == N else s["cur"][:kk]
+        step_count = episode_count = 0
+        written = []          # per step: uniform ring position (int) or the ptr array
+        ep_rows_host = []     # n_episode mode: finished rows in step order
+        while True:
+            info = Batch(env_id=s["env_id"][:kk] if ids_t is None else ids_t)
+            act, _policy = self._policy_act(cur, info, random, no_grad, kk)
+            act = act.to(act_dtype).reshape((kk,) + act_shape).contiguous()
+            action_remap = self.policy.map_action(act)
+            raw, rew = s["raw"][:kk], s["rew"][:kk]
+            term, trunc, done = s["term"][:kk], s["trunc"][:kk], s["done"][:kk]
+            b._step_raw(ids_t, kk, raw, rew, term, trunc, s["part"], action_remap)
+            norm = None
+            if self._norm is not None and not b.u8:
+                if self._norm.update_obs_rms:
+                    self._norm.obs_rms.merge_partials(s["part"], b.nblk_for(kk), None, kk)
+                norm = self._norm.obs_rms
+            ids_np = None if ready is None else ready
+            uni = buf._ring.uniform_rel() if ids_np is None and kk == buf.buffer_num else None
+            if ids_np is None and kk != buf.buffer_num:
+                ids_np = np.arange(kk)
+            ptr, next_rel = buf._ring.advance(ids_np)
+            if uni is not None:
+                kw = dict(uniform_rel=uni, uniform_next=int(next_rel[0]))
+                written.append(uni)
+            else:
+                kw = dict(ptr=torch.as_tensor(ptr, device=dev),
+                          next_rel=torch.as_tensor(next_rel, device=dev))
+                written.append(np.asarray(ptr))
+            if b.u8:
+                buf._launch_add(ids=ids_t, k=kk, obs=cur, act=act, obs_next_raw=raw, rew=rew,
+                                term=term, trunc=trunc, **kw)
+                cur.copy_(raw)
+            else:
+                buf._launch_add(ids=ids_t, k=kk, obs=cur, act=act, obs_next=raw, cur_obs=cur,
+                                norm=norm, rew=rew, term=term, trunc=trunc, **kw)
+            torch.logical_or(term, trunc, out=done)
+            b._reset_raw(ids_t, done, kk, s["reset_raw"][:kk], s["part2"])
+            self._finish_obs(s["reset_raw"][:kk], cur, s["part2"], done, kk)
+            step_count += kk
+            if n_episode:
+                done_np = done.cpu().numpy()
+                if done_np.any():
+                    env_ind_local = np.flatnonzero(done_np)
+                    episode_count += len(env_ind_local)
+                    ep_rows_host.append(np.asarray(ptr)[env_ind_local])
+                    surplus = kk - (n_episode - episode_count)
+                    if surplus > 0:
+                        mask = np.ones(kk, dtype=bool)
+                        mask[env_ind_local[:surplus]] = False
+                        keep = torch.as_tensor(np.flatnonzero(mask), device=dev)
+                        cur = cur[keep].contiguous()
+                        ready = (np.arange(kk) if ready is None else ready)[mask]
+                        ids_t = torch.as_tensor(ready, device=dev)
+                        kk = len(ready)
+                if episode_count >= n_episode:
+                    break
+            elif step_count >= n_step:
+                break
+        # one read-back of the episode statistics, in the reference's (step, env) order
+        d = buf._dev
+        if n_episode:
+            rows = np.concatenate(ep_rows_host) if ep_rows_host else np.zeros(0, np.int64)
+            rows_t = torch.as_tensor(rows, device=dev)
+        else:
+            if all(isinstance(w, int) for w in written):
+                rel = torch.as_tensor(np.asarray(written, np.int64), device=dev)
+                rows_t = (rel[:, None] + d["offset"][None, :]).reshape(-1)
+            else:
+                rows_t = torch.as_tensor(np.concatenate(
+                    [np.asarray(w).reshape(-1) if not isinstance(w, int) else w + buf._offset
+                     for w in written]), device=dev)
+            rows_t = rows_t[buf._meta.done[rows_t]]
+        rews = d["stat_rew"][rows_t].cpu().numpy()
+        lens = d["stat_len"][rows_t].cpu().numpy()
+        idxs = d["stat_idx"][rows_t].cpu().numpy()
+        if not n_episode:
+            episode_count = len(rews)
+        self.data.obs = s["cur"]
+        return step_count, episode_count, rews, lens, idxs
+
+    def _collect_generic(self, n_step, n_episode, random, render, no_grad, gym_reset_kwargs):
+        """The reference loop (collector.py:250-361) for host envs; buffer still on device."""
+        if n_step is not None:
+            ready_env_ids = np.arange(self.env_num)
+        else:
+            ready_env_ids = np.arange(min(self.env_num, n_episode))
+            self.data = self.data[:min(self.env_num, n_episode)]
+        step_count = episode_count = 0
+        episode_rews, episode_lens, episode_start_indices = [], [], []
+        while True:
+            obs = torch.as_tensor(np.asarray(self.data.obs), device=self.buffer._ensure_device())
+            act, policy = self._policy_act(obs, self.data.info, random, no_grad,
+                                           len(ready_env_ids))
+            act_np = act.detach().cpu().numpy() if isinstance(act, torch.Tensor) else act
+            self.data.update(policy=policy, act=act_np)
+            action_remap = self.policy.map_action(act_np)
+            obs_next, rew, terminated, truncated, info = self.env.step(action_remap,
+                                                                       ready_env_ids)
+            to_np = (lambda x: x.cpu().numpy() if isinstance(x, torch.Tensor) else np.asarray(x))
+            obs_next, rew, terminated, truncated = map(to_np, (obs_next, rew, terminated,
+                                                               truncated))
+            done = np.logical_or(terminated, truncated)
+            self.data.update(obs_next=obs_next, rew=rew, terminated=terminated,
+                             truncated=truncated, done=done, info=info)
+            if self.preprocess_fn:
+                self.data.update(self.preprocess_fn(
+                    obs_next=self.data.obs_next, rew=self.data.rew, done=self.data.done,
+                    info=self.data.info, policy=self.data.policy, env_id=ready_env_ids,
+                    act=self.data.act))
+            if render:
+                self.env.render()
+                if render > 0 and not np.isclose(render, 0):
+                    time.sleep(render)
+            ptr, ep_rew, ep_len, ep_idx = self.buffer.add(self.data, buffer_ids=ready_env_ids)
+            step_count += len(ready_env_ids)
+            if np.any(done):
+                env_ind_local = np.where(done)[0]
+                env_ind_global = ready_env_ids[env_ind_local]
+                episode_count += len(env_ind_local)
+                episode_lens.append(ep_len[env_ind_local])
+                episode_rews.append(ep_rew[env_ind_local])
+                episode_start_indices.append(ep_idx[env_ind_local])
+                gkw = gym_reset_kwargs or {}
+                obs_reset, info_r = self.env.reset(env_ind_global, **gkw)
+                obs_reset = to_np(obs_reset)
+                if self.preprocess_fn:
+                    processed = self.preprocess_fn(obs=obs_reset, info=info_r,
+                                                   env_id=env_ind_global)
+                    obs_reset = processed.get("obs", obs_reset)
+                obs_next = np.array(self.data.obs_next, copy=True)
+                obs_next[env_ind_local] = obs_reset
+                self.data.obs_next = obs_next
+                if n_episode:
+                    surplus = len(ready_env_ids) - (n_episode - episode_count)
+                    if surplus > 0:
+                        mask = np.ones_like(ready_env_ids, dtype=bool)
+                        mask[env_ind_local[:surplus]] = False
+                        ready_env_ids = ready_env_ids[mask]
+                        self.data = self.data[mask]
+            self.data.obs = self.data.obs_next
+            if (n_step and step_count >= n_step) or (n_episode and episode_count >= n_episode):
+                break
+        if episode_count > 0:
+            rews, lens, idxs = map(np.concatenate,
+                                   [episode_rews, episode_lens, episode_start_indices])
+        else:
+            rews, lens, idxs = np.array([]), np.array([], int), np.array([], int)
+        return step_count, episode_count, rews, lens, idxs

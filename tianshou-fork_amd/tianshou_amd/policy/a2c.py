@@ -1,0 +1,131 @@
+"""A2CPolicy (tianshou/policy/modelfree/a2c.py:14-160): critic values + GAE on device."""
+from typing import Any, Callable, Dict, List, Optional
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from tianshou_amd import _C
+from tianshou_amd.data.batch import Batch, split_indices
+from tianshou_amd.dist import default_dp
+from tianshou_amd.policy.base import gae_device
+from tianshou_amd.policy.pg import PGPolicy
+from tianshou_amd.utils.net import ActorCritic
+
+# Critic/actor evaluation chunk for process_fn.  The reference chunks by max_batchsize
+# (default 256, a2c.py:86-90) to bound host memory; per-row results do not depend on the
+# chunking, and 288 GB of HBM makes 2M-row chunks cheap.
+EVAL_CHUNK = 1 << 21
+
+
+class A2CPolicy(PGPolicy):
+    def __init__(self, actor: torch.nn.Module, critic: torch.nn.Module,
+                 optim: torch.optim.Optimizer, dist_fn: Callable, vf_coef: float = 0.5,
+                 ent_coef: float = 0.01, max_grad_norm: Optional[float] = None,
+                 gae_lambda: float = 0.95, max_batchsize: int = 256, **kwargs: Any) -> None:
+        super().__init__(actor, optim, dist_fn, **kwargs)
+        self.critic = critic
+        assert 0.0 <= gae_lambda <= 1.0, "GAE lambda should be in [0, 1]."
+        self._lambda = gae_lambda
+        self._weight_vf = vf_coef
+        self._weight_ent = ent_coef
+        self._grad_norm = max_grad_norm
+        self._batch = max_batchsize
+        self._actor_critic = ActorCritic(self.actor, self.critic)
+        self.dp = default_dp()
+
+    # -- process_fn -------------------------------------------------------------------------
+    def process_fn(self, batch: Batch, buffer, indices: np.ndarray) -> Batch:
+        batch = self._compute_returns(batch, buffer, indices)
+        batch.act = torch.as_tensor(batch.act, device=batch.v_s.device).to(batch.v_s.dtype)
+        return batch
+
+    def _chunks(self, n: int):
+        c = max(self._batch, EVAL_CHUNK)
+        return [(s, min(s + c, n)) for s in range(0, n, c)]
+
+    def _values(self, obs: torch.Tensor) -> torch.Tensor:
+        n = len(obs)
+        out = torch.empty(n, dtype=torch.float32, device=obs.device)
+        for s, e in self._chunks(n):
+            out[s:e] = self.critic(obs[s:e]).flatten()
+        return out
+
+    @staticmethod
+    def _gae_layout(buffer, indices):
+        """(row_len, end_extra): row_len > 0 when ``indices`` is the buffer's sample(0) order
+        with equal per-env chunks (each env's chunk ends at its unfinished/done row, so every
+        row_len-th element closes a segment); otherwise the reference's
+        ``np.isin(indices, buffer.unfinished_index())`` mask on device."""
+        ring = getattr(buffer, "_ring", None)
+        if ring is not None and indices is getattr(buffer, "_last_sample0", None):
+            row_len, _ = ring.chunk_layout()
+            if row_len:
+                return row_len, None
+        mask = np.isin(np.asarray(indices), buffer.unfinished_index()).astype(np.uint8)
+        return 0, torch.as_tensor(mask, device=buffer.device)
+
+    def _compute_returns(self, batch: Batch, buffer, indices: np.ndarray) -> Batch:
+        obs = torch.as_tensor(batch.obs)
+        dev = next(self.critic.parameters()).device
+        obs = obs.to(dev)
+        obs_next = torch.as_tensor(batch.obs_next).to(dev)
+        with torch.no_grad():
+            v_s = self._values(obs)
+            v_s_ = self._values(obs_next)
+        batch.v_s = v_s
+        rew = torch.as_tensor(batch.rew).to(dev, torch.float64).contiguous()
+        term = torch.as_tensor(batch.terminated).to(dev).bool().contiguous()
+        trunc = torch.as_tensor(batch.truncated).to(dev).bool().contiguous()
+        row_len, extra = self._gae_layout(buffer, indices)
+        n = len(v_s)
+        if self._rew_norm:
+            st = self.ret_rms.state
+            scale = (st[1:2] + self._eps).sqrt()
+            nparts = int(_C.lib().tsrl_gae_num_partials(n, row_len))
+            partials = torch.empty(max(nparts, 1) * 3, dtype=torch.float64, device=dev)
+            adv, ret, _, _ = gae_device(v_s, v_s_, rew, term, trunc, self._gamma, self._lambda,
+                                        row_len, extra, scale, ret_partials=partials)
+            if self.dp.active:  # every rank folds every rank's partials in rank order
+                partials = self.dp.all_gather_cat(partials[:nparts * 3])
+                nparts = partials.numel() // 3
+            self.ret_rms.update_from_partials(partials, nparts)
+        else:
+            adv, ret, _, _ = gae_device(v_s, v_s_, rew, term, trunc, self._gamma, self._lambda,
+                                        row_len, extra)
+        batch.returns = ret
+        batch.adv = adv
+        return batch
+
+    def learn(self, batch: Batch, batch_size: int, repeat: int, **kwargs: Any
+              ) -> Dict[str, List[float]]:
+        """a2c.py:119-160 (generic torch path on device)."""
+        losses, actor_losses, vf_losses, ent_losses = [], [], [], []
+        for _ in range(repeat):
+            for part in split_indices(len(batch), batch_size, True, True):
+                minibatch = batch[part]
+                dist = self(minibatch).dist
+                log_prob = dist.log_prob(minibatch.act)
+                log_prob = log_prob.reshape(len(minibatch.adv), -1).transpose(0, 1)
+                actor_loss = -(log_prob * minibatch.adv).mean()
+                value = self.critic(minibatch.obs).flatten()
+                vf_loss = F.mse_loss(minibatch.returns, value)
+                ent_loss = dist.entropy().mean()
+                loss = actor_loss + self._weight_vf * vf_loss - self._weight_ent * ent_loss
+                self.optim.zero_grad()
+                loss.backward()
+                self.dp.all_reduce_grads_(self._actor_critic.parameters(), average=True)
+                if self._grad_norm:
+                    nn.utils.clip_grad_norm_(self._actor_critic.parameters(),
+                                             max_norm=self._grad_norm)
+                self.optim.step()
+                actor_losses.append(actor_loss.detach())
+                vf_losses.append(vf_loss.detach())
+                ent_losses.append(ent_loss.detach())
+                losses.append(loss.detach())
+        out = {}
+        for k, v in (("loss", losses), ("loss/actor", actor_losses), ("loss/vf", vf_losses),
+                     ("loss/ent", ent_losses)):
+            out[k] = torch.stack(v).cpu().tolist() if v else []
+        return out

@@ -1,0 +1,90 @@
+"""PGPolicy (tianshou/policy/modelfree/pg.py:20-171)."""
+from typing import Any, Callable, Dict, List, Literal, Optional
+
+import numpy as np
+import torch
+
+from tianshou_amd.data.batch import Batch, split_indices
+from tianshou_amd.policy.base import BasePolicy
+from tianshou_amd.utils.statistics import DeviceScalarRMS
+
+
+class PGPolicy(BasePolicy):
+    def __init__(self, model: torch.nn.Module, optim: torch.optim.Optimizer,
+                 dist_fn: Callable[..., torch.distributions.Distribution],
+                 discount_factor: float = 0.99, reward_normalization: bool = False,
+                 action_scaling: bool = True,
+                 action_bound_method: Optional[Literal["clip", "tanh"]] = "clip",
+                 deterministic_eval: bool = False, **kwargs: Any) -> None:
+        super().__init__(action_scaling=action_scaling, action_bound_method=action_bound_method,
+                         **kwargs)
+        self.actor = model
+        self.optim = optim
+        self.dist_fn = dist_fn
+        assert 0.0 <= discount_factor <= 1.0, "discount factor should be in [0, 1]"
+        self._gamma = discount_factor
+        self._rew_norm = reward_normalization
+        self._ret_rms = None
+        self._eps = 1e-8
+        self._deterministic_eval = deterministic_eval
+
+    @property
+    def ret_rms(self) -> DeviceScalarRMS:
+        """Running mean/std of the returns, kept in HBM (pg.py:82)."""
+        if self._ret_rms is None:
+            dev = next(self.parameters()).device
+            self._ret_rms = DeviceScalarRMS(dev)
+        return self._ret_rms
+
+    def _get_deterministic_action(self, logits):
+        if self.action_type == "discrete":
+            return logits.argmax(-1)
+        return logits[0]
+
+    def forward(self, batch: Batch, state=None, **kwargs: Any) -> Batch:
+        """pg.py:133-171."""
+        logits, hidden = self.actor(batch.obs, state=state, info=batch.get("info", {}))
+        dist = self.dist_fn(*logits) if isinstance(logits, tuple) else self.dist_fn(logits)
+        if self._deterministic_eval and not self.training:
+            act = self._get_deterministic_action(logits)
+        else:
+            act = dist.sample()
+        return Batch(logits=logits, act=act, state=hidden, dist=dist)
+
+    def process_fn(self, batch, buffer, indices):
+        """pg.py:87-126: Monte-Carlo returns (GAE with lambda = 1, v_s_ = ret_rms.mean)."""
+        n = len(indices)
+        v_s_ = np.full(n, self.ret_rms.mean)
+        ret, _ = self.compute_episodic_return(batch, buffer, indices, v_s_=v_s_, gamma=self._gamma,
+                                              gae_lambda=1.0)
+        if self._rew_norm:
+            batch.returns = (ret - self.ret_rms.mean) / np.sqrt(self.ret_rms.var + self._eps)
+            r = torch.as_tensor(ret, device=self.ret_rms.state.device)
+            bm, bv, bc = r.mean(), r.var(unbiased=False), float(len(r))
+            st = self.ret_rms.state
+            delta = bm - st[0]
+            tot = st[2] + bc
+            m2 = st[1] * st[2] + bv * bc + delta ** 2 * st[2] * bc / tot
+            st.copy_(torch.stack([st[0] + delta * bc / tot, m2 / tot, tot]))
+        else:
+            batch.returns = ret
+        return batch
+
+    def learn(self, batch: Batch, batch_size: int, repeat: int, **kwargs: Any
+              ) -> Dict[str, List[float]]:
+        losses = []
+        for _ in range(repeat):
+            for part in split_indices(len(batch), batch_size, True, True):
+                minibatch = batch[part]
+                self.optim.zero_grad()
+                result = self(minibatch)
+                dist = result.dist
+                act = torch.as_tensor(minibatch.act, device=result.act.device)
+                ret = torch.as_tensor(minibatch.returns, device=result.act.device,
+                                      dtype=torch.float32)
+                log_prob = dist.log_prob(act).reshape(len(ret), -1).transpose(0, 1)
+                loss = -(log_prob * ret).mean()
+                loss.backward()
+                self.optim.step()
+                losses.append(loss.detach())
+        return {"loss": [float(x) for x in torch.stack(losses).cpu()] if losses else []}

@@ -1,0 +1,256 @@
+"""PPOPolicy (tianshou/policy/modelfree/ppo.py:13-162).
+
+For the Gaussian actor with state-independent log-std (ActorProb + Independent(Normal, 1),
+the MuJoCo/Box configuration of utils/models.py:34-97) the minibatch loss runs as the fused
+``tsrl_ppo_gauss_*`` kernels: the minibatch rows are addressed through the permutation
+index (no per-key minibatch copies except the obs rows the MLP GEMMs read), the clipped
+surrogate / value / entropy terms and their gradients come out of one pass, and the loss
+values are accumulated on device (no per-minibatch .item() syncs; the returned lists are
+read back once at the end).  Other actor/dist combinations run the reference's torch
+formulation on the GPU.
+"""
+from typing import Any, Callable, Dict, List, Optional
+
+import numpy as np
+import torch
+from torch import nn
+from torch.distributions import Independent, Normal
+
+from tianshou_amd import _C
+from tianshou_amd.data.batch import Batch, gather_rows, split_indices
+from tianshou_amd.policy.a2c import A2CPolicy
+from tianshou_amd.utils.net import ActorProb
+
+
+def _is_fixed_std_normal(dist_fn) -> bool:
+    try:
+        d = dist_fn(torch.zeros(1, 2), torch.ones(1, 2))
+    except Exception:
+        return False
+    return isinstance(d, Independent) and isinstance(d.base_dist, Normal) and \
+        d.reinterpreted_batch_ndims == 1
+
+
+def split_bounds(length: int, size: int, merge_last: bool):
+    """[start, end) of every Batch.split chunk (batch.py:896-912)."""
+    if size == -1:
+        size = length
+    assert 1 <= size
+    merge_last = merge_last and length % size > 0
+    out = []
+    for idx in range(0, length, size):
+        if merge_last and idx + size + size >= length:
+            out.append((idx, length))
+            break
+        out.append((idx, min(idx + size, length)))
+    return out
+
+
+class _GaussPPOLoss(torch.autograd.Function):
+    """Fused forward+backward: the kernels produce the loss terms and the gradients w.r.t.
+    mu, log-std and value in one pass; backward just scales them by the incoming grad."""
+
+    @staticmethod
+    def forward(ctx, mu, sigma_param, value, ctx_args):
+        (act, logp_old, adv, ret, v_s, idx, params, dp) = ctx_args
+        L = _C.lib()
+        s = _C.stream_ptr(mu.device)
+        mu = mu.contiguous()
+        value = value.contiguous()
+        log_std = sigma_param.detach().reshape(-1).contiguous()
+        B, A = mu.shape
+        nblk = int(L.tsrl_ppo_num_partials(B))
+        dev = mu.device
+        adv_sums = None
+        if params.norm_adv:
+            pa = torch.empty(nblk * 2, dtype=torch.float64, device=dev)
+            _C.check(L.tsrl_adv_moments(_C.ptr(adv), _C.ptr(idx), B, _C.ptr(pa), s),
+                     "tsrl_adv_moments")
+            adv_sums = torch.empty(2, dtype=torch.float64, device=dev)
+            _C.check(L.tsrl_reduce_partials(_C.ptr(pa), nblk, 2, _C.ptr(adv_sums), s),
+                     "tsrl_reduce_partials")
+            dp.all_reduce_(adv_sums)
+        grad_mu = torch.empty_like(mu)
+        grad_value = torch.empty_like(value)
+        partials = torch.empty(nblk * (4 + A), dtype=torch.float64, device=dev)
+        _C.check(L.tsrl_ppo_gauss_fwd_bwd(
+            _C.ptr(mu.detach()), _C.ptr(log_std), _C.ptr(value.detach()), _C.ptr(act),
+            _C.ptr(logp_old), _C.ptr(adv), _C.ptr(ret), _C.ptr(v_s), _C.ptr(idx), B, A,
+            _C.ptr(adv_sums), params, _C.ptr(grad_mu), _C.ptr(grad_value), _C.ptr(partials),
+            s), "tsrl_ppo_gauss_fwd_bwd")
+        sums = torch.empty(4 + A, dtype=torch.float64, device=dev)
+        _C.check(L.tsrl_reduce_partials(_C.ptr(partials), nblk, 4 + A, _C.ptr(sums), s),
+                 "tsrl_reduce_partials")
+        dp.all_reduce_(sums)
+        terms = torch.empty(4, dtype=torch.float32, device=dev)
+        grad_ls = torch.empty(A, dtype=torch.float32, device=dev)
+        _C.check(L.tsrl_ppo_gauss_finalize(_C.ptr(sums), A, _C.ptr(log_std), params,
+                                           _C.ptr(terms), _C.ptr(grad_ls), s),
+                 "tsrl_ppo_gauss_finalize")
+        ctx.save_for_backward(grad_mu, grad_value, grad_ls)
+        ctx.sp_shape = sigma_param.shape
+        loss = terms[0].clone()
+        ctx.mark_non_differentiable(terms)
+        return loss, terms
+
+    @staticmethod
+    def backward(ctx, g_loss, g_terms):
+        grad_mu, grad_value, grad_ls = ctx.saved_tensors
+        return (grad_mu * g_loss, (grad_ls * g_loss).reshape(ctx.sp_shape),
+                grad_value * g_loss, None)
+
+
+class PPOPolicy(A2CPolicy):
+    def __init__(self, actor: torch.nn.Module, critic: torch.nn.Module,
+                 optim: torch.optim.Optimizer, dist_fn: Callable, eps_clip: float = 0.2,
+                 dual_clip: Optional[float] = None, value_clip: bool = False,
+                 advantage_normalization: bool = True, recompute_advantage: bool = False,
+                 perm_device: bool = False, **kwargs: Any) -> None:
+        super().__init__(actor, critic, optim, dist_fn, **kwargs)
+        self._eps_clip = eps_clip
+        assert dual_clip is None or dual_clip > 1.0, \
+            "Dual-clip PPO parameter should greater than 1.0."
+        self._dual_clip = dual_clip
+        self._value_clip = value_clip
+        self._norm_adv = advantage_normalization
+        self._recompute_adv = recompute_advantage
+        # perm_device=False: minibatch order from np.random.permutation (the reference's
+        # global RandomState stream, bit-exact); True: torch.randperm on the GPU.
+        self.perm_device = perm_device
+        self._fused = isinstance(actor, ActorProb) and not actor._c_sigma and \
+            _is_fixed_std_normal(dist_fn)
+
+    def _params(self, b_global: float) -> _C.PPOParams:
+        p = _C.PPOParams()
+        p.eps_clip = float(self._eps_clip)
+        p.dual_clip = float(self._dual_clip) if self._dual_clip else 0.0
+        p.vf_coef = float(self._weight_vf)
+        p.ent_coef = float(self._weight_ent)
+        p.adv_eps = float(self._eps)
+        p.b_global = float(b_global)
+        p.value_clip = int(bool(self._value_clip))
+        p.norm_adv = int(bool(self._norm_adv))
+        return p
+
+    # -- process_fn -------------------------------------------------------------------------
+    def process_fn(self, batch: Batch, buffer, indices: np.ndarray) -> Batch:
+        """ppo.py:87-97."""
+        if self._recompute_adv:
+            self._buffer, self._indices = buffer, indices
+        batch = self._compute_returns(batch, buffer, indices)
+        batch.act = torch.as_tensor(batch.act, device=batch.v_s.device).to(batch.v_s.dtype)
+        with torch.no_grad():
+            if self._fused:
+                batch.logp_old = self._logp_fused(batch.obs, batch.act)
+            else:
+                batch.logp_old = self(batch).dist.log_prob(batch.act)
+        return batch
+
+    def _logp_fused(self, obs: torch.Tensor, act: torch.Tensor) -> torch.Tensor:
+        dev = act.device
+        n = len(act)
+        act = act.reshape(n, -1).contiguous()
+        A = act.shape[1]
+        out = torch.empty(n, dtype=torch.float32, device=dev)
+        log_std = self.actor.sigma_param.detach().reshape(-1).contiguous()
+        L = _C.lib()
+        for s, e in self._chunks(n):
+            mu = self.actor.forward_mu(obs[s:e]).contiguous()
+            _C.check(L.tsrl_gauss_logp(_C.ptr(mu), _C.ptr(log_std), _C.ptr(act[s:e]), e - s, A,
+                                       _C.ptr(out[s:e]), _C.stream_ptr(dev)), "tsrl_gauss_logp")
+        return out
+
+    # -- learn ----------------------------------------------------------------------------------
+    def _permutation(self, n: int, dev):
+        if self.perm_device:
+            return torch.randperm(n, device=dev)
+        return torch.as_tensor(np.random.permutation(n), device=dev)
+
+    def learn(self, batch: Batch, batch_size: int, repeat: int, **kwargs: Any
+              ) -> Dict[str, List[float]]:
+        if not self._fused:
+            return self._learn_generic(batch, batch_size, repeat)
+        dev = batch.v_s.device
+        n = len(batch.v_s)
+        terms = []
+        f32 = dict(device=dev, dtype=torch.float32)
+        for step in range(repeat):
+            if self._recompute_adv and step > 0:
+                batch = self._compute_returns(batch, self._buffer, self._indices)
+            act = batch.act.reshape(n, -1).contiguous()
+            logp_old = batch.logp_old.reshape(-1).to(**f32).contiguous()
+            adv = batch.adv.reshape(-1).to(**f32).contiguous()
+            ret = batch.returns.reshape(-1).to(**f32).contiguous()
+            v_s = batch.v_s.reshape(-1).to(**f32).contiguous()
+            perm = self._permutation(n, dev)
+            for s, e in split_bounds(n, batch_size, merge_last=True):
+                idx = perm[s:e]
+                obs_mb = gather_rows(batch.obs, idx)
+                mu = self.actor.forward_mu(obs_mb)
+                value = self.critic(obs_mb).flatten()
+                params = self._params((e - s) * self.dp.world)
+                loss, t = _GaussPPOLoss.apply(mu, self.actor.sigma_param, value,
+                                              (act, logp_old, adv, ret, v_s, idx, params,
+                                               self.dp))
+                self.optim.zero_grad()
+                loss.backward()
+                self.dp.all_reduce_grads_(self._actor_critic.parameters())
+                if self._grad_norm:
+                    nn.utils.clip_grad_norm_(self._actor_critic.parameters(),
+                                             max_norm=self._grad_norm)
+                self.optim.step()
+                terms.append(t)
+        vals = torch.stack(terms).cpu().numpy() if terms else np.zeros((0, 4), np.float32)
+        return {"loss": vals[:, 0].tolist(), "loss/clip": vals[:, 1].tolist(),
+                "loss/vf": vals[:, 2].tolist(), "loss/ent": vals[:, 3].tolist()}
+
+    def _learn_generic(self, batch: Batch, batch_size: int, repeat: int
+                       ) -> Dict[str, List[float]]:
+        """ppo.py:99-162 as written, on device tensors."""
+        losses, clip_losses, vf_losses, ent_losses = [], [], [], []
+        for step in range(repeat):
+            if self._recompute_adv and step > 0:
+                batch = self._compute_returns(batch, self._buffer, self._indices)
+            for part in split_indices(len(batch), batch_size, True, True):
+                minibatch = batch[part]
+                dist = self(minibatch).dist
+                adv = minibatch.adv
+                if self._norm_adv:
+                    mean, std = adv.mean(), adv.std()
+                    adv = (adv - mean) / (std + self._eps)
+                ratio = (dist.log_prob(minibatch.act) - minibatch.logp_old).exp().float()
+                ratio = ratio.reshape(ratio.size(0), -1).transpose(0, 1)
+                surr1 = ratio * adv
+                surr2 = ratio.clamp(1.0 - self._eps_clip, 1.0 + self._eps_clip) * adv
+                if self._dual_clip:
+                    clip1 = torch.min(surr1, surr2)
+                    clip2 = torch.max(clip1, self._dual_clip * adv)
+                    clip_loss = -torch.where(adv < 0, clip2, clip1).mean()
+                else:
+                    clip_loss = -torch.min(surr1, surr2).mean()
+                value = self.critic(minibatch.obs).flatten()
+                if self._value_clip:
+                    v_clip = minibatch.v_s + (value - minibatch.v_s).clamp(-self._eps_clip,
+                                                                           self._eps_clip)
+                    vf_loss = torch.max((minibatch.returns - value).pow(2),
+                                        (minibatch.returns - v_clip).pow(2)).mean()
+                else:
+                    vf_loss = (minibatch.returns - value).pow(2).mean()
+                ent_loss = dist.entropy().mean()
+                loss = clip_loss + self._weight_vf * vf_loss - self._weight_ent * ent_loss
+                self.optim.zero_grad()
+                loss.backward()
+                self.dp.all_reduce_grads_(self._actor_critic.parameters(), average=True)
+                if self._grad_norm:
+                    nn.utils.clip_grad_norm_(self._actor_critic.parameters(),
+                                             max_norm=self._grad_norm)
+                self.optim.step()
+                clip_losses.append(clip_loss.detach())
+                vf_losses.append(vf_loss.detach())
+                ent_losses.append(ent_loss.detach())
+                losses.append(loss.detach())
+        out = {}
+        for k, v in (("loss", losses), ("loss/clip", clip_losses), ("loss/vf", vf_losses),
+                     ("loss/ent", ent_losses)):
+            out[k] = torch.stack(v).cpu().tolist() if v else []
+        return out

@@ -1,0 +1,209 @@
+"""Actor/critic networks with the reference's module layout, so ``state_dict()`` keys match
+tianshou 0.5.1 checkpoints (utils/net/common.py:56-285, continuous.py:87-235,
+discrete.py:12-121).  The GEMMs run through PyTorch-ROCm (hipBLASLt) on the GPU."""
+from typing import Any, Dict, Optional, Sequence, Tuple, Type, Union
+
+import numpy as np
+import torch
+from torch import nn
+
+SIGMA_MIN = -20
+SIGMA_MAX = 2
+
+
+def miniblock(input_size, output_size=0, norm_layer=None, activation=None,
+              linear_layer: Type[nn.Linear] = nn.Linear):
+    layers = [linear_layer(input_size, output_size)]
+    if norm_layer is not None:
+        layers += [norm_layer(output_size)]
+    if activation is not None:
+        layers += [activation()]
+    return layers
+
+
+class MLP(nn.Module):
+    """MLP backbone (common.py:56-150): Linear/activation stack in ``self.model``."""
+
+    def __init__(self, input_dim: int, output_dim: int = 0, hidden_sizes: Sequence[int] = (),
+                 norm_layer=None, activation=nn.ReLU, device=None,
+                 linear_layer: Type[nn.Linear] = nn.Linear, flatten_input: bool = True):
+        super().__init__()
+        self.device = device
+        sizes = [input_dim] + list(hidden_sizes)
+        acts = activation if isinstance(activation, (list, tuple)) else \
+            [activation] * len(hidden_sizes)
+        norms = norm_layer if isinstance(norm_layer, (list, tuple)) else \
+            [norm_layer] * len(hidden_sizes)
+        model = []
+        for i, (din, dout) in enumerate(zip(sizes[:-1], sizes[1:])):
+            model += miniblock(din, dout, norms[i], acts[i], linear_layer)
+        if output_dim > 0:
+            model += [linear_layer(sizes[-1], output_dim)]
+        self.output_dim = output_dim or sizes[-1]
+        self.model = nn.Sequential(*model)
+        self.flatten_input = flatten_input
+
+    def forward(self, obs):
+        obs = torch.as_tensor(obs, device=self.device, dtype=torch.float32)
+        if self.flatten_input:
+            obs = obs.flatten(1)
+        return self.model(obs)
+
+
+class Net(nn.Module):
+    """common.py:161-285 (no dueling / atoms / concat beyond what PPO uses)."""
+
+    def __init__(self, state_shape, action_shape=0, hidden_sizes: Sequence[int] = (),
+                 norm_layer=None, activation=nn.ReLU, device="cpu", softmax: bool = False,
+                 concat: bool = False, num_atoms: int = 1, linear_layer=nn.Linear):
+        super().__init__()
+        self.device = device
+        self.softmax = softmax
+        self.num_atoms = num_atoms
+        input_dim = int(np.prod(state_shape))
+        action_dim = int(np.prod(action_shape)) * num_atoms
+        if concat:
+            input_dim += action_dim
+        output_dim = action_dim if not concat else 0
+        self.model = MLP(input_dim, output_dim, hidden_sizes, norm_layer, activation, device,
+                         linear_layer)
+        self.output_dim = self.model.output_dim
+
+    def forward(self, obs, state: Any = None, **kwargs):
+        logits = self.model(obs)
+        if self.num_atoms > 1:
+            logits = logits.view(logits.shape[0], -1, self.num_atoms)
+        if self.softmax:
+            logits = torch.softmax(logits, dim=-1)
+        return logits, state
+
+
+def _module_device(m: nn.Module):
+    try:
+        return next(m.parameters()).device
+    except StopIteration:
+        return None
+
+
+class _PreprocessWrapper(nn.Module):
+    """continuous.py:13-30: the preprocess net is registered under two names."""
+
+    def __init__(self, preprocess_net: nn.Module, device=None):
+        super().__init__()
+        device = device if device else _module_device(preprocess_net)
+        preprocess_net.to(device)
+        self.device = device
+        self.preprocess_net = preprocess_net
+        self.preprocess = preprocess_net
+
+
+class ActorProb(_PreprocessWrapper):
+    """Gaussian actor (continuous.py:153-235).  With ``conditioned_sigma=False`` the log-std
+    ``sigma_param`` is state-independent, which is what the fused HIP PPO loss consumes."""
+
+    def __init__(self, preprocess_net, action_shape, hidden_sizes=(), max_action=1.0,
+                 device="cpu", unbounded=False, conditioned_sigma=False,
+                 preprocess_net_output_dim=None):
+        super().__init__(preprocess_net, device=device)
+        if unbounded:
+            max_action = 1.0
+        self.output_dim = int(np.prod(action_shape))
+        input_dim = getattr(preprocess_net, "output_dim", preprocess_net_output_dim)
+        self.mu = MLP(input_dim, self.output_dim, hidden_sizes, device=self.device)
+        self._c_sigma = conditioned_sigma
+        if conditioned_sigma:
+            self.sigma = MLP(input_dim, self.output_dim, hidden_sizes, device=self.device)
+        else:
+            self.sigma_param = nn.Parameter(torch.zeros(self.output_dim, 1))
+        self.max_action = max_action
+        self._unbounded = unbounded
+
+    def forward_mu(self, obs):
+        logits, _ = self.preprocess(obs, None)
+        mu = self.mu(logits)
+        if not self._unbounded:
+            mu = self.max_action * torch.tanh(mu)
+        return mu
+
+    def forward(self, obs, state=None, info: Dict[str, Any] = {}):
+        logits, hidden = self.preprocess(obs, state)
+        mu = self.mu(logits)
+        if not self._unbounded:
+            mu = self.max_action * torch.tanh(mu)
+        if self._c_sigma:
+            sigma = torch.clamp(self.sigma(logits), min=SIGMA_MIN, max=SIGMA_MAX).exp()
+        else:
+            shape = [1] * len(mu.shape)
+            shape[1] = -1
+            sigma = (self.sigma_param.view(shape) + torch.zeros_like(mu)).exp()
+        return (mu, sigma), state
+
+
+class Critic(_PreprocessWrapper):
+    """V(s) head (continuous.py:87-150)."""
+
+    def __init__(self, preprocess_net, hidden_sizes=(), device=None,
+                 preprocess_net_output_dim=None, linear_layer=nn.Linear, flatten_input=True):
+        super().__init__(preprocess_net, device=device)
+        self.output_dim = 1
+        input_dim = getattr(preprocess_net, "output_dim", preprocess_net_output_dim)
+        self.last = MLP(input_dim, 1, hidden_sizes, device=self.device,
+                        linear_layer=linear_layer, flatten_input=flatten_input)
+
+    def forward(self, obs, act=None, info: Dict[str, Any] = {}):
+        obs = torch.as_tensor(obs, device=self.device, dtype=torch.float32).flatten(1)
+        if act is not None:
+            act = torch.as_tensor(act, device=self.device, dtype=torch.float32).flatten(1)
+            obs = torch.cat([obs, act], dim=1)
+        logits, _ = self.preprocess(obs)
+        return self.last(logits)
+
+
+class DiscreteActor(_PreprocessWrapper):
+    """Softmax actor (discrete.py:12-71); outputs probabilities unless softmax_output=False."""
+
+    def __init__(self, preprocess_net, action_shape, hidden_sizes=(), softmax_output=True,
+                 preprocess_net_output_dim=None, device="cpu"):
+        super().__init__(preprocess_net, device=device)
+        self.output_dim = int(np.prod(action_shape))
+        input_dim = getattr(preprocess_net, "output_dim", preprocess_net_output_dim)
+        self.last = MLP(input_dim, self.output_dim, hidden_sizes, device=self.device)
+        self.softmax_output = softmax_output
+
+    def forward(self, obs, state=None, info: Dict[str, Any] = {}):
+        logits, hidden = self.preprocess(obs, state)
+        logits = self.last(logits)
+        if self.softmax_output:
+            logits = torch.softmax(logits, dim=-1)
+        return logits, hidden
+
+
+class DiscreteCritic(Critic):
+    pass
+
+
+class ActorCritic(nn.Module):
+    """common.py:364-377."""
+
+    def __init__(self, actor: nn.Module, critic: nn.Module) -> None:
+        super().__init__()
+        self.actor = actor
+        self.critic = critic
+
+
+def build_actor_critic_from_state(state: Dict[str, torch.Tensor], device="cpu"):
+    """Rebuild get_actor_critic-shaped (Tanh MLP) actor/critic from a policy state_dict."""
+    w0 = state["actor.preprocess_net.model.model.0.weight"]
+    hidden = []
+    i = 0
+    while f"actor.preprocess_net.model.model.{i}.weight" in state:
+        hidden.append(state[f"actor.preprocess_net.model.model.{i}.weight"].shape[0])
+        i += 2
+    obs_dim = w0.shape[1]
+    act_dim = state["actor.mu.model.0.weight"].shape[0]
+    from tianshou_amd.utils.models import get_actor_critic
+    actor, critic = get_actor_critic((obs_dim,), hidden, (act_dim,), device)
+    ac = ActorCritic(actor, critic)
+    ac.load_state_dict({k: v for k, v in state.items()
+                        if k.startswith("actor.") or k.startswith("critic.")}, strict=False)
+    return actor.to(device), critic.to(device)

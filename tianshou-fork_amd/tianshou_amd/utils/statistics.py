@@ -1,0 +1,132 @@
+"""Running statistics.
+
+* ``RunningMeanStd``        -- host object with the reference's API
+                              (tianshou/utils/statistics.py:69-114).
+* ``DeviceRunningMeanStd``  -- the same statistics kept in HBM (obs_rms of VectorEnvNormObs,
+                              ret_rms of PGPolicy) so the rollout/update loop never syncs;
+                              ``mean``/``var``/``count`` read back on access.
+"""
+from typing import Optional
+
+import numpy as np
+import torch
+
+from tianshou_amd import _C
+
+
+class RunningMeanStd:
+    """Host RunningMeanStd (statistics.py:69-114): Chan parallel merge, clip on norm."""
+
+    def __init__(self, mean=0.0, std=1.0, clip_max: Optional[float] = 10.0,
+                 epsilon: float = np.finfo(np.float32).eps.item()) -> None:
+        self.mean, self.var = mean, std
+        self.clip_max = clip_max
+        self.count = 0
+        self.eps = epsilon
+
+    def norm(self, data_array):
+        data_array = (data_array - self.mean) / np.sqrt(self.var + self.eps)
+        if self.clip_max:
+            data_array = np.clip(data_array, -self.clip_max, self.clip_max)
+        return data_array
+
+    def update(self, data_array: np.ndarray) -> None:
+        batch_mean, batch_var = np.mean(data_array, axis=0), np.var(data_array, axis=0)
+        batch_count = len(data_array)
+        delta = batch_mean - self.mean
+        total_count = self.count + batch_count
+        new_mean = self.mean + delta * batch_count / total_count
+        m_a = self.var * self.count
+        m_b = batch_var * batch_count
+        m_2 = m_a + m_b + delta ** 2 * self.count * batch_count / total_count
+        self.mean, self.var = new_mean, m_2 / total_count
+        self.count = total_count
+
+
+class DeviceRunningMeanStd:
+    """Column RunningMeanStd over rows of a [k, dim] f32 device tensor (obs_rms)."""
+
+    def __init__(self, dim: int, device, clip_max: Optional[float] = 10.0,
+                 epsilon: float = np.finfo(np.float32).eps.item()) -> None:
+        self.dim = int(dim)
+        self.device = torch.device(device)
+        self.mean_t = torch.zeros(self.dim, dtype=torch.float32, device=self.device)
+        self.var_t = torch.ones(self.dim, dtype=torch.float32, device=self.device)
+        self.count_t = torch.zeros(1, dtype=torch.float64, device=self.device)
+        self.clip_max = clip_max
+        self.eps = epsilon
+
+    # -- reference-compatible views (sync on access) ------------------------------------
+    @property
+    def mean(self) -> np.ndarray:
+        return self.mean_t.cpu().numpy()
+
+    @property
+    def var(self) -> np.ndarray:
+        return self.var_t.cpu().numpy()
+
+    @property
+    def count(self) -> int:
+        return int(self.count_t.item())
+
+    def state_dict(self):
+        return dict(mean=self.mean, var=self.var, count=self.count)
+
+    def load(self, mean, var, count) -> None:
+        self.mean_t.copy_(torch.as_tensor(np.asarray(mean, np.float32)))
+        self.var_t.copy_(torch.as_tensor(np.asarray(var, np.float32)))
+        self.count_t.fill_(float(count))
+
+    # -- device operations ---------------------------------------------------------------
+    def merge_partials(self, partials: torch.Tensor, nblk: int, mask=None, k=None) -> None:
+        """Fold env-kernel column partials ([nblk, dim, 2] f64) of k rows (mask-selected)."""
+        k = int(k if k is not None else (mask.numel() if mask is not None else 0))
+        _C.check(_C.lib().tsrl_rms_merge(
+            _C.ptr(partials), nblk, self.dim, _C.ptr(mask), k, _C.ptr(self.mean_t),
+            _C.ptr(self.var_t), _C.ptr(self.count_t), _C.stream_ptr()), "tsrl_rms_merge")
+
+    def update(self, x: torch.Tensor, mask: Optional[torch.Tensor] = None) -> None:
+        x = x.reshape(len(x), -1)
+        if mask is not None:
+            xs = x[mask.bool()]
+        else:
+            xs = x
+        xd = xs.double()
+        partials = torch.stack([xd.sum(0), (xd * xd).sum(0)], dim=-1).contiguous()
+        self.merge_partials(partials.reshape(1, self.dim, 2), 1, None, len(xs))
+
+    def norm_rows(self, x: torch.Tensor, out: torch.Tensor, mask=None) -> torch.Tensor:
+        _C.check(_C.lib().tsrl_rms_norm_rows(
+            _C.ptr(x), _C.ptr(mask), len(x), self.dim, _C.ptr(self.mean_t), _C.ptr(self.var_t),
+            float(self.eps), float(self.clip_max or 0.0), _C.ptr(out), _C.stream_ptr()),
+            "tsrl_rms_norm_rows")
+        return out
+
+    def norm(self, x: torch.Tensor) -> torch.Tensor:
+        x = x.contiguous().float()
+        out = torch.empty_like(x)
+        return self.norm_rows(x.reshape(len(x), -1), out.reshape(len(x), -1))
+
+
+class DeviceScalarRMS:
+    """Scalar RunningMeanStd in HBM as double[3] = {mean, var, count} (ret_rms of
+    PGPolicy, tianshou/policy/modelfree/pg.py:82)."""
+
+    def __init__(self, device) -> None:
+        self.state = torch.tensor([0.0, 1.0, 0.0], dtype=torch.float64, device=device)
+
+    @property
+    def mean(self) -> float:
+        return float(self.state[0].item())
+
+    @property
+    def var(self) -> float:
+        return float(self.state[1].item())
+
+    @property
+    def count(self) -> int:
+        return int(self.state[2].item())
+
+    def update_from_partials(self, partials: torch.Tensor, nparts: int) -> None:
+        _C.check(_C.lib().tsrl_ret_rms_update(_C.ptr(partials), nparts, _C.ptr(self.state),
+                                              _C.stream_ptr()), "tsrl_ret_rms_update")
