@@ -59,6 +59,8 @@ def _parse(v):
     if isinstance(v, dict):
         return Batch(v)
     if isinstance(v, (list, tuple)) and not isinstance(v, Batch):
+        if any(isinstance(x, torch.Tensor) for x in v):
+            return v  # e.g. logits=(mu, sigma) of a Gaussian actor
         try:
             return np.asarray(v)
         except ValueError:

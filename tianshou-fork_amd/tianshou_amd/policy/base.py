@@ -202,7 +202,10 @@ class BasePolicy(nn.Module):
             v_s_ = torch.zeros(n, dtype=torch.float64, device=dev)
         else:
             v_s_ = _as_dev(v_s_, dev)
-        v_s = torch.roll(v_s_, 1) if v_s is None else _as_dev(v_s, dev)
+        if v_s is None:  # base.py:377: v_s = roll(v_s_ * value_mask, 1)
+            v_s = torch.roll(v_s_ * (term == 0).to(v_s_.dtype), 1)
+        else:
+            v_s = _as_dev(v_s, dev)
         unfinished = buffer.unfinished_index()
         extra = torch.as_tensor(np.isin(np.asarray(indices), unfinished).astype(np.uint8),
                                 device=dev)
