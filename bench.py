@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--minibatches", type=int, default=32)
     ap.add_argument("--ep-len", type=int, default=1000)
     ap.add_argument("--perm", choices=["numpy", "device"], default="device")
-    ap.add_argument("--cpu-steps", type=int, default=48,
+    ap.add_argument("--cpu-steps", type=int, default=256,
                     help="T' of the bounded CPU-baseline sample (envs x T')")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()

@@ -99,12 +99,14 @@ int tsrl_synth_u8_reset(const int64_t* ids, const uint8_t* mask, int64_t k,
  * RunningMeanStd, tianshou/utils/statistics.py:69-114).
  * rms_merge folds column partials of a batch of `count` rows (count = number of mask
  * bytes set, or k when mask == NULL; zero rows -> no update) into mean/var (f32 [dim])
- * and *count (f64 scalar on device).  rms_norm_rows writes
+ * and *count (f64 scalar on device).  `ticket` is a zero-initialised device word owned by
+ * the statistics object (the last workgroup publishes the count and re-arms it; no host
+ * state, so the call can be captured in a HIP graph).  rms_norm_rows writes
  * clip((x - mean) / sqrt(var + eps), +-clip) for rows with mask[r] (all when NULL).
  * ------------------------------------------------------------------------------- */
 int tsrl_rms_merge(const double* col_partials, int64_t nblk, int64_t dim,
                    const uint8_t* mask, int64_t k, float* mean, float* var, double* count,
-                   void* stream);
+                   unsigned int* ticket, void* stream);
 int tsrl_rms_norm_rows(const float* x, const uint8_t* mask, int64_t k, int64_t dim,
                        const float* mean, const float* var, float eps, float clip,
                        float* out, void* stream);
@@ -133,6 +135,10 @@ typedef struct tsrl_add_args {
     int64_t k;
     int64_t uniform_rel;     /* every env at the same sub-buffer index (n_step collect) */
     int64_t uniform_next;
+    const int64_t* rel_dev;  /* non-NULL: the uniform index is read from device memory (a
+                                HIP-graph-replayable step; advance it with
+                                tsrl_ring_advance), next = (rel + 1) % ring_size */
+    int64_t ring_size;
     /* row payloads */
     const void* obs_src; void* obs_dst; int64_t obs_row_bytes;
     const float* obs_next_src; float* obs_next_dst; float* cur_obs; int64_t obs_dim;
@@ -149,12 +155,22 @@ typedef struct tsrl_add_args {
     double* stat_rew; int64_t* stat_len; int64_t* stat_idx;       /* per storage row */
 } tsrl_add_args;
 int tsrl_buffer_add(const tsrl_add_args* a, void* stream);
+/* *rel_dev = (*rel_dev + 1) % ring_size (device-side ring cursor for graph-captured steps). */
+int tsrl_ring_advance(int64_t* rel_dev, int64_t ring_size, void* stream);
 
 /* Row gather: dst[i] = src[idx[i]] for rows of row_bytes bytes (Batch.__getitem__ /
  * ReplayBuffer.__getitem__ fancy indexing, tianshou/data/batch.py:446-460,
  * buffer/base.py:360-389). */
 int tsrl_gather_rows(const void* src, int64_t row_bytes, const int64_t* idx, int64_t k,
                      void* dst, void* stream);
+
+/* out[c] = sum_r x[r][c] for a row-major f32 [rows, cols] matrix: the bias gradients
+ * (db = sum over the minibatch of dY) and the reduction of the split-K partial products of
+ * the weight gradients (dW = dY^T X).  Tall inputs use a caller workspace for per-chunk
+ * partial rows (size from tsrl_sum_rows_workspace_bytes). */
+int64_t tsrl_sum_rows_workspace_bytes(int64_t rows, int64_t cols);
+int tsrl_sum_rows_f32(const float* x, int64_t rows, int64_t cols, float* out, void* workspace,
+                      int64_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------
  * PPO clipped surrogate + value + entropy loss, Gaussian Independent(Normal(mu, exp(s)),1)

@@ -10,7 +10,7 @@ namespace tsrl {
 namespace {
 
 constexpr int TPB = 256;
-constexpr int ROWS = 32;  // env rows per workgroup
+constexpr int ROWS = 16;  // env rows per workgroup
 constexpr uint64_t GOLD = 0x9E3779B97F4A7C15ull;
 constexpr uint64_t REW_SALT = 0xD1B54A32D192ED03ull;
 

@@ -85,19 +85,37 @@ __global__ __launch_bounds__(TPB) void reduce_partials_kernel(const double* part
     }
 }
 
+// One workgroup = 256 minibatch rows.  The [256, A] mu tile (contiguous) and the gathered
+// act rows are staged through LDS with coalesced / row-contiguous loads, the per-row math
+// reads LDS (row stride A: conflict-free for odd A), and grad_mu goes back out through the
+// same LDS tile as one contiguous coalesced store.
 __global__ __launch_bounds__(TPB) void gauss_fwd_bwd_kernel(
     const float* mu, const float* log_std, const float* value, const float* act,
     const float* logp_old, const float* adv, const float* ret, const float* v_s,
     const int64_t* idx, int64_t b, int64_t A, const double* adv_sums, Params p,
     float* grad_mu, float* grad_value, double* partials) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* s_mu = smem;             // [TPB * A]
+    float* s_act = smem + TPB * A;  // [TPB * A]
     __shared__ float s_var[MAX_ACT], s_ls[MAX_ACT];
     __shared__ double red[NW][4 + MAX_ACT];
     const int w = threadIdx.x / kWave;
     const int lane = threadIdx.x & (kWave - 1);
+    const int64_t r0 = (int64_t)blockIdx.x * TPB;
+    const int nrows = (int)min((int64_t)TPB, b - r0);
     for (int a = threadIdx.x; a < A; a += TPB) {
         const float sig = expf(log_std[a]);
         s_var[a] = sig * sig;
         s_ls[a] = logf(sig);
+    }
+    const int nel = nrows * (int)A;
+    const float* mu_blk = mu + r0 * A;
+    for (int f = threadIdx.x; f < nel; f += TPB) s_mu[f] = mu_blk[f];
+    for (int f = threadIdx.x; f < nel; f += TPB) {
+        const int row = f / (int)A;
+        const int a = f - row * (int)A;
+        const int64_t j = idx ? idx[r0 + row] : r0 + row;
+        s_act[f] = act[j * A + a];
     }
     __syncthreads();
     float mean_f = 0.0f, std_f = 1.0f;
@@ -108,9 +126,12 @@ __global__ __launch_bounds__(TPB) void gauss_fwd_bwd_kernel(
         mean_f = (float)m;
         std_f = (float)sqrt(var > 0.0 ? var : 0.0);
     }
-    const int64_t r = (int64_t)blockIdx.x * TPB + threadIdx.x;
-    const bool live = r < b;
+    const int t = threadIdx.x;
+    const bool live = t < nrows;
+    const int64_t r = r0 + t;
     const int64_t j = live ? (idx ? idx[r] : r) : 0;
+    float* my_mu = s_mu + t * A;
+    const float* my_act = s_act + t * A;
     float g_logp = 0.0f;
     double clip_term = 0.0, vf_term = 0.0;
     if (live) {
@@ -118,7 +139,7 @@ __global__ __launch_bounds__(TPB) void gauss_fwd_bwd_kernel(
         if (p.norm_adv) an = (an - mean_f) / (std_f + p.adv_eps);
         float logp = 0.0f;
         for (int64_t a = 0; a < A; ++a) {
-            const float diff = act[j * A + a] - mu[r * A + a];
+            const float diff = my_act[a] - my_mu[a];
             logp += -(diff * diff) / (2.0f * s_var[a]) - s_ls[a] - LOG_SQRT_2PI;
         }
         const float ratio = expf(logp - logp_old[j]);
@@ -139,11 +160,11 @@ __global__ __launch_bounds__(TPB) void gauss_fwd_bwd_kernel(
         }
         float obj = clip1, dobj = d1;
         if (p.use_dual && an < 0.0f) {
-            const float t = p.dual * an;
-            if (clip1 > t) {
+            const float tt = p.dual * an;
+            if (clip1 > tt) {
                 obj = clip1;
-            } else if (clip1 < t) {
-                obj = t;
+            } else if (clip1 < tt) {
+                obj = tt;
                 dobj = 0.0f;
             } else {
                 obj = clip1;
@@ -182,13 +203,13 @@ __global__ __launch_bounds__(TPB) void gauss_fwd_bwd_kernel(
         }
         grad_value[r] = (float)((double)p.vf_coef * (double)dv * p.inv_b);
     }
-    // gradients wrt mu, and per-dim d/d(log_std) partials
+    // d/d(mu) into the LDS tile (own row only), d/d(log_std) partials per dim
     for (int64_t a = 0; a < A; ++a) {
         double dls = 0.0;
         if (live) {
-            const float diff = act[j * A + a] - mu[r * A + a];
+            const float diff = my_act[a] - my_mu[a];
             const float var = s_var[a];
-            grad_mu[r * A + a] = g_logp * diff / var;
+            my_mu[a] = g_logp * diff / var;
             dls = (double)g_logp * ((double)(diff * diff) / (double)var - 1.0);
         }
         dls = wave_sum(dls);
@@ -204,10 +225,12 @@ __global__ __launch_bounds__(TPB) void gauss_fwd_bwd_kernel(
         red[w][3] = 0.0;
     }
     __syncthreads();
+    float* gm_blk = grad_mu + r0 * A;
+    for (int f = threadIdx.x; f < nel; f += TPB) gm_blk[f] = s_mu[f];
     for (int c = threadIdx.x; c < 4 + A; c += TPB) {
-        double t = 0.0;
-        for (int i = 0; i < NW; ++i) t += red[i][c];
-        partials[(int64_t)blockIdx.x * (4 + A) + c] = t;
+        double tsum = 0.0;
+        for (int i = 0; i < NW; ++i) tsum += red[i][c];
+        partials[(int64_t)blockIdx.x * (4 + A) + c] = tsum;
     }
 }
 
@@ -293,8 +316,9 @@ extern "C" int tsrl_ppo_gauss_fwd_bwd(const float* mu, const float* log_std, con
     TSRL_CHECK_ARG(!p.value_clip || v_s, "tsrl_ppo_gauss_fwd_bwd: value_clip needs v_s");
     TSRL_CHECK_ARG(!p.norm_adv || adv_sums, "tsrl_ppo_gauss_fwd_bwd: norm_adv needs adv_sums");
     TSRL_CHECK_ARG(p.b_global >= 1.0, "tsrl_ppo_gauss_fwd_bwd: b_global < 1");
+    const size_t lds = 2 * (size_t)TPB * (size_t)act_dim * sizeof(float);
     hipLaunchKernelGGL(gauss_fwd_bwd_kernel, dim3((unsigned)tsrl_ppo_num_partials(b)), dim3(TPB),
-                       0, as_stream(stream), mu, log_std, value, act, logp_old, adv, ret, v_s,
+                       lds, as_stream(stream), mu, log_std, value, act, logp_old, adv, ret, v_s,
                        idx, b, act_dim, adv_sums, make_params(p), grad_mu, grad_value, partials);
     TSRL_LAUNCH_CHECK("tsrl_ppo_gauss_fwd_bwd");
     return 0;

@@ -11,31 +11,63 @@ namespace {
 
 constexpr int TPB = 256;
 
-__global__ __launch_bounds__(TPB) void rms_merge_kernel(const double* partials, int64_t nblk,
-                                                        int64_t dim, const uint8_t* mask,
-                                                        int64_t k, float* mean, float* var,
-                                                        double* count) {
-    __shared__ double sh_cnt[TPB / kWave];
-    // batch count
+// Column-parallel merge.  Block = 64 columns x 16 partial lanes (1024 threads); every block
+// reads the OLD count, and the last block to finish (agent-scope ticket) publishes the new
+// count and re-arms the ticket, so no block can observe a half-updated count and the launch
+// needs no host-side state (graph-replay safe).
+constexpr int MCOLS = 64;
+constexpr int MLANES = 16;
+
+__global__ __launch_bounds__(MCOLS * MLANES) void rms_merge_kernel(
+    const double* partials, int64_t nblk, int64_t dim, const uint8_t* mask, int64_t k,
+    float* mean, float* var, double* count, unsigned int* ticket) {
+    __shared__ double sh_s[MLANES][MCOLS];
+    __shared__ double sh_ss[MLANES][MCOLS];
+    __shared__ double sh_cnt[MCOLS * MLANES / kWave];
+    const int tid = threadIdx.x;
+    const int col = tid % MCOLS;
+    const int lane = tid / MCOLS;
+    // batch count (mask bytes set, or k)
     double c = 0.0;
     if (mask) {
-        for (int64_t r = threadIdx.x; r < k; r += TPB) c += mask[r] ? 1.0 : 0.0;
-    } else if (threadIdx.x == 0) {
+        for (int64_t r = tid; r < k; r += MCOLS * MLANES) c += mask[r] ? 1.0 : 0.0;
+    } else if (tid == 0) {
         c = (double)k;
     }
     c = wave_sum(c);
-    if ((threadIdx.x & (kWave - 1)) == 0) sh_cnt[threadIdx.x / kWave] = c;
+    if ((tid & (kWave - 1)) == 0) sh_cnt[tid / kWave] = c;
+    const double old_count = *count;
     __syncthreads();
     double bc = 0.0;
-    for (int w = 0; w < TPB / kWave; ++w) bc += sh_cnt[w];
-    if (bc == 0.0) return;  // nothing reset / stepped: no update (the reference skips it)
-    const double old_count = *count;
+    for (int w = 0; w < MCOLS * MLANES / kWave; ++w) bc += sh_cnt[w];
     const double tot = old_count + bc;
-    for (int64_t d = threadIdx.x; d < dim; d += TPB) {
+    const int64_t d = (int64_t)blockIdx.x * MCOLS + col;
+    double s0 = 0.0, s1 = 0.0, q0 = 0.0, q1 = 0.0;
+    if (bc > 0.0 && d < dim) {
+        int64_t b = lane;
+        for (; b + MLANES < nblk; b += 2 * MLANES) {
+            const double2 p0 = *reinterpret_cast<const double2*>(partials + (b * dim + d) * 2);
+            const double2 p1 = *reinterpret_cast<const double2*>(
+                partials + ((b + MLANES) * dim + d) * 2);
+            s0 += p0.x;
+            q0 += p0.y;
+            s1 += p1.x;
+            q1 += p1.y;
+        }
+        if (b < nblk) {
+            const double2 p0 = *reinterpret_cast<const double2*>(partials + (b * dim + d) * 2);
+            s0 += p0.x;
+            q0 += p0.y;
+        }
+    }
+    sh_s[lane][col] = s0 + s1;
+    sh_ss[lane][col] = q0 + q1;
+    __syncthreads();
+    if (lane == 0 && bc > 0.0 && d < dim) {
         double s = 0.0, ss = 0.0;
-        for (int64_t b = 0; b < nblk; ++b) {
-            s += partials[(b * dim + d) * 2];
-            ss += partials[(b * dim + d) * 2 + 1];
+        for (int l = 0; l < MLANES; ++l) {
+            s += sh_s[l][col];
+            ss += sh_ss[l][col];
         }
         const double bm = s / bc;
         double bv = ss / bc - bm * bm;
@@ -48,8 +80,14 @@ __global__ __launch_bounds__(TPB) void rms_merge_kernel(const double* partials, 
         mean[d] = (float)new_mean;
         var[d] = (float)(m2 / tot);
     }
-    __syncthreads();
-    if (threadIdx.x == 0) *count = tot;
+    if (tid == 0) {
+        const unsigned int t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+        if (t == gridDim.x - 1) {  // every block has read the old count
+            __hip_atomic_store(count, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
 __device__ __forceinline__ float norm1(float x, float m, float v, float eps, float clip) {
@@ -79,12 +117,16 @@ using namespace tsrl;
 
 extern "C" int tsrl_rms_merge(const double* col_partials, int64_t nblk, int64_t dim,
                               const uint8_t* mask, int64_t k, float* mean, float* var,
-                              double* count, void* stream) {
-    TSRL_CHECK_ARG(col_partials && mean && var && count && dim > 0 && nblk >= 0 && k >= 0,
+                              double* count, unsigned int* ticket, void* stream) {
+    TSRL_CHECK_ARG(col_partials && mean && var && count && ticket && dim > 0 && nblk >= 0 &&
+                       k >= 0,
                    "tsrl_rms_merge: bad arguments");
+    TSRL_CHECK_ARG(((uintptr_t)col_partials & 15) == 0, "tsrl_rms_merge: partials not 16B aligned");
     if (k == 0) return 0;
-    hipLaunchKernelGGL(rms_merge_kernel, dim3(1), dim3(TPB), 0, as_stream(stream), col_partials,
-                       nblk, dim, mask, k, mean, var, count);
+    const int64_t grid = (dim + MCOLS - 1) / MCOLS;
+    hipLaunchKernelGGL(rms_merge_kernel, dim3((unsigned)grid), dim3(MCOLS * MLANES), 0,
+                       as_stream(stream), col_partials, nblk, dim, mask, k, mean, var, count,
+                       ticket);
     TSRL_LAUNCH_CHECK("tsrl_rms_merge");
     return 0;
 }

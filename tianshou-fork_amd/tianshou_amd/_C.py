@@ -22,7 +22,7 @@ class AddArgs(ctypes.Structure):
     """Mirror of ``tsrl_add_args`` (field order must match include/tsrl.h)."""
     _fields_ = [
         ("ids", _p), ("ptr", _p), ("next_rel", _p), ("offset", _p), ("k", _i64),
-        ("uniform_rel", _i64), ("uniform_next", _i64),
+        ("uniform_rel", _i64), ("uniform_next", _i64), ("rel_dev", _p), ("ring_size", _i64),
         ("obs_src", _p), ("obs_dst", _p), ("obs_row_bytes", _i64),
         ("obs_next_src", _p), ("obs_next_dst", _p), ("cur_obs", _p), ("obs_dim", _i64),
         ("norm_mean", _p), ("norm_var", _p), ("norm_eps", _f), ("norm_clip", _f),
@@ -62,10 +62,13 @@ _SIGS = {
     "tsrl_synth_u8_step": ([_p, _i64, _i64, _u64, _i64, _p, _p, _p, _p, _p, _p, _p],
                            ctypes.c_int),
     "tsrl_synth_u8_reset": ([_p, _p, _i64, _i64, _u64, _i64, _p, _p, _p, _p], ctypes.c_int),
-    "tsrl_rms_merge": ([_p, _i64, _i64, _p, _i64, _p, _p, _p, _p], ctypes.c_int),
+    "tsrl_rms_merge": ([_p, _i64, _i64, _p, _i64, _p, _p, _p, _p, _p], ctypes.c_int),
     "tsrl_rms_norm_rows": ([_p, _p, _i64, _i64, _p, _p, _f, _f, _p, _p], ctypes.c_int),
     "tsrl_buffer_add": ([ctypes.POINTER(AddArgs), _p], ctypes.c_int),
+    "tsrl_ring_advance": ([_p, _i64, _p], ctypes.c_int),
     "tsrl_gather_rows": ([_p, _i64, _p, _i64, _p, _p], ctypes.c_int),
+    "tsrl_sum_rows_workspace_bytes": ([_i64, _i64], _i64),
+    "tsrl_sum_rows_f32": ([_p, _i64, _i64, _p, _p, _i64, _p], ctypes.c_int),
     "tsrl_ppo_num_partials": ([_i64], _i64),
     "tsrl_adv_moments": ([_p, _p, _i64, _p, _p], ctypes.c_int),
     "tsrl_reduce_partials": ([_p, _i64, _i64, _p, _p], ctypes.c_int),

@@ -275,8 +275,8 @@ class VectorReplayBuffer:
             dst.__dict__[k][pt] = t.to(dst.__dict__[k].dtype)
 
     def _launch_add(self, *, ids, k, ptr=None, next_rel=None, uniform_rel=0, uniform_next=0,
-                    obs=None, act=None, obs_next=None, obs_next_raw=None, cur_obs=None,
-                    norm=None, rew=None, term=None, trunc=None, out=None,
+                    rel_dev=None, obs=None, act=None, obs_next=None, obs_next_raw=None,
+                    cur_obs=None, norm=None, rew=None, term=None, trunc=None, out=None,
                     stats=True) -> None:
         """One tsrl_buffer_add launch (see include/tsrl.h)."""
         m = self._meta
@@ -289,6 +289,8 @@ class VectorReplayBuffer:
         a.k = k
         a.uniform_rel = uniform_rel
         a.uniform_next = uniform_next
+        a.rel_dev = _C.ptr(rel_dev)
+        a.ring_size = self._ring.size
         if obs is not None:
             a.obs_src = _C.ptr(obs)
             a.obs_dst = _C.ptr(m.obs)

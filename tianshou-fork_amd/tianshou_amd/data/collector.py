@@ -18,6 +18,7 @@ from typing import Any, Callable, Dict, Optional
 import numpy as np
 import torch
 
+from tianshou_amd import _C
 from tianshou_amd.data.batch import Batch
 from tianshou_amd.data.buffer import ReplayBuffer, VectorReplayBuffer
 from tianshou_amd.env.synthetic import DeviceVectorEnv
@@ -45,6 +46,9 @@ class Collector:
         self.device = getattr(self._base, "device", None)
         self._assign_buffer(buffer)
         self._scratch = None
+        # vector steps per captured HIP graph (0 disables graph replay of the fused step)
+        self.graph_steps = 16
+        self._graph = None
         self.reset(False)
 
     def _assign_buffer(self, buffer) -> None:
@@ -192,15 +196,92 @@ class Collector:
         policy = result.get("policy", Batch())
         return act, policy
 
+    # -- fused device path ------------------------------------------------------------------
+    def _act_spec(self):
+        act_space = self._action_space
+        if hasattr(act_space, "n"):
+            return (), torch.int64
+        return tuple(act_space.shape), torch.float32
+
+    def _device_step(self, cur, kk, ids_t, random, no_grad, add_kw) -> None:
+        """All device work of one vector step: policy -> map_action -> env kernel (+ column
+        partials) -> obs_rms merge -> buffer add (+ fused obs_next normalisation) -> masked
+        reset (+ merge + normalisation).  No host synchronisation, so the sequence can be
+        captured in a HIP graph."""
+        s, b, buf = self._scratch, self._base, self.buffer
+        act_shape, act_dtype = self._act_spec()
+        info = Batch(env_id=s["env_id"][:kk] if ids_t is None else ids_t)
+        act, _policy = self._policy_act(cur, info, random, no_grad, kk)
+        act = act.to(act_dtype).reshape((kk,) + act_shape).contiguous()
+        action_remap = self.policy.map_action(act)
+        raw, rew = s["raw"][:kk], s["rew"][:kk]
+        term, trunc, done = s["term"][:kk], s["trunc"][:kk], s["done"][:kk]
+        b._step_raw(ids_t, kk, raw, rew, term, trunc, s["part"], action_remap)
+        norm = None
+        if self._norm is not None and not b.u8:
+            if self._norm.update_obs_rms:
+                self._norm.obs_rms.merge_partials(s["part"], b.nblk_for(kk), None, kk)
+            norm = self._norm.obs_rms
+        if b.u8:
+            buf._launch_add(ids=ids_t, k=kk, obs=cur, act=act, obs_next_raw=raw, rew=rew,
+                            term=term, trunc=trunc, **add_kw)
+            cur.copy_(raw)
+        else:
+            buf._launch_add(ids=ids_t, k=kk, obs=cur, act=act, obs_next=raw, cur_obs=cur,
+                            norm=norm, rew=rew, term=term, trunc=trunc, **add_kw)
+        if "rel_dev" in add_kw:
+            _C.check(_C.lib().tsrl_ring_advance(_C.ptr(add_kw["rel_dev"]), buf._ring.size,
+                                                _C.stream_ptr(b.device)), "tsrl_ring_advance")
+        torch.logical_or(term, trunc, out=done)
+        b._reset_raw(ids_t, done, kk, s["reset_raw"][:kk], s["part2"])
+        self._finish_obs(s["reset_raw"][:kk], cur, s["part2"], done, kk)
+
+    def _graph_key(self, G: int):
+        buf, b = self.buffer, self._base
+        ptrs = [t.data_ptr() for t in buf._meta.values() if isinstance(t, torch.Tensor)]
+        ptrs += [t.data_ptr() for t in buf._dev.values()]
+        ptrs += [b.ep_j.data_ptr(), b.ep_t.data_ptr()]
+        ptrs += [t.data_ptr() for t in self._scratch.values() if isinstance(t, torch.Tensor)]
+        ptrs += [p.data_ptr() for p in self.policy.parameters()]
+        if self._norm is not None:
+            r = self._norm.obs_rms
+            ptrs += [r.mean_t.data_ptr(), r.var_t.data_ptr(), r.count_t.data_ptr(),
+                     self._norm.update_obs_rms]
+        return (G, self.policy.training, self.exploration_noise, tuple(ptrs))
+
+    def _replay_steps(self, no_grad, n_steps: int, written: list) -> int:
+        """Run up to n_steps uniform steps as replays of a captured G-step HIP graph; returns
+        the number of steps done (the rest is left to the eager loop)."""
+        G = self.graph_steps
+        if n_steps < G:
+            return 0
+        buf, dev = self.buffer, self._base.device
+        key = self._graph_key(G)
+        if getattr(self, "_graph", None) is None or self._graph[0] != key:
+            rel_dev = torch.zeros(1, dtype=torch.int64, device=dev)
+            graph = torch.cuda.CUDAGraph()
+            torch.cuda.synchronize()
+            with torch.cuda.graph(graph):
+                for _ in range(G):
+                    self._device_step(self._scratch["cur"], self.env_num, None, False,
+                                      no_grad, dict(rel_dev=rel_dev))
+            self._graph = (key, graph, rel_dev)
+        _, graph, rel_dev = self._graph
+        rel_dev.fill_(int(buf._ring.index[0]))
+        done = 0
+        while n_steps - done >= G:
+            graph.replay()
+            for _ in range(G):
+                written.append(int(buf._ring.index[0]))
+                buf._ring.advance(None)
+            done += G
+        return done
+
     def _collect_fused(self, n_step, n_episode, random, no_grad):
         self._alloc_scratch()
         s, b, buf = self._scratch, self._base, self.buffer
         N = self.env_num
-        act_space = self._action_space
-        if hasattr(act_space, "n"):
-            act_shape, act_dtype = (), torch.int64
-        else:
-            act_shape, act_dtype = tuple(act_space.shape), torch.float32
+        act_shape, act_dtype = self._act_spec()
         buf._alloc_storage(b.obs_shape, b.obs_torch_dtype, act_shape, act_dtype)
         dev = buf.device
         # rows r < kk of the scratch arrays belong to env ready[r] (ready None: env r)
@@ -211,19 +292,16 @@ class Collector:
         step_count = episode_count = 0
         written = []          # per step: uniform ring position (int) or the ptr array
         ep_rows_host = []     # n_episode mode: finished rows in step order
+        eager_steps = 0
         while True:
-            info = Batch(env_id=s["env_id"][:kk] if ids_t is None else ids_t)
-            act, _policy = self._policy_act(cur, info, random, no_grad, kk)
-            act = act.to(act_dtype).reshape((kk,) + act_shape).contiguous()
-            action_remap = self.policy.map_action(act)
-            raw, rew = s["raw"][:kk], s["rew"][:kk]
-            term, trunc, done = s["term"][:kk], s["trunc"][:kk], s["done"][:kk]
-            b._step_raw(ids_t, kk, raw, rew, term, trunc, s["part"], action_remap)
-            norm = None
-            if self._norm is not None and not b.u8:
-                if self._norm.update_obs_rms:
-                    self._norm.obs_rms.merge_partials(s["part"], b.nblk_for(kk), None, kk)
-                norm = self._norm.obs_rms
+            if (n_step is not None and self.graph_steps and not random and kk == N
+                    and kk == buf.buffer_num and buf._ring.uniform_rel() is not None
+                    and eager_steps > 0 and not self.exploration_noise):
+                n_left = -(-(n_step - step_count) // N)
+                done_steps = self._replay_steps(no_grad, n_left, written)
+                step_count += done_steps * N
+                if step_count >= n_step:
+                    break
             ids_np = None if ready is None else ready
             uni = buf._ring.uniform_rel() if ids_np is None and kk == buf.buffer_num else None
             if ids_np is None and kk != buf.buffer_num:
@@ -236,19 +314,11 @@ class Collector:
                 kw = dict(ptr=torch.as_tensor(ptr, device=dev),
                           next_rel=torch.as_tensor(next_rel, device=dev))
                 written.append(np.asarray(ptr))
-            if b.u8:
-                buf._launch_add(ids=ids_t, k=kk, obs=cur, act=act, obs_next_raw=raw, rew=rew,
-                                term=term, trunc=trunc, **kw)
-                cur.copy_(raw)
-            else:
-                buf._launch_add(ids=ids_t, k=kk, obs=cur, act=act, obs_next=raw, cur_obs=cur,
-                                norm=norm, rew=rew, term=term, trunc=trunc, **kw)
-            torch.logical_or(term, trunc, out=done)
-            b._reset_raw(ids_t, done, kk, s["reset_raw"][:kk], s["part2"])
-            self._finish_obs(s["reset_raw"][:kk], cur, s["part2"], done, kk)
+            self._device_step(cur, kk, ids_t, random, no_grad, kw)
+            eager_steps += 1
             step_count += kk
             if n_episode:
-                done_np = done.cpu().numpy()
+                done_np = s["done"][:kk].cpu().numpy()
                 if done_np.any():
                     env_ind_local = np.flatnonzero(done_np)
                     episode_count += len(env_ind_local)

@@ -9,6 +9,19 @@ from tianshou_amd.policy.base import BasePolicy
 from tianshou_amd.utils.statistics import DeviceScalarRMS
 
 
+def make_dist(dist_fn, logits):
+    """dist_fn(*logits) without torch.distributions argument validation: its checks are
+    device reductions followed by a host-side ``if not valid.all()`` -- a device->host sync
+    per construction, i.e. per collector step.  (The reference validates; invalid
+    parameters here surface as NaN losses instead of ValueError.)"""
+    prev = torch.distributions.Distribution._validate_args
+    torch.distributions.Distribution.set_default_validate_args(False)
+    try:
+        return dist_fn(*logits) if isinstance(logits, tuple) else dist_fn(logits)
+    finally:
+        torch.distributions.Distribution.set_default_validate_args(prev)
+
+
 class PGPolicy(BasePolicy):
     def __init__(self, model: torch.nn.Module, optim: torch.optim.Optimizer,
                  dist_fn: Callable[..., torch.distributions.Distribution],
@@ -43,8 +56,21 @@ class PGPolicy(BasePolicy):
 
     def forward(self, batch: Batch, state=None, **kwargs: Any) -> Batch:
         """pg.py:133-171."""
+        if getattr(self, "_gauss_dist", False):
+            # ActorProb with state-independent sigma + Independent(Normal): sigma is
+            # exp(sigma_param) broadcast (continuous.py:229-233) and dist.sample() is
+            # torch.normal(mu, sigma) = standard normal * sigma + mu; written out directly,
+            # because torch.normal's tensor-std path checks std >= 0 with a host sync.
+            mu = self.actor.forward_mu(batch.obs)
+            sigma = self.actor.sigma_param.view(1, -1).exp().expand_as(mu)
+            dist = make_dist(self.dist_fn, (mu, sigma))
+            if self._deterministic_eval and not self.training:
+                act = mu
+            else:
+                act = torch.randn_like(mu).mul_(sigma).add_(mu)
+            return Batch(logits=(mu, sigma), act=act, state=state, dist=dist)
         logits, hidden = self.actor(batch.obs, state=state, info=batch.get("info", {}))
-        dist = self.dist_fn(*logits) if isinstance(logits, tuple) else self.dist_fn(logits)
+        dist = make_dist(self.dist_fn, logits)
         if self._deterministic_eval and not self.training:
             act = self._get_deterministic_action(logits)
         else:

@@ -119,6 +119,7 @@ class PPOPolicy(A2CPolicy):
         self.perm_device = perm_device
         self._fused = isinstance(actor, ActorProb) and not actor._c_sigma and \
             _is_fixed_std_normal(dist_fn)
+        self._gauss_dist = self._fused
 
     def _params(self, b_global: float) -> _C.PPOParams:
         p = _C.PPOParams()

@@ -53,6 +53,7 @@ class DeviceRunningMeanStd:
         self.mean_t = torch.zeros(self.dim, dtype=torch.float32, device=self.device)
         self.var_t = torch.ones(self.dim, dtype=torch.float32, device=self.device)
         self.count_t = torch.zeros(1, dtype=torch.float64, device=self.device)
+        self.ticket_t = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.clip_max = clip_max
         self.eps = epsilon
 
@@ -83,7 +84,8 @@ class DeviceRunningMeanStd:
         k = int(k if k is not None else (mask.numel() if mask is not None else 0))
         _C.check(_C.lib().tsrl_rms_merge(
             _C.ptr(partials), nblk, self.dim, _C.ptr(mask), k, _C.ptr(self.mean_t),
-            _C.ptr(self.var_t), _C.ptr(self.count_t), _C.stream_ptr()), "tsrl_rms_merge")
+            _C.ptr(self.var_t), _C.ptr(self.count_t), _C.ptr(self.ticket_t), _C.stream_ptr()),
+            "tsrl_rms_merge")
 
     def update(self, x: torch.Tensor, mask: Optional[torch.Tensor] = None) -> None:
         x = x.reshape(len(x), -1)
