@@ -153,6 +153,14 @@ def main():
     gae_ms = timer.mean_ms()
     gae_bytes = GAE_BYTES_PER_TRANSITION * n
     achieved = gae_bytes / (gae_ms * 1e-3) / 1e9
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "r01_gae_pmc.json")
+    if os.path.exists(pmc) and E == 4096 and T == 2048:
+        # HBM bytes per launch of the same kernel/shape from rocprofv3 --pmc FETCH_SIZE /
+        # WRITE_SIZE passes (FETCH doubled per the gfx950 calibration), committed under
+        # profiles/; PMC collection needs the profiler, so it is not re-measured here.
+        with open(pmc) as f:
+            traffic = json.load(f)["derived"]["traffic_bytes"]
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -183,7 +191,7 @@ def main():
                        "update_s": phase["update"] / args.steps},
             "roofline": {"kernel": "tsrl_gae (gae_rows_kernel)", "bound": "hbm",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "launch_us": gae_ms * 1e3,
                          "bytes_per_launch": gae_bytes},
             "cpu_baseline": cpu,

@@ -99,14 +99,15 @@ int tsrl_synth_u8_reset(const int64_t* ids, const uint8_t* mask, int64_t k,
  * RunningMeanStd, tianshou/utils/statistics.py:69-114).
  * rms_merge folds column partials of a batch of `count` rows (count = number of mask
  * bytes set, or k when mask == NULL; zero rows -> no update) into mean/var (f32 [dim])
- * and *count (f64 scalar on device).  `ticket` is a zero-initialised device word owned by
+ * and *count (f64 scalar on device).  A non-NULL batch_count (device f64) overrides the
+ * mask/k row count (data-parallel: partials and count summed over ranks).  `ticket` is a zero-initialised device word owned by
  * the statistics object (the last workgroup publishes the count and re-arms it; no host
  * state, so the call can be captured in a HIP graph).  rms_norm_rows writes
  * clip((x - mean) / sqrt(var + eps), +-clip) for rows with mask[r] (all when NULL).
  * ------------------------------------------------------------------------------- */
 int tsrl_rms_merge(const double* col_partials, int64_t nblk, int64_t dim,
-                   const uint8_t* mask, int64_t k, float* mean, float* var, double* count,
-                   unsigned int* ticket, void* stream);
+                   const uint8_t* mask, int64_t k, const double* batch_count, float* mean,
+                   float* var, double* count, unsigned int* ticket, void* stream);
 int tsrl_rms_norm_rows(const float* x, const uint8_t* mask, int64_t k, int64_t dim,
                        const float* mean, const float* var, float eps, float clip,
                        float* out, void* stream);

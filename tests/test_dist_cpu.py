@@ -1,0 +1,81 @@
+"""Data-parallel host logic on CPU with a world_size-2 gloo group (no GPU): gradient
+all-reduce (sum and average), all_gather_cat order, and the scaling convention the fused PPO
+loss relies on -- per-rank sums divided by the GLOBAL minibatch size, then summed across
+ranks -- reproduces the single-process full-batch gradient."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out):
+    import sys
+    from tests.conftest import PKG, ROOT
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from tianshou_amd.dist import DataParallel
+    dp = DataParallel()
+    assert dp.active and dp.world == world and dp.rank == rank
+    # all_gather_cat keeps rank order
+    g = dp.all_gather_cat(torch.tensor([float(rank), rank + 0.5]))
+    assert g.tolist() == [0.0, 0.5, 1.0, 1.5]
+    # gradient all-reduce: global-mean convention
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(7, 16), torch.nn.Tanh(), torch.nn.Linear(16, 3))
+    x = torch.randn(64, 7, generator=torch.Generator().manual_seed(1))
+    y = torch.randn(64, 3, generator=torch.Generator().manual_seed(2))
+    xs, ys = x[rank::world], y[rank::world]
+    b_global = y.numel()  # elements of the global minibatch the mean runs over
+    loss = ((net(xs) - ys) ** 2).sum() / b_global  # per-rank sum / global count
+    loss.backward()
+    dp.all_reduce_grads_(net.parameters())
+    grads_sum = [p.grad.clone() for p in net.parameters()]
+    for p in net.parameters():
+        p.grad = None
+    ((net(xs) - ys) ** 2).mean().backward()          # per-rank mean -> average
+    dp.all_reduce_grads_(net.parameters(), average=True)
+    grads_avg = [p.grad.clone() for p in net.parameters()]
+    # advantage moments: (sum, sumsq) all-reduced == full-batch moments
+    a = torch.randn(64, dtype=torch.float64, generator=torch.Generator().manual_seed(3))
+    mine = a[rank::world]
+    sums = dp.all_reduce_(torch.stack([mine.sum(), (mine * mine).sum()]))
+    out[rank] = (grads_sum, grads_avg, sums)
+    dist.destroy_process_group()
+
+
+def test_data_parallel_gloo_two_ranks():
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(2, port, out), nprocs=2, join=True)
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(7, 16), torch.nn.Tanh(), torch.nn.Linear(16, 3))
+    x = torch.randn(64, 7, generator=torch.Generator().manual_seed(1))
+    y = torch.randn(64, 3, generator=torch.Generator().manual_seed(2))
+    ((net(x) - y) ** 2).mean().backward()
+    full = [p.grad for p in net.parameters()]
+    for r in range(2):
+        gs, ga, sums = out[r]
+        for a, b in zip(gs, full):
+            np.testing.assert_allclose(a.numpy(), b.numpy(), rtol=1e-5, atol=1e-7)
+        for a, b in zip(ga, full):  # equal shards: mean of means == global mean
+            np.testing.assert_allclose(a.numpy(), b.numpy(), rtol=1e-5, atol=1e-7)
+        a = torch.randn(64, dtype=torch.float64, generator=torch.Generator().manual_seed(3))
+        np.testing.assert_allclose(sums.numpy(), [a.sum().item(), (a * a).sum().item()],
+                                   rtol=1e-12)

@@ -1,0 +1,59 @@
+"""Data-parallel (env-sharded) PPO update with 2 ranks on one MI355X over gloo: one global
+minibatch split across ranks must give the single-process full-batch update (up to
+summation order), and sync_obs_rms must leave both ranks with identical global statistics.
+
+Runs first among the GPU tests (file name) so that this pytest process has not initialised
+HIP when it starts the rank processes."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from tests.conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_two_rank_update_matches_single_process(tmp_path):
+    port = str(_free_port())
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "dist_worker.py"),
+                               str(r), "2", port, str(tmp_path)], env=env)
+             for r in range(2)]
+    rcs = [p.wait(timeout=240) for p in procs]
+    assert rcs == [0, 0], rcs
+    r0 = torch.load(tmp_path / "rank0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "rank1.pt", weights_only=True)
+    # identical parameters on both ranks
+    for k in r0["sd"]:
+        assert torch.equal(r0["sd"][k], r1["sd"][k]), k
+    np.testing.assert_allclose(r0["loss"].numpy(), r1["loss"].numpy(), rtol=1e-6)
+    # global obs_rms identical on both ranks, counting both shards' rows
+    assert torch.equal(r0["rms_mean"], r1["rms_mean"])
+    assert torch.equal(r0["rms_var"], r1["rms_var"])
+    assert int(r0["rms_count"]) == int(r1["rms_count"]) > 0
+    # single-process reference: the whole batch as one minibatch
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import dist_worker as w
+    dev = torch.device("cuda", 0)
+    data = w.make_data(4096, 23, 5, dev)
+    policy = w.build_policy(23, 5, dev)
+    from tianshou_amd.data import Batch
+    np.random.seed(0)
+    res = policy.learn(Batch(**data), batch_size=4096, repeat=1)
+    np.testing.assert_allclose(r0["loss"].numpy(), res["loss"], rtol=1e-4, atol=1e-6)
+    sd = policy.state_dict()
+    for k, v in r0["sd"].items():
+        np.testing.assert_allclose(v.numpy(), sd[k].cpu().numpy(), rtol=1e-4, atol=1e-6)

@@ -118,3 +118,15 @@ def test_product_refuses_cpu_tensors():
     from tianshou_amd import _C
     with pytest.raises(_C.TsrlError):
         _C.ptr(torch.zeros(3))
+
+
+def test_device_stats_construct_without_gpu_use():
+    """Host-side state of the device statistics objects (constructed on CPU tensors; no
+    kernel is launched)."""
+    from tianshou_amd.utils.statistics import DeviceRunningMeanStd, DeviceScalarRMS
+    r = DeviceRunningMeanStd(4, "cpu")
+    assert r.dp is None and r.count == 0 and r.mean.tolist() == [0.0] * 4
+    r.sync_with("dp")
+    assert r.dp == "dp"
+    s = DeviceScalarRMS("cpu")
+    assert (s.mean, s.var, s.count) == (0.0, 1.0, 0)

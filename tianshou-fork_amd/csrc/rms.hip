@@ -20,7 +20,7 @@ constexpr int MLANES = 16;
 
 __global__ __launch_bounds__(MCOLS * MLANES) void rms_merge_kernel(
     const double* partials, int64_t nblk, int64_t dim, const uint8_t* mask, int64_t k,
-    float* mean, float* var, double* count, unsigned int* ticket) {
+    const double* batch_count, float* mean, float* var, double* count, unsigned int* ticket) {
     __shared__ double sh_s[MLANES][MCOLS];
     __shared__ double sh_ss[MLANES][MCOLS];
     __shared__ double sh_cnt[MCOLS * MLANES / kWave];
@@ -40,6 +40,7 @@ __global__ __launch_bounds__(MCOLS * MLANES) void rms_merge_kernel(
     __syncthreads();
     double bc = 0.0;
     for (int w = 0; w < MCOLS * MLANES / kWave; ++w) bc += sh_cnt[w];
+    if (batch_count) bc = *batch_count;  // e.g. summed over data-parallel ranks
     const double tot = old_count + bc;
     const int64_t d = (int64_t)blockIdx.x * MCOLS + col;
     double s0 = 0.0, s1 = 0.0, q0 = 0.0, q1 = 0.0;
@@ -116,8 +117,9 @@ __global__ __launch_bounds__(TPB) void rms_norm_kernel(const float* x, const uin
 using namespace tsrl;
 
 extern "C" int tsrl_rms_merge(const double* col_partials, int64_t nblk, int64_t dim,
-                              const uint8_t* mask, int64_t k, float* mean, float* var,
-                              double* count, unsigned int* ticket, void* stream) {
+                              const uint8_t* mask, int64_t k, const double* batch_count,
+                              float* mean, float* var, double* count, unsigned int* ticket,
+                              void* stream) {
     TSRL_CHECK_ARG(col_partials && mean && var && count && ticket && dim > 0 && nblk >= 0 &&
                        k >= 0,
                    "tsrl_rms_merge: bad arguments");
@@ -125,8 +127,8 @@ extern "C" int tsrl_rms_merge(const double* col_partials, int64_t nblk, int64_t 
     if (k == 0) return 0;
     const int64_t grid = (dim + MCOLS - 1) / MCOLS;
     hipLaunchKernelGGL(rms_merge_kernel, dim3((unsigned)grid), dim3(MCOLS * MLANES), 0,
-                       as_stream(stream), col_partials, nblk, dim, mask, k, mean, var, count,
-                       ticket);
+                       as_stream(stream), col_partials, nblk, dim, mask, k, batch_count, mean,
+                       var, count, ticket);
     TSRL_LAUNCH_CHECK("tsrl_rms_merge");
     return 0;
 }

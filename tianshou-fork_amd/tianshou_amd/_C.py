@@ -62,7 +62,7 @@ _SIGS = {
     "tsrl_synth_u8_step": ([_p, _i64, _i64, _u64, _i64, _p, _p, _p, _p, _p, _p, _p],
                            ctypes.c_int),
     "tsrl_synth_u8_reset": ([_p, _p, _i64, _i64, _u64, _i64, _p, _p, _p, _p], ctypes.c_int),
-    "tsrl_rms_merge": ([_p, _i64, _i64, _p, _i64, _p, _p, _p, _p, _p], ctypes.c_int),
+    "tsrl_rms_merge": ([_p, _i64, _i64, _p, _i64, _p, _p, _p, _p, _p, _p], ctypes.c_int),
     "tsrl_rms_norm_rows": ([_p, _p, _i64, _i64, _p, _p, _f, _f, _p, _p], ctypes.c_int),
     "tsrl_buffer_add": ([ctypes.POINTER(AddArgs), _p], ctypes.c_int),
     "tsrl_ring_advance": ([_p, _i64, _p], ctypes.c_int),

@@ -33,7 +33,11 @@ def _empty_data() -> Batch:
 class Collector:
     def __init__(self, policy, env, buffer: Optional[ReplayBuffer] = None,
                  preprocess_fn: Optional[Callable[..., Batch]] = None,
-                 exploration_noise: bool = False) -> None:
+                 exploration_noise: bool = False, sync_obs_rms: bool = False) -> None:
+        """``sync_obs_rms`` (data-parallel runs only): keep ONE global VectorEnvNormObs
+        statistic across ranks (an all-reduce of the batch moments per env step; the fused
+        step then runs eagerly, without HIP-graph replay).  Default: each rank's env shard
+        normalises with its own running statistics."""
         self.env = env
         self.env_num = len(env)
         self.exploration_noise = exploration_noise
@@ -49,6 +53,11 @@ class Collector:
         # vector steps per captured HIP graph (0 disables graph replay of the fused step)
         self.graph_steps = 16
         self._graph = None
+        from tianshou_amd.dist import default_dp
+        self.dp = default_dp()
+        if sync_obs_rms and self.dp.active and self._norm is not None:
+            self._norm.obs_rms.sync_with(self.dp)
+            self.graph_steps = 0
         self.reset(False)
 
     def _assign_buffer(self, buffer) -> None:

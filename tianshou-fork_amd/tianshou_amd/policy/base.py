@@ -40,15 +40,17 @@ def gae_device(v_s: torch.Tensor, v_s_: torch.Tensor, rew: torch.Tensor, term: t
     L = _C.lib()
     ws_bytes = int(L.tsrl_gae_workspace_bytes(n, row_len))
     ws = torch.empty(max(ws_bytes, 8), dtype=torch.uint8, device=dev) if ws_bytes else None
+    args = (_C.ptr(v_s), _C.ptr(v_s_), _C.ptr(rew), _C.ptr(term), _C.ptr(trunc),
+            _C.ptr(end_extra), n, row_len, _C.ptr(value_scale), float(gamma),
+            float(gae_lambda), _C.ptr(adv32), _C.ptr(ret32), _C.ptr(adv64), _C.ptr(ret64),
+            _C.ptr(ret_partials), _C.ptr(ws), ws_bytes, _C.stream_ptr(dev))
+    fn = L.tsrl_gae
     if GAE_HOOK is not None:
         GAE_HOOK("start", n)
-    _C.check(L.tsrl_gae(_C.ptr(v_s), _C.ptr(v_s_), _C.ptr(rew), _C.ptr(term), _C.ptr(trunc),
-                        _C.ptr(end_extra), n, row_len, _C.ptr(value_scale), float(gamma),
-                        float(gae_lambda), _C.ptr(adv32), _C.ptr(ret32), _C.ptr(adv64),
-                        _C.ptr(ret64), _C.ptr(ret_partials), _C.ptr(ws), ws_bytes,
-                        _C.stream_ptr(dev)), "tsrl_gae")
+    rc = fn(*args)
     if GAE_HOOK is not None:
         GAE_HOOK("end", n)
+    _C.check(rc, "tsrl_gae")
     return adv32, ret32, adv64, ret64
 
 

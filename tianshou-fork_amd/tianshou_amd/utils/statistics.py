@@ -56,6 +56,10 @@ class DeviceRunningMeanStd:
         self.ticket_t = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.clip_max = clip_max
         self.eps = epsilon
+        self.dp = None  # tianshou_amd.dist.DataParallel: sync the moments over ranks
+
+    def sync_with(self, dp) -> None:
+        self.dp = dp
 
     # -- reference-compatible views (sync on access) ------------------------------------
     @property
@@ -80,12 +84,27 @@ class DeviceRunningMeanStd:
 
     # -- device operations ---------------------------------------------------------------
     def merge_partials(self, partials: torch.Tensor, nblk: int, mask=None, k=None) -> None:
-        """Fold env-kernel column partials ([nblk, dim, 2] f64) of k rows (mask-selected)."""
+        """Fold env-kernel column partials ([nblk, dim, 2] f64) of k rows (mask-selected).
+        With ``self.dp`` active the batch moments and row count are first summed over the
+        data-parallel ranks (one all-reduce), so every rank holds the global statistics the
+        reference's single VectorEnvNormObs would (venv_wrappers.py:93-99)."""
         k = int(k if k is not None else (mask.numel() if mask is not None else 0))
+        batch_count = None
+        if self.dp is not None and self.dp.active:
+            buf = torch.empty(2 * self.dim + 1, dtype=torch.float64, device=self.device)
+            buf[:2 * self.dim] = partials[:nblk].sum(0).reshape(-1)
+            if mask is not None:
+                buf[2 * self.dim] = mask[:k].sum()
+            else:
+                buf[2 * self.dim] = float(k)
+            self.dp.all_reduce_(buf)
+            partials, nblk, mask = buf[:2 * self.dim].reshape(1, self.dim, 2), 1, None
+            batch_count = buf[2 * self.dim:]
+            k = max(k, 1)
         _C.check(_C.lib().tsrl_rms_merge(
-            _C.ptr(partials), nblk, self.dim, _C.ptr(mask), k, _C.ptr(self.mean_t),
-            _C.ptr(self.var_t), _C.ptr(self.count_t), _C.ptr(self.ticket_t), _C.stream_ptr()),
-            "tsrl_rms_merge")
+            _C.ptr(partials), nblk, self.dim, _C.ptr(mask), k, _C.ptr(batch_count),
+            _C.ptr(self.mean_t), _C.ptr(self.var_t), _C.ptr(self.count_t),
+            _C.ptr(self.ticket_t), _C.stream_ptr()), "tsrl_rms_merge")
 
     def update(self, x: torch.Tensor, mask: Optional[torch.Tensor] = None) -> None:
         x = x.reshape(len(x), -1)
