@@ -213,6 +213,50 @@ int tsrl_ppo_gauss_finalize(const double* sums, int64_t act_dim, const float* lo
 int tsrl_gauss_logp(const float* mu, const float* log_std, const float* act, int64_t b,
                     int64_t act_dim, float* out, void* stream);
 
+/* ---------------------------------------------------------------------------------
+ * Fused actor/critic MLP of the PPO minibatch for the MuJoCo network shape
+ * (tianshou/utils/models.py:34-97: Net(D, (64, 64), Tanh) trunks, ActorProb mu head
+ * Linear(64, A) unbounded, Critic head Linear(64, 1)); replaces the per-layer nn.Linear /
+ * nn.Tanh forward and autograd backward of ppo.py:121-146 (utils/net/common.py:56-150,
+ * continuous.py:87-235).
+ *
+ * tsrl_mlp_l1_fwd: H1 = act(X[idx] W^T + b) for the stacked first layers (Wa, ba: actor
+ *   [64, D]; Wc, bc: critic [64, D]) -> 128 features per row.  frag_out = 1 writes the MFMA
+ *   fragment layout consumed by tsrl_ppo_tail (tsrl_mlp_frag_floats(n) floats); 0 writes
+ *   row-major [n, 128].  D and ldx multiples of 4, 16-byte aligned X / W / out.
+ * tsrl_ppo_tail: layers 2-3 of both nets, the PPO loss of tsrl_ppo_gauss_fwd_bwd and the
+ *   backward to dZ1 [n, 128] (row-major), writing the layer-2/3 parameter gradients of the
+ *   mean loss and the loss sums [4 + A] (layout of tsrl_ppo_gauss_finalize's input).
+ * tsrl_mlp_dw: first-layer gradients dW = dZ1^T X[idx], db = column sums of dZ1.
+ * ------------------------------------------------------------------------------- */
+typedef struct tsrl_tail_weights {
+    const float *w2a, *b2a;   /* actor layer 2 [64,64], [64] */
+    const float *w2c, *b2c;   /* critic layer 2 */
+    const float *w3a, *b3a;   /* actor mu head [A,64], [A] */
+    const float *w3c, *b3c;   /* critic head [1,64], [1] */
+    const float *log_std;     /* [A] (sigma_param) */
+} tsrl_tail_weights;
+
+typedef struct tsrl_tail_grads {
+    float *w2a, *b2a, *w2c, *b2c, *w3a, *b3a, *w3c, *b3c;
+} tsrl_tail_grads;
+
+int tsrl_mlp_l1_fwd(const float* X, int64_t ldx, const int64_t* idx, int64_t n, int64_t D,
+                    const float* Wa, const float* ba, const float* Wc, const float* bc,
+                    int act_tanh, float* out, int frag_out, void* stream);
+int64_t tsrl_mlp_frag_floats(int64_t n);
+int64_t tsrl_ppo_tail_workspace_bytes(int64_t n);
+int tsrl_ppo_tail(const float* h1frag, int64_t n, const int64_t* idx,
+                  const tsrl_tail_weights* w, int64_t act_dim, const float* act,
+                  const float* logp_old, const float* adv, const float* ret, const float* v_s,
+                  const double* adv_sums, tsrl_ppo_params p, float* dz1,
+                  const tsrl_tail_grads* grads, double* sums, void* workspace,
+                  int64_t ws_bytes, void* stream);
+int64_t tsrl_mlp_dw_workspace_bytes(int64_t n, int64_t D);
+int tsrl_mlp_dw(const float* dz1, const float* X, int64_t ldx, const int64_t* idx, int64_t n,
+                int64_t D, float* gWa, float* gba, float* gWc, float* gbc, void* workspace,
+                int64_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -55,5 +55,7 @@ def test_two_rank_update_matches_single_process(tmp_path):
     res = policy.learn(Batch(**data), batch_size=4096, repeat=1)
     np.testing.assert_allclose(r0["loss"].numpy(), res["loss"], rtol=1e-4, atol=1e-6)
     sd = policy.state_dict()
+    # one Adam step moves a weight by up to lr = 3e-4 whatever its gradient's size, so a
+    # near-zero gradient summed in another order can move it differently: atol = lr / 3
     for k, v in r0["sd"].items():
-        np.testing.assert_allclose(v.numpy(), sd[k].cpu().numpy(), rtol=1e-4, atol=1e-6)
+        np.testing.assert_allclose(v.numpy(), sd[k].cpu().numpy(), rtol=1e-4, atol=1e-4)

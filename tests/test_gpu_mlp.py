@@ -1,0 +1,216 @@
+"""Fused actor/critic MLP kernels (csrc/mlp.hip) vs PyTorch.
+
+* tsrl_mlp_l1_fwd vs torch fp32 (both output layouts), rtol 1e-5 / atol 1e-5.
+* One whole PPO minibatch (forward, loss, backward of both nets) vs a float64 CPU autograd
+  restatement of ppo.py:121-142 on the same weights: the fused f32 gradients must be as
+  accurate as torch's own f32 GPU autograd of the same graph (relative L2 error within 4x
+  of torch's, or below 2e-6), loss terms rtol 1e-5.
+* PPOPolicy.learn with and without the fused MLP: same losses (rtol 1e-4) and parameters
+  (atol 2e-3 after Adam, which turns noise-level gradient differences into lr-sized steps).
+"""
+import copy
+
+import numpy as np
+import pytest
+import torch
+from torch.distributions import Independent, Normal
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    return torch.device("cuda", 0)
+
+
+def _rho(r):
+    return (r & 3) + 8 * (r >> 2)
+
+
+def frag_to_rows(frag, n, nt=4):
+    """[row tile][feature tile][lane][16] MFMA-fragment layout -> [n, 32*nt]."""
+    ntile = (n + 31) // 32
+    f = frag[:ntile * nt * 64 * 16].view(ntile, nt, 64, 16).cpu()
+    out = torch.empty(ntile * 32, nt * 32)
+    lane = torch.arange(64)
+    for r in range(16):
+        feat = _rho(r) + 4 * (lane >> 5)
+        rows = lane & 31
+        for ft in range(nt):
+            out[(torch.arange(ntile)[:, None] * 32 + rows[None, :]).reshape(-1),
+                (32 * ft + feat).repeat(ntile)] = f[:, ft, :, r].reshape(-1)
+    return out[:n]
+
+
+def _nets(D, A, dev, seed):
+    from tianshou_amd.utils.models import get_actor_critic, init_actor_critic
+    torch.manual_seed(seed)
+    actor, critic = get_actor_critic((D,), (64, 64), (A,), dev)
+    actor, critic = actor.to(dev), critic.to(dev)
+    init_actor_critic(actor, critic)
+    with torch.no_grad():
+        for p in list(actor.parameters()) + list(critic.parameters()):
+            p.add_(0.02 * torch.randn_like(p))
+    return actor, critic
+
+
+@pytest.mark.parametrize("D,n", [(376, 1000), (24, 4096), (8, 33), (128, 128)])
+def test_l1_fwd_matches_torch(dev, D, n):
+    from tianshou_amd import _C
+    g = torch.Generator().manual_seed(D + n)
+    N = n + 50
+    X = torch.randn(N, D, generator=g).to(dev)
+    idx = torch.randperm(N, generator=g)[:n].to(dev)
+    Wa, Wc = torch.randn(64, D, generator=g).to(dev) * 0.1, torch.randn(64, D, generator=g).to(dev) * 0.1
+    ba, bc = torch.randn(64, generator=g).to(dev), torch.randn(64, generator=g).to(dev)
+    L = _C.lib()
+    s = _C.stream_ptr(dev)
+    want = torch.tanh(X[idx] @ torch.cat([Wa, Wc]).T + torch.cat([ba, bc]))
+    rows = torch.empty(n, 128, device=dev)
+    _C.check(L.tsrl_mlp_l1_fwd(_C.ptr(X), D, _C.ptr(idx), n, D, _C.ptr(Wa), _C.ptr(ba),
+                               _C.ptr(Wc), _C.ptr(bc), 1, _C.ptr(rows), 0, s))
+    frag = torch.empty(int(L.tsrl_mlp_frag_floats(n)), device=dev)
+    _C.check(L.tsrl_mlp_l1_fwd(_C.ptr(X), D, _C.ptr(idx), n, D, _C.ptr(Wa), _C.ptr(ba),
+                               _C.ptr(Wc), _C.ptr(bc), 1, _C.ptr(frag), 1, s))
+    lin = torch.empty(n, 128, device=dev)
+    _C.check(L.tsrl_mlp_l1_fwd(_C.ptr(X), D, None, n, D, _C.ptr(Wa), _C.ptr(ba),
+                               _C.ptr(Wc), _C.ptr(bc), 0, _C.ptr(lin), 0, s))
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(rows.cpu(), want.cpu(), rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(frag_to_rows(frag, n), want.cpu(), rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(lin.cpu(), (X[:n] @ torch.cat([Wa, Wc]).T +
+                                           torch.cat([ba, bc])).cpu(), rtol=1e-5, atol=1e-5)
+
+
+def _ref_minibatch(W, obs, act, logp_old, adv, ret, v_s, kw, dtype, device):
+    """ppo.py:121-142 on the functional form of get_actor_critic's networks."""
+    P = {k: v.detach().to(device, dtype).clone().requires_grad_(True) for k, v in W.items()}
+    x = obs.to(device, dtype)
+    c = lambda t: t.to(device, dtype)  # noqa: E731
+    ha = torch.tanh(torch.tanh(x @ P["w1a"].T + P["b1a"]) @ P["w2a"].T + P["b2a"])
+    mu = ha @ P["w3a"].T + P["b3a"]
+    hc = torch.tanh(torch.tanh(x @ P["w1c"].T + P["b1c"]) @ P["w2c"].T + P["b2c"])
+    value = (hc @ P["w3c"].T + P["b3c"]).flatten()
+    sigma = (P["sigma"].view(1, -1) + torch.zeros_like(mu)).exp()
+    dist = Independent(Normal(mu, sigma), 1)
+    adv = c(adv)
+    if kw.get("norm_adv", True):
+        adv = (adv - adv.mean()) / (adv.std() + 1e-8)
+    eps_clip = kw.get("eps_clip", 0.2)
+    ratio = (dist.log_prob(c(act)) - c(logp_old)).exp()
+    surr1 = ratio * adv
+    surr2 = ratio.clamp(1.0 - eps_clip, 1.0 + eps_clip) * adv
+    if kw.get("dual_clip"):
+        clip1 = torch.min(surr1, surr2)
+        clip2 = torch.max(clip1, kw["dual_clip"] * adv)
+        clip_loss = -torch.where(adv < 0, clip2, clip1).mean()
+    else:
+        clip_loss = -torch.min(surr1, surr2).mean()
+    ret, v_s = c(ret), c(v_s)
+    if kw.get("value_clip"):
+        v_clip = v_s + (value - v_s).clamp(-eps_clip, eps_clip)
+        vf_loss = torch.max((ret - value).pow(2), (ret - v_clip).pow(2)).mean()
+    else:
+        vf_loss = (ret - value).pow(2).mean()
+    ent = dist.entropy().mean()
+    loss = clip_loss + kw.get("vf_coef", 0.25) * vf_loss - kw.get("ent_coef", 0.01) * ent
+    loss.backward()
+    terms = torch.stack([loss, clip_loss, vf_loss, ent]).detach().cpu().double()
+    return terms, {k: v.grad.detach().cpu().double() for k, v in P.items()}
+
+
+CASES = [
+    (376, 17, 4096, {}),
+    (24, 5, 1000, dict(dual_clip=3.0)),
+    (8, 1, 257, dict(value_clip=True)),
+    (376, 17, 2048, dict(norm_adv=False, ent_coef=0.0)),
+    (64, 32, 4096, dict(dual_clip=5.0, value_clip=True, eps_clip=0.1, ent_coef=0.05)),
+]
+
+
+@pytest.mark.parametrize("D,A,B,kw", CASES)
+def test_fused_minibatch_matches_autograd(dev, D, A, B, kw):
+    from tianshou_amd import _C
+    from tianshou_amd.dist import DataParallel
+    from tianshou_amd.policy import fused_mlp
+    from tianshou_amd.utils.net import ActorCritic
+    actor, critic = _nets(D, A, dev, D + A + B)
+    layers = fused_mlp.match(actor, critic)
+    assert layers is not None
+    fm = fused_mlp.FusedActorCritic(layers, ActorCritic(actor, critic).parameters())
+    g = torch.Generator().manual_seed(B)
+    n = B + 101
+    obs = torch.randn(n, D, generator=g).to(dev)
+    act = torch.randn(n, A, generator=g).to(dev)
+    adv = (torch.randn(n, generator=g) * 2 + 0.3).to(dev)
+    ret = torch.randn(n, generator=g).to(dev)
+    v_s = (ret.cpu() + torch.randn(n, generator=g) * 0.3).to(dev)
+    idx = torch.randperm(n, generator=g)[:B].to(dev)
+    with torch.no_grad():
+        mu = actor.forward_mu(obs)
+        lp = Independent(Normal(mu, actor.sigma_param.view(1, -1).exp().expand_as(mu)),
+                         1).log_prob(act)
+        logp_old = (lp + 0.2 * torch.randn(n, generator=g).to(dev)).contiguous()
+    W = {"w1a": layers["w1a"].weight, "b1a": layers["w1a"].bias,
+         "w2a": layers["w2a"].weight, "b2a": layers["w2a"].bias,
+         "w3a": layers["w3a"].weight, "b3a": layers["w3a"].bias,
+         "w1c": layers["w1c"].weight, "b1c": layers["w1c"].bias,
+         "w2c": layers["w2c"].weight, "b2c": layers["w2c"].bias,
+         "w3c": layers["w3c"].weight, "b3c": layers["w3c"].bias,
+         "sigma": layers["sigma"]}
+    p = _C.PPOParams()
+    p.eps_clip = kw.get("eps_clip", 0.2)
+    p.dual_clip = kw.get("dual_clip") or 0.0
+    p.vf_coef = kw.get("vf_coef", 0.25)
+    p.ent_coef = kw.get("ent_coef", 0.01)
+    p.adv_eps = 1e-8
+    p.b_global = float(B)
+    p.value_clip = int(bool(kw.get("value_clip")))
+    p.norm_adv = int(kw.get("norm_adv", True))
+    terms = fm.minibatch(obs, idx, B, act, logp_old, adv, ret, v_s, p, DataParallel())
+    torch.cuda.synchronize()
+    got = {k: v.grad.detach().cpu().double() for k, v in W.items()}
+    mb = [t[idx] for t in (obs, act, logp_old, adv, ret, v_s)]
+    t64, g64 = _ref_minibatch(W, *mb, kw, torch.float64, "cpu")
+    t32, g32 = _ref_minibatch(W, *mb, kw, torch.float32, dev)
+    np.testing.assert_allclose(terms.cpu().double().numpy(), t64.numpy(), rtol=1e-5, atol=1e-6)
+    for k in W:
+        ref = g64[k]
+        den = ref.norm().item() + 1e-30
+        e_fused = (got[k] - ref).norm().item() / den
+        e_torch = (g32[k] - ref).norm().item() / den
+        assert e_fused <= max(4 * e_torch, 2e-6), (k, e_fused, e_torch)
+
+
+@pytest.mark.parametrize("value_clip", [False, True])
+def test_learn_fused_mlp_vs_layers(dev, value_clip):
+    from tianshou_amd.data import Batch
+    from tianshou_amd.env import Box
+    from tianshou_amd.policy import PPOPolicy
+    from tianshou_amd.utils.models import fixed_std_normal
+    D, A, n = 40, 6, 3000
+    base_a, base_c = _nets(D, A, dev, 5)
+    res, states = [], []
+    for fused in (True, False):
+        actor, critic = copy.deepcopy(base_a), copy.deepcopy(base_c)
+        params = list(actor.parameters()) + [p for p in critic.parameters()
+                                             if all(p is not q for q in actor.parameters())]
+        optim = torch.optim.Adam(params, lr=3e-4)
+        pol = PPOPolicy(actor, critic, optim, fixed_std_normal, action_space=Box(-1.0, 1.0, (A,)),
+                        max_grad_norm=0.5, vf_coef=0.25, ent_coef=0.01, value_clip=value_clip,
+                        fused_mlp=fused)
+        assert (pol._mlp is not None) == fused
+        g = torch.Generator().manual_seed(1)
+        data = dict(obs=torch.randn(n, D, generator=g), act=torch.randn(n, A, generator=g),
+                    logp_old=torch.randn(n, generator=g) * 0.2 - A * 1.2,
+                    adv=torch.randn(n, generator=g), returns=torch.randn(n, generator=g))
+        data["v_s"] = data["returns"] + 0.3 * torch.randn(n, generator=g)
+        batch = Batch(**{k: v.to(dev) for k, v in data.items()})
+        np.random.seed(3)
+        res.append(pol.learn(batch, batch_size=512, repeat=2))
+        states.append({k: v.detach().cpu() for k, v in pol.state_dict().items()})
+    for k in res[0]:
+        np.testing.assert_allclose(res[0][k], res[1][k], rtol=1e-4, atol=1e-5, err_msg=k)
+    for k in states[0]:
+        np.testing.assert_allclose(states[0][k].numpy(), states[1][k].numpy(), rtol=1e-3,
+                                   atol=2e-3, err_msg=k)

@@ -45,6 +45,17 @@ class PPOParams(ctypes.Structure):
     ]
 
 
+class TailWeights(ctypes.Structure):
+    """Mirror of ``tsrl_tail_weights``."""
+    _fields_ = [(k, _p) for k in ("w2a", "b2a", "w2c", "b2c", "w3a", "b3a", "w3c", "b3c",
+                                  "log_std")]
+
+
+class TailGrads(ctypes.Structure):
+    """Mirror of ``tsrl_tail_grads``."""
+    _fields_ = [(k, _p) for k in ("w2a", "b2a", "w2c", "b2c", "w3a", "b3a", "w3c", "b3c")]
+
+
 _SIGS = {
     "tsrl_version": ([], ctypes.c_char_p),
     "tsrl_last_error": ([], ctypes.c_char_p),
@@ -76,6 +87,15 @@ _SIGS = {
                                 _p, _p, _p, _p], ctypes.c_int),
     "tsrl_ppo_gauss_finalize": ([_p, _i64, _p, PPOParams, _p, _p, _p], ctypes.c_int),
     "tsrl_gauss_logp": ([_p, _p, _p, _i64, _i64, _p, _p], ctypes.c_int),
+    "tsrl_mlp_l1_fwd": ([_p, _i64, _p, _i64, _i64, _p, _p, _p, _p, ctypes.c_int, _p,
+                         ctypes.c_int, _p], ctypes.c_int),
+    "tsrl_mlp_frag_floats": ([_i64], _i64),
+    "tsrl_ppo_tail_workspace_bytes": ([_i64], _i64),
+    "tsrl_ppo_tail": ([_p, _i64, _p, ctypes.POINTER(TailWeights), _i64, _p, _p, _p, _p, _p, _p,
+                       PPOParams, _p, ctypes.POINTER(TailGrads), _p, _p, _i64, _p],
+                      ctypes.c_int),
+    "tsrl_mlp_dw_workspace_bytes": ([_i64, _i64], _i64),
+    "tsrl_mlp_dw": ([_p, _p, _i64, _p, _i64, _i64, _p, _p, _p, _p, _p, _i64, _p], ctypes.c_int),
 }
 
 EXPORTED = tuple(_SIGS)

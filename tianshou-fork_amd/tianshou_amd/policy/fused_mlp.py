@@ -1,0 +1,177 @@
+"""One PPO minibatch of the MuJoCo actor/critic shape through the fused MLP kernels.
+
+The networks of tianshou/utils/models.py:34-97 (``get_actor_critic``: two
+``Net(D, (64, 64), Tanh)`` trunks, an unbounded ``ActorProb`` mu head ``Linear(64, A)`` with a
+state-independent log-std, a ``Critic`` head ``Linear(64, 1)``) are run as three HIP kernels per
+minibatch instead of ~60 framework ops (include/tsrl.h, csrc/mlp.hip):
+
+1. ``tsrl_mlp_l1_fwd``  first layers of both nets, rows read through the minibatch index,
+2. ``tsrl_ppo_tail``    layers 2-3, the PPO loss (ppo.py:121-142) and its backward,
+3. ``tsrl_mlp_dw``      first-layer weight/bias gradients.
+
+The gradients land in one flat buffer that the parameters' ``.grad`` views point into, so the
+data-parallel all-reduce is a single call and torch's (fused) Adam and ``clip_grad_norm_``
+consume them unchanged (ppo.py:143-151).  Every gradient element is overwritten each
+minibatch, which is what ``optim.zero_grad()`` + ``loss.backward()`` amount to.
+"""
+from typing import Dict, Optional
+
+import torch
+from torch import nn
+
+from tianshou_amd import _C
+
+HIDDEN = 64
+MAX_ACT = 32
+
+
+def _seq(mlp) -> Optional[list]:
+    model = getattr(mlp, "model", None)
+    return list(model) if isinstance(model, nn.Sequential) else None
+
+
+def _trunk(net, D: int) -> Optional[list]:
+    """[Linear(D,64), Tanh, Linear(64,64), Tanh] of a utils.net.Net, else None."""
+    if getattr(net, "softmax", False) or getattr(net, "num_atoms", 1) != 1:
+        return None
+    mods = _seq(getattr(net, "model", None))
+    if mods is None or len(mods) != 4:
+        return None
+    l1, a1, l2, a2 = mods
+    if not (isinstance(l1, nn.Linear) and isinstance(l2, nn.Linear) and isinstance(a1, nn.Tanh)
+            and isinstance(a2, nn.Tanh)):
+        return None
+    if l1.in_features != D or l1.out_features != HIDDEN or l2.in_features != HIDDEN or \
+            l2.out_features != HIDDEN or l1.bias is None or l2.bias is None:
+        return None
+    return [l1, l2]
+
+
+def match(actor, critic) -> Optional[Dict[str, nn.Linear]]:
+    """The layers of a get_actor_critic-shaped actor/critic pair, or None."""
+    from tianshou_amd.utils.net import ActorProb, Critic
+    if not isinstance(actor, ActorProb) or not isinstance(critic, Critic):
+        return None
+    if actor._c_sigma or not actor._unbounded:
+        return None
+    l1 = getattr(actor.preprocess, "model", None)
+    D = getattr(getattr(l1, "model", [None])[0], "in_features", None) if l1 is not None else None
+    if not isinstance(D, int) or D % 4 != 0:
+        return None
+    ta, tc = _trunk(actor.preprocess, D), _trunk(critic.preprocess, D)
+    mu, last = _seq(actor.mu), _seq(critic.last)
+    if ta is None or tc is None or mu is None or last is None or len(mu) != 1 or len(last) != 1:
+        return None
+    (h_a,), (h_c,) = mu, last
+    if not (isinstance(h_a, nn.Linear) and isinstance(h_c, nn.Linear)):
+        return None
+    if h_a.in_features != HIDDEN or not 0 < h_a.out_features <= MAX_ACT or h_a.bias is None:
+        return None
+    if h_c.in_features != HIDDEN or h_c.out_features != 1 or h_c.bias is None:
+        return None
+    if actor.sigma_param.numel() != h_a.out_features:
+        return None
+    return {"w1a": ta[0], "w2a": ta[1], "w3a": h_a, "w1c": tc[0], "w2c": tc[1], "w3c": h_c,
+            "D": D, "A": h_a.out_features, "sigma": actor.sigma_param}
+
+
+class FusedActorCritic:
+    def __init__(self, layers: Dict, params) -> None:
+        self.L = layers
+        self.D = layers["D"]
+        self.A = layers["A"]
+        self.params = [p for p in params]
+        self._flat = None
+        self._bufs: Dict[str, torch.Tensor] = {}
+
+    # -- gradient storage -----------------------------------------------------------------------
+    def bind_grads(self) -> None:
+        """Point every parameter's .grad at a slice of one flat buffer (kept across
+        minibatches; re-bound if the optimiser or user replaced a .grad)."""
+        dev = self.params[0].device
+        if self._flat is not None and all(
+                p.grad is not None and p.grad.data_ptr() == v.data_ptr()
+                for p, v in zip(self.params, self._views)):
+            return
+        n = sum(p.numel() for p in self.params)
+        self._flat = torch.zeros(n, dtype=torch.float32, device=dev)
+        self._views = []
+        o = 0
+        for p in self.params:
+            v = self._flat[o:o + p.numel()].view_as(p)
+            p.grad = v
+            self._views.append(v)
+            o += p.numel()
+        L = self.L
+        g = lambda m: _C.ptr(m.grad)  # noqa: E731
+        self._tail_grads = _C.TailGrads(
+            g(L["w2a"].weight), g(L["w2a"].bias), g(L["w2c"].weight), g(L["w2c"].bias),
+            g(L["w3a"].weight), g(L["w3a"].bias), g(L["w3c"].weight), g(L["w3c"].bias))
+        self._tail_w = _C.TailWeights(
+            _C.ptr(L["w2a"].weight), _C.ptr(L["w2a"].bias), _C.ptr(L["w2c"].weight),
+            _C.ptr(L["w2c"].bias), _C.ptr(L["w3a"].weight), _C.ptr(L["w3a"].bias),
+            _C.ptr(L["w3c"].weight), _C.ptr(L["w3c"].bias), _C.ptr(L["sigma"]))
+
+    @property
+    def flat_grad(self) -> torch.Tensor:
+        return self._flat
+
+    def _buf(self, key: str, numel: int, dtype=torch.float32) -> torch.Tensor:
+        b = self._bufs.get(key)
+        if b is None or b.numel() < numel or b.dtype != dtype:
+            b = torch.empty(max(numel, 1), dtype=dtype, device=self.params[0].device)
+            self._bufs[key] = b
+        return b
+
+    # -- one minibatch --------------------------------------------------------------------------
+    def minibatch(self, obs: torch.Tensor, idx: Optional[torch.Tensor], b: int,
+                  act: torch.Tensor, logp_old: torch.Tensor, adv: torch.Tensor,
+                  ret: torch.Tensor, v_s: torch.Tensor, params: "_C.PPOParams", dp
+                  ) -> torch.Tensor:
+        """Gradients of the minibatch loss into the parameters' .grad; returns the device
+        tensor [loss, clip, vf, ent] (ppo.py:140-142)."""
+        self.bind_grads()
+        L, lib = self.L, _C.lib()
+        dev = obs.device
+        s = _C.stream_ptr(dev)
+        D, A = self.D, self.A
+        assert obs.dim() == 2 and obs.shape[1] == D and obs.is_contiguous()
+        assert act.shape[-1] == A and act.is_contiguous()
+        ip = _C.ptr(idx) if idx is not None else None
+        # advantage moments of the (global) minibatch
+        adv_sums = None
+        if params.norm_adv:
+            nblk = int(lib.tsrl_ppo_num_partials(b))
+            pa = self._buf("adv_part", 2 * nblk, torch.float64)
+            _C.check(lib.tsrl_adv_moments(_C.ptr(adv), ip, b, _C.ptr(pa), s), "tsrl_adv_moments")
+            adv_sums = self._buf("adv_sums", 2, torch.float64)[:2]
+            _C.check(lib.tsrl_reduce_partials(_C.ptr(pa), nblk, 2, _C.ptr(adv_sums), s),
+                     "tsrl_reduce_partials")
+            dp.all_reduce_(adv_sums)
+        h1 = self._buf("h1", int(lib.tsrl_mlp_frag_floats(b)))
+        _C.check(lib.tsrl_mlp_l1_fwd(
+            _C.ptr(obs), D, ip, b, D, _C.ptr(L["w1a"].weight), _C.ptr(L["w1a"].bias),
+            _C.ptr(L["w1c"].weight), _C.ptr(L["w1c"].bias), 1, _C.ptr(h1), 1, s),
+            "tsrl_mlp_l1_fwd")
+        dz1 = self._buf("dz1", b * 2 * 64)
+        sums = self._buf("sums", 4 + A, torch.float64)[:4 + A]
+        wsb = int(lib.tsrl_ppo_tail_workspace_bytes(b))
+        ws = self._buf("tail_ws", wsb, torch.uint8)
+        _C.check(lib.tsrl_ppo_tail(
+            _C.ptr(h1), b, ip, self._tail_w, A, _C.ptr(act), _C.ptr(logp_old), _C.ptr(adv),
+            _C.ptr(ret), _C.ptr(v_s), _C.ptr(adv_sums) if adv_sums is not None else None,
+            params, _C.ptr(dz1), self._tail_grads, _C.ptr(sums), _C.ptr(ws), wsb, s),
+            "tsrl_ppo_tail")
+        wsb2 = int(lib.tsrl_mlp_dw_workspace_bytes(b, D))
+        ws2 = self._buf("dw_ws", wsb2, torch.uint8)
+        _C.check(lib.tsrl_mlp_dw(
+            _C.ptr(dz1), _C.ptr(obs), D, ip, b, D, _C.ptr(L["w1a"].weight.grad),
+            _C.ptr(L["w1a"].bias.grad), _C.ptr(L["w1c"].weight.grad),
+            _C.ptr(L["w1c"].bias.grad), _C.ptr(ws2), wsb2, s), "tsrl_mlp_dw")
+        dp.all_reduce_(self._flat)
+        dp.all_reduce_(sums)
+        terms = torch.empty(4, dtype=torch.float32, device=dev)
+        _C.check(lib.tsrl_ppo_gauss_finalize(
+            _C.ptr(sums), A, _C.ptr(L["sigma"]), params, _C.ptr(terms),
+            _C.ptr(L["sigma"].grad), s), "tsrl_ppo_gauss_finalize")
+        return terms

@@ -18,6 +18,7 @@ from torch.distributions import Independent, Normal
 
 from tianshou_amd import _C
 from tianshou_amd.data.batch import Batch, gather_rows, split_indices
+from tianshou_amd.policy import fused_mlp as _fmlp
 from tianshou_amd.policy.a2c import A2CPolicy
 from tianshou_amd.utils.net import ActorProb
 
@@ -105,7 +106,7 @@ class PPOPolicy(A2CPolicy):
                  optim: torch.optim.Optimizer, dist_fn: Callable, eps_clip: float = 0.2,
                  dual_clip: Optional[float] = None, value_clip: bool = False,
                  advantage_normalization: bool = True, recompute_advantage: bool = False,
-                 perm_device: bool = False, **kwargs: Any) -> None:
+                 perm_device: bool = False, fused_mlp: bool = True, **kwargs: Any) -> None:
         super().__init__(actor, critic, optim, dist_fn, **kwargs)
         self._eps_clip = eps_clip
         assert dual_clip is None or dual_clip > 1.0, \
@@ -120,6 +121,14 @@ class PPOPolicy(A2CPolicy):
         self._fused = isinstance(actor, ActorProb) and not actor._c_sigma and \
             _is_fixed_std_normal(dist_fn)
         self._gauss_dist = self._fused
+        # the whole minibatch (MLP forward, loss, backward) as three HIP kernels when the
+        # networks have the get_actor_critic shape (policy/fused_mlp.py); fused_mlp=False
+        # keeps the torch layers + fused loss kernel.
+        self._mlp = None
+        if self._fused and fused_mlp:
+            layers = _fmlp.match(actor, critic)
+            if layers is not None:
+                self._mlp = _fmlp.FusedActorCritic(layers, self._actor_critic.parameters())
 
     def _params(self, b_global: float) -> _C.PPOParams:
         p = _C.PPOParams()
@@ -184,8 +193,21 @@ class PPOPolicy(A2CPolicy):
             ret = batch.returns.reshape(-1).to(**f32).contiguous()
             v_s = batch.v_s.reshape(-1).to(**f32).contiguous()
             perm = self._permutation(n, dev)
+            mlp_ok = self._mlp is not None and batch.obs.is_cuda and \
+                batch.obs.dtype == torch.float32 and batch.obs.dim() == 2
+            obs_all = batch.obs.contiguous() if mlp_ok else None
             for s, e in split_bounds(n, batch_size, merge_last=True):
                 idx = perm[s:e]
+                if mlp_ok:
+                    params = self._params((e - s) * self.dp.world)
+                    t = self._mlp.minibatch(obs_all, idx, e - s, act, logp_old, adv, ret, v_s,
+                                            params, self.dp)
+                    if self._grad_norm:
+                        nn.utils.clip_grad_norm_(self._actor_critic.parameters(),
+                                                 max_norm=self._grad_norm)
+                    self.optim.step()
+                    terms.append(t)
+                    continue
                 obs_mb = gather_rows(batch.obs, idx)
                 mu = self.actor.forward_mu(obs_mb)
                 value = self.critic(obs_mb).flatten()
