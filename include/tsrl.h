@@ -257,6 +257,24 @@ int tsrl_mlp_dw(const float* dz1, const float* X, int64_t ldx, const int64_t* id
                 int64_t D, float* gWa, float* gba, float* gWc, float* gbc, void* workspace,
                 int64_t ws_bytes, void* stream);
 
+/* ---------------------------------------------------------------------------------
+ * Fused Gaussian policy step of the collector (collector.py:286-303 -> pg.py:133-171 ->
+ * base.py:183-215) for the get_actor_critic actor (two Tanh layers of 64, unbounded mu
+ * head, state-independent log-std): act = eps * exp(log_std) + mu(obs) (eps NULL: act =
+ * mu, deterministic eval), act_remap = scale(bound(act)) with bound_method 0 none / 1 clip /
+ * 2 tanh and scaling to [low, high] when low/high are given.  The first-layer weight [64, D]
+ * is packed once (tsrl_policy_pack_l1, tsrl_policy_pack_floats(D) floats) after each
+ * parameter update.
+ * ------------------------------------------------------------------------------- */
+int64_t tsrl_policy_pack_floats(int64_t D);
+int tsrl_policy_pack_l1(const float* W, int64_t D, float* packed, void* stream);
+int tsrl_gauss_policy_act(const float* obs, int64_t ldx, int64_t n, int64_t D,
+                          const float* w1packed, const float* b1, const float* w2,
+                          const float* b2, const float* w3, const float* b3,
+                          const float* log_std, int64_t act_dim, const float* eps,
+                          int bound_method, const float* low, const float* high, float* act,
+                          float* act_remap, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -65,52 +65,55 @@ __global__ __launch_bounds__(256, 2) void l1_fwd_kernel(
     const float* __restrict__ bc, int act_tanh, float* __restrict__ out, int frag_out) {
     __shared__ __attribute__((aligned(16))) float Xs[2][L1_ROWS][LS];
     __shared__ __attribute__((aligned(16))) float Ws[2][HC][LS];
+    __shared__ float sb[HC];
     const int t = threadIdx.x;
     const int w = t >> 6, l = t & 63, h = l >> 5, c = l & 31;
     const int64_t row0 = (int64_t)blockIdx.x * L1_ROWS;
-    // staging assignment: thread t moves float4 column (t&7) of rows (t>>3) + 32q
+    if (t < HC) sb[t] = t < H ? ba[t] : bc[t - H];
+    // staging assignment: thread t moves float4 column (t&7) of rows (t>>3) + 32q.  Dead
+    // rows read row 0 and are zeroed (branch-free loads; D % 4 == 0 so a float4 is either
+    // wholly inside the row or wholly past its end).
     const int sc = 4 * (t & 7);
     const float* xsrc[4];
     const float* wsrc[4];
+    bool xlive[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const int64_t r = row0 + (t >> 3) + 32 * q;
-        xsrc[q] = r < n ? X + (idx ? idx[r] : r) * ldx : nullptr;
+        xlive[q] = r < n;
+        xsrc[q] = X + (xlive[q] ? (idx ? idx[r] : r) : 0) * ldx;
         const int f = (t >> 3) + 32 * q;
         wsrc[q] = f < H ? Wa + (int64_t)f * D : Wc + (int64_t)(f - H) * D;
     }
     const int nchunks = (D + KC - 1) / KC;
     float4 xr[4], wr[4];
+    bool kin_ld = true;
+    // loads go straight to registers; the masks are applied when the registers are
+    // written to LDS (after the MFMA phase), so no wait sits between the loads
     auto load = [&](int kc) {
         const int k = kc * KC + sc;
+        kin_ld = k < D;
+        const int kk = kin_ld ? k : 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            float4 xv = make_float4(0.f, 0.f, 0.f, 0.f), wv = xv;
-            if (k + 3 < D) {
-                if (xsrc[q]) xv = *reinterpret_cast<const float4*>(xsrc[q] + k);
-                wv = *reinterpret_cast<const float4*>(wsrc[q] + k);
-            } else if (k < D) {
-                float xa[4] = {0.f, 0.f, 0.f, 0.f}, wa[4] = {0.f, 0.f, 0.f, 0.f};
-                for (int e = 0; e < 4 && k + e < D; ++e) {
-                    if (xsrc[q]) xa[e] = xsrc[q][k + e];
-                    wa[e] = wsrc[q][k + e];
-                }
-                xv = make_float4(xa[0], xa[1], xa[2], xa[3]);
-                wv = make_float4(wa[0], wa[1], wa[2], wa[3]);
-            }
-            xr[q] = xv;
-            wr[q] = wv;
+            xr[q] = *reinterpret_cast<const float4*>(xsrc[q] + kk);
+            wr[q] = *reinterpret_cast<const float4*>(wsrc[q] + kk);
         }
     };
     auto store = [&](int buf) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
+            const bool xo = kin_ld && xlive[q];
             float* xd = &Xs[buf][(t >> 3) + 32 * q][sc];
             float* wd = &Ws[buf][(t >> 3) + 32 * q][sc];
-            *reinterpret_cast<float2*>(xd) = make_float2(xr[q].x, xr[q].y);
-            *reinterpret_cast<float2*>(xd + 2) = make_float2(xr[q].z, xr[q].w);
-            *reinterpret_cast<float2*>(wd) = make_float2(wr[q].x, wr[q].y);
-            *reinterpret_cast<float2*>(wd + 2) = make_float2(wr[q].z, wr[q].w);
+            *reinterpret_cast<float2*>(xd) =
+                make_float2(xo ? xr[q].x : 0.f, xo ? xr[q].y : 0.f);
+            *reinterpret_cast<float2*>(xd + 2) =
+                make_float2(xo ? xr[q].z : 0.f, xo ? xr[q].w : 0.f);
+            *reinterpret_cast<float2*>(wd) =
+                make_float2(kin_ld ? wr[q].x : 0.f, kin_ld ? wr[q].y : 0.f);
+            *reinterpret_cast<float2*>(wd + 2) =
+                make_float2(kin_ld ? wr[q].z : 0.f, kin_ld ? wr[q].w : 0.f);
         }
     };
     f32x16 acc[NT];
@@ -144,7 +147,7 @@ __global__ __launch_bounds__(256, 2) void l1_fwd_kernel(
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int f = 32 * i + rho(r) + 4 * h;
-            float z = acc[i][r] + (f < H ? ba[f] : bc[f - H]);
+            float z = acc[i][r] + sb[f];
             v[r] = act_tanh ? tanhf(z) : z;
         }
         if (frag_out) {
@@ -213,63 +216,119 @@ __device__ __forceinline__ int rs_reg(int l) {
     return 8 * ((l >> 4) & 1) + 4 * ((l >> 3) & 1) + 2 * ((l >> 2) & 1) + ((l >> 1) & 1);
 }
 
-__global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
+// Workgroups with blockIdx.y == 0 run the actor half (layer 2, mu head, clipped surrogate,
+// backward), blockIdx.y == 1 the critic half (layer 2, value head, value loss, backward):
+// the loss gradient w.r.t. mu depends only on actor outputs and w.r.t. the value only on
+// critic outputs, so the halves are independent and each keeps half the live state.
+constexpr int SH = 18;   // half-tile transpose scratch: [64 features][16 rows], stride 18
+constexpr int T_W2 = 0, T_W3 = T_W2 + H * WS2, T_B2 = T_W3 + AMAX * WS2, T_B3 = T_B2 + H,
+              T_W3C = T_B3 + AMAX, T_VAR = T_W3C + H, T_LS = T_VAR + AMAX, T_SCR = T_LS + AMAX,
+              T_END = T_SCR + 4 * 2 * H * SH;
+
+// Accumulate D += A^T-in-LDS . B^T-in-LDS over 16 minibatch rows: the two operands were
+// written feature-major ([feature][row], stride SH) from the C layout; tiles ot x ft.
+template <int NOT, int NFT>
+__device__ __forceinline__ void acc_wgrad(f32x16 (&g)[NOT][NFT], const float* S1, const float* S2,
+                                          int c, int h) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        float2 a2[NOT], b2[NFT];
+#pragma unroll
+        for (int i = 0; i < NOT; ++i)
+            a2[i] = *reinterpret_cast<const float2*>(&S1[(32 * i + c) * SH + 4 * s + 2 * h]);
+#pragma unroll
+        for (int i = 0; i < NFT; ++i)
+            b2[i] = *reinterpret_cast<const float2*>(&S2[(32 * i + c) * SH + 4 * s + 2 * h]);
+#pragma unroll
+        for (int ot = 0; ot < NOT; ++ot)
+#pragma unroll
+            for (int ft = 0; ft < NFT; ++ft) {
+                g[ot][ft] = mfma(a2[ot].x, b2[ft].x, g[ot][ft]);
+                g[ot][ft] = mfma(a2[ot].y, b2[ft].y, g[ot][ft]);
+            }
+    }
+}
+
+// Write a C-layout activation (NT32 tiles of 32 features) rows [16*half, 16*half+16) into
+// feature-major scratch [feature][row - 16*half].
+template <int NT32>
+__device__ __forceinline__ void put_half(float* S, const float (&v)[NT32][16], int c, int h,
+                                         int half) {
+    if ((c >> 4) == half) {
+#pragma unroll
+        for (int it = 0; it < NT32; ++it)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) S[(32 * it + rho(r) + 4 * h) * SH + (c & 15)] = v[it][r];
+    }
+}
+
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// the actor half needs ~330 registers (1 wave per SIMD); the critic half fits 2 per SIMD
+template <int NET>
+__global__ __launch_bounds__(TAIL_TPB, NET == 0 ? 1 : 2) void ppo_tail_kernel(
     const float* __restrict__ h1f, int64_t n, const int64_t* __restrict__ idx, TailWeights wt,
     const float* __restrict__ act, const float* __restrict__ logp_old,
     const float* __restrict__ adv, const float* __restrict__ ret, const float* __restrict__ v_s,
     const double* __restrict__ adv_sums, TailParams p, float* __restrict__ dz1,
     float* __restrict__ slab_f, double* __restrict__ slab_d) {
-    __shared__ float sW2a[H * WS2], sW2c[H * WS2], sW3a[AMAX * WS2];
-    __shared__ float sb2a[H], sb2c[H], sb3a[AMAX], sw3c[H], svar[AMAX], sls[AMAX];
-    __shared__ __attribute__((aligned(16))) float scr[4][2][H * SS];
+    __shared__ __attribute__((aligned(16))) float sm[T_END];
     __shared__ double sred[4][SL_D];
     const int t = threadIdx.x;
     const int w = t >> 6, l = t & 63, h = l >> 5, c = l & 31;
     const int A = p.A;
-    for (int i = t; i < H * H; i += TAIL_TPB) {
-        const int o = i / H, f = i - o * H;
-        sW2a[o * WS2 + f] = wt.w2a[i];
-        sW2c[o * WS2 + f] = wt.w2c[i];
-    }
-    for (int i = t; i < AMAX * H; i += TAIL_TPB) {
-        const int a = i / H, f = i - a * H;
-        sW3a[a * WS2 + f] = a < A ? wt.w3a[i] : 0.0f;
-    }
-    if (t < H) {
-        sb2a[t] = wt.b2a[t];
-        sb2c[t] = wt.b2c[t];
-        sw3c[t] = wt.w3c[t];
-    }
-    if (t < AMAX) {
-        sb3a[t] = t < A ? wt.b3a[t] : 0.0f;
-        const float sig = t < A ? expf(wt.log_std[t]) : 1.0f;
-        svar[t] = sig * sig;
-        sls[t] = logf(sig);
+    constexpr bool actor = NET == 0;
+    constexpr int net = NET;
+    {
+        const float* w2 = actor ? wt.w2a : wt.w2c;
+        const float* b2 = actor ? wt.b2a : wt.b2c;
+        for (int i = t; i < H * H; i += TAIL_TPB) sm[T_W2 + (i >> 6) * WS2 + (i & 63)] = w2[i];
+        if (t < H) sm[T_B2 + t] = b2[t];
+        if (actor) {
+            for (int i = t; i < AMAX * H; i += TAIL_TPB) {
+                const int a = i >> 6;
+                sm[T_W3 + a * WS2 + (i & 63)] = a < A ? wt.w3a[i] : 0.0f;
+            }
+            if (t < AMAX) {
+                sm[T_B3 + t] = t < A ? wt.b3a[t] : 0.0f;
+                const float sig = t < A ? expf(wt.log_std[t]) : 1.0f;
+                sm[T_VAR + t] = sig * sig;
+                sm[T_LS + t] = logf(sig);
+            }
+        } else if (t < H) {
+            sm[T_W3C + t] = wt.w3c[t];
+        }
     }
     __syncthreads();
+    const float* sW2 = sm + T_W2;
+    const float* sW3 = sm + T_W3;
+    float* S1 = sm + T_SCR + w * 2 * H * SH;
+    float* S2 = S1 + H * SH;
     const float b3c = wt.b3c[0];
     float mean_f = 0.0f, std_f = 1.0f;
-    if (p.norm_adv) {
+    if (actor && p.norm_adv) {
         const double nn = 1.0 / p.inv_b64;
         const double m = adv_sums[0] / nn;
         const double var = (adv_sums[1] - adv_sums[0] * m) / (nn - 1.0);
         mean_f = (float)m;
         std_f = (float)sqrt(var > 0.0 ? var : 0.0);
     }
-    float* S1 = scr[w][0];
-    float* S2 = scr[w][1];
 
     // persistent per-wave accumulators
-    f32x16 gW2a[2][2], gW2c[2][2], gW3a[2];
+    f32x16 gW2[2][2], gW3[1][actor ? 2 : 1];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        gW3a[i] = zero16();
+    for (int i = 0; i < (actor ? 2 : 1); ++i) gW3[0][i] = zero16();
 #pragma unroll
-        for (int j = 0; j < 2; ++j) gW2a[i][j] = gW2c[i][j] = zero16();
-    }
-    float gb2a[2] = {0.f, 0.f}, gb2c[2] = {0.f, 0.f}, gw3c[2] = {0.f, 0.f};
-    float gb3a = 0.f, gb3c = 0.f;
-    double dls_acc = 0.0, clip_acc = 0.0, vf_acc = 0.0, cnt_acc = 0.0;
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) gW2[i][j] = zero16();
+    float gb2[2] = {0.f, 0.f}, gw3c[2] = {0.f, 0.f};
+    float gb3 = 0.f;
+    double dls_acc = 0.0, loss_acc = 0.0, cnt_acc = 0.0;
 
     const int64_t ntiles = (n + 31) / 32;
     const int64_t gw = (int64_t)blockIdx.x * 4 + w, nw = (int64_t)gridDim.x * 4;
@@ -277,11 +336,12 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
         const int64_t brow = bt * 32 + c;
         const bool live = brow < n;
         const int64_t j = live ? (idx ? idx[brow] : brow) : 0;
-        // ---- H1 tiles (actor 0,1; critic 2,3) ------------------------------------------
-        float h1[NT][16];
+        // ---- this net's H1 tiles -----------------------------------------------------------
+        float h1[2][16];
 #pragma unroll
-        for (int i = 0; i < NT; ++i) {
-            const float4* src = reinterpret_cast<const float4*>(h1f + ((bt * NT + i) * 64 + l) * 16);
+        for (int i = 0; i < 2; ++i) {
+            const float4* src =
+                reinterpret_cast<const float4*>(h1f + ((bt * NT + 2 * net + i) * 64 + l) * 16);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const float4 v = src[q];
@@ -291,312 +351,271 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
                 h1[i][4 * q + 3] = v.w;
             }
         }
-        // ---- layer 2 (both nets) ---------------------------------------------------------
-        float h2a[2][16], h2c[2][16];
+        // ---- layer 2 -----------------------------------------------------------------------
+        float h2[2][16];
 #pragma unroll
         for (int ot = 0; ot < 2; ++ot) {
-            f32x16 za = zero16(), zc = zero16();
-            const float* wa = sW2a + (32 * ot + c) * WS2 + 4 * h;
-            const float* wc = sW2c + (32 * ot + c) * WS2 + 4 * h;
+            f32x16 z = zero16();
+            const float* wa = sW2 + (32 * ot + c) * WS2 + 4 * h;
 #pragma unroll
             for (int it = 0; it < 2; ++it)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    za = mfma(wa[32 * it + rho(r)], h1[it][r], za);
-                    zc = mfma(wc[32 * it + rho(r)], h1[2 + it][r], zc);
-                }
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int f = 32 * ot + rho(r) + 4 * h;
-                h2a[ot][r] = tanhf(za[r] + sb2a[f]);
-                h2c[ot][r] = tanhf(zc[r] + sb2c[f]);
-            }
-        }
-        // ---- heads ----------------------------------------------------------------------
-        f32x16 mu = zero16();
-        float vpart = 0.0f;
-        {
-            const float* wa = sW3a + c * WS2 + 4 * h;
-#pragma unroll
-            for (int it = 0; it < 2; ++it)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    mu = mfma(wa[32 * it + rho(r)], h2a[it][r], mu);
-                    vpart += sw3c[32 * it + rho(r) + 4 * h] * h2c[it][r];
-                }
-        }
-        const float value = vpart + __shfl_xor(vpart, 32, 64) + b3c;
-        // ---- loss (both lanes of a row compute the row scalars) -------------------------
-        float diff[16];
-        float lp = 0.0f;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int a = rho(r) + 4 * h;
-            const float m = mu[r] + sb3a[a];
-            diff[r] = 0.0f;
-            if (a < A && live) {
-                diff[r] = act[j * A + a] - m;
-                lp += -(diff[r] * diff[r]) / (2.0f * svar[a]) - sls[a] - LOG_SQRT_2PI;
-            }
-        }
-        const float logp = lp + __shfl_xor(lp, 32, 64);
-        float g_logp = 0.0f, gv = 0.0f;
-        if (live) {
-            float an = adv[j];
-            if (p.norm_adv) an = (an - mean_f) / (std_f + p.adv_eps);
-            const float ratio = expf(logp - logp_old[j]);
-            const float surr1 = ratio * an;
-            const float rc = fminf(fmaxf(ratio, p.lo), p.hi);
-            const float surr2 = rc * an;
-            const float in_rng = (ratio >= p.lo && ratio <= p.hi) ? 1.0f : 0.0f;
-            float clip1, d1;
-            if (surr1 < surr2) {
-                clip1 = surr1;
-                d1 = an;
-            } else if (surr2 < surr1) {
-                clip1 = surr2;
-                d1 = in_rng * an;
-            } else {
-                clip1 = surr1;
-                d1 = 0.5f * an + 0.5f * in_rng * an;
-            }
-            float obj = clip1, dobj = d1;
-            if (p.use_dual && an < 0.0f) {
-                const float tt = p.dual * an;
-                if (clip1 > tt) {
-                    obj = clip1;
-                } else if (clip1 < tt) {
-                    obj = tt;
-                    dobj = 0.0f;
-                } else {
-                    obj = clip1;
-                    dobj = 0.5f * d1;
-                }
-            }
-            g_logp = (float)(-(double)dobj * (double)ratio * p.inv_b64);
-            const float rt = ret[j];
-            float dv, vf;
-            if (p.value_clip) {
-                const float vs = v_s[j];
-                const float dlt = value - vs;
-                const float dcl = fminf(fmaxf(dlt, -p.eps_clip), p.eps_clip);
-                const float vcl = vs + dcl;
-                const float e1 = rt - value, e2 = rt - vcl;
-                const float vf1 = e1 * e1, vf2 = e2 * e2;
-                const float g1 = -2.0f * e1;
-                const float g2 = (dlt >= -p.eps_clip && dlt <= p.eps_clip) ? -2.0f * e2 : 0.0f;
-                if (vf1 > vf2) {
-                    vf = vf1;
-                    dv = g1;
-                } else if (vf2 > vf1) {
-                    vf = vf2;
-                    dv = g2;
-                } else {
-                    vf = vf1;
-                    dv = 0.5f * g1 + 0.5f * g2;
-                }
-            } else {
-                const float e1 = rt - value;
-                vf = e1 * e1;
-                dv = -2.0f * e1;
-            }
-            gv = (float)((double)p.vf_coef * (double)dv * p.inv_b64);
-            if (h == 0) {
-                clip_acc += -(double)obj;
-                vf_acc += (double)vf;
-                cnt_acc += 1.0;
-            }
-        }
-        // d/d(mu) in C layout (action a = rho(r)+4h), d/d(log_std) partials
-        float dmu[16], dls[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int a = rho(r) + 4 * h;
-            const float var = svar[a];
-            dmu[r] = g_logp * diff[r] / var;
-            dls[r] = (a < A && live) ? g_logp * (diff[r] * diff[r] / var - 1.0f) : 0.0f;
-        }
-        dls_acc += (double)rs_sum16(dls, l);
-        gb3a += rs_sum16(dmu, l);
-        {
-            float gvh[16];
-#pragma unroll
-            for (int it = 0; it < 2; ++it) {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) gvh[r] = gv * h2c[it][r];
-                gw3c[it] += rs_sum16(gvh, l);
-            }
-        }
-        {
-            float gsum = h == 0 ? gv : 0.0f;
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) gsum += __shfl_xor(gsum, off, 64);
-            gb3c += gsum;
-        }
-        // ---- dW3a = dMu^T . H2a   (S1 = dMu^T [a][b], S2 = H2a^T [f][b]) ------------------
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            S1[(rho(r) + 4 * h) * SS + c] = dmu[r];
-#pragma unroll
-            for (int it = 0; it < 2; ++it) S2[(32 * it + rho(r) + 4 * h) * SS + c] = h2a[it][r];
-        }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-#pragma unroll
-        for (int s = 0; s < 8; ++s) {
-            const float2 a2 = *reinterpret_cast<const float2*>(&S1[c * SS + 4 * s + 2 * h]);
-#pragma unroll
-            for (int ft = 0; ft < 2; ++ft) {
-                const float2 b2 = *reinterpret_cast<const float2*>(&S2[(32 * ft + c) * SS + 4 * s + 2 * h]);
-                gW3a[ft] = mfma(a2.x, b2.x, gW3a[ft]);
-                gW3a[ft] = mfma(a2.y, b2.y, gW3a[ft]);
-            }
-        }
-        // ---- dZ2 (actor: W3a^T dMu, critic: gv w3c) ---------------------------------------
-        float dz2a[2][16], dz2c[2][16];
-#pragma unroll
-        for (int ft = 0; ft < 2; ++ft) {
-            f32x16 d = zero16();
+                for (int r = 0; r < 16; ++r) z = mfma(wa[32 * it + rho(r)], h1[it][r], z);
 #pragma unroll
             for (int r = 0; r < 16; ++r)
-                d = mfma(sW3a[(rho(r) + 4 * h) * WS2 + 32 * ft + c], dmu[r], d);
+                h2[ot][r] = tanhf(z[r] + sm[T_B2 + 32 * ot + rho(r) + 4 * h]);
+        }
+        float dz2[2][16];
+        if constexpr (actor) {
+            // ---- mu head + clipped surrogate ----------------------------------------------
+            f32x16 mu = zero16();
+            {
+                const float* wa = sW3 + c * WS2 + 4 * h;
+#pragma unroll
+                for (int it = 0; it < 2; ++it)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) mu = mfma(wa[32 * it + rho(r)], h2[it][r], mu);
+            }
+            float diff[16];
+            float lp = 0.0f;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int f = 32 * ft + rho(r) + 4 * h;
-                dz2a[ft][r] = d[r] * (1.0f - h2a[ft][r] * h2a[ft][r]);
-                dz2c[ft][r] = gv * sw3c[f] * (1.0f - h2c[ft][r] * h2c[ft][r]);
+                const int a = rho(r) + 4 * h;
+                diff[r] = 0.0f;
+                if (a < A && live) {
+                    diff[r] = act[j * A + a] - (mu[r] + sm[T_B3 + a]);
+                    lp += -(diff[r] * diff[r]) / (2.0f * sm[T_VAR + a]) - sm[T_LS + a] -
+                          LOG_SQRT_2PI;
+                }
             }
-        }
-        // ---- per net: dZ1 = (W2^T dZ2) * (1 - H1^2), dW2 = dZ2^T H1, db2 -----------------
+            const float logp = lp + __shfl_xor(lp, 32, 64);
+            float g_logp = 0.0f;
+            if (live) {
+                float an = adv[j];
+                if (p.norm_adv) an = (an - mean_f) / (std_f + p.adv_eps);
+                const float ratio = expf(logp - logp_old[j]);
+                const float surr1 = ratio * an;
+                const float rc = fminf(fmaxf(ratio, p.lo), p.hi);
+                const float surr2 = rc * an;
+                const float in_rng = (ratio >= p.lo && ratio <= p.hi) ? 1.0f : 0.0f;
+                float clip1, d1;
+                if (surr1 < surr2) {
+                    clip1 = surr1;
+                    d1 = an;
+                } else if (surr2 < surr1) {
+                    clip1 = surr2;
+                    d1 = in_rng * an;
+                } else {
+                    clip1 = surr1;
+                    d1 = 0.5f * an + 0.5f * in_rng * an;
+                }
+                float obj = clip1, dobj = d1;
+                if (p.use_dual && an < 0.0f) {
+                    const float tt = p.dual * an;
+                    if (clip1 > tt) {
+                        obj = clip1;
+                    } else if (clip1 < tt) {
+                        obj = tt;
+                        dobj = 0.0f;
+                    } else {
+                        obj = clip1;
+                        dobj = 0.5f * d1;
+                    }
+                }
+                g_logp = (float)(-(double)dobj * (double)ratio * p.inv_b64);
+                if (h == 0) {
+                    loss_acc += -(double)obj;
+                    cnt_acc += 1.0;
+                }
+            }
+            float dmu[1][16], dls[16];
 #pragma unroll
-        for (int net = 0; net < 2; ++net) {
-            const float* sW2 = net ? sW2c : sW2a;
-            float (&dz2)[2][16] = net ? dz2c : dz2a;
+            for (int r = 0; r < 16; ++r) {
+                const int a = rho(r) + 4 * h;
+                const float var = sm[T_VAR + a];
+                dmu[0][r] = g_logp * diff[r] / var;
+                dls[r] = (a < A && live) ? g_logp * (diff[r] * diff[r] / var - 1.0f) : 0.0f;
+            }
+            dls_acc += (double)rs_sum16(dls, l);
+            gb3 += rs_sum16(dmu[0], l);
+            // dW3a = dMu^T . H2a over the 32 rows, two half passes
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+                wave_sync_lds();
+                put_half<1>(S1, dmu, c, h, half);
+                put_half<2>(S2, h2, c, h, half);
+                wave_sync_lds();
+                acc_wgrad<1, 2>(gW3, S1, S2, c, h);
+            }
+            // dZ2 = (W3a^T dMu) * (1 - H2^2)
 #pragma unroll
             for (int ft = 0; ft < 2; ++ft) {
                 f32x16 d = zero16();
 #pragma unroll
-                for (int ot = 0; ot < 2; ++ot)
+                for (int r = 0; r < 16; ++r)
+                    d = mfma(sW3[(rho(r) + 4 * h) * WS2 + 32 * ft + c], dmu[0][r], d);
 #pragma unroll
-                    for (int r = 0; r < 16; ++r)
-                        d = mfma(sW2[(32 * ot + rho(r) + 4 * h) * WS2 + 32 * ft + c], dz2[ot][r], d);
-                float v[16];
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const float hv = h1[2 * net + ft][r];
-                    v[r] = live ? d[r] * (1.0f - hv * hv) : 0.0f;
-                }
-                if (live) {
-                    float* o = dz1 + brow * HC + 64 * net + 32 * ft + 4 * h;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        *reinterpret_cast<float4*>(o + 8 * q) =
-                            make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
-                }
+                for (int r = 0; r < 16; ++r) dz2[ft][r] = d[r] * (1.0f - h2[ft][r] * h2[ft][r]);
             }
-            // db2
+        } else {
+            // ---- value head + value loss ----------------------------------------------------
+            float vpart = 0.0f;
 #pragma unroll
-            for (int ot = 0; ot < 2; ++ot) {
-                const float s = rs_sum16(dz2[ot], l);
-                if (net) gb2c[ot] += s; else gb2a[ot] += s;
+            for (int it = 0; it < 2; ++it)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    vpart += sm[T_W3C + 32 * it + rho(r) + 4 * h] * h2[it][r];
+            const float value = vpart + __shfl_xor(vpart, 32, 64) + b3c;
+            float gv = 0.0f;
+            if (live) {
+                const float rt = ret[j];
+                float dv, vf;
+                if (p.value_clip) {
+                    const float vs = v_s[j];
+                    const float dlt = value - vs;
+                    const float dcl = fminf(fmaxf(dlt, -p.eps_clip), p.eps_clip);
+                    const float vcl = vs + dcl;
+                    const float e1 = rt - value, e2 = rt - vcl;
+                    const float vf1 = e1 * e1, vf2 = e2 * e2;
+                    const float g1 = -2.0f * e1;
+                    const float g2 = (dlt >= -p.eps_clip && dlt <= p.eps_clip) ? -2.0f * e2 : 0.0f;
+                    if (vf1 > vf2) {
+                        vf = vf1;
+                        dv = g1;
+                    } else if (vf2 > vf1) {
+                        vf = vf2;
+                        dv = g2;
+                    } else {
+                        vf = vf1;
+                        dv = 0.5f * g1 + 0.5f * g2;
+                    }
+                } else {
+                    const float e1 = rt - value;
+                    vf = e1 * e1;
+                    dv = -2.0f * e1;
+                }
+                gv = (float)((double)p.vf_coef * (double)dv * p.inv_b64);
+                if (h == 0) loss_acc += (double)vf;
             }
-            // dW2 via LDS transposes (S1 = dZ2^T [o][b], S2 = H1^T [f][b])
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
+            {
+                float gvh[16];
 #pragma unroll
                 for (int it = 0; it < 2; ++it) {
-                    S1[(32 * it + rho(r) + 4 * h) * SS + c] = dz2[it][r];
-                    S2[(32 * it + rho(r) + 4 * h) * SS + c] = h1[2 * net + it][r];
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) gvh[r] = gv * h2[it][r];
+                    gw3c[it] += rs_sum16(gvh, l);
                 }
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                float gsum = h == 0 ? gv : 0.0f;
 #pragma unroll
-            for (int s = 0; s < 8; ++s) {
-                float2 a2[2], b2[2];
-#pragma unroll
-                for (int i = 0; i < 2; ++i) {
-                    a2[i] = *reinterpret_cast<const float2*>(&S1[(32 * i + c) * SS + 4 * s + 2 * h]);
-                    b2[i] = *reinterpret_cast<const float2*>(&S2[(32 * i + c) * SS + 4 * s + 2 * h]);
-                }
-#pragma unroll
-                for (int ot = 0; ot < 2; ++ot)
-#pragma unroll
-                    for (int ft = 0; ft < 2; ++ft) {
-                        f32x16& g = net ? gW2c[ot][ft] : gW2a[ot][ft];
-                        g = mfma(a2[ot].x, b2[ft].x, g);
-                        g = mfma(a2[ot].y, b2[ft].y, g);
-                    }
+                for (int off = 32; off > 0; off >>= 1) gsum += __shfl_xor(gsum, off, 64);
+                gb3 += gsum;
             }
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        }
-    }
-    // ---- fold the 4 waves' accumulators (fixed order) into this workgroup's slab -------
-    __syncthreads();
-    float* red = &scr[0][0][0];  // 4 * 2 * H * SS floats >= 4 * H * H
-    float* slab = slab_f + (int64_t)blockIdx.x * SL_F;
-    auto fold_tile = [&](const f32x16 (&g)[2][2], int base, int rows) {
-        // wave w writes its [o][f] matrix (C layout: o = 32ot+rho(r)+4h, f = 32ft+c)
-#pragma unroll
-        for (int ot = 0; ot < 2; ++ot)
 #pragma unroll
             for (int ft = 0; ft < 2; ++ft)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int o = 32 * ot + rho(r) + 4 * h;
-                    if (o < rows) red[w * H * H + o * H + 32 * ft + c] = g[ot][ft][r];
-                }
+                for (int r = 0; r < 16; ++r)
+                    dz2[ft][r] = gv * sm[T_W3C + 32 * ft + rho(r) + 4 * h] *
+                                 (1.0f - h2[ft][r] * h2[ft][r]);
+        }
+        // ---- dZ1 = (W2^T dZ2) * (1 - H1^2) -> HBM (row-major [n][128]) -------------------
+#pragma unroll
+        for (int ft = 0; ft < 2; ++ft) {
+            f32x16 d = zero16();
+#pragma unroll
+            for (int ot = 0; ot < 2; ++ot)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    d = mfma(sW2[(32 * ot + rho(r) + 4 * h) * WS2 + 32 * ft + c], dz2[ot][r], d);
+            if (live) {
+                float v[16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) v[r] = d[r] * (1.0f - h1[ft][r] * h1[ft][r]);
+                float* o = dz1 + brow * HC + 64 * net + 32 * ft + 4 * h;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    *reinterpret_cast<float4*>(o + 8 * q) =
+                        make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+            }
+        }
+        // ---- db2, dW2 = dZ2^T . H1 ---------------------------------------------------------
+#pragma unroll
+        for (int ot = 0; ot < 2; ++ot) gb2[ot] += rs_sum16(dz2[ot], l);
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            wave_sync_lds();
+            put_half<2>(S1, dz2, c, h, half);
+            put_half<2>(S2, h1, c, h, half);
+            wave_sync_lds();
+            acc_wgrad<2, 2>(gW2, S1, S2, c, h);
+        }
+    }
+    // ---- fold the 4 waves (fixed order) into this workgroup's slab --------------------------
+    __syncthreads();
+    float* red = sm;  // T_END >= 4 * 32 * 64 floats
+    float* slab = slab_f + (int64_t)blockIdx.x * SL_F;
+    auto fold = [&](const f32x16 (&g)[2], int o0, int base) {
+        // rows [o0, o0+32) of a [rows][64] matrix held as C layout (o = rho(r)+4h, f = 32ft+c)
+#pragma unroll
+        for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                red[w * 32 * H + (rho(r) + 4 * h) * H + 32 * ft + c] = g[ft][r];
         __syncthreads();
-        for (int i = t; i < rows * H; i += TAIL_TPB)
-            slab[base + i] = ((red[i] + red[H * H + i]) + red[2 * H * H + i]) + red[3 * H * H + i];
+        for (int i = t; i < 32 * H; i += TAIL_TPB)
+            slab[base + o0 * H + i] =
+                ((red[i] + red[32 * H + i]) + red[2 * 32 * H + i]) + red[3 * 32 * H + i];
         __syncthreads();
     };
-    fold_tile(gW2a, SL_W2A, H);
-    fold_tile(gW2c, SL_W2C, H);
-    {
-        f32x16 g3[2][2] = {{gW3a[0], gW3a[1]}, {zero16(), zero16()}};
-        fold_tile(g3, SL_W3A, AMAX);
-    }
+    const int base2 = actor ? SL_W2A : SL_W2C;
+    fold(gW2[0], 0, base2);
+    fold(gW2[1], 32, base2);
+    if constexpr (actor) fold(gW3[0], 0, SL_W3A);
     // vectors: lanes with bit0 == 0 own feature rho(rs_reg(l)) + 4h of each tile
-    float* vred = red;  // [4 waves][SL_F - SL_B2A region], reuse
     const int fr = rho(rs_reg(l)) + 4 * h;
-    constexpr int VW = 4 * H + AMAX + 4;  // b2a, b2c, w3c(H) ... packed per wave
+    constexpr int VW = 3 * H + 4;
     if ((l & 1) == 0) {
 #pragma unroll
         for (int it = 0; it < 2; ++it) {
-            vred[w * VW + 32 * it + fr] = gb2a[it];
-            vred[w * VW + H + 32 * it + fr] = gb2c[it];
-            vred[w * VW + 2 * H + 32 * it + fr] = gw3c[it];
+            red[w * VW + 32 * it + fr] = gb2[it];
+            red[w * VW + H + 32 * it + fr] = gw3c[it];
         }
-        vred[w * VW + 3 * H + fr] = gb3a;
+        red[w * VW + 2 * H + fr] = gb3;  // actor: db3a[a]; critic: lane 0's gb3 is db3c
     }
-    if (l == 0) vred[w * VW + 3 * H + AMAX] = gb3c;
     __syncthreads();
     if (t < VW) {
-        const float s = ((vred[t] + vred[VW + t]) + vred[2 * VW + t]) + vred[3 * VW + t];
-        if (t < H) slab[SL_B2A + t] = s;
-        else if (t < 2 * H) slab[SL_B2C + t - H] = s;
-        else if (t < 3 * H) slab[SL_W3C + t - 2 * H] = s;
-        else if (t < 3 * H + AMAX) slab[SL_B3A + t - 3 * H] = s;
-        else if (t == 3 * H + AMAX) slab[SL_B3C] = s;
+        const float v = ((red[t] + red[VW + t]) + red[2 * VW + t]) + red[3 * VW + t];
+        if (t < H) {
+            slab[(actor ? SL_B2A : SL_B2C) + t] = v;
+        } else if (t < 2 * H) {
+            if (!actor) slab[SL_W3C + t - H] = v;
+        } else if (t < 2 * H + AMAX) {
+            if (actor) slab[SL_B3A + t - 2 * H] = v;
+        }
     }
-    // doubles: loss sums (wave reduce) and d/dlog_std
-    clip_acc = wave_sum(clip_acc);
-    vf_acc = wave_sum(vf_acc);
+    if (!actor && t == 0) {
+        // every lane of a critic wave holds the same gb3 (full-wave sum)
+        slab[SL_B3C] = ((red[2 * H] + red[VW + 2 * H]) + red[2 * VW + 2 * H]) + red[3 * VW + 2 * H];
+    }
+    loss_acc = wave_sum(loss_acc);
     cnt_acc = wave_sum(cnt_acc);
-    if ((l & 1) == 0) sred[w][4 + fr] = dls_acc;
+    if (actor && (l & 1) == 0) sred[w][4 + fr] = dls_acc;
     if (l == 0) {
-        sred[w][0] = clip_acc;
-        sred[w][1] = vf_acc;
-        sred[w][2] = cnt_acc;
-        sred[w][3] = 0.0;
+        sred[w][0] = loss_acc;
+        sred[w][1] = cnt_acc;
     }
     __syncthreads();
-    if (t < SL_D)
-        slab_d[(int64_t)blockIdx.x * SL_D + t] =
-            ((sred[0][t] + sred[1][t]) + sred[2][t]) + sred[3][t];
+    double* sd = slab_d + (int64_t)blockIdx.x * SL_D;
+    if (t < SL_D) {
+        const double v = ((sred[0][t] + sred[1][t]) + sred[2][t]) + sred[3][t];
+        if (actor) {
+            if (t == 0) sd[0] = v;            // clip sum
+            else if (t == 1) sd[2] = v;       // row count
+            else if (t >= 4) sd[t] = v;       // d/dlog_std
+        } else if (t == 0) {
+            sd[1] = v;                        // vf sum
+        }
+    }
+    if (actor && t == 3) sd[3] = 0.0;
 }
 
 // Folds the per-workgroup slabs (fixed order) into the parameter gradients and the loss sums.
@@ -640,6 +659,8 @@ __global__ __launch_bounds__(256, 2) void dw_kernel(
     const float* __restrict__ dz, const float* __restrict__ X, int64_t ldx,
     const int64_t* __restrict__ idx, int64_t n, int D, int64_t rows_per_split,
     int ncolpad, float* __restrict__ part) {
+    // Zs holds dZ1 rows with feature f = 32i + c at [c][i], so a lane's four A fragments
+    // (one per feature tile) are one 16-byte LDS read.
     __shared__ __attribute__((aligned(16))) float Zs[2][DW_KB][HC];
     __shared__ __attribute__((aligned(16))) float Xs[2][DW_KB][DW_COLS];
     const int t = threadIdx.x;
@@ -647,37 +668,48 @@ __global__ __launch_bounds__(256, 2) void dw_kernel(
     const int col0 = blockIdx.x * DW_COLS;
     const int64_t r0 = (int64_t)blockIdx.y * rows_per_split;
     const int64_t r1 = min(n, r0 + rows_per_split);
-    // staging: thread t moves float4 (t & 31) of rows (t >> 5) + 8q, q = 0..3
+    // staging: thread t moves float4 (t & 31) of rows (t >> 5) + 8q, q = 0..3.  The gather
+    // index of chunk ch+1 is loaded one chunk ahead (no dependent-load stall per chunk).
     const int sc = 4 * (t & 31);
+    const int k = col0 + sc;
+    const bool kin = k + 3 < D;  // whole float4 inside the row (D % 4 == 0)
     float4 zr[4], xr[4];
+    int64_t rid[4];       // gather rows of the NEXT chunk to load (raw index values)
+    bool live_ld[4];      // row liveness of the chunk whose loads are in flight
+    auto load_idx = [&](int64_t rb) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t r = min(rb + (t >> 5) + 8 * q, r1 - 1);
+            rid[q] = idx ? idx[r] : r;
+        }
+    };
+    // loads go straight to registers; masks are applied in store() after the MFMA phase
     auto load = [&](int64_t rb) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int64_t r = rb + (t >> 5) + 8 * q;
-            float4 zv = make_float4(0.f, 0.f, 0.f, 0.f), xv = zv;
-            if (r < r1) {
-                zv = *reinterpret_cast<const float4*>(dz + r * HC + sc);
-                const float* xrow = X + (idx ? idx[r] : r) * ldx;
-                const int k = col0 + sc;
-                if (k + 3 < D) {
-                    xv = *reinterpret_cast<const float4*>(xrow + k);
-                } else {
-                    float xa[4];
-#pragma unroll
-                    for (int e = 0; e < 4; ++e)
-                        xa[e] = k + e < D ? xrow[k + e] : (k + e == D ? 1.0f : 0.0f);
-                    xv = make_float4(xa[0], xa[1], xa[2], xa[3]);
-                }
-            }
-            zr[q] = zv;
-            xr[q] = xv;
+            live_ld[q] = r < r1;
+            const int64_t rr = min(r, r1 - 1);
+            zr[q] = *reinterpret_cast<const float4*>(dz + rr * HC + sc);
+            xr[q] = *reinterpret_cast<const float4*>(X + rid[q] * ldx + (kin ? k : 0));
         }
     };
     auto store = [&](int buf) {
+        const int i = sc >> 5, c0 = sc & 31;
+        // ones column (db) at k == D
+        const float o0 = k == D ? 1.f : 0.f, o1 = k + 1 == D ? 1.f : 0.f,
+                    o2 = k + 2 == D ? 1.f : 0.f, o3 = k + 3 == D ? 1.f : 0.f;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            *reinterpret_cast<float4*>(&Zs[buf][(t >> 5) + 8 * q][sc]) = zr[q];
-            *reinterpret_cast<float4*>(&Xs[buf][(t >> 5) + 8 * q][sc]) = xr[q];
+            const bool lv = live_ld[q];
+            float* zd = &Zs[buf][(t >> 5) + 8 * q][0];
+            zd[(c0 + 0) * 4 + i] = lv ? zr[q].x : 0.f;
+            zd[(c0 + 1) * 4 + i] = lv ? zr[q].y : 0.f;
+            zd[(c0 + 2) * 4 + i] = lv ? zr[q].z : 0.f;
+            zd[(c0 + 3) * 4 + i] = lv ? zr[q].w : 0.f;
+            *reinterpret_cast<float4*>(&Xs[buf][(t >> 5) + 8 * q][sc]) =
+                make_float4(lv ? (kin ? xr[q].x : o0) : 0.f, lv ? (kin ? xr[q].y : o1) : 0.f,
+                            lv ? (kin ? xr[q].z : o2) : 0.f, lv ? (kin ? xr[q].w : o3) : 0.f);
         }
     };
     f32x16 acc[NT];
@@ -685,18 +717,26 @@ __global__ __launch_bounds__(256, 2) void dw_kernel(
     for (int i = 0; i < NT; ++i) acc[i] = zero16();
     const int64_t nchunk = r1 > r0 ? (r1 - r0 + DW_KB - 1) / DW_KB : 0;
     if (nchunk > 0) {
+        load_idx(r0);
         load(r0);
         store(0);
+        if (nchunk > 1) load_idx(r0 + DW_KB);
     }
     __syncthreads();
     for (int64_t ch = 0; ch < nchunk; ++ch) {
         const int buf = ch & 1;
-        if (ch + 1 < nchunk) load(r0 + (ch + 1) * DW_KB);
+        if (ch + 1 < nchunk) {
+            load(r0 + (ch + 1) * DW_KB);
+            if (ch + 2 < nchunk) load_idx(r0 + (ch + 2) * DW_KB);
+        }
 #pragma unroll
         for (int s = 0; s < DW_KB / 2; ++s) {
+            const float4 a4 = *reinterpret_cast<const float4*>(&Zs[buf][2 * s + h][4 * c]);
             const float b = Xs[buf][2 * s + h][32 * w + c];
-#pragma unroll
-            for (int i = 0; i < NT; ++i) acc[i] = mfma(Zs[buf][2 * s + h][32 * i + c], b, acc[i]);
+            acc[0] = mfma(a4.x, b, acc[0]);
+            acc[1] = mfma(a4.y, b, acc[1]);
+            acc[2] = mfma(a4.z, b, acc[2]);
+            acc[3] = mfma(a4.w, b, acc[3]);
         }
         if (ch + 1 < nchunk) store(buf ^ 1);
         __syncthreads();
@@ -747,6 +787,7 @@ TailParams make_tail_params(const tsrl_ppo_params& q, int A) {
 }
 
 int tail_grid(int64_t n) {
+    // workgroups per net (grid.y = 2: actor, critic); 2 resident per CU
     const int64_t tiles = (n + 31) / 32;
     const int64_t g = (tiles + 3) / 4;
     return (int)std::min<int64_t>(g, 256);
@@ -812,9 +853,12 @@ extern "C" int tsrl_ppo_tail(const float* h1frag, int64_t n, const int64_t* idx,
     double* slab_d = reinterpret_cast<double*>(dptr);
     TailWeights w{wt->w2a, wt->b2a, wt->w2c, wt->b2c, wt->w3a, wt->b3a, wt->w3c, wt->b3c,
                   wt->log_std};
-    hipLaunchKernelGGL(ppo_tail_kernel, dim3(g), dim3(TAIL_TPB), 0, as_stream(stream), h1frag, n,
-                       idx, w, act, logp_old, adv, ret, v_s, adv_sums,
-                       make_tail_params(prm, (int)act_dim), dz1, slab_f, slab_d);
+    const TailParams tp = make_tail_params(prm, (int)act_dim);
+    hipLaunchKernelGGL(ppo_tail_kernel<0>, dim3(g), dim3(TAIL_TPB), 0, as_stream(stream), h1frag, n,
+                       idx, w, act, logp_old, adv, ret, v_s, adv_sums, tp, dz1, slab_f, slab_d);
+    TSRL_LAUNCH_CHECK("tsrl_ppo_tail(actor)");
+    hipLaunchKernelGGL(ppo_tail_kernel<1>, dim3(g), dim3(TAIL_TPB), 0, as_stream(stream), h1frag, n,
+                       idx, w, act, logp_old, adv, ret, v_s, adv_sums, tp, dz1, slab_f, slab_d);
     TSRL_LAUNCH_CHECK("tsrl_ppo_tail");
     TailGrads gg{grads->w2a, grads->b2a, grads->w2c, grads->b2c, grads->w3a, grads->b3a,
                  grads->w3c, grads->b3c};

@@ -1,0 +1,202 @@
+// Fused Gaussian policy step for the collector (Collector.collect -> policy.forward ->
+// dist.sample -> map_action; tianshou/data/collector.py:286-303, policy/modelfree/pg.py:
+// 133-171, policy/base.py:183-215) for the MuJoCo actor of utils/models.py:34-97:
+//   mu  = Linear(64,A)(tanh(Linear(64,64)(tanh(Linear(D,64)(obs)))))   (unbounded)
+//   act = eps * exp(log_std) + mu        (dist.sample() = torch.normal(mu, sigma))
+//   act_remap = scale(bound(act))         (clip / tanh to [-1,1], then to [low, high])
+// One workgroup = 32 env rows.  The first layer's K (= obs dim) is split over the 4 waves
+// (f32 MFMA 32x32x2, batch rows on lanes, features on accumulator registers as in
+// mlp.hip); wave 0 folds the partials in fixed order and runs layer 2, the mu head and the
+// sampling/mapping epilogue.  The first-layer weight is pre-packed once per collect into the
+// per-lane fragment order so every weight load is a contiguous 1 KB wave access.
+#include "tsrl_common.h"
+
+namespace tsrl {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+constexpr int H = 64;
+constexpr int AMAX = 32;
+constexpr int WS = 65;
+
+__device__ __forceinline__ int rho(int r) { return (r & 3) + 8 * (r >> 2); }
+__device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x16 zero16() {
+    f32x16 z;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) z[i] = 0.0f;
+    return z;
+}
+
+// K padded to a multiple of 16; lane half h owns k in [h*S, (h+1)*S), S = Kp/2.
+__host__ __device__ inline int64_t kpad(int64_t D) { return (D + 15) / 16 * 16; }
+
+// packed[ot][g][lane][4] = W[32*ot + (lane&31)][(lane>>5)*S + 4*g + e]   (0 beyond D)
+__global__ void pack_l1_kernel(const float* __restrict__ W, int64_t D, float* __restrict__ out) {
+    const int64_t S = kpad(D) / 2, G = S / 4;
+    const int64_t total = 2 * G * 64 * 4;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int e = (int)(i & 3);
+        const int lane = (int)((i >> 2) & 63);
+        const int64_t g = (i >> 8) % G;
+        const int ot = (int)((i >> 8) / G);
+        const int64_t k = (lane >> 5) * S + 4 * g + e;
+        out[i] = k < D ? W[(int64_t)(32 * ot + (lane & 31)) * D + k] : 0.0f;
+    }
+}
+
+struct ActParams {
+    int A, bound, scale, sample;
+};
+
+__global__ __launch_bounds__(256) void gauss_act_kernel(
+    const float* __restrict__ obs, int64_t ldx, int64_t n, int64_t D,
+    const float* __restrict__ w1p, const float* __restrict__ b1, const float* __restrict__ w2,
+    const float* __restrict__ b2, const float* __restrict__ w3, const float* __restrict__ b3,
+    const float* __restrict__ log_std, const float* __restrict__ eps,
+    const float* __restrict__ low, const float* __restrict__ high, ActParams p,
+    float* __restrict__ act, float* __restrict__ act_remap) {
+#pragma clang fp contract(off)
+    __shared__ float sW2[H * WS], sW3[AMAX * WS];
+    __shared__ float sb1[H], sb2[H], sb3[AMAX], ssig[AMAX], slo[AMAX], shi[AMAX];
+    __shared__ float red[3][2][16][64];
+    const int t = threadIdx.x;
+    const int w = t >> 6, l = t & 63, h = l >> 5, c = l & 31;
+    const int A = p.A;
+    const int64_t row = (int64_t)blockIdx.x * 32 + c;
+    const bool live = row < n;
+    // stage the small weights (all waves), then the layer-1 partial products
+    for (int i = t; i < H * H; i += 256) sW2[(i >> 6) * WS + (i & 63)] = w2[i];
+    for (int i = t; i < AMAX * H; i += 256) {
+        const int a = i >> 6;
+        sW3[a * WS + (i & 63)] = a < A ? w3[i] : 0.0f;
+    }
+    if (t < H) {
+        sb1[t] = b1[t];
+        sb2[t] = b2[t];
+    }
+    if (t < AMAX) {
+        sb3[t] = t < A ? b3[t] : 0.0f;
+        ssig[t] = t < A ? expf(log_std[t]) : 1.0f;
+        slo[t] = (p.scale && t < A) ? low[t] : -1.0f;
+        shi[t] = (p.scale && t < A) ? high[t] : 1.0f;
+    }
+    const int64_t S = kpad(D) / 2, G = S / 4;
+    const int64_t g0 = G * w / 4, g1 = G * (w + 1) / 4;
+    f32x16 acc0 = zero16(), acc1 = zero16();
+    const float* xrow = obs + (live ? row : 0) * ldx;
+    const float4* wp0 = reinterpret_cast<const float4*>(w1p) + l;
+    const float4* wp1 = reinterpret_cast<const float4*>(w1p) + G * 64 + l;
+    for (int64_t g = g0; g < g1; ++g) {
+        const int64_t k = h * S + 4 * g;
+        float4 xv = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (live && k < D) xv = *reinterpret_cast<const float4*>(xrow + k);
+        const float4 a0 = wp0[g * 64], a1 = wp1[g * 64];
+        acc0 = mfma(a0.x, xv.x, acc0);
+        acc1 = mfma(a1.x, xv.x, acc1);
+        acc0 = mfma(a0.y, xv.y, acc0);
+        acc1 = mfma(a1.y, xv.y, acc1);
+        acc0 = mfma(a0.z, xv.z, acc0);
+        acc1 = mfma(a1.z, xv.z, acc1);
+        acc0 = mfma(a0.w, xv.w, acc0);
+        acc1 = mfma(a1.w, xv.w, acc1);
+    }
+    if (w > 0) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            red[w - 1][0][r][l] = acc0[r];
+            red[w - 1][1][r][l] = acc1[r];
+        }
+    }
+    __syncthreads();
+    if (w != 0) return;
+    float h1[2][16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const float z0 = ((acc0[r] + red[0][0][r][l]) + red[1][0][r][l]) + red[2][0][r][l];
+        const float z1 = ((acc1[r] + red[0][1][r][l]) + red[1][1][r][l]) + red[2][1][r][l];
+        h1[0][r] = tanhf(z0 + sb1[rho(r) + 4 * h]);
+        h1[1][r] = tanhf(z1 + sb1[32 + rho(r) + 4 * h]);
+    }
+    float h2[2][16];
+#pragma unroll
+    for (int ot = 0; ot < 2; ++ot) {
+        f32x16 z = zero16();
+        const float* wa = sW2 + (32 * ot + c) * WS + 4 * h;
+#pragma unroll
+        for (int it = 0; it < 2; ++it)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) z = mfma(wa[32 * it + rho(r)], h1[it][r], z);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) h2[ot][r] = tanhf(z[r] + sb2[32 * ot + rho(r) + 4 * h]);
+    }
+    f32x16 mu = zero16();
+    {
+        const float* wa = sW3 + c * WS + 4 * h;
+#pragma unroll
+        for (int it = 0; it < 2; ++it)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) mu = mfma(wa[32 * it + rho(r)], h2[it][r], mu);
+    }
+    if (!live) return;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int a = rho(r) + 4 * h;
+        if (a >= A) continue;
+        const float m = mu[r] + sb3[a];
+        // randn * sigma + mu (two roundings, as torch's mul_ then add_)
+        const float x = p.sample ? __fadd_rn(__fmul_rn(eps[row * A + a], ssig[a]), m) : m;
+        act[row * A + a] = x;
+        float y = x;
+        if (p.bound == 1) y = y < -1.0f ? -1.0f : (y > 1.0f ? 1.0f : y);  // clamp, NaN passes
+        else if (p.bound == 2) y = tanhf(y);
+        if (p.scale) {
+            const float lo = slo[a], hi = shi[a];
+            y = __fadd_rn(lo, __fdiv_rn(__fmul_rn(__fsub_rn(hi, lo), __fadd_rn(y, 1.0f)), 2.0f));
+        }
+        act_remap[row * A + a] = y;
+    }
+}
+
+}  // namespace
+}  // namespace tsrl
+
+using namespace tsrl;
+
+extern "C" int64_t tsrl_policy_pack_floats(int64_t D) { return 2 * (kpad(D) / 2) * 64; }
+
+extern "C" int tsrl_policy_pack_l1(const float* W, int64_t D, float* packed, void* stream) {
+    TSRL_CHECK_ARG(W && packed && D > 0, "tsrl_policy_pack_l1: bad arguments");
+    const int64_t total = tsrl_policy_pack_floats(D);
+    const unsigned grid = (unsigned)std::min<int64_t>((total + 255) / 256, 1024);
+    hipLaunchKernelGGL(pack_l1_kernel, dim3(grid), dim3(256), 0, as_stream(stream), W, D, packed);
+    TSRL_LAUNCH_CHECK("tsrl_policy_pack_l1");
+    return 0;
+}
+
+extern "C" int tsrl_gauss_policy_act(const float* obs, int64_t ldx, int64_t n, int64_t D,
+                                     const float* w1packed, const float* b1, const float* w2,
+                                     const float* b2, const float* w3, const float* b3,
+                                     const float* log_std, int64_t act_dim, const float* eps,
+                                     int bound_method, const float* low, const float* high,
+                                     float* act, float* act_remap, void* stream) {
+    TSRL_CHECK_ARG(n >= 0 && D > 0 && D % 4 == 0 && ldx >= D && ldx % 4 == 0 && act_dim > 0 &&
+                       act_dim <= AMAX && bound_method >= 0 && bound_method <= 2,
+                   "tsrl_gauss_policy_act: bad sizes (D, ldx multiples of 4; 0 < act_dim <= %d)",
+                   AMAX);
+    if (n == 0) return 0;
+    TSRL_CHECK_ARG(obs && w1packed && b1 && w2 && b2 && w3 && b3 && log_std && act && act_remap,
+                   "tsrl_gauss_policy_act: null pointer");
+    TSRL_CHECK_ARG(aligned16(obs) && aligned16(w1packed),
+                   "tsrl_gauss_policy_act: obs / packed weights must be 16-byte aligned");
+    TSRL_CHECK_ARG((low == nullptr) == (high == nullptr), "tsrl_gauss_policy_act: low/high");
+    ActParams p{(int)act_dim, bound_method, low != nullptr, eps != nullptr};
+    hipLaunchKernelGGL(gauss_act_kernel, dim3((unsigned)((n + 31) / 32)), dim3(256), 0,
+                       as_stream(stream), obs, ldx, n, D, w1packed, b1, w2, b2, w3, b3, log_std,
+                       eps, low, high, p, act, act_remap);
+    TSRL_LAUNCH_CHECK("tsrl_gauss_policy_act");
+    return 0;
+}

@@ -95,6 +95,10 @@ _SIGS = {
                        PPOParams, _p, ctypes.POINTER(TailGrads), _p, _p, _i64, _p],
                       ctypes.c_int),
     "tsrl_mlp_dw_workspace_bytes": ([_i64, _i64], _i64),
+    "tsrl_policy_pack_floats": ([_i64], _i64),
+    "tsrl_policy_pack_l1": ([_p, _i64, _p, _p], ctypes.c_int),
+    "tsrl_gauss_policy_act": ([_p, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p, _p, _i64, _p,
+                               ctypes.c_int, _p, _p, _p, _p, _p], ctypes.c_int),
     "tsrl_mlp_dw": ([_p, _p, _i64, _p, _i64, _i64, _p, _p, _p, _p, _p, _i64, _p], ctypes.c_int),
 }
 

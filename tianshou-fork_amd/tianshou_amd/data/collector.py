@@ -53,6 +53,9 @@ class Collector:
         # vector steps per captured HIP graph (0 disables graph replay of the fused step)
         self.graph_steps = 16
         self._graph = None
+        # run the policy step as the fused HIP kernel when the policy offers one
+        self.use_fused_act = True
+        self._fused_act_on = False
         from tianshou_amd.dist import default_dp
         self.dp = default_dp()
         if sync_obs_rms and self.dp.active and self._norm is not None:
@@ -108,6 +111,9 @@ class Collector:
             part2=b.alloc_partials(N),
             env_id=torch.arange(N, device=dev),
         )
+        act_shape, act_dtype = self._act_spec()
+        self._scratch["act"] = torch.empty((N,) + act_shape, dtype=act_dtype, device=dev)
+        self._scratch["act_remap"] = torch.empty((N,) + act_shape, dtype=act_dtype, device=dev)
 
     def reset_env(self, gym_reset_kwargs: Optional[Dict[str, Any]] = None) -> None:
         if not self._fused:
@@ -219,10 +225,15 @@ class Collector:
         captured in a HIP graph."""
         s, b, buf = self._scratch, self._base, self.buffer
         act_shape, act_dtype = self._act_spec()
-        info = Batch(env_id=s["env_id"][:kk] if ids_t is None else ids_t)
-        act, _policy = self._policy_act(cur, info, random, no_grad, kk)
-        act = act.to(act_dtype).reshape((kk,) + act_shape).contiguous()
-        action_remap = self.policy.map_action(act)
+        if self._fused_act_on and not random:
+            # policy forward + sampling + map_action as one kernel (policy/fused_act.py)
+            act, action_remap = s["act"][:kk], s["act_remap"][:kk]
+            self.policy.fused_act(cur, act, action_remap)
+        else:
+            info = Batch(env_id=s["env_id"][:kk] if ids_t is None else ids_t)
+            act, _policy = self._policy_act(cur, info, random, no_grad, kk)
+            act = act.to(act_dtype).reshape((kk,) + act_shape).contiguous()
+            action_remap = self.policy.map_action(act)
         raw, rew = s["raw"][:kk], s["rew"][:kk]
         term, trunc, done = s["term"][:kk], s["trunc"][:kk], s["done"][:kk]
         b._step_raw(ids_t, kk, raw, rew, term, trunc, s["part"], action_remap)
@@ -256,7 +267,8 @@ class Collector:
             r = self._norm.obs_rms
             ptrs += [r.mean_t.data_ptr(), r.var_t.data_ptr(), r.count_t.data_ptr(),
                      self._norm.update_obs_rms]
-        return (G, self.policy.training, self.exploration_noise, tuple(ptrs))
+        return (G, self.policy.training, self.exploration_noise, self._fused_act_on,
+                tuple(ptrs))
 
     def _replay_steps(self, no_grad, n_steps: int, written: list) -> int:
         """Run up to n_steps uniform steps as replays of a captured G-step HIP graph; returns
@@ -288,6 +300,9 @@ class Collector:
 
     def _collect_fused(self, n_step, n_episode, random, no_grad):
         self._alloc_scratch()
+        prep = getattr(self.policy, "prepare_fused_act", None)
+        self._fused_act_on = bool(not random and not self.exploration_noise and
+                                  self.use_fused_act and prep is not None and prep())
         s, b, buf = self._scratch, self._base, self.buffer
         N = self.env_num
         act_shape, act_dtype = self._act_spec()

@@ -100,6 +100,10 @@ class BasePolicy(nn.Module):
     def forward(self, batch: Batch, state=None, **kwargs) -> Batch:
         raise NotImplementedError
 
+    def _is_box_action(self) -> bool:
+        return isinstance(self.action_space, Box) or (
+            hasattr(self.action_space, "low") and not hasattr(self.action_space, "n"))
+
     def _low_high(self, device):
         key = str(device)
         if key not in self._act_low_high:
@@ -112,9 +116,7 @@ class BasePolicy(nn.Module):
         """base.py:183-215: bound to [-1, 1] (clip / tanh), then scale to [low, high].
         Device tensors stay on device (the reference's [-1, 1] assert would need a
         device->host sync; it holds by construction after clip/tanh)."""
-        is_box = isinstance(self.action_space, Box) or (
-            hasattr(self.action_space, "low") and not hasattr(self.action_space, "n"))
-        if not is_box:
+        if not self._is_box_action():
             return act
         if isinstance(act, torch.Tensor):
             if self.action_bound_method == "clip":

@@ -49,6 +49,29 @@ class PGPolicy(BasePolicy):
             self._ret_rms = DeviceScalarRMS(dev)
         return self._ret_rms
 
+    # -- fused collector step (policy/fused_act.py) ------------------------------------------
+    def prepare_fused_act(self) -> bool:
+        """True when the collector may run this policy's act + map_action as the fused
+        kernel (Gaussian ActorProb of the get_actor_critic shape, Box actions); packs the
+        current first-layer weight."""
+        if not getattr(self, "_gauss_dist", False) or not self._is_box_action():
+            return False
+        fa = getattr(self, "_fused_act", None)
+        if fa is None:
+            from tianshou_amd.policy.fused_act import FusedGaussAct, match_actor
+            layers = match_actor(self.actor)
+            fa = FusedGaussAct(layers) if layers is not None else False
+            self._fused_act = fa
+        if fa is False or not next(self.actor.parameters()).is_cuda:
+            return False
+        fa.pack()
+        return True
+
+    def fused_act(self, obs, act_out, remap_out) -> None:
+        sample = not (self._deterministic_eval and not self.training)
+        low_high = self._low_high(obs.device) if self.action_scaling else None
+        self._fused_act(obs, act_out, remap_out, sample, self.action_bound_method, low_high)
+
     def _get_deterministic_action(self, logits):
         if self.action_type == "discrete":
             return logits.argmax(-1)

@@ -1,0 +1,97 @@
+"""Time the fused MLP kernels of one PPO minibatch at the benchmark shape (262144 rows,
+Box(376)/Box(17), 64-64 tanh nets) with HIP events, and report achieved f32 MFMA TFLOP/s.
+
+    python tools/mlp_kernel_bench.py [--rows 262144] [--D 376] [--A 17] [--iters 20]
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tianshou-fork_amd"))
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=262144)
+    ap.add_argument("--N", type=int, default=4096 * 2048)
+    ap.add_argument("--D", type=int, default=376)
+    ap.add_argument("--A", type=int, default=17)
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    from tianshou_amd import _C
+    from tianshou_amd.dist import DataParallel
+    from tianshou_amd.policy import fused_mlp
+    from tianshou_amd.utils.models import get_actor_critic, init_actor_critic
+    from tianshou_amd.utils.net import ActorCritic
+    dev = torch.device("cuda", 0)
+    actor, critic = get_actor_critic((a.D,), (64, 64), (a.A,), dev)
+    actor, critic = actor.to(dev), critic.to(dev)
+    init_actor_critic(actor, critic)
+    layers = fused_mlp.match(actor, critic)
+    fm = fused_mlp.FusedActorCritic(layers, ActorCritic(actor, critic).parameters())
+    N, B, D, A = a.N, a.rows, a.D, a.A
+    obs = torch.randn(N, D, device=dev)
+    act = torch.randn(N, A, device=dev)
+    logp_old = torch.randn(N, device=dev) - A
+    adv = torch.randn(N, device=dev)
+    ret = torch.randn(N, device=dev)
+    v_s = torch.randn(N, device=dev)
+    idx = torch.randperm(N, device=dev)[:B]
+    p = _C.PPOParams()
+    p.eps_clip, p.dual_clip, p.vf_coef, p.ent_coef, p.adv_eps = 0.2, 0.0, 0.25, 0.0, 1e-8
+    p.b_global, p.value_clip, p.norm_adv = float(B), 0, 1
+    dp = DataParallel()
+    fm.minibatch(obs, idx, B, act, logp_old, adv, ret, v_s, p, dp)
+    torch.cuda.synchronize()
+    L = _C.lib()
+    s = _C.stream_ptr(dev)
+    h1 = fm._bufs["h1"]
+    dz1 = fm._bufs["dz1"]
+    W = layers
+    flop_l1 = 2.0 * B * D * 128
+    flop_tail = 2.0 * B * (64 * 64 * 2 * 3 + 64 * 32 * 3 + 64 * 2)
+    sums = fm._bufs["sums"]
+    ws = fm._bufs["tail_ws"]
+    ws2 = fm._bufs["dw_ws"]
+    adv_sums = fm._bufs["adv_sums"]
+
+    def l1():
+        _C.check(L.tsrl_mlp_l1_fwd(_C.ptr(obs), D, _C.ptr(idx), B, D, _C.ptr(W["w1a"].weight),
+                                   _C.ptr(W["w1a"].bias), _C.ptr(W["w1c"].weight),
+                                   _C.ptr(W["w1c"].bias), 1, _C.ptr(h1), 1, s))
+
+    def tail():
+        _C.check(L.tsrl_ppo_tail(_C.ptr(h1), B, _C.ptr(idx), fm._tail_w, A, _C.ptr(act),
+                                 _C.ptr(logp_old), _C.ptr(adv), _C.ptr(ret), _C.ptr(v_s),
+                                 _C.ptr(adv_sums), p, _C.ptr(dz1), fm._tail_grads,
+                                 _C.ptr(sums), _C.ptr(ws), ws.numel(), s))
+
+    def dw():
+        _C.check(L.tsrl_mlp_dw(_C.ptr(dz1), _C.ptr(obs), D, _C.ptr(idx), B, D,
+                               _C.ptr(W["w1a"].weight.grad), _C.ptr(W["w1a"].bias.grad),
+                               _C.ptr(W["w1c"].weight.grad), _C.ptr(W["w1c"].bias.grad),
+                               _C.ptr(ws2), ws2.numel(), s))
+
+    def whole():
+        fm.minibatch(obs, idx, B, act, logp_old, adv, ret, v_s, p, dp)
+
+    for name, fn, flop in (("l1_fwd", l1, flop_l1), ("tail(+reduce)", tail, flop_tail),
+                           ("dw(+reduce)", dw, flop_l1), ("minibatch", whole, None)):
+        fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(a.iters):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / a.iters
+        tf = f"  {flop / us / 1e6:7.1f} TFLOP/s" if flop else ""
+        print(f"{name:16s} {us:9.1f} us{tf}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
