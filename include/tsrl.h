@@ -84,6 +84,15 @@ int tsrl_synth_box_step(const int64_t* ids, int64_t k, int64_t dim, uint64_t see
                         int64_t ep_len, int64_t* ep_j, int64_t* ep_t, float* obs_out,
                         double* rew_out, uint8_t* term_out, uint8_t* trunc_out,
                         double* col_partials, void* stream);
+/* Step every env (ids = identity) and reset the finished ones in the same launch: step rows
+ * -> obs_out with partials_step over all k rows; finished rows (done_out) -> reset_out with
+ * partials_reset over those rows only and blk_done[nblk] = finished rows per partial block
+ * (partials / blk_done all NULL when no obs normalisation is attached). */
+int tsrl_synth_box_step_reset(int64_t k, int64_t dim, uint64_t seed, int64_t ep_len,
+                              int64_t* ep_j, int64_t* ep_t, float* obs_out, float* reset_out,
+                              double* rew_out, uint8_t* term_out, uint8_t* trunc_out,
+                              uint8_t* done_out, double* partials_step,
+                              double* partials_reset, double* blk_done, void* stream);
 int tsrl_synth_box_reset(const int64_t* ids, const uint8_t* mask, int64_t k, int64_t dim,
                          uint64_t seed, int64_t ep_len, int64_t* ep_j, int64_t* ep_t,
                          float* obs_out, double* col_partials, void* stream);
@@ -108,6 +117,13 @@ int tsrl_synth_u8_reset(const int64_t* ids, const uint8_t* mask, int64_t k,
 int tsrl_rms_merge(const double* col_partials, int64_t nblk, int64_t dim,
                    const uint8_t* mask, int64_t k, const double* batch_count, float* mean,
                    float* var, double* count, unsigned int* ticket, void* stream);
+/* Two consecutive updates (step batch of k rows from partials_step, then the reset rows from
+ * partials_reset counted by blk_done) in one launch; snap_mean / snap_var receive the state
+ * after the first update (the statistics that normalise the step observations). */
+int tsrl_rms_merge2(const double* partials_step, const double* partials_reset,
+                    const double* blk_done, int64_t nblk, int64_t dim, int64_t k, float* mean,
+                    float* var, double* count, float* snap_mean, float* snap_var,
+                    unsigned int* ticket, void* stream);
 int tsrl_rms_norm_rows(const float* x, const uint8_t* mask, int64_t k, int64_t dim,
                        const float* mean, const float* var, float eps, float clip,
                        float* out, void* stream);
@@ -126,6 +142,11 @@ int tsrl_rms_norm_rows(const float* x, const uint8_t* mask, int64_t k, int64_t d
  *   ep_rew[b] += rew ; ep_len[b] += 1 ; on done record (ep_rew, ep_len, ep_idx+offset) in
  *   out_ep_* (per row, nullable) and stat_*[ptr] (per storage row, nullable), then reset
  *   and set ep_idx[b] = next_rel[r].
+ * Auto-reset (nullable): rows with reset_mask[r] set take cur_obs[r] <- norm(reset_src[r])
+ *   with reset_mean / reset_var (collector.py:342-361, the obs of the new episode).
+ * rel_ticket (nullable, zeroed device word, with rel_dev): the last workgroup advances
+ *   *rel_dev = (*rel_dev + 1) % ring_size after every workgroup has read it, replacing a
+ *   separate tsrl_ring_advance launch.
  * ------------------------------------------------------------------------------- */
 typedef struct tsrl_add_args {
     const int64_t* ids;      /* [k] env ids or NULL (identity) */
@@ -154,6 +175,10 @@ typedef struct tsrl_add_args {
     double* ep_rew; int64_t* ep_len; int64_t* ep_idx;
     double* out_ep_rew; int64_t* out_ep_len; int64_t* out_ep_idx; /* per row, nullable */
     double* stat_rew; int64_t* stat_len; int64_t* stat_idx;       /* per storage row */
+    /* auto-reset rows and fused ring advance (nullable) */
+    const float* reset_src; const uint8_t* reset_mask;
+    const float* reset_mean; const float* reset_var;
+    unsigned int* rel_ticket;
 } tsrl_add_args;
 int tsrl_buffer_add(const tsrl_add_args* a, void* stream);
 /* *rel_dev = (*rel_dev + 1) % ring_size (device-side ring cursor for graph-captured steps). */
@@ -252,6 +277,12 @@ int tsrl_ppo_tail(const float* h1frag, int64_t n, const int64_t* idx,
                   const double* adv_sums, tsrl_ppo_params p, float* dz1,
                   const tsrl_tail_grads* grads, double* sums, void* workspace,
                   int64_t ws_bytes, void* stream);
+/* tsrl_ppo_eval: forward only (process_fn): value_out[n] = critic(obs) and, when logp_out is
+ * given, logp_out[n] = log N(act | mu(obs), exp(log_std)) summed over the action dims, from
+ * the fragment-layout layer-1 activations of tsrl_mlp_l1_fwd (critic only: the actor tiles
+ * are not read). */
+int tsrl_ppo_eval(const float* h1frag, int64_t n, const tsrl_tail_weights* w, int64_t act_dim,
+                  const float* act, float* value_out, float* logp_out, void* stream);
 int64_t tsrl_mlp_dw_workspace_bytes(int64_t n, int64_t D);
 int tsrl_mlp_dw(const float* dz1, const float* X, int64_t ldx, const int64_t* idx, int64_t n,
                 int64_t D, float* gWa, float* gba, float* gWc, float* gbc, void* workspace,
@@ -274,6 +305,16 @@ int tsrl_gauss_policy_act(const float* obs, int64_t ldx, int64_t n, int64_t D,
                           const float* log_std, int64_t act_dim, const float* eps,
                           int bound_method, const float* low, const float* high, float* act,
                           float* act_remap, void* stream);
+/* Same step drawing the noise in-kernel: standard normals from a splitmix64 counter hash of
+ * (seed, *rng_ctr, row, dim) through Box-Muller; the last workgroup increments *rng_ctr
+ * (rng_ticket: a zeroed device word), so HIP-graph replays draw fresh noise each step. */
+int tsrl_gauss_policy_act_rng(const float* obs, int64_t ldx, int64_t n, int64_t D,
+                              const float* w1packed, const float* b1, const float* w2,
+                              const float* b2, const float* w3, const float* b3,
+                              const float* log_std, int64_t act_dim, uint64_t seed,
+                              int64_t* rng_ctr, unsigned int* rng_ticket, int bound_method,
+                              const float* low, const float* high, float* act,
+                              float* act_remap, void* stream);
 
 #ifdef __cplusplus
 }

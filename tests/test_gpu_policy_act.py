@@ -86,6 +86,7 @@ def test_collector_fused_act_matches_torch_path(dev):
         optim = init_and_get_optim(actor.to(dev), critic.to(dev), 3e-4)
         pol = PPOPolicy(actor, critic, optim, fixed_std_normal,
                         action_space=Box(-1.0, 1.0, (A,))).to(dev)
+        pol.fused_act_rng = "torch"  # the torch path's noise stream, for an exact comparison
         env = VectorEnvNormObs(SyntheticVectorEnv(E, (D,), A, ep_len=13, seed=3, device=dev))
         buf = VectorReplayBuffer(E * T, E, device=dev)
         c = Collector(pol, env, buf)
@@ -100,3 +101,32 @@ def test_collector_fused_act_matches_torch_path(dev):
         assert torch.equal(out[0][k], out[1][k]), k
     np.testing.assert_allclose(out[0]["act"].numpy(), out[1]["act"].numpy(), rtol=1e-5,
                                atol=1e-5)
+
+
+def test_device_rng_noise_is_standard_normal(dev):
+    """tsrl_gauss_policy_act_rng: zero weights make mu = b3 = 0 and sigma = 1, so the actions
+    are the raw noise: mean ~ 0, std ~ 1, fresh per call, reproducible per seed."""
+    from tianshou_amd import _C
+    from tianshou_amd.policy.fused_act import FusedGaussAct, match_actor
+    D, A, n = 8, 6, 8192
+    actor = _actor(D, A, dev, 1)
+    with torch.no_grad():
+        for p in actor.parameters():
+            p.zero_()
+    fa = FusedGaussAct(match_actor(actor))
+    obs = torch.randn(n, D, device=dev)
+    outs = []
+    for rep in range(2):
+        torch.manual_seed(123)
+        fa.pack()
+        for _ in range(2):
+            act = torch.empty(n, A, device=dev)
+            remap = torch.empty(n, A, device=dev)
+            fa(obs, act, remap, True, None, None)
+            outs.append(act.cpu())
+    x = torch.cat(outs[:2]).double()
+    assert abs(x.mean().item()) < 0.02 and abs(x.std().item() - 1.0) < 0.02
+    assert abs(((x - x.mean()) ** 3).mean().item()) < 0.05        # symmetric
+    assert abs(((x - x.mean()) ** 4).mean().item() - 3.0) < 0.15  # normal kurtosis
+    assert not torch.equal(outs[0], outs[1])      # counter advances per call
+    assert torch.equal(outs[0], outs[2]) and torch.equal(outs[1], outs[3])  # seeded

@@ -39,60 +39,83 @@ __device__ __forceinline__ float norm1(float x, float m, float v, float eps, flo
 __global__ __launch_bounds__(TPB) void buffer_add_kernel(tsrl_add_args a) {
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t r = (int64_t)blockIdx.x * ROWS_PER_BLOCK + threadIdx.x / kWave;
-    if (r >= a.k) return;
-    const int64_t b = a.ids ? a.ids[r] : r;
     const int64_t urel = a.rel_dev ? *a.rel_dev : a.uniform_rel;
-    const int64_t ptr = a.ptr ? a.ptr[r] : a.offset[b] + urel;
+    if (r < a.k) {
+        const int64_t b = a.ids ? a.ids[r] : r;
+        const int64_t ptr = a.ptr ? a.ptr[r] : a.offset[b] + urel;
 
-    if (a.obs_src && a.obs_dst)
-        copy_row((const char*)a.obs_src + r * a.obs_row_bytes,
-                 (char*)a.obs_dst + ptr * a.obs_row_bytes, a.obs_row_bytes, lane);
-    if (a.act_src && a.act_dst)
-        copy_row((const char*)a.act_src + r * a.act_row_bytes,
-                 (char*)a.act_dst + ptr * a.act_row_bytes, a.act_row_bytes, lane);
-    if (a.obs_next_src_raw && a.obs_next_dst_raw)
-        copy_row((const char*)a.obs_next_src_raw + r * a.obs_row_bytes,
-                 (char*)a.obs_next_dst_raw + ptr * a.obs_row_bytes, a.obs_row_bytes, lane);
-    if (a.obs_next_src && (a.obs_next_dst || a.cur_obs)) {
-        const float* src = a.obs_next_src + r * a.obs_dim;
-        float* dst = a.obs_next_dst ? a.obs_next_dst + ptr * a.obs_dim : nullptr;
-        float* cur = a.cur_obs ? a.cur_obs + r * a.obs_dim : nullptr;
-        const bool nrm = a.norm_mean != nullptr;
-        for (int64_t d = lane; d < a.obs_dim; d += kWave) {
-            float x = src[d];
-            if (nrm) x = norm1(x, a.norm_mean[d], a.norm_var[d], a.norm_eps, a.norm_clip);
-            if (dst) dst[d] = x;
-            if (cur) cur[d] = x;
+        if (a.obs_src && a.obs_dst)
+            copy_row((const char*)a.obs_src + r * a.obs_row_bytes,
+                     (char*)a.obs_dst + ptr * a.obs_row_bytes, a.obs_row_bytes, lane);
+        if (a.act_src && a.act_dst)
+            copy_row((const char*)a.act_src + r * a.act_row_bytes,
+                     (char*)a.act_dst + ptr * a.act_row_bytes, a.act_row_bytes, lane);
+        if (a.obs_next_src_raw && a.obs_next_dst_raw)
+            copy_row((const char*)a.obs_next_src_raw + r * a.obs_row_bytes,
+                     (char*)a.obs_next_dst_raw + ptr * a.obs_row_bytes, a.obs_row_bytes, lane);
+        if (a.obs_next_src && (a.obs_next_dst || a.cur_obs)) {
+            const float* src = a.obs_next_src + r * a.obs_dim;
+            float* dst = a.obs_next_dst ? a.obs_next_dst + ptr * a.obs_dim : nullptr;
+            float* cur = a.cur_obs ? a.cur_obs + r * a.obs_dim : nullptr;
+            const bool nrm = a.norm_mean != nullptr;
+            const bool rst = a.reset_mask && a.reset_mask[r];
+            for (int64_t d = lane; d < a.obs_dim; d += kWave) {
+                float x = src[d];
+                if (nrm) x = norm1(x, a.norm_mean[d], a.norm_var[d], a.norm_eps, a.norm_clip);
+                if (dst) dst[d] = x;
+                if (cur) {
+                    if (rst) {
+                        x = a.reset_src[r * a.obs_dim + d];
+                        if (a.reset_mean)
+                            x = norm1(x, a.reset_mean[d], a.reset_var[d], a.norm_eps, a.norm_clip);
+                    }
+                    cur[d] = x;
+                }
+            }
+        }
+        if (lane == 0) {
+            const double rew = a.rew ? a.rew[r] : 0.0;
+            const uint8_t tm = a.term ? a.term[r] : 0;
+            const uint8_t tr = a.trunc ? a.trunc[r] : 0;
+            const uint8_t done = (uint8_t)((tm != 0) | (tr != 0));
+            if (a.rew_dst) a.rew_dst[ptr] = rew;
+            if (a.term_dst) a.term_dst[ptr] = (uint8_t)(tm != 0);
+            if (a.trunc_dst) a.trunc_dst[ptr] = (uint8_t)(tr != 0);
+            if (a.done_dst) a.done_dst[ptr] = done;
+            if (a.env_id_dst) a.env_id_dst[ptr] = b;
+            // ReplayBuffer._add_index episode bookkeeping (base.py:205-214)
+            const double er = a.ep_rew[b] + rew;
+            const int64_t el = a.ep_len[b] + 1;
+            const int64_t ei = a.ep_idx[b] + a.offset[b];
+            if (a.out_ep_rew) a.out_ep_rew[r] = done ? er : er * 0.0;
+            if (a.out_ep_len) a.out_ep_len[r] = done ? el : 0;
+            if (a.out_ep_idx) a.out_ep_idx[r] = ei;
+            if (done) {
+                if (a.stat_rew) a.stat_rew[ptr] = er;
+                if (a.stat_len) a.stat_len[ptr] = el;
+                if (a.stat_idx) a.stat_idx[ptr] = ei;
+                a.ep_rew[b] = 0.0;
+                a.ep_len[b] = 0;
+                a.ep_idx[b] = a.next_rel ? a.next_rel[r]
+                                          : (a.rel_dev ? (urel + 1) % a.ring_size : a.uniform_next);
+            } else {
+                a.ep_rew[b] = er;
+                a.ep_len[b] = el;
+            }
         }
     }
-    if (lane == 0) {
-        const double rew = a.rew ? a.rew[r] : 0.0;
-        const uint8_t tm = a.term ? a.term[r] : 0;
-        const uint8_t tr = a.trunc ? a.trunc[r] : 0;
-        const uint8_t done = (uint8_t)((tm != 0) | (tr != 0));
-        if (a.rew_dst) a.rew_dst[ptr] = rew;
-        if (a.term_dst) a.term_dst[ptr] = (uint8_t)(tm != 0);
-        if (a.trunc_dst) a.trunc_dst[ptr] = (uint8_t)(tr != 0);
-        if (a.done_dst) a.done_dst[ptr] = done;
-        if (a.env_id_dst) a.env_id_dst[ptr] = b;
-        // ReplayBuffer._add_index episode bookkeeping (base.py:205-214)
-        const double er = a.ep_rew[b] + rew;
-        const int64_t el = a.ep_len[b] + 1;
-        const int64_t ei = a.ep_idx[b] + a.offset[b];
-        if (a.out_ep_rew) a.out_ep_rew[r] = done ? er : er * 0.0;
-        if (a.out_ep_len) a.out_ep_len[r] = done ? el : 0;
-        if (a.out_ep_idx) a.out_ep_idx[r] = ei;
-        if (done) {
-            if (a.stat_rew) a.stat_rew[ptr] = er;
-            if (a.stat_len) a.stat_len[ptr] = el;
-            if (a.stat_idx) a.stat_idx[ptr] = ei;
-            a.ep_rew[b] = 0.0;
-            a.ep_len[b] = 0;
-            a.ep_idx[b] = a.next_rel ? a.next_rel[r]
-                                      : (a.rel_dev ? (urel + 1) % a.ring_size : a.uniform_next);
-        } else {
-            a.ep_rew[b] = er;
-            a.ep_len[b] = el;
+    if (a.rel_ticket && a.rel_dev) {
+        // every workgroup has read *rel_dev above; the last one to arrive advances it
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const unsigned int t = __hip_atomic_fetch_add(a.rel_ticket, 1u, __ATOMIC_ACQ_REL,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
+            if (t == gridDim.x - 1) {
+                int64_t* rd = const_cast<int64_t*>(a.rel_dev);
+                __hip_atomic_store(rd, (urel + 1) % a.ring_size, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(a.rel_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
     }
 }
@@ -234,6 +257,10 @@ extern "C" int tsrl_buffer_add(const tsrl_add_args* a, void* stream) {
     TSRL_CHECK_ARG(!a->norm_mean || a->norm_var, "tsrl_buffer_add: norm_var missing");
     TSRL_CHECK_ARG(!a->rel_dev || (a->ring_size > 0 && !a->ptr),
                    "tsrl_buffer_add: rel_dev needs ring_size and ptr == NULL");
+    TSRL_CHECK_ARG(!a->reset_mask || (a->reset_src && a->cur_obs),
+                   "tsrl_buffer_add: reset_mask needs reset_src and cur_obs");
+    TSRL_CHECK_ARG(!a->reset_mean || a->reset_var, "tsrl_buffer_add: reset_var missing");
+    TSRL_CHECK_ARG(!a->rel_ticket || a->rel_dev, "tsrl_buffer_add: rel_ticket needs rel_dev");
     const int64_t grid = (a->k + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK;
     hipLaunchKernelGGL(buffer_add_kernel, dim3((unsigned)grid), dim3(TPB), 0, as_stream(stream),
                        *a);

@@ -104,6 +104,57 @@ __global__ __launch_bounds__(TPB) void box_reset_kernel(const int64_t* ids, cons
     box_rows(rs, r0, k, dim, obs, partials);
 }
 
+// Step + auto-reset in one launch (the Collector's step followed by reset of the finished
+// envs, collector.py:310-361): raw step rows -> obs_out with partials P1 over every row;
+// rows whose episode ended are reset at once -> reset_out with partials P2 over those rows
+// only, and blk_done[block] counts them (the reset batch size of the second obs_rms update).
+__global__ __launch_bounds__(TPB) void box_step_reset_kernel(
+    int64_t k, int64_t dim, uint64_t s_seed, int64_t ep_len, int64_t* ep_j, int64_t* ep_t,
+    float* obs, float* reset_obs, double* rew, uint8_t* term, uint8_t* trunc, uint8_t* done,
+    double* p_step, double* p_reset, double* blk_done) {
+    __shared__ RowState rs[ROWS], rr[ROWS];
+    __shared__ int nd;
+    const int64_t r0 = (int64_t)blockIdx.x * ROWS;
+    if (threadIdx.x == 0) nd = 0;
+    __syncthreads();
+    if (threadIdx.x < ROWS) {
+        const int64_t r = r0 + threadIdx.x;
+        RowState st = {0ull, 0}, sr = {0ull, 0};
+        if (r < k) {
+            const int64_t e = r;
+            int64_t j = ep_j[e];
+            int64_t t = ep_t[e] + 1;
+            st.key = env_key(s_seed, (uint64_t)e, j, t);
+            st.active = 1;
+            const uint64_t h = sm64(st.key ^ REW_SALT);
+            rew[r] = (double)(h >> 40) * 0x1p-24;
+            const bool dn = t >= ep_len;
+            term[r] = (uint8_t)(dn && (e % 2 == 0));
+            trunc[r] = (uint8_t)(dn && (e % 2 == 1));
+            done[r] = (uint8_t)dn;
+            if (dn) {
+                j += 1;
+                t = (j == 0) ? (e % ep_len) : 0;
+                ep_j[e] = j;
+                sr.key = env_key(s_seed, (uint64_t)e, j, t);
+                sr.active = 1;
+                atomicAdd(&nd, 1);
+            }
+            ep_t[e] = t;
+        }
+        rs[threadIdx.x] = st;
+        rr[threadIdx.x] = sr;
+    }
+    __syncthreads();
+    box_rows(rs, r0, k, dim, obs, p_step);
+    if (nd > 0) {
+        box_rows(rr, r0, k, dim, reset_obs, p_reset);
+    } else if (p_reset) {
+        // no reset row in this block: the merge skips blocks with blk_done == 0
+    }
+    if (threadIdx.x == 0 && blk_done) blk_done[blockIdx.x] = (double)nd;
+}
+
 // u8 (Atari-shaped) observations: 4 bytes per thread-iteration, packed 32-bit stores.
 __device__ void u8_rows(const RowState* rs, int64_t r0, int64_t k, int64_t nbytes,
                         uint8_t* obs) {
@@ -204,6 +255,28 @@ extern "C" int tsrl_synth_box_step(const int64_t* ids, int64_t k, int64_t dim, u
                        ids, k, dim, sm64(seed), ep_len, ep_j, ep_t, obs_out, rew_out, term_out,
                        trunc_out, col_partials);
     TSRL_LAUNCH_CHECK("tsrl_synth_box_step");
+    return 0;
+}
+
+extern "C" int tsrl_synth_box_step_reset(int64_t k, int64_t dim, uint64_t seed, int64_t ep_len,
+                                         int64_t* ep_j, int64_t* ep_t, float* obs_out,
+                                         float* reset_out, double* rew_out, uint8_t* term_out,
+                                         uint8_t* trunc_out, uint8_t* done_out,
+                                         double* partials_step, double* partials_reset,
+                                         double* blk_done, void* stream) {
+    TSRL_CHECK_ARG(k >= 0 && dim > 0 && ep_len > 0, "tsrl_synth_box_step_reset: bad sizes");
+    if (k == 0) return 0;
+    TSRL_CHECK_ARG(ep_j && ep_t && obs_out && reset_out && rew_out && term_out && trunc_out &&
+                       done_out,
+                   "tsrl_synth_box_step_reset: null pointer");
+    TSRL_CHECK_ARG((partials_step == nullptr) == (partials_reset == nullptr) &&
+                       (partials_step == nullptr) == (blk_done == nullptr),
+                   "tsrl_synth_box_step_reset: partials / blk_done must be all set or all NULL");
+    hipLaunchKernelGGL(box_step_reset_kernel, dim3(blocks_for(k)), dim3(TPB), 0,
+                       as_stream(stream), k, dim, sm64(seed), ep_len, ep_j, ep_t, obs_out,
+                       reset_out, rew_out, term_out, trunc_out, done_out, partials_step,
+                       partials_reset, blk_done);
+    TSRL_LAUNCH_CHECK("tsrl_synth_box_step_reset");
     return 0;
 }
 

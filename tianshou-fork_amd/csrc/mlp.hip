@@ -148,7 +148,7 @@ __global__ __launch_bounds__(256, 2) void l1_fwd_kernel(
         for (int r = 0; r < 16; ++r) {
             const int f = 32 * i + rho(r) + 4 * h;
             float z = acc[i][r] + sb[f];
-            v[r] = act_tanh ? tanhf(z) : z;
+            v[r] = act_tanh ? tanh_nb(z) : z;
         }
         if (frag_out) {
             float4* o = reinterpret_cast<float4*>(out + ((bt * NT + i) * 64 + l) * 16);
@@ -270,7 +270,7 @@ __device__ __forceinline__ void wave_sync_lds() {
 
 // the actor half needs ~330 registers (1 wave per SIMD); the critic half fits 2 per SIMD
 template <int NET>
-__global__ __launch_bounds__(TAIL_TPB, NET == 0 ? 1 : 2) void ppo_tail_kernel(
+__global__ __launch_bounds__(TAIL_TPB, 2) void ppo_tail_kernel(
     const float* __restrict__ h1f, int64_t n, const int64_t* __restrict__ idx, TailWeights wt,
     const float* __restrict__ act, const float* __restrict__ logp_old,
     const float* __restrict__ adv, const float* __restrict__ ret, const float* __restrict__ v_s,
@@ -352,9 +352,11 @@ __global__ __launch_bounds__(TAIL_TPB, NET == 0 ? 1 : 2) void ppo_tail_kernel(
             }
         }
         // ---- layer 2 -----------------------------------------------------------------------
+        __builtin_amdgcn_sched_barrier(0);
         float h2[2][16];
 #pragma unroll
         for (int ot = 0; ot < 2; ++ot) {
+            __builtin_amdgcn_sched_barrier(0);
             f32x16 z = zero16();
             const float* wa = sW2 + (32 * ot + c) * WS2 + 4 * h;
 #pragma unroll
@@ -363,11 +365,12 @@ __global__ __launch_bounds__(TAIL_TPB, NET == 0 ? 1 : 2) void ppo_tail_kernel(
                 for (int r = 0; r < 16; ++r) z = mfma(wa[32 * it + rho(r)], h1[it][r], z);
 #pragma unroll
             for (int r = 0; r < 16; ++r)
-                h2[ot][r] = tanhf(z[r] + sm[T_B2 + 32 * ot + rho(r) + 4 * h]);
+                h2[ot][r] = tanh_nb(z[r] + sm[T_B2 + 32 * ot + rho(r) + 4 * h]);
         }
         float dz2[2][16];
         if constexpr (actor) {
             // ---- mu head + clipped surrogate ----------------------------------------------
+            __builtin_amdgcn_sched_barrier(0);
             f32x16 mu = zero16();
             {
                 const float* wa = sW3 + c * WS2 + 4 * h;
@@ -428,6 +431,7 @@ __global__ __launch_bounds__(TAIL_TPB, NET == 0 ? 1 : 2) void ppo_tail_kernel(
                     cnt_acc += 1.0;
                 }
             }
+            __builtin_amdgcn_sched_barrier(0);
             float dmu[1][16], dls[16];
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
@@ -438,9 +442,12 @@ __global__ __launch_bounds__(TAIL_TPB, NET == 0 ? 1 : 2) void ppo_tail_kernel(
             }
             dls_acc += (double)rs_sum16(dls, l);
             gb3 += rs_sum16(dmu[0], l);
+            __builtin_amdgcn_sched_barrier(0);
             // dW3a = dMu^T . H2a over the 32 rows, two half passes
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int half = 0; half < 2; ++half) {
+                __builtin_amdgcn_sched_barrier(0);
                 wave_sync_lds();
                 put_half<1>(S1, dmu, c, h, half);
                 put_half<2>(S2, h2, c, h, half);
@@ -448,8 +455,10 @@ __global__ __launch_bounds__(TAIL_TPB, NET == 0 ? 1 : 2) void ppo_tail_kernel(
                 acc_wgrad<1, 2>(gW3, S1, S2, c, h);
             }
             // dZ2 = (W3a^T dMu) * (1 - H2^2)
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int ft = 0; ft < 2; ++ft) {
+                __builtin_amdgcn_sched_barrier(0);
                 f32x16 d = zero16();
 #pragma unroll
                 for (int r = 0; r < 16; ++r)
@@ -518,8 +527,29 @@ __global__ __launch_bounds__(TAIL_TPB, NET == 0 ? 1 : 2) void ppo_tail_kernel(
                                  (1.0f - h2[ft][r] * h2[ft][r]);
         }
         // ---- dZ1 = (W2^T dZ2) * (1 - H1^2) -> HBM (row-major [n][128]) -------------------
+        __builtin_amdgcn_sched_barrier(0);
+        {
+            // re-read this tile's H1 (L2-hot) instead of keeping it live through the loss and
+            // head phases: an opaque zero offset stops the compiler from reusing the first load
+            int zoff;
+            asm volatile("s_mov_b32 %0, 0" : "=s"(zoff));
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const float4* src = reinterpret_cast<const float4*>(
+                    h1f + ((bt * NT + 2 * net + i) * 64 + l) * 16 + zoff);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 v = src[q];
+                    h1[i][4 * q] = v.x;
+                    h1[i][4 * q + 1] = v.y;
+                    h1[i][4 * q + 2] = v.z;
+                    h1[i][4 * q + 3] = v.w;
+                }
+            }
+        }
 #pragma unroll
         for (int ft = 0; ft < 2; ++ft) {
+            __builtin_amdgcn_sched_barrier(0);
             f32x16 d = zero16();
 #pragma unroll
             for (int ot = 0; ot < 2; ++ot)
@@ -538,10 +568,12 @@ __global__ __launch_bounds__(TAIL_TPB, NET == 0 ? 1 : 2) void ppo_tail_kernel(
             }
         }
         // ---- db2, dW2 = dZ2^T . H1 ---------------------------------------------------------
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int ot = 0; ot < 2; ++ot) gb2[ot] += rs_sum16(dz2[ot], l);
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
+            __builtin_amdgcn_sched_barrier(0);
             wave_sync_lds();
             put_half<2>(S1, dz2, c, h, half);
             put_half<2>(S2, h1, c, h, half);
@@ -618,19 +650,153 @@ __global__ __launch_bounds__(TAIL_TPB, NET == 0 ? 1 : 2) void ppo_tail_kernel(
     if (actor && t == 3) sd[3] = 0.0;
 }
 
+// ---------------------------------------------------------------------------------------
+// Forward-only evaluation for PPOPolicy.process_fn: critic values V(s) (a2c.py:83-100) and,
+// with LOGP, the Gaussian log-prob of the stored actions (logp_old, ppo.py:95-96), from the
+// layer-1 activations of tsrl_mlp_l1_fwd.  One wave = 32 rows.
+// ---------------------------------------------------------------------------------------
+constexpr int E_W2A = 0, E_W2C = E_W2A + H * WS2, E_W3 = E_W2C + H * WS2, E_B2A = E_W3 + AMAX * WS2,
+              E_B2C = E_B2A + H, E_B3 = E_B2C + H, E_W3C = E_B3 + AMAX, E_VAR = E_W3C + H,
+              E_LS = E_VAR + AMAX, E_END = E_LS + AMAX;
+
+template <bool LOGP>
+__global__ __launch_bounds__(256, 2) void eval_tail_kernel(const float* __restrict__ h1f,
+                                                           int64_t n, TailWeights wt, int A,
+                                                           const float* __restrict__ act,
+                                                           float* __restrict__ value_out,
+                                                           float* __restrict__ logp_out) {
+    __shared__ float sm[E_END];
+    const int t = threadIdx.x;
+    const int w = t >> 6, l = t & 63, h = l >> 5, c = l & 31;
+    for (int i = t; i < H * H; i += 256) {
+        sm[E_W2C + (i >> 6) * WS2 + (i & 63)] = wt.w2c[i];
+        if (LOGP) sm[E_W2A + (i >> 6) * WS2 + (i & 63)] = wt.w2a[i];
+    }
+    if (LOGP) {
+        for (int i = t; i < AMAX * H; i += 256) {
+            const int a = i >> 6;
+            sm[E_W3 + a * WS2 + (i & 63)] = a < A ? wt.w3a[i] : 0.0f;
+        }
+    }
+    if (t < H) {
+        sm[E_B2C + t] = wt.b2c[t];
+        sm[E_W3C + t] = wt.w3c[t];
+        if (LOGP) sm[E_B2A + t] = wt.b2a[t];
+    }
+    if (LOGP && t < AMAX) {
+        sm[E_B3 + t] = t < A ? wt.b3a[t] : 0.0f;
+        const float sig = t < A ? expf(wt.log_std[t]) : 1.0f;
+        sm[E_VAR + t] = sig * sig;
+        sm[E_LS + t] = logf(sig);
+    }
+    __syncthreads();
+    const float b3c = wt.b3c[0];
+    const int64_t ntiles = (n + 31) / 32;
+    for (int64_t bt = (int64_t)blockIdx.x * 4 + w; bt < ntiles; bt += (int64_t)gridDim.x * 4) {
+        const int64_t brow = bt * 32 + c;
+        const bool live = brow < n;
+#pragma unroll
+        for (int net = LOGP ? 0 : 1; net < 2; ++net) {
+            __builtin_amdgcn_sched_barrier(0);  // one net at a time (register pressure)
+            float h1[2][16];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const float4* src = reinterpret_cast<const float4*>(
+                    h1f + ((bt * NT + 2 * net + i) * 64 + l) * 16);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 v = src[q];
+                    h1[i][4 * q] = v.x;
+                    h1[i][4 * q + 1] = v.y;
+                    h1[i][4 * q + 2] = v.z;
+                    h1[i][4 * q + 3] = v.w;
+                }
+            }
+            const float* sW2 = sm + (net ? E_W2C : E_W2A);
+            const float* sb2 = sm + (net ? E_B2C : E_B2A);
+            float h2[2][16];
+#pragma unroll
+            for (int ot = 0; ot < 2; ++ot) {
+                f32x16 z = zero16();
+                const float* wa = sW2 + (32 * ot + c) * WS2 + 4 * h;
+#pragma unroll
+                for (int it = 0; it < 2; ++it)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) z = mfma(wa[32 * it + rho(r)], h1[it][r], z);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) h2[ot][r] = tanh_nb(z[r] + sb2[32 * ot + rho(r) + 4 * h]);
+            }
+            if (net == 1) {
+                float vpart = 0.0f;
+#pragma unroll
+                for (int it = 0; it < 2; ++it)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        vpart += sm[E_W3C + 32 * it + rho(r) + 4 * h] * h2[it][r];
+                const float value = vpart + __shfl_xor(vpart, 32, 64) + b3c;
+                if (live && h == 0) value_out[brow] = value;
+            } else {
+                f32x16 mu = zero16();
+                const float* wa = sm + E_W3 + c * WS2 + 4 * h;
+#pragma unroll
+                for (int it = 0; it < 2; ++it)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) mu = mfma(wa[32 * it + rho(r)], h2[it][r], mu);
+                float lp = 0.0f;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int a = rho(r) + 4 * h;
+                    if (a < A && live) {
+                        const float diff = act[brow * A + a] - (mu[r] + sm[E_B3 + a]);
+                        lp += -(diff * diff) / (2.0f * sm[E_VAR + a]) - sm[E_LS + a] - LOG_SQRT_2PI;
+                    }
+                }
+                const float logp = lp + __shfl_xor(lp, 32, 64);
+                if (live && h == 0) logp_out[brow] = logp;
+            }
+        }
+    }
+}
+
 // Folds the per-workgroup slabs (fixed order) into the parameter gradients and the loss sums.
 struct TailGrads {
     float *w2a, *b2a, *w2c, *b2c, *w3a, *b3a, *w3c, *b3c;
 };
 
+// Sum over `nslab` slabs (stride `stride` elements) of element i, fixed order: 4 lane groups
+// of the workgroup take slabs g, g+4, ... with 4 independent accumulators each (loads stay in
+// flight), then the groups combine in order through LDS.  Block = 64 outputs x 4 groups.
+template <typename T>
+__device__ __forceinline__ T slab_sum(const T* __restrict__ base, int64_t stride, int nslab,
+                                      int64_t i, bool valid, T* sh) {
+    const int o = threadIdx.x & 63, g = threadIdx.x >> 6;
+    T a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    if (valid) {
+        int k = g;
+        for (; k + 12 < nslab; k += 16) {
+            a0 += base[(int64_t)k * stride + i];
+            a1 += base[(int64_t)(k + 4) * stride + i];
+            a2 += base[(int64_t)(k + 8) * stride + i];
+            a3 += base[(int64_t)(k + 12) * stride + i];
+        }
+        for (; k < nslab; k += 4) a0 += base[(int64_t)k * stride + i];
+    }
+    sh[g * 64 + o] = (a0 + a1) + (a2 + a3);
+    __syncthreads();
+    return ((sh[o] + sh[64 + o]) + sh[128 + o]) + sh[192 + o];
+}
+
 __global__ __launch_bounds__(256) void tail_reduce_kernel(const float* __restrict__ slab_f,
                                                           const double* __restrict__ slab_d,
                                                           int nslab, int A, TailGrads g,
                                                           double* __restrict__ sums) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i < SL_F) {
-        float s = 0.0f;
-        for (int k = 0; k < nslab; ++k) s += slab_f[(int64_t)k * SL_F + i];
+    __shared__ float shf[256];
+    __shared__ double shd[256];
+    const int nfb = (SL_F + 63) / 64;
+    if ((int)blockIdx.x < nfb) {
+        const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+        const float s = slab_sum(slab_f, SL_F, nslab, i, i < SL_F, shf);
+        if (threadIdx.x >= 64 || i >= SL_F) return;
         if (i < SL_B2A) g.w2a[i] = s;
         else if (i < SL_W2C) g.b2a[i - SL_B2A] = s;
         else if (i < SL_B2C) g.w2c[i - SL_W2C] = s;
@@ -639,11 +805,10 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(const float* __restric
         else if (i < SL_W3C) { if (i - SL_B3A < A) g.b3a[i - SL_B3A] = s; }
         else if (i < SL_B3C) g.w3c[i - SL_W3C] = s;
         else if (i == SL_B3C) g.b3c[0] = s;
-    } else if (i < SL_F + SL_D) {
-        const int k0 = i - SL_F;
-        double s = 0.0;
-        for (int k = 0; k < nslab; ++k) s += slab_d[(int64_t)k * SL_D + k0];
-        if (k0 < 4 + A) sums[k0] = s;
+    } else {
+        const int k0 = threadIdx.x & 63;
+        const double s = slab_sum(slab_d, SL_D, nslab, k0, k0 < SL_D, shd);
+        if (threadIdx.x < 64 && k0 < 4 + A) sums[k0] = s;
     }
 }
 
@@ -756,12 +921,13 @@ __global__ __launch_bounds__(256) void dw_reduce_kernel(const float* __restrict_
                                                         float* __restrict__ gba,
                                                         float* __restrict__ gWc,
                                                         float* __restrict__ gbc) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= (int64_t)HC * ncolpad) return;
+    __shared__ float sh[256];
+    const int64_t i = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+    const int64_t total = (int64_t)HC * ncolpad;
     const int f = (int)(i / ncolpad), k = (int)(i - (int64_t)f * ncolpad);
-    if (k > D) return;
-    float s = 0.0f;
-    for (int sp = 0; sp < nsplit; ++sp) s += part[(int64_t)sp * HC * ncolpad + i];
+    const bool valid = i < total && k <= D;
+    const float s = slab_sum(part, total, nsplit, i, valid, sh);
+    if (threadIdx.x >= 64 || !valid) return;
     if (k == D) {
         if (f < H) gba[f] = s; else gbc[f - H] = s;
     } else {
@@ -862,7 +1028,7 @@ extern "C" int tsrl_ppo_tail(const float* h1frag, int64_t n, const int64_t* idx,
     TSRL_LAUNCH_CHECK("tsrl_ppo_tail");
     TailGrads gg{grads->w2a, grads->b2a, grads->w2c, grads->b2c, grads->w3a, grads->b3a,
                  grads->w3c, grads->b3c};
-    hipLaunchKernelGGL(tail_reduce_kernel, dim3((SL_F + SL_D + 255) / 256), dim3(256), 0,
+    hipLaunchKernelGGL(tail_reduce_kernel, dim3((SL_F + 63) / 64 + 1), dim3(256), 0,
                        as_stream(stream), slab_f, slab_d, g, (int)act_dim, gg, sums);
     TSRL_LAUNCH_CHECK("tsrl_ppo_tail(reduce)");
     return 0;
@@ -890,8 +1056,30 @@ extern "C" int tsrl_mlp_dw(const float* dz1, const float* X, int64_t ldx, const 
                        idx, n, (int)D, rps, ncolpad, part);
     TSRL_LAUNCH_CHECK("tsrl_mlp_dw");
     const int64_t outs = (int64_t)HC * ncolpad;
-    hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((outs + 255) / 256)), dim3(256), 0,
+    hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((outs + 63) / 64)), dim3(256), 0,
                        as_stream(stream), part, nsplit, ncolpad, (int)D, gWa, gba, gWc, gbc);
     TSRL_LAUNCH_CHECK("tsrl_mlp_dw(reduce)");
+    return 0;
+}
+
+extern "C" int tsrl_ppo_eval(const float* h1frag, int64_t n, const tsrl_tail_weights* wt,
+                             int64_t act_dim, const float* act, float* value_out,
+                             float* logp_out, void* stream) {
+    TSRL_CHECK_ARG(n >= 0 && act_dim > 0 && act_dim <= AMAX, "tsrl_ppo_eval: bad sizes");
+    if (n == 0) return 0;
+    TSRL_CHECK_ARG(h1frag && wt && value_out && (!logp_out || act),
+                   "tsrl_ppo_eval: null pointer");
+    TSRL_CHECK_ARG(aligned16(h1frag), "tsrl_ppo_eval: h1frag not 16-byte aligned");
+    TailWeights w{wt->w2a, wt->b2a, wt->w2c, wt->b2c, wt->w3a, wt->b3a, wt->w3c, wt->b3c,
+                  wt->log_std};
+    const int64_t tiles = (n + 31) / 32;
+    const unsigned g = (unsigned)std::min<int64_t>((tiles + 3) / 4, 1024);
+    if (logp_out)
+        hipLaunchKernelGGL(eval_tail_kernel<true>, dim3(g), dim3(256), 0, as_stream(stream), h1frag,
+                           n, w, (int)act_dim, act, value_out, logp_out);
+    else
+        hipLaunchKernelGGL(eval_tail_kernel<false>, dim3(g), dim3(256), 0, as_stream(stream),
+                           h1frag, n, w, (int)act_dim, act, value_out, logp_out);
+    TSRL_LAUNCH_CHECK("tsrl_ppo_eval");
     return 0;
 }

@@ -50,7 +50,18 @@ __global__ void pack_l1_kernel(const float* __restrict__ W, int64_t D, float* __
 
 struct ActParams {
     int A, bound, scale, sample;
+    uint64_t seed;  // rng mode (eps == NULL, sample): counter-based normals
 };
+
+// Standard normal for (seed, step, row, a): splitmix64 counter hash -> two uniforms ->
+// Box-Muller.  Replaces torch.randn_like(mu) of the torch path (a separate launch).
+__device__ __forceinline__ float counter_normal(uint64_t seed, int64_t step, int64_t row, int a) {
+    const uint64_t k = sm64(sm64(seed ^ (uint64_t)step) ^ (((uint64_t)row << 6) | (uint64_t)a));
+    const uint64_t h1 = sm64(k), h2 = sm64(k ^ 0x5851F42D4C957F2Dull);
+    const float u1 = ((float)(h1 >> 40) + 1.0f) * 0x1p-24f;  // (0, 1]
+    const float u2 = (float)(h2 >> 40) * 0x1p-24f;           // [0, 1)
+    return sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2);
+}
 
 __global__ __launch_bounds__(256) void gauss_act_kernel(
     const float* __restrict__ obs, int64_t ldx, int64_t n, int64_t D,
@@ -58,7 +69,8 @@ __global__ __launch_bounds__(256) void gauss_act_kernel(
     const float* __restrict__ b2, const float* __restrict__ w3, const float* __restrict__ b3,
     const float* __restrict__ log_std, const float* __restrict__ eps,
     const float* __restrict__ low, const float* __restrict__ high, ActParams p,
-    float* __restrict__ act, float* __restrict__ act_remap) {
+    float* __restrict__ act, float* __restrict__ act_remap, int64_t* rng_ctr,
+    unsigned int* rng_ticket) {
 #pragma clang fp contract(off)
     __shared__ float sW2[H * WS], sW3[AMAX * WS];
     __shared__ float sb1[H], sb2[H], sb3[AMAX], ssig[AMAX], slo[AMAX], shi[AMAX];
@@ -68,21 +80,28 @@ __global__ __launch_bounds__(256) void gauss_act_kernel(
     const int A = p.A;
     const int64_t row = (int64_t)blockIdx.x * 32 + c;
     const bool live = row < n;
-    // stage the small weights (all waves), then the layer-1 partial products
-    for (int i = t; i < H * H; i += 256) sW2[(i >> 6) * WS + (i & 63)] = w2[i];
-    for (int i = t; i < AMAX * H; i += 256) {
-        const int a = i >> 6;
-        sW3[a * WS + (i & 63)] = a < A ? w3[i] : 0.0f;
+    const int64_t rng_step = rng_ctr ? *rng_ctr : 0;
+    // small weights: loads issued now, LDS stores after the layer-1 loop (latency hidden)
+    float4 w2r[4], w3r[2];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w2r[j] = reinterpret_cast<const float4*>(w2)[t + 256 * j];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int q4 = t + 256 * j;
+        w3r[j] = reinterpret_cast<const float4*>(w3)[q4 < A * 16 ? q4 : 0];
     }
+    float vb1 = 0.f, vb2 = 0.f, vb3 = 0.f, vls = 0.f, vlo = -1.f, vhi = 1.f;
     if (t < H) {
-        sb1[t] = b1[t];
-        sb2[t] = b2[t];
+        vb1 = b1[t];
+        vb2 = b2[t];
     }
-    if (t < AMAX) {
-        sb3[t] = t < A ? b3[t] : 0.0f;
-        ssig[t] = t < A ? expf(log_std[t]) : 1.0f;
-        slo[t] = (p.scale && t < A) ? low[t] : -1.0f;
-        shi[t] = (p.scale && t < A) ? high[t] : 1.0f;
+    if (t < A) {
+        vb3 = b3[t];
+        vls = log_std[t];
+        if (p.scale) {
+            vlo = low[t];
+            vhi = high[t];
+        }
     }
     const int64_t S = kpad(D) / 2, G = S / 4;
     const int64_t g0 = G * w / 4, g1 = G * (w + 1) / 4;
@@ -90,19 +109,33 @@ __global__ __launch_bounds__(256) void gauss_act_kernel(
     const float* xrow = obs + (live ? row : 0) * ldx;
     const float4* wp0 = reinterpret_cast<const float4*>(w1p) + l;
     const float4* wp1 = reinterpret_cast<const float4*>(w1p) + G * 64 + l;
-    for (int64_t g = g0; g < g1; ++g) {
-        const int64_t k = h * S + 4 * g;
-        float4 xv = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (live && k < D) xv = *reinterpret_cast<const float4*>(xrow + k);
-        const float4 a0 = wp0[g * 64], a1 = wp1[g * 64];
-        acc0 = mfma(a0.x, xv.x, acc0);
-        acc1 = mfma(a1.x, xv.x, acc1);
-        acc0 = mfma(a0.y, xv.y, acc0);
-        acc1 = mfma(a1.y, xv.y, acc1);
-        acc0 = mfma(a0.z, xv.z, acc0);
-        acc1 = mfma(a1.z, xv.z, acc1);
-        acc0 = mfma(a0.w, xv.w, acc0);
-        acc1 = mfma(a1.w, xv.w, acc1);
+    // batches of 6 groups: all loads of a batch are in flight before its first MFMA
+    constexpr int GB = 6;
+    for (int64_t gb = g0; gb < g1; gb += GB) {
+        float4 xv[GB], a0[GB], a1[GB];
+#pragma unroll
+        for (int j = 0; j < GB; ++j) {
+            const int64_t g = gb + j;
+            const bool gin = g < g1;
+            const int64_t k = h * S + 4 * (gin ? g : g0);
+            const bool xin = gin && live && k < D;
+            xv[j] = *reinterpret_cast<const float4*>(xrow + (xin ? k : 0));
+            a0[j] = wp0[(gin ? g : g0) * 64];
+            a1[j] = wp1[(gin ? g : g0) * 64];
+            if (!xin) xv[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (!gin) a0[j] = a1[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int j = 0; j < GB; ++j) {
+            acc0 = mfma(a0[j].x, xv[j].x, acc0);
+            acc1 = mfma(a1[j].x, xv[j].x, acc1);
+            acc0 = mfma(a0[j].y, xv[j].y, acc0);
+            acc1 = mfma(a1[j].y, xv[j].y, acc1);
+            acc0 = mfma(a0[j].z, xv[j].z, acc0);
+            acc1 = mfma(a1[j].z, xv[j].z, acc1);
+            acc0 = mfma(a0[j].w, xv[j].w, acc0);
+            acc1 = mfma(a1[j].w, xv[j].w, acc1);
+        }
     }
     if (w > 0) {
 #pragma unroll
@@ -111,15 +144,55 @@ __global__ __launch_bounds__(256) void gauss_act_kernel(
             red[w - 1][1][r][l] = acc1[r];
         }
     }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int e = 4 * (t + 256 * j), row = e >> 6, col = e & 63;
+        float* d = sW2 + row * WS + col;
+        d[0] = w2r[j].x;
+        d[1] = w2r[j].y;
+        d[2] = w2r[j].z;
+        d[3] = w2r[j].w;
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int e = 4 * (t + 256 * j), row = e >> 6, col = e & 63;
+        if (row < AMAX) {
+            const bool ok = row < A;
+            float* d = sW3 + row * WS + col;
+            d[0] = ok ? w3r[j].x : 0.f;
+            d[1] = ok ? w3r[j].y : 0.f;
+            d[2] = ok ? w3r[j].z : 0.f;
+            d[3] = ok ? w3r[j].w : 0.f;
+        }
+    }
+    if (t < H) {
+        sb1[t] = vb1;
+        sb2[t] = vb2;
+    }
+    if (t < AMAX) {
+        sb3[t] = vb3;
+        ssig[t] = t < A ? expf(vls) : 1.0f;
+        slo[t] = vlo;
+        shi[t] = vhi;
+    }
     __syncthreads();
+    if (rng_ctr && t == 0) {
+        // every workgroup has read the counter; the last one advances it (graph-replay safe)
+        const unsigned int tk = __hip_atomic_fetch_add(rng_ticket, 1u, __ATOMIC_ACQ_REL,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+        if (tk == gridDim.x - 1) {
+            __hip_atomic_store(rng_ctr, rng_step + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(rng_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
     if (w != 0) return;
     float h1[2][16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const float z0 = ((acc0[r] + red[0][0][r][l]) + red[1][0][r][l]) + red[2][0][r][l];
         const float z1 = ((acc1[r] + red[0][1][r][l]) + red[1][1][r][l]) + red[2][1][r][l];
-        h1[0][r] = tanhf(z0 + sb1[rho(r) + 4 * h]);
-        h1[1][r] = tanhf(z1 + sb1[32 + rho(r) + 4 * h]);
+        h1[0][r] = tanh_nb(z0 + sb1[rho(r) + 4 * h]);
+        h1[1][r] = tanh_nb(z1 + sb1[32 + rho(r) + 4 * h]);
     }
     float h2[2][16];
 #pragma unroll
@@ -131,7 +204,7 @@ __global__ __launch_bounds__(256) void gauss_act_kernel(
 #pragma unroll
             for (int r = 0; r < 16; ++r) z = mfma(wa[32 * it + rho(r)], h1[it][r], z);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) h2[ot][r] = tanhf(z[r] + sb2[32 * ot + rho(r) + 4 * h]);
+        for (int r = 0; r < 16; ++r) h2[ot][r] = tanh_nb(z[r] + sb2[32 * ot + rho(r) + 4 * h]);
     }
     f32x16 mu = zero16();
     {
@@ -148,11 +221,15 @@ __global__ __launch_bounds__(256) void gauss_act_kernel(
         if (a >= A) continue;
         const float m = mu[r] + sb3[a];
         // randn * sigma + mu (two roundings, as torch's mul_ then add_)
-        const float x = p.sample ? __fadd_rn(__fmul_rn(eps[row * A + a], ssig[a]), m) : m;
+        float x = m;
+        if (p.sample) {
+            const float e = eps ? eps[row * A + a] : counter_normal(p.seed, rng_step, row, a);
+            x = __fadd_rn(__fmul_rn(e, ssig[a]), m);
+        }
         act[row * A + a] = x;
         float y = x;
         if (p.bound == 1) y = y < -1.0f ? -1.0f : (y > 1.0f ? 1.0f : y);  // clamp, NaN passes
-        else if (p.bound == 2) y = tanhf(y);
+        else if (p.bound == 2) y = tanh_nb(y);
         if (p.scale) {
             const float lo = slo[a], hi = shi[a];
             y = __fadd_rn(lo, __fdiv_rn(__fmul_rn(__fsub_rn(hi, lo), __fadd_rn(y, 1.0f)), 2.0f));
@@ -193,10 +270,35 @@ extern "C" int tsrl_gauss_policy_act(const float* obs, int64_t ldx, int64_t n, i
     TSRL_CHECK_ARG(aligned16(obs) && aligned16(w1packed),
                    "tsrl_gauss_policy_act: obs / packed weights must be 16-byte aligned");
     TSRL_CHECK_ARG((low == nullptr) == (high == nullptr), "tsrl_gauss_policy_act: low/high");
-    ActParams p{(int)act_dim, bound_method, low != nullptr, eps != nullptr};
+    ActParams p{(int)act_dim, bound_method, low != nullptr, eps != nullptr, 0ull};
     hipLaunchKernelGGL(gauss_act_kernel, dim3((unsigned)((n + 31) / 32)), dim3(256), 0,
                        as_stream(stream), obs, ldx, n, D, w1packed, b1, w2, b2, w3, b3, log_std,
-                       eps, low, high, p, act, act_remap);
+                       eps, low, high, p, act, act_remap, nullptr, nullptr);
     TSRL_LAUNCH_CHECK("tsrl_gauss_policy_act");
+    return 0;
+}
+
+extern "C" int tsrl_gauss_policy_act_rng(const float* obs, int64_t ldx, int64_t n, int64_t D,
+                                         const float* w1packed, const float* b1, const float* w2,
+                                         const float* b2, const float* w3, const float* b3,
+                                         const float* log_std, int64_t act_dim, uint64_t seed,
+                                         int64_t* rng_ctr, unsigned int* rng_ticket,
+                                         int bound_method, const float* low, const float* high,
+                                         float* act, float* act_remap, void* stream) {
+    TSRL_CHECK_ARG(n >= 0 && D > 0 && D % 4 == 0 && ldx >= D && ldx % 4 == 0 && act_dim > 0 &&
+                       act_dim <= AMAX && bound_method >= 0 && bound_method <= 2,
+                   "tsrl_gauss_policy_act_rng: bad sizes");
+    if (n == 0) return 0;
+    TSRL_CHECK_ARG(obs && w1packed && b1 && w2 && b2 && w3 && b3 && log_std && act && act_remap &&
+                       rng_ctr && rng_ticket,
+                   "tsrl_gauss_policy_act_rng: null pointer");
+    TSRL_CHECK_ARG(aligned16(obs) && aligned16(w1packed),
+                   "tsrl_gauss_policy_act_rng: obs / packed weights must be 16-byte aligned");
+    TSRL_CHECK_ARG((low == nullptr) == (high == nullptr), "tsrl_gauss_policy_act_rng: low/high");
+    ActParams p{(int)act_dim, bound_method, low != nullptr, 1, sm64(seed)};
+    hipLaunchKernelGGL(gauss_act_kernel, dim3((unsigned)((n + 31) / 32)), dim3(256), 0,
+                       as_stream(stream), obs, ldx, n, D, w1packed, b1, w2, b2, w3, b3, log_std,
+                       nullptr, low, high, p, act, act_remap, rng_ctr, rng_ticket);
+    TSRL_LAUNCH_CHECK("tsrl_gauss_policy_act_rng");
     return 0;
 }

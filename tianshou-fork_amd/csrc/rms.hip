@@ -91,6 +91,93 @@ __global__ __launch_bounds__(MCOLS * MLANES) void rms_merge_kernel(
     }
 }
 
+// Two consecutive RunningMeanStd updates in one launch (VectorEnvNormObs.step's update over
+// the step batch, then VectorEnvNormObs.reset's update over the reset rows): P1 covers k rows,
+// P2 the rows counted in blk_done (blocks with none are skipped).  The state after the first
+// update (rounded to f32 like the reference's stored arrays) goes to snap_mean / snap_var for
+// normalising the step observations; the second update's result to mean / var / count.
+__global__ __launch_bounds__(MCOLS * MLANES) void rms_merge2_kernel(
+    const double* p1, const double* p2, const double* blk_done, int64_t nblk, int64_t dim,
+    int64_t k, float* mean, float* var, double* count, float* snap_mean, float* snap_var,
+    unsigned int* ticket) {
+    __shared__ double sh[4][MLANES][MCOLS];
+    __shared__ double sh_nd[MCOLS * MLANES / kWave];
+    const int tid = threadIdx.x;
+    const int col = tid % MCOLS;
+    const int lane = tid / MCOLS;
+    double c = 0.0;
+    for (int64_t b = tid; b < nblk; b += MCOLS * MLANES) c += blk_done[b];
+    c = wave_sum(c);
+    if ((tid & (kWave - 1)) == 0) sh_nd[tid / kWave] = c;
+    const double old_count = *count;
+    __syncthreads();
+    double nd = 0.0;
+    for (int w = 0; w < MCOLS * MLANES / kWave; ++w) nd += sh_nd[w];
+    const double bc1 = (double)k;
+    const double tot1 = old_count + bc1, tot2 = tot1 + nd;
+    const int64_t d = (int64_t)blockIdx.x * MCOLS + col;
+    double s1 = 0.0, q1 = 0.0, s2 = 0.0, q2 = 0.0;
+    if (d < dim) {
+        for (int64_t b = lane; b < nblk; b += MLANES) {
+            const double2 a = *reinterpret_cast<const double2*>(p1 + (b * dim + d) * 2);
+            s1 += a.x;
+            q1 += a.y;
+            if (blk_done[b] > 0.0) {
+                const double2 r = *reinterpret_cast<const double2*>(p2 + (b * dim + d) * 2);
+                s2 += r.x;
+                q2 += r.y;
+            }
+        }
+    }
+    sh[0][lane][col] = s1;
+    sh[1][lane][col] = q1;
+    sh[2][lane][col] = s2;
+    sh[3][lane][col] = q2;
+    __syncthreads();
+    if (lane == 0 && d < dim) {
+        double S1 = 0.0, Q1 = 0.0, S2 = 0.0, Q2 = 0.0;
+        for (int l = 0; l < MLANES; ++l) {
+            S1 += sh[0][l][col];
+            Q1 += sh[1][l][col];
+            S2 += sh[2][l][col];
+            Q2 += sh[3][l][col];
+        }
+        double m0 = (double)mean[d], v0 = (double)var[d];
+        if (bc1 > 0.0) {
+            const double bm = S1 / bc1;
+            double bv = Q1 / bc1 - bm * bm;
+            bv = bv < 0.0 ? 0.0 : bv;
+            const double delta = bm - m0;
+            const double nm = m0 + delta * bc1 / tot1;
+            const double m2 = v0 * old_count + bv * bc1 + delta * delta * old_count * bc1 / tot1;
+            m0 = (double)(float)nm;
+            v0 = (double)(float)(m2 / tot1);
+        }
+        snap_mean[d] = (float)m0;
+        snap_var[d] = (float)v0;
+        if (nd > 0.0) {
+            const double bm = S2 / nd;
+            double bv = Q2 / nd - bm * bm;
+            bv = bv < 0.0 ? 0.0 : bv;
+            const double delta = bm - m0;
+            const double nm = m0 + delta * nd / tot2;
+            const double m2 = v0 * tot1 + bv * nd + delta * delta * tot1 * nd / tot2;
+            m0 = (double)(float)nm;
+            v0 = (double)(float)(m2 / tot2);
+        }
+        mean[d] = (float)m0;
+        var[d] = (float)v0;
+    }
+    if (tid == 0) {
+        const unsigned int t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+        if (t == gridDim.x - 1) {
+            __hip_atomic_store(count, tot2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 __device__ __forceinline__ float norm1(float x, float m, float v, float eps, float clip) {
     float y = (x - m) / __builtin_sqrtf(v + eps);
     if (clip > 0.0f) y = fminf(fmaxf(y, -clip), clip);
@@ -130,6 +217,23 @@ extern "C" int tsrl_rms_merge(const double* col_partials, int64_t nblk, int64_t 
                        as_stream(stream), col_partials, nblk, dim, mask, k, batch_count, mean,
                        var, count, ticket);
     TSRL_LAUNCH_CHECK("tsrl_rms_merge");
+    return 0;
+}
+
+extern "C" int tsrl_rms_merge2(const double* partials_step, const double* partials_reset,
+                               const double* blk_done, int64_t nblk, int64_t dim, int64_t k,
+                               float* mean, float* var, double* count, float* snap_mean,
+                               float* snap_var, unsigned int* ticket, void* stream) {
+    TSRL_CHECK_ARG(partials_step && partials_reset && blk_done && mean && var && count &&
+                       snap_mean && snap_var && ticket && dim > 0 && nblk >= 0 && k >= 0,
+                   "tsrl_rms_merge2: bad arguments");
+    TSRL_CHECK_ARG(aligned16(partials_step) && aligned16(partials_reset),
+                   "tsrl_rms_merge2: partials not 16B aligned");
+    const int64_t grid = (dim + MCOLS - 1) / MCOLS;
+    hipLaunchKernelGGL(rms_merge2_kernel, dim3((unsigned)grid), dim3(MCOLS * MLANES), 0,
+                       as_stream(stream), partials_step, partials_reset, blk_done, nblk, dim, k,
+                       mean, var, count, snap_mean, snap_var, ticket);
+    TSRL_LAUNCH_CHECK("tsrl_rms_merge2");
     return 0;
 }
 

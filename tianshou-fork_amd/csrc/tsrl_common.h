@@ -44,6 +44,22 @@ __host__ __device__ __forceinline__ uint64_t sm64(uint64_t x) {
     return z ^ (z >> 31);
 }
 
+// tanhf without branches: both halves of ROCm's __ocml_tanh_f32 (the |x| < 0.625 polynomial
+// and 1 - 2/(exp(2|x|) + 1)) are evaluated and selected, so the result is bit-identical to
+// tanhf while unrolled MFMA code keeps one basic block (ocml's branch splits it per call).
+__device__ __forceinline__ float tanh_nb(float x) {
+    const float ax = __builtin_fabsf(x);
+    const float x2 = x * x;
+    float p = __builtin_fmaf(x2, -0x1.758e7ap-8f, 0x1.521192p-6f);
+    p = __builtin_fmaf(x2, p, -0x1.b8389cp-5f);
+    p = __builtin_fmaf(x2, p, 0x1.110704p-3f);
+    p = __builtin_fmaf(x2, p, -0x1.555532p-2f);
+    const float small = __builtin_fmaf(x2, ax * p, ax);
+    const float e = __builtin_expf(ax * 2.0f);
+    const float large = __builtin_fmaf(-2.0f, __builtin_amdgcn_rcpf(e + 1.0f), 1.0f);
+    return __builtin_copysignf(ax < 0.625f ? small : large, x);
+}
+
 // Wave-wide sum of a double (64 lanes, xor butterfly).
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll

@@ -34,6 +34,8 @@ class AddArgs(ctypes.Structure):
         ("ep_rew", _p), ("ep_len", _p), ("ep_idx", _p),
         ("out_ep_rew", _p), ("out_ep_len", _p), ("out_ep_idx", _p),
         ("stat_rew", _p), ("stat_len", _p), ("stat_idx", _p),
+        ("reset_src", _p), ("reset_mask", _p), ("reset_mean", _p), ("reset_var", _p),
+        ("rel_ticket", _p),
     ]
 
 
@@ -69,6 +71,10 @@ _SIGS = {
     "tsrl_env_num_partials": ([_i64], _i64),
     "tsrl_synth_box_step": ([_p, _i64, _i64, _u64, _i64, _p, _p, _p, _p, _p, _p, _p, _p],
                             ctypes.c_int),
+    "tsrl_synth_box_step_reset": ([_i64, _i64, _u64, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p,
+                                   _p, _p, _p], ctypes.c_int),
+    "tsrl_rms_merge2": ([_p, _p, _p, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p, _p],
+                        ctypes.c_int),
     "tsrl_synth_box_reset": ([_p, _p, _i64, _i64, _u64, _i64, _p, _p, _p, _p, _p], ctypes.c_int),
     "tsrl_synth_u8_step": ([_p, _i64, _i64, _u64, _i64, _p, _p, _p, _p, _p, _p, _p],
                            ctypes.c_int),
@@ -94,8 +100,12 @@ _SIGS = {
     "tsrl_ppo_tail": ([_p, _i64, _p, ctypes.POINTER(TailWeights), _i64, _p, _p, _p, _p, _p, _p,
                        PPOParams, _p, ctypes.POINTER(TailGrads), _p, _p, _i64, _p],
                       ctypes.c_int),
+    "tsrl_ppo_eval": ([_p, _i64, ctypes.POINTER(TailWeights), _i64, _p, _p, _p, _p],
+                      ctypes.c_int),
     "tsrl_mlp_dw_workspace_bytes": ([_i64, _i64], _i64),
     "tsrl_policy_pack_floats": ([_i64], _i64),
+    "tsrl_gauss_policy_act_rng": ([_p, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p, _p, _i64, _u64,
+                                   _p, _p, ctypes.c_int, _p, _p, _p, _p, _p], ctypes.c_int),
     "tsrl_policy_pack_l1": ([_p, _i64, _p, _p], ctypes.c_int),
     "tsrl_gauss_policy_act": ([_p, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p, _p, _i64, _p,
                                ctypes.c_int, _p, _p, _p, _p, _p], ctypes.c_int),

@@ -277,7 +277,8 @@ class VectorReplayBuffer:
     def _launch_add(self, *, ids, k, ptr=None, next_rel=None, uniform_rel=0, uniform_next=0,
                     rel_dev=None, obs=None, act=None, obs_next=None, obs_next_raw=None,
                     cur_obs=None, norm=None, rew=None, term=None, trunc=None, out=None,
-                    stats=True) -> None:
+                    stats=True, norm_snapshot=False, reset_src=None, reset_mask=None,
+                    reset_norm=None, rel_ticket=None) -> None:
         """One tsrl_buffer_add launch (see include/tsrl.h)."""
         m = self._meta
         d = self._dev
@@ -302,10 +303,20 @@ class VectorReplayBuffer:
             a.cur_obs = _C.ptr(cur_obs)
             a.obs_dim = int(np.prod(m.obs.shape[1:]))
             if norm is not None:
-                a.norm_mean = _C.ptr(norm.mean_t)
-                a.norm_var = _C.ptr(norm.var_t)
+                # norm_snapshot: the statistics after merge2's first (step-batch) update
+                a.norm_mean = _C.ptr(norm.snap_mean_t if norm_snapshot else norm.mean_t)
+                a.norm_var = _C.ptr(norm.snap_var_t if norm_snapshot else norm.var_t)
                 a.norm_eps = float(norm.eps)
                 a.norm_clip = float(norm.clip_max or 0.0)
+            if reset_mask is not None:
+                a.reset_src = _C.ptr(reset_src)
+                a.reset_mask = _C.ptr(reset_mask)
+                if reset_norm is not None:
+                    a.reset_mean = _C.ptr(reset_norm.mean_t)
+                    a.reset_var = _C.ptr(reset_norm.var_t)
+                    a.norm_eps = float(reset_norm.eps)
+                    a.norm_clip = float(reset_norm.clip_max or 0.0)
+        a.rel_ticket = _C.ptr(rel_ticket)
         if obs_next_raw is not None and has_next:
             a.obs_next_src_raw = _C.ptr(obs_next_raw)
             a.obs_next_dst_raw = _C.ptr(m.obs_next)

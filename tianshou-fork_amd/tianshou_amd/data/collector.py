@@ -112,6 +112,9 @@ class Collector:
             env_id=torch.arange(N, device=dev),
         )
         act_shape, act_dtype = self._act_spec()
+        nblk = b.nblk_for(N)
+        self._scratch["blk_done"] = torch.zeros(max(nblk, 1), dtype=torch.float64, device=dev)
+        self._scratch["rel_ticket"] = torch.zeros(1, dtype=torch.int32, device=dev)
         self._scratch["act"] = torch.empty((N,) + act_shape, dtype=act_dtype, device=dev)
         self._scratch["act_remap"] = torch.empty((N,) + act_shape, dtype=act_dtype, device=dev)
 
@@ -236,6 +239,28 @@ class Collector:
             action_remap = self.policy.map_action(act)
         raw, rew = s["raw"][:kk], s["rew"][:kk]
         term, trunc, done = s["term"][:kk], s["trunc"][:kk], s["done"][:kk]
+        norm_obj = self._norm
+        if (ids_t is None and not b.u8 and getattr(b, "supports_step_reset", False)
+                and (norm_obj is None or norm_obj.obs_rms.dp is None
+                     or not norm_obj.obs_rms.dp.active)):
+            # step + auto-reset (one env launch), both obs_rms updates (one launch), buffer
+            # add with the step/reset normalisation and the ring advance (one launch)
+            upd = norm_obj is not None and norm_obj.update_obs_rms
+            blk = s["blk_done"]
+            b._step_reset_raw(kk, raw, s["reset_raw"][:kk], rew, term, trunc, done,
+                              s["part"] if upd else None, s["part2"] if upd else None,
+                              blk if upd else None)
+            rms = norm_obj.obs_rms if norm_obj is not None else None
+            if upd:
+                rms.merge2(s["part"], s["part2"], blk, b.nblk_for(kk), kk)
+            kw = dict(add_kw)
+            if "rel_dev" in kw:
+                kw["rel_ticket"] = s["rel_ticket"]
+            buf._launch_add(ids=None, k=kk, obs=cur, act=act, obs_next=raw, cur_obs=cur,
+                            norm=rms, norm_snapshot=upd, reset_src=s["reset_raw"][:kk],
+                            reset_mask=done, reset_norm=rms, rew=rew, term=term, trunc=trunc,
+                            **kw)
+            return
         b._step_raw(ids_t, kk, raw, rew, term, trunc, s["part"], action_remap)
         norm = None
         if self._norm is not None and not b.u8:

@@ -83,6 +83,19 @@ class SyntheticVectorEnv(DeviceVectorEnv):
                                            _C.ptr(trunc_out), _C.ptr(partials), s),
                      "tsrl_synth_box_step")
 
+    @property
+    def supports_step_reset(self) -> bool:
+        return not self.u8
+
+    def _step_reset_raw(self, k: int, obs_out, reset_out, rew_out, term_out, trunc_out,
+                        done_out, partials=None, partials_reset=None, blk_done=None) -> None:
+        """Step all k envs and reset the finished ones in one launch (f32 obs only)."""
+        _C.check(_C.lib().tsrl_synth_box_step_reset(
+            k, self.obs_numel, self.seed_, self.ep_len, _C.ptr(self.ep_j), _C.ptr(self.ep_t),
+            _C.ptr(obs_out), _C.ptr(reset_out), _C.ptr(rew_out), _C.ptr(term_out),
+            _C.ptr(trunc_out), _C.ptr(done_out), _C.ptr(partials), _C.ptr(partials_reset),
+            _C.ptr(blk_done), _C.stream_ptr(self.device)), "tsrl_synth_box_step_reset")
+
     def _reset_raw(self, ids: Optional[torch.Tensor], mask: Optional[torch.Tensor], k: int,
                    obs_out, partials=None) -> None:
         L = _C.lib()

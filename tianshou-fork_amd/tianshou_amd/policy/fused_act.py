@@ -46,6 +46,12 @@ class FusedGaussAct:
         self.D, self.A = layers["D"], layers["A"]
         self.packed = None
         self._eps = None
+        # "device": noise drawn in-kernel from a counter hash seeded from torch's CPU
+        # generator at each pack() (reproducible under torch.manual_seed); "torch": noise
+        # from torch.randn on the GPU stream (the torch path's exact noise, one extra launch)
+        self.rng = "device"
+        self._seed = 0
+        self._ctr = None
 
     def pack(self) -> None:
         """Pack the first-layer weight (call after every parameter update; the collector
@@ -57,18 +63,33 @@ class FusedGaussAct:
             self.packed = torch.empty(n, dtype=torch.float32, device=w.device)
         _C.check(lib.tsrl_policy_pack_l1(_C.ptr(w.detach()), self.D, _C.ptr(self.packed),
                                          _C.stream_ptr(w.device)), "tsrl_policy_pack_l1")
+        if self.rng == "device":
+            self._seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+            if self._ctr is None or self._ctr.device != w.device:
+                self._ctr = torch.zeros(2, dtype=torch.int64, device=w.device)
+            self._ctr.zero_()
 
     def __call__(self, obs: torch.Tensor, act_out: torch.Tensor, remap_out: torch.Tensor,
                  sample: bool, bound_method, low_high) -> None:
         L, lib = self.L, _C.lib()
         n = obs.shape[0]
+        low, high = low_high if low_high is not None else (None, None)
+        if sample and self.rng == "device":
+            _C.check(lib.tsrl_gauss_policy_act_rng(
+                _C.ptr(obs), obs.stride(0), n, self.D, _C.ptr(self.packed),
+                _C.ptr(L["w1"].bias.detach()), _C.ptr(L["w2"].weight.detach()),
+                _C.ptr(L["w2"].bias.detach()), _C.ptr(L["w3"].weight.detach()),
+                _C.ptr(L["w3"].bias.detach()), _C.ptr(L["sigma"].detach()), self.A,
+                self._seed, _C.ptr(self._ctr[:1]), _C.ptr(self._ctr[1:]),
+                _BOUND[bound_method], _C.ptr(low), _C.ptr(high), _C.ptr(act_out),
+                _C.ptr(remap_out), _C.stream_ptr(obs.device)), "tsrl_gauss_policy_act_rng")
+            return
         eps = None
         if sample:
             if self._eps is None or self._eps.shape[0] < n or self._eps.device != obs.device:
                 self._eps = torch.empty(n, self.A, device=obs.device)
             eps = self._eps[:n]
             eps.normal_()
-        low, high = low_high if low_high is not None else (None, None)
         _C.check(lib.tsrl_gauss_policy_act(
             _C.ptr(obs), obs.stride(0), n, self.D, _C.ptr(self.packed),
             _C.ptr(L["w1"].bias.detach()), _C.ptr(L["w2"].weight.detach()),

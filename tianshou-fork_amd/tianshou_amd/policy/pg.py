@@ -64,6 +64,7 @@ class PGPolicy(BasePolicy):
             self._fused_act = fa
         if fa is False or not next(self.actor.parameters()).is_cuda:
             return False
+        fa.rng = getattr(self, "fused_act_rng", "device")
         fa.pack()
         return True
 

@@ -57,6 +57,8 @@ class DeviceRunningMeanStd:
         self.clip_max = clip_max
         self.eps = epsilon
         self.dp = None  # tianshou_amd.dist.DataParallel: sync the moments over ranks
+        self.snap_mean_t = None  # state after the step-batch update of merge2
+        self.snap_var_t = None
 
     def sync_with(self, dp) -> None:
         self.dp = dp
@@ -105,6 +107,19 @@ class DeviceRunningMeanStd:
             _C.ptr(partials), nblk, self.dim, _C.ptr(mask), k, _C.ptr(batch_count),
             _C.ptr(self.mean_t), _C.ptr(self.var_t), _C.ptr(self.count_t),
             _C.ptr(self.ticket_t), _C.stream_ptr()), "tsrl_rms_merge")
+
+    def merge2(self, partials_step: torch.Tensor, partials_reset: torch.Tensor,
+               blk_done: torch.Tensor, nblk: int, k: int) -> None:
+        """The step-batch update followed by the reset-rows update in one launch; the state
+        after the first lands in ``snap_mean_t`` / ``snap_var_t`` (single-process only)."""
+        if self.snap_mean_t is None:
+            self.snap_mean_t = torch.empty_like(self.mean_t)
+            self.snap_var_t = torch.empty_like(self.var_t)
+        _C.check(_C.lib().tsrl_rms_merge2(
+            _C.ptr(partials_step), _C.ptr(partials_reset), _C.ptr(blk_done), nblk, self.dim, k,
+            _C.ptr(self.mean_t), _C.ptr(self.var_t), _C.ptr(self.count_t),
+            _C.ptr(self.snap_mean_t), _C.ptr(self.snap_var_t), _C.ptr(self.ticket_t),
+            _C.stream_ptr()), "tsrl_rms_merge2")
 
     def update(self, x: torch.Tensor, mask: Optional[torch.Tensor] = None) -> None:
         x = x.reshape(len(x), -1)
