@@ -99,6 +99,7 @@ def main():
     env = VectorEnvNormObs(SyntheticVectorEnv(E, (D,), A, ep_len=args.ep_len, seed=rank,
                                               device=dev))
     actor, critic = get_actor_critic((D,), (64, 64), (A,), dev)
+    actor, critic = actor.to(dev), critic.to(dev)  # before the optimiser: fused + capturable Adam
     optim = init_and_get_optim(actor, critic, 3e-4)
     policy = PPOPolicy(actor, critic, optim, fixed_std_normal, action_space=env.action_space,
                        discount_factor=0.99, gae_lambda=0.95, max_grad_norm=0.5, vf_coef=0.25,

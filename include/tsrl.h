@@ -144,9 +144,9 @@ int tsrl_rms_norm_rows(const float* x, const uint8_t* mask, int64_t k, int64_t d
  *   and set ep_idx[b] = next_rel[r].
  * Auto-reset (nullable): rows with reset_mask[r] set take cur_obs[r] <- norm(reset_src[r])
  *   with reset_mean / reset_var (collector.py:342-361, the obs of the new episode).
- * rel_ticket (nullable, zeroed device word, with rel_dev): the last workgroup advances
- *   *rel_dev = (*rel_dev + 1) % ring_size after every workgroup has read it, replacing a
- *   separate tsrl_ring_advance launch.
+ * rel_next (nullable, with rel_dev): receives (*rel_dev + 1) % ring_size -- the cursor of the
+ *   next step in the other slot of a ping-pong pair (graph-captured steps alternate the two
+ *   slots), replacing a separate tsrl_ring_advance launch.
  * ------------------------------------------------------------------------------- */
 typedef struct tsrl_add_args {
     const int64_t* ids;      /* [k] env ids or NULL (identity) */
@@ -178,7 +178,7 @@ typedef struct tsrl_add_args {
     /* auto-reset rows and fused ring advance (nullable) */
     const float* reset_src; const uint8_t* reset_mask;
     const float* reset_mean; const float* reset_var;
-    unsigned int* rel_ticket;
+    int64_t* rel_next;
 } tsrl_add_args;
 int tsrl_buffer_add(const tsrl_add_args* a, void* stream);
 /* *rel_dev = (*rel_dev + 1) % ring_size (device-side ring cursor for graph-captured steps). */
@@ -306,13 +306,13 @@ int tsrl_gauss_policy_act(const float* obs, int64_t ldx, int64_t n, int64_t D,
                           int bound_method, const float* low, const float* high, float* act,
                           float* act_remap, void* stream);
 /* Same step drawing the noise in-kernel: standard normals from a splitmix64 counter hash of
- * (seed, *rng_ctr, row, dim) through Box-Muller; the last workgroup increments *rng_ctr
- * (rng_ticket: a zeroed device word), so HIP-graph replays draw fresh noise each step. */
+ * (seed, *rng_ctr, row, dim) through Box-Muller; *rng_next = *rng_ctr + 1 (the other slot of
+ * a ping-pong pair), so HIP-graph replays draw fresh noise each step. */
 int tsrl_gauss_policy_act_rng(const float* obs, int64_t ldx, int64_t n, int64_t D,
                               const float* w1packed, const float* b1, const float* w2,
                               const float* b2, const float* w3, const float* b3,
                               const float* log_std, int64_t act_dim, uint64_t seed,
-                              int64_t* rng_ctr, unsigned int* rng_ticket, int bound_method,
+                              const int64_t* rng_ctr, int64_t* rng_next, int bound_method,
                               const float* low, const float* high, float* act,
                               float* act_remap, void* stream);
 

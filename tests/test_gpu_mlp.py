@@ -214,3 +214,70 @@ def test_learn_fused_mlp_vs_layers(dev, value_clip):
     for k in states[0]:
         np.testing.assert_allclose(states[0][k].numpy(), states[1][k].numpy(), rtol=1e-3,
                                    atol=2e-3, err_msg=k)
+
+
+def test_process_fn_fused_eval_matches_torch_layers(dev):
+    """PPOPolicy.process_fn with the fused evaluation (layer-1 kernel + eval kernel, V(s')
+    reused from V(s) along the Collector's obs chain) vs the torch layers on the same
+    collected buffer: v_s, returns, adv, logp_old within rtol 1e-5 / atol 1e-5."""
+    import copy
+    from tianshou_amd.data import Collector, VectorReplayBuffer
+    from tianshou_amd.env import Box, SyntheticVectorEnv, VectorEnvNormObs
+    from tianshou_amd.policy import PPOPolicy
+    from tianshou_amd.utils.models import fixed_std_normal
+    E, D, A, T = 64, 40, 6, 50
+    base_a, base_c = _nets(D, A, dev, 11)
+    out = []
+    for fused in (True, False):
+        actor, critic = copy.deepcopy(base_a), copy.deepcopy(base_c)
+        optim = torch.optim.Adam(list(actor.parameters()) + list(critic.parameters()), lr=1e-4)
+        pol = PPOPolicy(actor, critic, optim, fixed_std_normal, action_space=Box(-1.0, 1.0, (A,)),
+                        reward_normalization=True, fused_mlp=fused)
+        assert (pol._mlp is not None) == fused
+        env = VectorEnvNormObs(SyntheticVectorEnv(E, (D,), A, ep_len=17, seed=2, device=dev))
+        buf = VectorReplayBuffer(E * T, E, device=dev)
+        torch.manual_seed(4)
+        Collector(pol, env, buf).collect(n_step=E * T)
+        assert buf.obs_chain
+        batch, idx = buf.sample(0)
+        batch = pol.process_fn(batch, buf, idx)
+        out.append({k: batch[k].detach().cpu() for k in ("v_s", "returns", "adv", "logp_old")})
+    for k in out[0]:
+        np.testing.assert_allclose(out[0][k].numpy(), out[1][k].numpy(), rtol=1e-5, atol=1e-5,
+                                   err_msg=k)
+
+
+def test_learn_graph_replay_matches_eager(dev):
+    """Epochs replayed from the captured HIP graph give exactly the eager fused result (same
+    kernels in the same order): losses and parameters bit-identical over 3 updates."""
+    from tianshou_amd.data import Batch
+    from tianshou_amd.env import Box
+    from tianshou_amd.policy import PPOPolicy
+    from tianshou_amd.utils.models import fixed_std_normal
+    D, A, n = 40, 6, 3000
+    base_a, base_c = _nets(D, A, dev, 21)
+    res, states = [], []
+    for graph in (True, False):
+        actor, critic = copy.deepcopy(base_a), copy.deepcopy(base_c)
+        params = list(actor.parameters()) + [p for p in critic.parameters()
+                                             if all(p is not q for q in actor.parameters())]
+        optim = torch.optim.Adam(params, lr=3e-4, fused=True, capturable=True)
+        pol = PPOPolicy(actor, critic, optim, fixed_std_normal, action_space=Box(-1.0, 1.0, (A,)),
+                        max_grad_norm=0.5, vf_coef=0.25, ent_coef=0.01, perm_device=True)
+        pol.graph_learn = graph
+        g = torch.Generator().manual_seed(1)
+        data = dict(obs=torch.randn(n, D, generator=g), act=torch.randn(n, A, generator=g),
+                    logp_old=torch.randn(n, generator=g) * 0.2 - A * 1.2,
+                    adv=torch.randn(n, generator=g), returns=torch.randn(n, generator=g))
+        data["v_s"] = data["returns"] + 0.3 * torch.randn(n, generator=g)
+        batch = Batch(**{k: v.to(dev) for k, v in data.items()})
+        torch.manual_seed(3)
+        out = [pol.learn(batch, batch_size=512, repeat=2) for _ in range(3)]
+        assert (pol._learn_graph is not None) == graph
+        res.append(out)
+        states.append({k: v.detach().cpu() for k, v in pol.state_dict().items()})
+    for a, b in zip(res[0], res[1]):
+        for k in a:
+            assert a[k] == b[k], k
+    for k in states[0]:
+        assert torch.equal(states[0][k], states[1][k]), k

@@ -104,20 +104,9 @@ __global__ __launch_bounds__(TPB) void buffer_add_kernel(tsrl_add_args a) {
             }
         }
     }
-    if (a.rel_ticket && a.rel_dev) {
-        // every workgroup has read *rel_dev above; the last one to arrive advances it
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const unsigned int t = __hip_atomic_fetch_add(a.rel_ticket, 1u, __ATOMIC_ACQ_REL,
-                                                          __HIP_MEMORY_SCOPE_AGENT);
-            if (t == gridDim.x - 1) {
-                int64_t* rd = const_cast<int64_t*>(a.rel_dev);
-                __hip_atomic_store(rd, (urel + 1) % a.ring_size, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(a.rel_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-    }
+    // ring cursor for the next step: written to the other slot of a ping-pong pair, so no
+    // workgroup can observe it before every workgroup of this launch has read *rel_dev
+    if (a.rel_next && blockIdx.x == 0 && threadIdx.x == 0) *a.rel_next = (urel + 1) % a.ring_size;
 }
 
 __global__ __launch_bounds__(TPB) void gather_rows_kernel(const char* src, int64_t row_bytes,
@@ -260,7 +249,8 @@ extern "C" int tsrl_buffer_add(const tsrl_add_args* a, void* stream) {
     TSRL_CHECK_ARG(!a->reset_mask || (a->reset_src && a->cur_obs),
                    "tsrl_buffer_add: reset_mask needs reset_src and cur_obs");
     TSRL_CHECK_ARG(!a->reset_mean || a->reset_var, "tsrl_buffer_add: reset_var missing");
-    TSRL_CHECK_ARG(!a->rel_ticket || a->rel_dev, "tsrl_buffer_add: rel_ticket needs rel_dev");
+    TSRL_CHECK_ARG(!a->rel_next || (a->rel_dev && a->rel_next != a->rel_dev),
+                   "tsrl_buffer_add: rel_next needs rel_dev (a different word)");
     const int64_t grid = (a->k + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK;
     hipLaunchKernelGGL(buffer_add_kernel, dim3((unsigned)grid), dim3(TPB), 0, as_stream(stream),
                        *a);

@@ -32,7 +32,7 @@ struct RowState {
 __device__ void box_rows(const RowState* rs, int64_t r0, int64_t k, int64_t dim, float* obs,
                          double* partials) {
     const int nrows = (int)min((int64_t)ROWS, k - r0);
-    for (int64_t d = threadIdx.x; d < dim; d += TPB) {
+    for (int64_t d = threadIdx.x; d < dim; d += blockDim.x) {
         double s = 0.0, ss = 0.0;
         for (int r = 0; r < nrows; ++r) {
             if (!rs[r].active) continue;
@@ -108,7 +108,7 @@ __global__ __launch_bounds__(TPB) void box_reset_kernel(const int64_t* ids, cons
 // envs, collector.py:310-361): raw step rows -> obs_out with partials P1 over every row;
 // rows whose episode ended are reset at once -> reset_out with partials P2 over those rows
 // only, and blk_done[block] counts them (the reset batch size of the second obs_rms update).
-__global__ __launch_bounds__(TPB) void box_step_reset_kernel(
+__global__ __launch_bounds__(1024) void box_step_reset_kernel(
     int64_t k, int64_t dim, uint64_t s_seed, int64_t ep_len, int64_t* ep_j, int64_t* ep_t,
     float* obs, float* reset_obs, double* rew, uint8_t* term, uint8_t* trunc, uint8_t* done,
     double* p_step, double* p_reset, double* blk_done) {
@@ -272,7 +272,10 @@ extern "C" int tsrl_synth_box_step_reset(int64_t k, int64_t dim, uint64_t seed, 
     TSRL_CHECK_ARG((partials_step == nullptr) == (partials_reset == nullptr) &&
                        (partials_step == nullptr) == (blk_done == nullptr),
                    "tsrl_synth_box_step_reset: partials / blk_done must be all set or all NULL");
-    hipLaunchKernelGGL(box_step_reset_kernel, dim3(blocks_for(k)), dim3(TPB), 0,
+    // one thread per observation column (up to 1024), so each thread's 16 rows are its
+    // whole share of the block's work
+    const unsigned tpb = (unsigned)std::min<int64_t>(1024, std::max<int64_t>(64, (dim + 63) / 64 * 64));
+    hipLaunchKernelGGL(box_step_reset_kernel, dim3(blocks_for(k)), dim3(tpb), 0,
                        as_stream(stream), k, dim, sm64(seed), ep_len, ep_j, ep_t, obs_out,
                        reset_out, rew_out, term_out, trunc_out, done_out, partials_step,
                        partials_reset, blk_done);

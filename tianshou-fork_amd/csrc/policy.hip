@@ -53,43 +53,48 @@ struct ActParams {
     uint64_t seed;  // rng mode (eps == NULL, sample): counter-based normals
 };
 
-// Standard normal for (seed, step, row, a): splitmix64 counter hash -> two uniforms ->
-// Box-Muller.  Replaces torch.randn_like(mu) of the torch path (a separate launch).
-__device__ __forceinline__ float counter_normal(uint64_t seed, int64_t step, int64_t row, int a) {
-    const uint64_t k = sm64(sm64(seed ^ (uint64_t)step) ^ (((uint64_t)row << 6) | (uint64_t)a));
-    const uint64_t h1 = sm64(k), h2 = sm64(k ^ 0x5851F42D4C957F2Dull);
-    const float u1 = ((float)(h1 >> 40) + 1.0f) * 0x1p-24f;  // (0, 1]
-    const float u2 = (float)(h2 >> 40) * 0x1p-24f;           // [0, 1)
-    return sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2);
+// Two standard normals for (seed, step, row, pair): one splitmix64 counter hash gives two
+// 24-bit uniforms -> Box-Muller (cos and sin branches).  Replaces torch.randn_like(mu) of the
+// torch path (a separate launch).
+__device__ __forceinline__ float2 counter_normal2(uint64_t seed, int64_t step, int64_t row,
+                                                 int pair) {
+    const uint64_t h = sm64(sm64(seed ^ (uint64_t)step) ^ (((uint64_t)row << 5) | (uint64_t)pair));
+    const float u1 = ((float)(h >> 40) + 1.0f) * 0x1p-24f;                // (0, 1]
+    const float u2 = (float)((h >> 16) & 0xFFFFFFu) * 0x1p-24f;          // [0, 1)
+    const float r = sqrtf(-2.0f * logf(u1));
+    float sn, cs;
+    sincospif(2.0f * u2, &sn, &cs);
+    return make_float2(r * cs, r * sn);
 }
 
-__global__ __launch_bounds__(256) void gauss_act_kernel(
+constexpr int ANW = 8;  // waves per workgroup: the first layer's K is split 8 ways
+
+__global__ __launch_bounds__(ANW * 64) void gauss_act_kernel(
     const float* __restrict__ obs, int64_t ldx, int64_t n, int64_t D,
     const float* __restrict__ w1p, const float* __restrict__ b1, const float* __restrict__ w2,
     const float* __restrict__ b2, const float* __restrict__ w3, const float* __restrict__ b3,
     const float* __restrict__ log_std, const float* __restrict__ eps,
     const float* __restrict__ low, const float* __restrict__ high, ActParams p,
-    float* __restrict__ act, float* __restrict__ act_remap, int64_t* rng_ctr,
-    unsigned int* rng_ticket) {
+    float* __restrict__ act, float* __restrict__ act_remap, const int64_t* rng_ctr,
+    int64_t* rng_next) {
 #pragma clang fp contract(off)
+    constexpr int NT = ANW * 64;
     __shared__ float sW2[H * WS], sW3[AMAX * WS];
     __shared__ float sb1[H], sb2[H], sb3[AMAX], ssig[AMAX], slo[AMAX], shi[AMAX];
-    __shared__ float red[3][2][16][64];
+    __shared__ float seps[32][AMAX + 1];
+    __shared__ float red[ANW / 2][2][16][64];
     const int t = threadIdx.x;
     const int w = t >> 6, l = t & 63, h = l >> 5, c = l & 31;
     const int A = p.A;
-    const int64_t row = (int64_t)blockIdx.x * 32 + c;
+    const int64_t row0 = (int64_t)blockIdx.x * 32;
+    const int64_t row = row0 + c;
     const bool live = row < n;
     const int64_t rng_step = rng_ctr ? *rng_ctr : 0;
     // small weights: loads issued now, LDS stores after the layer-1 loop (latency hidden)
-    float4 w2r[4], w3r[2];
+    float4 w2r[2], w3r;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) w2r[j] = reinterpret_cast<const float4*>(w2)[t + 256 * j];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const int q4 = t + 256 * j;
-        w3r[j] = reinterpret_cast<const float4*>(w3)[q4 < A * 16 ? q4 : 0];
-    }
+    for (int j = 0; j < 2; ++j) w2r[j] = reinterpret_cast<const float4*>(w2)[t + NT * j];
+    w3r = reinterpret_cast<const float4*>(w3)[t < A * 16 ? t : 0];
     float vb1 = 0.f, vb2 = 0.f, vb3 = 0.f, vls = 0.f, vlo = -1.f, vhi = 1.f;
     if (t < H) {
         vb1 = b1[t];
@@ -103,8 +108,23 @@ __global__ __launch_bounds__(256) void gauss_act_kernel(
             vhi = high[t];
         }
     }
+    // noise of this workgroup's 32 rows: thread -> (row, pair of action dims)
+    if (p.sample) {
+        const int er = t >> 4, pr = t & 15, a0 = 2 * pr;
+        float2 z = make_float2(0.f, 0.f);
+        if (row0 + er < n && a0 < A) {
+            if (eps) {
+                z.x = eps[(row0 + er) * A + a0];
+                if (a0 + 1 < A) z.y = eps[(row0 + er) * A + a0 + 1];
+            } else {
+                z = counter_normal2(p.seed, rng_step, row0 + er, pr);
+            }
+        }
+        seps[er][a0] = z.x;
+        seps[er][a0 + 1] = z.y;
+    }
     const int64_t S = kpad(D) / 2, G = S / 4;
-    const int64_t g0 = G * w / 4, g1 = G * (w + 1) / 4;
+    const int64_t g0 = G * w / ANW, g1 = G * (w + 1) / ANW;
     f32x16 acc0 = zero16(), acc1 = zero16();
     const float* xrow = obs + (live ? row : 0) * ldx;
     const float4* wp0 = reinterpret_cast<const float4*>(w1p) + l;
@@ -137,32 +157,25 @@ __global__ __launch_bounds__(256) void gauss_act_kernel(
             acc1 = mfma(a1[j].w, xv[j].w, acc1);
         }
     }
-    if (w > 0) {
+    // weights to LDS
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            red[w - 1][0][r][l] = acc0[r];
-            red[w - 1][1][r][l] = acc1[r];
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int e = 4 * (t + 256 * j), row = e >> 6, col = e & 63;
-        float* d = sW2 + row * WS + col;
+    for (int j = 0; j < 2; ++j) {
+        const int e = 4 * (t + NT * j), rr = e >> 6, col = e & 63;
+        float* d = sW2 + rr * WS + col;
         d[0] = w2r[j].x;
         d[1] = w2r[j].y;
         d[2] = w2r[j].z;
         d[3] = w2r[j].w;
     }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const int e = 4 * (t + 256 * j), row = e >> 6, col = e & 63;
-        if (row < AMAX) {
-            const bool ok = row < A;
-            float* d = sW3 + row * WS + col;
-            d[0] = ok ? w3r[j].x : 0.f;
-            d[1] = ok ? w3r[j].y : 0.f;
-            d[2] = ok ? w3r[j].z : 0.f;
-            d[3] = ok ? w3r[j].w : 0.f;
+    {
+        const int e = 4 * t, rr = e >> 6, col = e & 63;
+        if (rr < AMAX) {
+            const bool ok = rr < A;
+            float* d = sW3 + rr * WS + col;
+            d[0] = ok ? w3r.x : 0.f;
+            d[1] = ok ? w3r.y : 0.f;
+            d[2] = ok ? w3r.z : 0.f;
+            d[3] = ok ? w3r.w : 0.f;
         }
     }
     if (t < H) {
@@ -175,24 +188,34 @@ __global__ __launch_bounds__(256) void gauss_act_kernel(
         slo[t] = vlo;
         shi[t] = vhi;
     }
-    __syncthreads();
-    if (rng_ctr && t == 0) {
-        // every workgroup has read the counter; the last one advances it (graph-replay safe)
-        const unsigned int tk = __hip_atomic_fetch_add(rng_ticket, 1u, __ATOMIC_ACQ_REL,
-                                                       __HIP_MEMORY_SCOPE_AGENT);
-        if (tk == gridDim.x - 1) {
-            __hip_atomic_store(rng_ctr, rng_step + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(rng_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // next step's noise counter into the other slot of a ping-pong pair (no atomics)
+    if (rng_next && blockIdx.x == 0 && t == 0) *rng_next = rng_step + 1;
+    // fixed-order tree over the 8 waves' layer-1 partials
+#pragma unroll
+    for (int half = ANW / 2; half >= 1; half >>= 1) {
+        if (w >= half && w < 2 * half) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                red[w - half][0][r][l] = acc0[r];
+                red[w - half][1][r][l] = acc1[r];
+            }
         }
+        __syncthreads();
+        if (w < half) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                acc0[r] += red[w][0][r][l];
+                acc1[r] += red[w][1][r][l];
+            }
+        }
+        if (half > 1) __syncthreads();
     }
     if (w != 0) return;
     float h1[2][16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-        const float z0 = ((acc0[r] + red[0][0][r][l]) + red[1][0][r][l]) + red[2][0][r][l];
-        const float z1 = ((acc1[r] + red[0][1][r][l]) + red[1][1][r][l]) + red[2][1][r][l];
-        h1[0][r] = tanh_nb(z0 + sb1[rho(r) + 4 * h]);
-        h1[1][r] = tanh_nb(z1 + sb1[32 + rho(r) + 4 * h]);
+        h1[0][r] = tanh_nb(acc0[r] + sb1[rho(r) + 4 * h]);
+        h1[1][r] = tanh_nb(acc1[r] + sb1[32 + rho(r) + 4 * h]);
     }
     float h2[2][16];
 #pragma unroll
@@ -220,12 +243,9 @@ __global__ __launch_bounds__(256) void gauss_act_kernel(
         const int a = rho(r) + 4 * h;
         if (a >= A) continue;
         const float m = mu[r] + sb3[a];
-        // randn * sigma + mu (two roundings, as torch's mul_ then add_)
         float x = m;
-        if (p.sample) {
-            const float e = eps ? eps[row * A + a] : counter_normal(p.seed, rng_step, row, a);
-            x = __fadd_rn(__fmul_rn(e, ssig[a]), m);
-        }
+        // randn * sigma + mu (two roundings, as torch's mul_ then add_)
+        if (p.sample) x = __fadd_rn(__fmul_rn(seps[c][a], ssig[a]), m);
         act[row * A + a] = x;
         float y = x;
         if (p.bound == 1) y = y < -1.0f ? -1.0f : (y > 1.0f ? 1.0f : y);  // clamp, NaN passes
@@ -271,7 +291,7 @@ extern "C" int tsrl_gauss_policy_act(const float* obs, int64_t ldx, int64_t n, i
                    "tsrl_gauss_policy_act: obs / packed weights must be 16-byte aligned");
     TSRL_CHECK_ARG((low == nullptr) == (high == nullptr), "tsrl_gauss_policy_act: low/high");
     ActParams p{(int)act_dim, bound_method, low != nullptr, eps != nullptr, 0ull};
-    hipLaunchKernelGGL(gauss_act_kernel, dim3((unsigned)((n + 31) / 32)), dim3(256), 0,
+    hipLaunchKernelGGL(gauss_act_kernel, dim3((unsigned)((n + 31) / 32)), dim3(ANW * 64), 0,
                        as_stream(stream), obs, ldx, n, D, w1packed, b1, w2, b2, w3, b3, log_std,
                        eps, low, high, p, act, act_remap, nullptr, nullptr);
     TSRL_LAUNCH_CHECK("tsrl_gauss_policy_act");
@@ -282,7 +302,7 @@ extern "C" int tsrl_gauss_policy_act_rng(const float* obs, int64_t ldx, int64_t 
                                          const float* w1packed, const float* b1, const float* w2,
                                          const float* b2, const float* w3, const float* b3,
                                          const float* log_std, int64_t act_dim, uint64_t seed,
-                                         int64_t* rng_ctr, unsigned int* rng_ticket,
+                                         const int64_t* rng_ctr, int64_t* rng_next,
                                          int bound_method, const float* low, const float* high,
                                          float* act, float* act_remap, void* stream) {
     TSRL_CHECK_ARG(n >= 0 && D > 0 && D % 4 == 0 && ldx >= D && ldx % 4 == 0 && act_dim > 0 &&
@@ -290,15 +310,15 @@ extern "C" int tsrl_gauss_policy_act_rng(const float* obs, int64_t ldx, int64_t 
                    "tsrl_gauss_policy_act_rng: bad sizes");
     if (n == 0) return 0;
     TSRL_CHECK_ARG(obs && w1packed && b1 && w2 && b2 && w3 && b3 && log_std && act && act_remap &&
-                       rng_ctr && rng_ticket,
+                       rng_ctr && rng_next && rng_ctr != rng_next,
                    "tsrl_gauss_policy_act_rng: null pointer");
     TSRL_CHECK_ARG(aligned16(obs) && aligned16(w1packed),
                    "tsrl_gauss_policy_act_rng: obs / packed weights must be 16-byte aligned");
     TSRL_CHECK_ARG((low == nullptr) == (high == nullptr), "tsrl_gauss_policy_act_rng: low/high");
     ActParams p{(int)act_dim, bound_method, low != nullptr, 1, sm64(seed)};
-    hipLaunchKernelGGL(gauss_act_kernel, dim3((unsigned)((n + 31) / 32)), dim3(256), 0,
+    hipLaunchKernelGGL(gauss_act_kernel, dim3((unsigned)((n + 31) / 32)), dim3(ANW * 64), 0,
                        as_stream(stream), obs, ldx, n, D, w1packed, b1, w2, b2, w3, b3, log_std,
-                       nullptr, low, high, p, act, act_remap, rng_ctr, rng_ticket);
+                       nullptr, low, high, p, act, act_remap, rng_ctr, rng_next);
     TSRL_LAUNCH_CHECK("tsrl_gauss_policy_act_rng");
     return 0;
 }

@@ -96,29 +96,31 @@ __global__ __launch_bounds__(MCOLS * MLANES) void rms_merge_kernel(
 // P2 the rows counted in blk_done (blocks with none are skipped).  The state after the first
 // update (rounded to f32 like the reference's stored arrays) goes to snap_mean / snap_var for
 // normalising the step observations; the second update's result to mean / var / count.
-__global__ __launch_bounds__(MCOLS * MLANES) void rms_merge2_kernel(
+constexpr int M2COLS = 16, M2LANES = 64;
+
+__global__ __launch_bounds__(M2COLS * M2LANES) void rms_merge2_kernel(
     const double* p1, const double* p2, const double* blk_done, int64_t nblk, int64_t dim,
     int64_t k, float* mean, float* var, double* count, float* snap_mean, float* snap_var,
     unsigned int* ticket) {
-    __shared__ double sh[4][MLANES][MCOLS];
-    __shared__ double sh_nd[MCOLS * MLANES / kWave];
+    __shared__ double sh[4][M2LANES][M2COLS];
+    __shared__ double sh_nd[M2COLS * M2LANES / kWave];
     const int tid = threadIdx.x;
-    const int col = tid % MCOLS;
-    const int lane = tid / MCOLS;
+    const int col = tid % M2COLS;
+    const int lane = tid / M2COLS;
     double c = 0.0;
-    for (int64_t b = tid; b < nblk; b += MCOLS * MLANES) c += blk_done[b];
+    for (int64_t b = tid; b < nblk; b += M2COLS * M2LANES) c += blk_done[b];
     c = wave_sum(c);
     if ((tid & (kWave - 1)) == 0) sh_nd[tid / kWave] = c;
     const double old_count = *count;
     __syncthreads();
     double nd = 0.0;
-    for (int w = 0; w < MCOLS * MLANES / kWave; ++w) nd += sh_nd[w];
+    for (int w = 0; w < M2COLS * M2LANES / kWave; ++w) nd += sh_nd[w];
     const double bc1 = (double)k;
     const double tot1 = old_count + bc1, tot2 = tot1 + nd;
-    const int64_t d = (int64_t)blockIdx.x * MCOLS + col;
+    const int64_t d = (int64_t)blockIdx.x * M2COLS + col;
     double s1 = 0.0, q1 = 0.0, s2 = 0.0, q2 = 0.0;
     if (d < dim) {
-        for (int64_t b = lane; b < nblk; b += MLANES) {
+        for (int64_t b = lane; b < nblk; b += M2LANES) {
             const double2 a = *reinterpret_cast<const double2*>(p1 + (b * dim + d) * 2);
             s1 += a.x;
             q1 += a.y;
@@ -134,14 +136,17 @@ __global__ __launch_bounds__(MCOLS * MLANES) void rms_merge2_kernel(
     sh[2][lane][col] = s2;
     sh[3][lane][col] = q2;
     __syncthreads();
-    if (lane == 0 && d < dim) {
-        double S1 = 0.0, Q1 = 0.0, S2 = 0.0, Q2 = 0.0;
-        for (int l = 0; l < MLANES; ++l) {
-            S1 += sh[0][l][col];
-            Q1 += sh[1][l][col];
-            S2 += sh[2][l][col];
-            Q2 += sh[3][l][col];
+    // fixed-order tree over the lanes
+    for (int st = M2LANES / 2; st > 0; st >>= 1) {
+        if (lane < st) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) sh[q][lane][col] += sh[q][lane + st][col];
         }
+        __syncthreads();
+    }
+    if (lane == 0 && d < dim) {
+        const double S1 = sh[0][0][col], Q1 = sh[1][0][col], S2 = sh[2][0][col],
+                     Q2 = sh[3][0][col];
         double m0 = (double)mean[d], v0 = (double)var[d];
         if (bc1 > 0.0) {
             const double bm = S1 / bc1;
@@ -229,8 +234,8 @@ extern "C" int tsrl_rms_merge2(const double* partials_step, const double* partia
                    "tsrl_rms_merge2: bad arguments");
     TSRL_CHECK_ARG(aligned16(partials_step) && aligned16(partials_reset),
                    "tsrl_rms_merge2: partials not 16B aligned");
-    const int64_t grid = (dim + MCOLS - 1) / MCOLS;
-    hipLaunchKernelGGL(rms_merge2_kernel, dim3((unsigned)grid), dim3(MCOLS * MLANES), 0,
+    const int64_t grid = (dim + M2COLS - 1) / M2COLS;
+    hipLaunchKernelGGL(rms_merge2_kernel, dim3((unsigned)grid), dim3(M2COLS * M2LANES), 0,
                        as_stream(stream), partials_step, partials_reset, blk_done, nblk, dim, k,
                        mean, var, count, snap_mean, snap_var, ticket);
     TSRL_LAUNCH_CHECK("tsrl_rms_merge2");

@@ -35,7 +35,7 @@ class AddArgs(ctypes.Structure):
         ("out_ep_rew", _p), ("out_ep_len", _p), ("out_ep_idx", _p),
         ("stat_rew", _p), ("stat_len", _p), ("stat_idx", _p),
         ("reset_src", _p), ("reset_mask", _p), ("reset_mean", _p), ("reset_var", _p),
-        ("rel_ticket", _p),
+        ("rel_next", _p),
     ]
 
 

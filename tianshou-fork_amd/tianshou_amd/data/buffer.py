@@ -123,6 +123,7 @@ class VectorReplayBuffer:
         self._meta = Batch()
         self._dev = None  # device-side episode state, allocated with the storage
         self._last_sample0 = None
+        self.obs_chain = True  # see reset()
 
     # -- bookkeeping views ------------------------------------------------------------------
     @property
@@ -193,6 +194,10 @@ class VectorReplayBuffer:
     def reset(self, keep_statistics: bool = False) -> None:
         """manager.py:54-58 (+ base.py:140-146 per sub-buffer)."""
         self._ring.reset()
+        # obs_chain: every row since the reset came from a Collector step, so within an
+        # episode the stored obs of step t+1 is the stored obs_next of step t (process_fn
+        # reuses V(s) for V(s') on that basis).  Cleared by add() of arbitrary batches.
+        self.obs_chain = True
         if not keep_statistics and self._dev is not None:
             self._dev["ep_rew"].zero_()
             self._dev["ep_len"].zero_()
@@ -222,6 +227,7 @@ class VectorReplayBuffer:
         the Collector uses the fused, sync-free ``_add_step`` instead)."""
         for key in ("obs", "act", "rew", "terminated", "truncated"):
             assert key in batch.keys(), f"missing key {key}"
+        self.obs_chain = False
         ids = np.arange(self.buffer_num) if buffer_ids is None else \
             np.asarray(buffer_ids, dtype=np.int64)
         k = len(ids)
@@ -278,7 +284,7 @@ class VectorReplayBuffer:
                     rel_dev=None, obs=None, act=None, obs_next=None, obs_next_raw=None,
                     cur_obs=None, norm=None, rew=None, term=None, trunc=None, out=None,
                     stats=True, norm_snapshot=False, reset_src=None, reset_mask=None,
-                    reset_norm=None, rel_ticket=None) -> None:
+                    reset_norm=None, rel_next=None) -> None:
         """One tsrl_buffer_add launch (see include/tsrl.h)."""
         m = self._meta
         d = self._dev
@@ -316,7 +322,7 @@ class VectorReplayBuffer:
                     a.reset_var = _C.ptr(reset_norm.var_t)
                     a.norm_eps = float(reset_norm.eps)
                     a.norm_clip = float(reset_norm.clip_max or 0.0)
-        a.rel_ticket = _C.ptr(rel_ticket)
+        a.rel_next = _C.ptr(rel_next)
         if obs_next_raw is not None and has_next:
             a.obs_next_src_raw = _C.ptr(obs_next_raw)
             a.obs_next_dst_raw = _C.ptr(m.obs_next)

@@ -114,7 +114,10 @@ class Collector:
         act_shape, act_dtype = self._act_spec()
         nblk = b.nblk_for(N)
         self._scratch["blk_done"] = torch.zeros(max(nblk, 1), dtype=torch.float64, device=dev)
-        self._scratch["rel_ticket"] = torch.zeros(1, dtype=torch.int32, device=dev)
+        # ping-pong step counters [slot][ring cursor, noise counter]: step i reads slot i%2
+        # and writes slot (i+1)%2, so graph-captured steps need no atomics or extra launches
+        self._scratch["step_ctr"] = torch.zeros((2, 2), dtype=torch.int64, device=dev)
+        self._parity = 0
         self._scratch["act"] = torch.empty((N,) + act_shape, dtype=act_dtype, device=dev)
         self._scratch["act_remap"] = torch.empty((N,) + act_shape, dtype=act_dtype, device=dev)
 
@@ -231,7 +234,9 @@ class Collector:
         if self._fused_act_on and not random:
             # policy forward + sampling + map_action as one kernel (policy/fused_act.py)
             act, action_remap = s["act"][:kk], s["act_remap"][:kk]
-            self.policy.fused_act(cur, act, action_remap)
+            p = self._parity
+            sc = s["step_ctr"]
+            self.policy.fused_act(cur, act, action_remap, (sc[p, 1:2], sc[1 - p, 1:2]))
         else:
             info = Batch(env_id=s["env_id"][:kk] if ids_t is None else ids_t)
             act, _policy = self._policy_act(cur, info, random, no_grad, kk)
@@ -254,12 +259,11 @@ class Collector:
             if upd:
                 rms.merge2(s["part"], s["part2"], blk, b.nblk_for(kk), kk)
             kw = dict(add_kw)
-            if "rel_dev" in kw:
-                kw["rel_ticket"] = s["rel_ticket"]
             buf._launch_add(ids=None, k=kk, obs=cur, act=act, obs_next=raw, cur_obs=cur,
                             norm=rms, norm_snapshot=upd, reset_src=s["reset_raw"][:kk],
                             reset_mask=done, reset_norm=rms, rew=rew, term=term, trunc=trunc,
                             **kw)
+            self._parity ^= 1
             return
         b._step_raw(ids_t, kk, raw, rew, term, trunc, s["part"], action_remap)
         norm = None
@@ -274,12 +278,10 @@ class Collector:
         else:
             buf._launch_add(ids=ids_t, k=kk, obs=cur, act=act, obs_next=raw, cur_obs=cur,
                             norm=norm, rew=rew, term=term, trunc=trunc, **add_kw)
-        if "rel_dev" in add_kw:
-            _C.check(_C.lib().tsrl_ring_advance(_C.ptr(add_kw["rel_dev"]), buf._ring.size,
-                                                _C.stream_ptr(b.device)), "tsrl_ring_advance")
         torch.logical_or(term, trunc, out=done)
         b._reset_raw(ids_t, done, kk, s["reset_raw"][:kk], s["part2"])
         self._finish_obs(s["reset_raw"][:kk], cur, s["part2"], done, kk)
+        self._parity ^= 1
 
     def _graph_key(self, G: int):
         buf, b = self.buffer, self._base
@@ -301,19 +303,25 @@ class Collector:
         G = self.graph_steps
         if n_steps < G:
             return 0
+        assert G % 2 == 0, "graph_steps must be even (ping-pong step counters)"
         buf, dev = self.buffer, self._base.device
+        sc = self._scratch["step_ctr"]
+        if self._parity:  # the live counters sit in slot 1: the graph starts from slot 0
+            sc[0].copy_(sc[1])
+            self._parity = 0
         key = self._graph_key(G)
         if getattr(self, "_graph", None) is None or self._graph[0] != key:
-            rel_dev = torch.zeros(1, dtype=torch.int64, device=dev)
             graph = torch.cuda.CUDAGraph()
             torch.cuda.synchronize()
             with torch.cuda.graph(graph):
-                for _ in range(G):
-                    self._device_step(self._scratch["cur"], self.env_num, None, False,
-                                      no_grad, dict(rel_dev=rel_dev))
-            self._graph = (key, graph, rel_dev)
-        _, graph, rel_dev = self._graph
-        rel_dev.fill_(int(buf._ring.index[0]))
+                for i in range(G):
+                    self._device_step(self._scratch["cur"], self.env_num, None, False, no_grad,
+                                      dict(rel_dev=sc[i % 2, 0:1],
+                                           rel_next=sc[(i + 1) % 2, 0:1]))
+            self._graph = (key, graph)
+            self._parity = 0
+        _, graph = self._graph
+        sc[0, 0].fill_(int(buf._ring.index[0]))
         done = 0
         while n_steps - done >= G:
             graph.replay()
@@ -409,6 +417,7 @@ class Collector:
 
     def _collect_generic(self, n_step, n_episode, random, render, no_grad, gym_reset_kwargs):
         """The reference loop (collector.py:250-361) for host envs; buffer still on device."""
+        self.buffer.obs_chain = False  # host envs: no guarantee on obs / obs_next identity
         if n_step is not None:
             ready_env_ids = np.arange(self.env_num)
         else:

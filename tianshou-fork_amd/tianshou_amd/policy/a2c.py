@@ -52,6 +52,10 @@ class A2CPolicy(PGPolicy):
             out[s:e] = self.critic(obs[s:e]).flatten()
         return out
 
+    def _eval_values(self, batch, obs, obs_next, buffer, indices):
+        """V(s) and V(s') of a2c.py:86-93."""
+        return self._values(obs), self._values(obs_next)
+
     @staticmethod
     def _gae_layout(buffer, indices):
         """(row_len, end_extra): row_len > 0 when ``indices`` is the buffer's sample(0) order
@@ -72,8 +76,7 @@ class A2CPolicy(PGPolicy):
         obs = obs.to(dev)
         obs_next = torch.as_tensor(batch.obs_next).to(dev)
         with torch.no_grad():
-            v_s = self._values(obs)
-            v_s_ = self._values(obs_next)
+            v_s, v_s_ = self._eval_values(batch, obs, obs_next, buffer, indices)
         batch.v_s = v_s
         rew = torch.as_tensor(batch.rew).to(dev, torch.float64).contiguous()
         term = torch.as_tensor(batch.terminated).to(dev).bool().contiguous()

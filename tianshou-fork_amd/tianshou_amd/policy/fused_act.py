@@ -51,7 +51,8 @@ class FusedGaussAct:
         # from torch.randn on the GPU stream (the torch path's exact noise, one extra launch)
         self.rng = "device"
         self._seed = 0
-        self._ctr = None
+        self._ctr = None      # own [2] counter pair when the caller passes none
+        self._parity = 0
 
     def pack(self) -> None:
         """Pack the first-layer weight (call after every parameter update; the collector
@@ -68,19 +69,26 @@ class FusedGaussAct:
             if self._ctr is None or self._ctr.device != w.device:
                 self._ctr = torch.zeros(2, dtype=torch.int64, device=w.device)
             self._ctr.zero_()
+            self._parity = 0
 
     def __call__(self, obs: torch.Tensor, act_out: torch.Tensor, remap_out: torch.Tensor,
-                 sample: bool, bound_method, low_high) -> None:
+                 sample: bool, bound_method, low_high, ctr=None) -> None:
+        """ctr: optional (in, out) device int64 words of the noise step counter (the
+        collector passes its ping-pong slots); default: this object's own pair."""
         L, lib = self.L, _C.lib()
         n = obs.shape[0]
         low, high = low_high if low_high is not None else (None, None)
         if sample and self.rng == "device":
+            if ctr is None:
+                ctr = (self._ctr[self._parity:self._parity + 1],
+                       self._ctr[1 - self._parity:2 - self._parity])
+                self._parity ^= 1
             _C.check(lib.tsrl_gauss_policy_act_rng(
                 _C.ptr(obs), obs.stride(0), n, self.D, _C.ptr(self.packed),
                 _C.ptr(L["w1"].bias.detach()), _C.ptr(L["w2"].weight.detach()),
                 _C.ptr(L["w2"].bias.detach()), _C.ptr(L["w3"].weight.detach()),
                 _C.ptr(L["w3"].bias.detach()), _C.ptr(L["sigma"].detach()), self.A,
-                self._seed, _C.ptr(self._ctr[:1]), _C.ptr(self._ctr[1:]),
+                self._seed, _C.ptr(ctr[0]), _C.ptr(ctr[1]),
                 _BOUND[bound_method], _C.ptr(low), _C.ptr(high), _C.ptr(act_out),
                 _C.ptr(remap_out), _C.stream_ptr(obs.device)), "tsrl_gauss_policy_act_rng")
             return

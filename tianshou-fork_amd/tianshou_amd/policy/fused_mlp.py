@@ -112,6 +112,52 @@ class FusedActorCritic:
             _C.ptr(L["w2c"].bias), _C.ptr(L["w3a"].weight), _C.ptr(L["w3a"].bias),
             _C.ptr(L["w3c"].weight), _C.ptr(L["w3c"].bias), _C.ptr(L["sigma"]))
 
+    def _weights(self) -> "_C.TailWeights":
+        L = self.L
+        return _C.TailWeights(
+            _C.ptr(L["w2a"].weight.detach()), _C.ptr(L["w2a"].bias.detach()),
+            _C.ptr(L["w2c"].weight.detach()), _C.ptr(L["w2c"].bias.detach()),
+            _C.ptr(L["w3a"].weight.detach()), _C.ptr(L["w3a"].bias.detach()),
+            _C.ptr(L["w3c"].weight.detach()), _C.ptr(L["w3c"].bias.detach()),
+            _C.ptr(L["sigma"].detach()))
+
+    # -- forward-only evaluation (process_fn) ---------------------------------------------------
+    EVAL_CHUNK = 1 << 21
+
+    def evaluate(self, obs: torch.Tensor, act: Optional[torch.Tensor] = None,
+                 idx: Optional[torch.Tensor] = None):
+        """Critic values of the rows obs[idx] (all rows when idx is None) and, with act, the
+        Gaussian log-prob of act[row] (a2c.py:83-100, ppo.py:95-96).  Per-row results do not
+        depend on the chunking or on the other rows."""
+        L, lib = self.L, _C.lib()
+        dev = obs.device
+        s = _C.stream_ptr(dev)
+        D, A = self.D, self.A
+        assert obs.dim() == 2 and obs.shape[1] == D and obs.is_contiguous()
+        n = obs.shape[0] if idx is None else idx.numel()
+        values = torch.empty(n, dtype=torch.float32, device=dev)
+        logp = torch.empty(n, dtype=torch.float32, device=dev) if act is not None else None
+        w = self._weights()
+        W = [L["w1a"].weight.detach(), L["w1a"].bias.detach(), L["w1c"].weight.detach(),
+             L["w1c"].bias.detach()]
+        for s0 in range(0, n, self.EVAL_CHUNK):
+            e0 = min(n, s0 + self.EVAL_CHUNK)
+            m = e0 - s0
+            h1 = self._buf("eval_h1", int(lib.tsrl_mlp_frag_floats(m)))
+            if idx is None:
+                xp, ip = obs.data_ptr() + s0 * D * 4, None
+            else:
+                xp, ip = obs.data_ptr(), idx.data_ptr() + s0 * 8
+            _C.check(lib.tsrl_mlp_l1_fwd(xp, D, ip, m, D, *(_C.ptr(t) for t in W), 1,
+                                         _C.ptr(h1), 1, s), "tsrl_mlp_l1_fwd")
+            ap = None
+            if act is not None:
+                ap = act.data_ptr() + s0 * A * 4
+            _C.check(lib.tsrl_ppo_eval(_C.ptr(h1), m, w, A, ap, values.data_ptr() + s0 * 4,
+                                       logp.data_ptr() + s0 * 4 if logp is not None else None,
+                                       s), "tsrl_ppo_eval")
+        return values, logp
+
     @property
     def flat_grad(self) -> torch.Tensor:
         return self._flat

@@ -68,10 +68,11 @@ class PGPolicy(BasePolicy):
         fa.pack()
         return True
 
-    def fused_act(self, obs, act_out, remap_out) -> None:
+    def fused_act(self, obs, act_out, remap_out, ctr=None) -> None:
         sample = not (self._deterministic_eval and not self.training)
         low_high = self._low_high(obs.device) if self.action_scaling else None
-        self._fused_act(obs, act_out, remap_out, sample, self.action_bound_method, low_high)
+        self._fused_act(obs, act_out, remap_out, sample, self.action_bound_method, low_high,
+                        ctr)
 
     def _get_deterministic_action(self, logits):
         if self.action_type == "discrete":

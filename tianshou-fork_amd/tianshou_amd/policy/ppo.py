@@ -125,6 +125,9 @@ class PPOPolicy(A2CPolicy):
         # networks have the get_actor_critic shape (policy/fused_mlp.py); fused_mlp=False
         # keeps the torch layers + fused loss kernel.
         self._mlp = None
+        # replay whole epochs of the fused minibatch step from a captured HIP graph
+        self.graph_learn = True
+        self._learn_graph = None
         if self._fused and fused_mlp:
             layers = _fmlp.match(actor, critic)
             if layers is not None:
@@ -147,14 +150,46 @@ class PPOPolicy(A2CPolicy):
         """ppo.py:87-97."""
         if self._recompute_adv:
             self._buffer, self._indices = buffer, indices
+        self._pending_logp = None
         batch = self._compute_returns(batch, buffer, indices)
         batch.act = torch.as_tensor(batch.act, device=batch.v_s.device).to(batch.v_s.dtype)
         with torch.no_grad():
-            if self._fused:
+            if self._pending_logp is not None:
+                batch.logp_old = self._pending_logp
+            elif self._fused:
                 batch.logp_old = self._logp_fused(batch.obs, batch.act)
             else:
                 batch.logp_old = self(batch).dist.log_prob(batch.act)
+        self._pending_logp = None
         return batch
+
+    def _eval_values(self, batch, obs, obs_next, buffer, indices):
+        """Fused path: one layer-1 pass over obs gives V(s) and logp_old together (the latter
+        kept for process_fn).  V(s') reuses V(s) of the next row of the same env whenever the
+        buffer was filled by the Collector (``buffer.obs_chain``: the stored obs of step t+1 is
+        the stored obs_next of step t unless the episode ended at t), so only the episode-end
+        and segment-end rows are evaluated on obs_next; the values are bit-identical to a full
+        evaluation because every row's arithmetic is independent of the other rows."""
+        if self._mlp is None or not obs.is_cuda or obs.dtype != torch.float32 or obs.dim() != 2:
+            return super()._eval_values(batch, obs, obs_next, buffer, indices)
+        obs = obs.contiguous()
+        obs_next = obs_next.contiguous()
+        n = obs.shape[0]
+        act = torch.as_tensor(batch.act, device=obs.device).to(torch.float32).reshape(n, -1)
+        v_s, logp = self._mlp.evaluate(obs, act.contiguous())
+        self._pending_logp = logp
+        row_len, _ = self._gae_layout(buffer, indices)
+        if row_len and getattr(buffer, "obs_chain", False) and n % row_len == 0:
+            done = torch.as_tensor(batch.done, device=obs.device).bool().reshape(n).clone()
+            done[row_len - 1::row_len] = True
+            rows = done.nonzero().flatten()
+            v_s_ = torch.roll(v_s, -1)
+            if rows.numel():
+                vals, _ = self._mlp.evaluate(obs_next, None, rows)
+                v_s_[rows] = vals
+        else:
+            v_s_, _ = self._mlp.evaluate(obs_next)
+        return v_s, v_s_
 
     def _logp_fused(self, obs: torch.Tensor, act: torch.Tensor) -> torch.Tensor:
         dev = act.device
@@ -196,6 +231,10 @@ class PPOPolicy(A2CPolicy):
             mlp_ok = self._mlp is not None and batch.obs.is_cuda and \
                 batch.obs.dtype == torch.float32 and batch.obs.dim() == 2
             obs_all = batch.obs.contiguous() if mlp_ok else None
+            if mlp_ok and self._graph_ready():
+                terms.append(self._epoch_graph(obs_all, (act, logp_old, adv, ret, v_s), perm, n,
+                                               batch_size, first=(step == 0)))
+                continue
             for s, e in split_bounds(n, batch_size, merge_last=True):
                 idx = perm[s:e]
                 if mlp_ok:
@@ -223,9 +262,63 @@ class PPOPolicy(A2CPolicy):
                                              max_norm=self._grad_norm)
                 self.optim.step()
                 terms.append(t)
-        vals = torch.stack(terms).cpu().numpy() if terms else np.zeros((0, 4), np.float32)
+        vals = torch.cat([t.reshape(-1, 4) for t in terms]).cpu().numpy() if terms else \
+            np.zeros((0, 4), np.float32)
         return {"loss": vals[:, 0].tolist(), "loss/clip": vals[:, 1].tolist(),
                 "loss/vf": vals[:, 2].tolist(), "loss/ent": vals[:, 3].tolist()}
+
+    # -- HIP-graph replay of whole epochs ------------------------------------------------------
+    def _graph_ready(self) -> bool:
+        """An epoch of fused minibatches can be captured once and replayed: single process
+        (no collective in the step), no advantage recomputation, and a capturable optimiser
+        whose state already exists (the first update runs eagerly)."""
+        if not self.graph_learn or self.dp.active or self._recompute_adv:
+            return False
+        opt = self.optim
+        if not opt.defaults.get("capturable", False) or len(opt.state) == 0:
+            return False
+        return all(p in opt.state for g in opt.param_groups for p in g["params"])
+
+    def _epoch_graph(self, obs_all, arrays, perm, n: int, batch_size: int, first: bool):
+        """One epoch (every minibatch of Batch.split over ``perm``: forward, loss, backward,
+        clip_grad_norm_, optimiser step) as a replay of a captured HIP graph.  The per-update
+        arrays and the permutation are copied into static buffers the graph reads; returns
+        the [n_minibatch, 4] loss terms."""
+        bounds = split_bounds(n, batch_size, merge_last=True)
+        key = (n, batch_size, obs_all.data_ptr(), tuple(obs_all.shape),
+               tuple(a.shape for a in arrays), self._mlp.flat_grad is not None and
+               self._mlp.flat_grad.data_ptr())
+        st = self._learn_graph
+        if st is None or st["key"] != key:
+            st = None
+            self._learn_graph = None
+            static = [torch.empty_like(a) for a in arrays]
+            sperm = torch.empty(n, dtype=torch.int64, device=perm.device)
+            sterms = torch.empty(len(bounds), 4, dtype=torch.float32, device=perm.device)
+            for d, a in zip(static, arrays):
+                d.copy_(a)
+            sperm.copy_(perm)
+            self._mlp.bind_grads()
+            torch.cuda.synchronize()
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                for i, (s, e) in enumerate(bounds):
+                    t = self._mlp.minibatch(obs_all, sperm[s:e], e - s, *static,
+                                            self._params(e - s), self.dp)
+                    if self._grad_norm:
+                        nn.utils.clip_grad_norm_(self._actor_critic.parameters(),
+                                                 max_norm=self._grad_norm)
+                    self.optim.step()
+                    sterms[i].copy_(t)
+            st = dict(key=key, graph=graph, static=static, perm=sperm, terms=sterms)
+            self._learn_graph = st
+            first = False  # static arrays already hold this update's data
+        if first:
+            for d, a in zip(st["static"], arrays):
+                d.copy_(a)
+        st["perm"].copy_(perm)
+        st["graph"].replay()
+        return st["terms"].clone()
 
     def _learn_generic(self, batch: Batch, batch_size: int, repeat: int
                        ) -> Dict[str, List[float]]:

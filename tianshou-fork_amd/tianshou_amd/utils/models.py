@@ -34,11 +34,15 @@ def init_actor_critic(actor: nn.Module, critic: nn.Module) -> ActorCritic:
 
 def init_and_get_optim(actor, critic, lr: float, optim_class=None):
     """models.py:77-93.  Default optimiser: Adam, fused single-kernel form on the GPU (same
-    update rule; the foreach form launches ~10 kernels per step over 14 small tensors)."""
+    update rule; the foreach form launches ~10 kernels per step over 14 small tensors), and
+    capturable (step counts on device) so PPO epochs can be replayed from a HIP graph."""
     actor_critic = init_actor_critic(actor, critic)
     if optim_class is None:
         on_gpu = next(actor_critic.parameters()).is_cuda
-        return torch.optim.Adam(actor_critic.parameters(), lr=lr, fused=on_gpu or None)
+        if on_gpu:
+            return torch.optim.Adam(actor_critic.parameters(), lr=lr, fused=True,
+                                    capturable=True)
+        return torch.optim.Adam(actor_critic.parameters(), lr=lr)
     return optim_class(actor_critic.parameters(), lr=lr)
 
 
