@@ -30,6 +30,7 @@ import torch  # noqa: E402
 
 GAE_BYTES_PER_TRANSITION = 26  # rew f64 8 + v_s 4 + v_s_ 4 + term 1 + trunc 1 + adv 4 + ret 4
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+SPIN_CYCLES = 100_000          # device spin ahead of the GAE start event (see GaeTimer)
 
 
 def parse():
@@ -48,11 +49,19 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=256,
                     help="T' of the bounded CPU-baseline sample (envs x T')")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--eager-learn", action="store_true",
+                    help="diagnostic: run learn() eagerly (no HIP-graph epoch replay), as the "
+                         "data-parallel (N>1) path does")
     return ap.parse_args()
 
 
 class GaeTimer:
-    """HIP-event timing of every tsrl_gae launch (on the stream it is launched on)."""
+    """HIP-event timing of every tsrl_gae launch (on the stream it is launched on).
+
+    A short device-side spin (``torch.cuda._sleep``) is queued before the start event so that
+    the GPU is still busy while the host enqueues the event and the kernel: the event pair
+    then brackets the kernel alone, not host launch latency (the spin costs ~50 us per
+    update, outside the bracket)."""
 
     def __init__(self):
         self.events = []
@@ -62,6 +71,8 @@ class GaeTimer:
     def __call__(self, phase, n):
         if not self.on:
             return
+        if phase == "start":
+            torch.cuda._sleep(SPIN_CYCLES)
         ev = torch.cuda.Event(enable_timing=True)
         ev.record(torch.cuda.current_stream())
         if phase == "start":
@@ -107,6 +118,7 @@ def main():
                        recompute_advantage=False, eps_clip=0.2, value_clip=False,
                        dual_clip=None, action_bound_method="clip",
                        perm_device=(args.perm == "device")).to(dev)
+    policy.graph_learn = not args.eager_learn
     buf = VectorReplayBuffer(n, E, device=dev)
     coll = Collector(policy, env, buf)
     timer = GaeTimer()

@@ -91,6 +91,7 @@ def test_collector_fused_act_matches_torch_path(dev):
         buf = VectorReplayBuffer(E * T, E, device=dev)
         c = Collector(pol, env, buf)
         c.use_fused_act = fused
+        c.graph_steps = 8  # T = 40: replayed from a captured HIP graph after the first step
         torch.manual_seed(1)
         c.collect(n_step=E * T)
         assert c._fused_act_on == fused

@@ -113,7 +113,9 @@ def _collector_setup(z, dev, n_envs=None):
     sd = {k[len("init_"):]: torch.as_tensor(z[k]) for k in z.files if k.startswith("init_")}
     policy.load_state_dict(sd)
     buf = VectorReplayBuffer(E * T, E, device=dev)
-    return env, policy, buf, Collector(policy, env, buf), (E, D, A, L, T)
+    c = Collector(policy, env, buf)
+    c.graph_steps = 4  # T = 20: exercise the HIP-graph replay of the fused step
+    return env, policy, buf, c, (E, D, A, L, T)
 
 
 def _check_buf(z, prefix, buf, D):

@@ -73,6 +73,17 @@ class RingIndex:
             n = int(L[0])
             if n == 0:
                 return np.zeros(0, np.int64)
+            if n == self.size and not self.index.any():
+                # every env full with its cursor at 0 (the on-policy layout after
+                # reset_buffer + collect(n_step=maxsize)): storage order.  One read-only
+                # arange is kept and handed out again (building 8.4M indices costs ~30 ms
+                # of host time per update otherwise).
+                ident = getattr(self, "_ident", None)
+                if ident is None or len(ident) != self.maxsize:
+                    ident = np.arange(self.maxsize, dtype=np.int64)
+                    ident.flags.writeable = False
+                    self._ident = ident
+                return ident
             p = np.arange(n, dtype=np.int64)
             rel = (self.index[:, None] + p[None, :]) % n
             return (rel + self.offset[:, None]).reshape(-1)

@@ -51,7 +51,7 @@ class Collector:
         self._assign_buffer(buffer)
         self._scratch = None
         # vector steps per captured HIP graph (0 disables graph replay of the fused step)
-        self.graph_steps = 16
+        self.graph_steps = 64
         self._graph = None
         # run the policy step as the fused HIP kernel when the policy offers one
         self.use_fused_act = True
