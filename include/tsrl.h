@@ -96,12 +96,16 @@ int tsrl_synth_box_step_reset(int64_t k, int64_t dim, uint64_t seed, int64_t ep_
 int tsrl_synth_box_reset(const int64_t* ids, const uint8_t* mask, int64_t k, int64_t dim,
                          uint64_t seed, int64_t ep_len, int64_t* ep_j, int64_t* ep_t,
                          float* obs_out, double* col_partials, void* stream);
-int tsrl_synth_u8_step(const int64_t* ids, int64_t k, int64_t obs_bytes, uint64_t seed,
-                       int64_t ep_len, int64_t* ep_j, int64_t* ep_t, uint8_t* obs_out,
-                       double* rew_out, uint8_t* term_out, uint8_t* trunc_out, void* stream);
+/* u8 observations of obs_bytes per row; frame_stack S > 1 emulates gymnasium's FrameStack:
+ * the row is S frames of obs_bytes/S, frame q = the frame of episode time
+ * max(t - (S-1-q), episode start) (a reset repeats its first frame S times). */
+int tsrl_synth_u8_step(const int64_t* ids, int64_t k, int64_t obs_bytes, int64_t frame_stack,
+                       uint64_t seed, int64_t ep_len, int64_t* ep_j, int64_t* ep_t,
+                       uint8_t* obs_out, double* rew_out, uint8_t* term_out,
+                       uint8_t* trunc_out, void* stream);
 int tsrl_synth_u8_reset(const int64_t* ids, const uint8_t* mask, int64_t k,
-                        int64_t obs_bytes, uint64_t seed, int64_t ep_len, int64_t* ep_j,
-                        int64_t* ep_t, uint8_t* obs_out, void* stream);
+                        int64_t obs_bytes, int64_t frame_stack, uint64_t seed, int64_t ep_len,
+                        int64_t* ep_j, int64_t* ep_t, uint8_t* obs_out, void* stream);
 
 /* ---------------------------------------------------------------------------------
  * Observation RunningMeanStd (VectorEnvNormObs, tianshou/env/venv_wrappers.py:65-112;
@@ -179,10 +183,36 @@ typedef struct tsrl_add_args {
     const float* reset_src; const uint8_t* reset_mask;
     const float* reset_mean; const float* reset_var;
     int64_t* rel_next;
+    /* source row pitches in bytes (0: the destination row size).  save_only_last_obs
+     * (manager.py:127-132) stores the last frame of each [stack, ...] observation: the
+     * source then points at frame stack-1 of row 0 and the pitch is the whole row. */
+    int64_t obs_src_pitch;
+    int64_t obs_next_src_pitch;
 } tsrl_add_args;
 int tsrl_buffer_add(const tsrl_add_args* a, void* stream);
 /* *rel_dev = (*rel_dev + 1) % ring_size (device-side ring cursor for graph-captured steps). */
 int tsrl_ring_advance(int64_t* rel_dev, int64_t ring_size, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * Episode-aware index stepping and frame stacking of a VectorReplayBuffer whose `num`
+ * sub-buffers of `size` rows each hold lengths[b] rows and last wrote last_index[b]
+ * (global row), with per-row done flags (ReplayBufferManager, manager.py:24-297).
+ * tsrl_ring_step_index: out[r] = prev^steps(idx[r]) for steps > 0 (manager.py:259-277,
+ *   _prev_index), next^(-steps)(idx[r]) for steps < 0 (manager.py:280-297, _next_index),
+ *   idx[r] mod (size*num) for steps == 0.
+ * tsrl_stack_gather: ReplayBuffer.get(idx, key, stack_num) (buffer/base.py:317-358):
+ *   dst[r][s] = src[prev^(stack_num-1-s)(idx[r])] for rows of frame_bytes bytes (the
+ *   save_only_last_obs frame store of the Atari setup, examples/atari/atari_ppo.py:183-189,
+ *   or whole stored rows); chain_out [k][stack_num] (nullable) receives the row indices so
+ *   that other keys (info, policy) can be stacked alike; dst may be NULL (chain only).
+ * ------------------------------------------------------------------------------- */
+int tsrl_ring_step_index(const int64_t* idx, int64_t k, const uint8_t* done,
+                         const int64_t* last_index, const int64_t* lengths, int64_t size,
+                         int64_t num, int steps, int64_t* out, void* stream);
+int tsrl_stack_gather(const void* src, int64_t frame_bytes, const int64_t* idx, int64_t k,
+                      int64_t stack_num, const uint8_t* done, const int64_t* last_index,
+                      const int64_t* lengths, int64_t size, int64_t num, void* dst,
+                      int64_t* chain_out, void* stream);
 
 /* Row gather: dst[i] = src[idx[i]] for rows of row_bytes bytes (Batch.__getitem__ /
  * ReplayBuffer.__getitem__ fancy indexing, tianshou/data/batch.py:446-460,
@@ -237,6 +267,26 @@ int tsrl_ppo_gauss_finalize(const double* sums, int64_t act_dim, const float* lo
  * used for logp_old in PPOPolicy.process_fn (ppo.py:95-96). */
 int tsrl_gauss_logp(const float* mu, const float* log_std, const float* act, int64_t b,
                     int64_t act_dim, float* out, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * The same PPO minibatch loss for Categorical policies (discrete actions):
+ * mode 0 = Categorical(logits=x) (examples/atari/atari_ppo.py:136-137), mode 1 =
+ * Categorical(probs=x) (test/discrete/test_ppo.py:95 with the softmax Actor,
+ * utils/net/discrete.py:69-70).  x [b, num_actions] is the dist_fn input of the minibatch
+ * rows (minibatch order); act (i64 action indices), logp_old, adv, ret, v_s are read through
+ * idx.  Writes d(mean loss)/dx [b, num_actions] and d/d(value) [b]; partials [nblk][4] =
+ * (clip_sum, vf_sum, count, entropy_sum) for tsrl_reduce_partials, then
+ * tsrl_ppo_cat_finalize -> losses [4] = (loss, clip, vf, ent).  tsrl_cat_logp is
+ * dist.log_prob(act) for logp_old (ppo.py:95-96).
+ * ------------------------------------------------------------------------------- */
+int tsrl_ppo_cat_fwd_bwd(const float* x, const float* value, const int64_t* act,
+                         const float* logp_old, const float* adv, const float* ret,
+                         const float* v_s, const int64_t* idx, int64_t b, int64_t num_actions,
+                         int mode, const double* adv_sums, tsrl_ppo_params p, float* grad_x,
+                         float* grad_value, double* partials, void* stream);
+int tsrl_ppo_cat_finalize(const double* sums, tsrl_ppo_params p, float* losses, void* stream);
+int tsrl_cat_logp(const float* x, const int64_t* act, int64_t b, int64_t num_actions, int mode,
+                  float* out, void* stream);
 
 /* ---------------------------------------------------------------------------------
  * Fused actor/critic MLP of the PPO minibatch for the MuJoCo network shape

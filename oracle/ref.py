@@ -178,6 +178,30 @@ class VecBufferIndex:
         return (index - start + 1 - end) % cur + start
 
 
+def stack_get(val, index, stack_num, prev):
+    """ReplayBuffer.get(index, key, stack_num) restated (buffer/base.py:317-358): the newest
+    frame is val[index], older frames step back through prev (episode-aware)."""
+    indices = np.asarray(index)
+    if stack_num == 1:
+        return val[indices]
+    stack = []
+    for _ in range(stack_num):
+        stack = [val[indices]] + stack
+        indices = prev(indices)
+    return np.stack(stack, axis=indices.ndim)
+
+
+def avail_indices(ix, stack_num):
+    """sample_indices(0) with sample_avail and stack_num > 1 (manager.py:165-171 ->
+    base.py:291-303 per sub-buffer): rows whose stack_num-1 predecessors are all in the
+    same episode."""
+    all_idx = ix.sample_indices0()
+    p = all_idx
+    for _ in range(stack_num - 2):
+        p = ix.prev(p)
+    return all_idx[p != ix.prev(p)]
+
+
 # ---------------------------------------------------------------------------------------
 # RunningMeanStd: tianshou/utils/statistics.py:69-114
 # ---------------------------------------------------------------------------------------
@@ -260,3 +284,41 @@ def ppo_gaussian_loss_torch(mu, sigma_param, value, act, logp_old, adv, returns,
     loss.backward()
     return (loss.detach(), clip_loss.detach(), vf_loss.detach(), ent_loss.detach(),
             dict(mu=mu.grad, sigma_param=sp.grad, value=value.grad))
+
+
+# ---------------------------------------------------------------------------------------
+# PPO minibatch loss (ppo.py:106-151) for Categorical policies: Categorical(logits=x)
+# (examples/atari/atari_ppo.py:136-137) or Categorical(probs=x) (test/discrete/test_ppo.py:95).
+# torch fp32 on CPU = the fp32 reference of the fused tsrl_ppo_cat kernel.
+# ---------------------------------------------------------------------------------------
+def ppo_categorical_loss_torch(x, value, act, logp_old, adv, returns, v_s, mode,
+                               eps_clip=0.2, dual_clip=None, value_clip=False, norm_adv=True,
+                               vf_coef=0.5, ent_coef=0.01, eps=1e-8):
+    """Returns (loss, clip_loss, vf_loss, ent_loss, grads{x, value})."""
+    import torch
+    x = x.detach().clone().requires_grad_(True)
+    value = value.detach().clone().requires_grad_(True)
+    dist = torch.distributions.Categorical(logits=x) if mode == 0 else \
+        torch.distributions.Categorical(probs=x, validate_args=False)
+    if norm_adv:
+        adv = (adv - adv.mean()) / (adv.std() + eps)
+    ratio = (dist.log_prob(act) - logp_old).exp().float()
+    ratio = ratio.reshape(ratio.size(0), -1).transpose(0, 1)
+    surr1 = ratio * adv
+    surr2 = ratio.clamp(1.0 - eps_clip, 1.0 + eps_clip) * adv
+    if dual_clip:
+        clip1 = torch.min(surr1, surr2)
+        clip2 = torch.max(clip1, dual_clip * adv)
+        clip_loss = -torch.where(adv < 0, clip2, clip1).mean()
+    else:
+        clip_loss = -torch.min(surr1, surr2).mean()
+    if value_clip:
+        v_clip = v_s + (value - v_s).clamp(-eps_clip, eps_clip)
+        vf_loss = torch.max((returns - value).pow(2), (returns - v_clip).pow(2)).mean()
+    else:
+        vf_loss = (returns - value).pow(2).mean()
+    ent_loss = dist.entropy().mean()
+    loss = clip_loss + vf_coef * vf_loss - ent_coef * ent_loss
+    loss.backward()
+    return (loss.detach(), clip_loss.detach(), vf_loss.detach(), ent_loss.detach(),
+            dict(x=x.grad, value=value.grad))

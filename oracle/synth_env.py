@@ -63,6 +63,16 @@ def u8_obs(k, shape):
     return (h & np.uint64(0xFF)).astype(np.uint8).reshape(k.shape + tuple(shape))
 
 
+def u8_obs_stacked(seed, e, j, t, t0, shape):
+    """frame_stack mode (shape = (S, *frame)): frame q is the u8 frame of time
+    max(t - (S-1-q), t0), t0 the episode's first step (gymnasium FrameStack over a one-frame
+    env; a reset repeats its first frame)."""
+    S, frame = shape[0], tuple(shape[1:])
+    e, j, t, t0 = (np.asarray(a, np.int64) for a in (e, j, t, t0))
+    out = [u8_obs(key(seed, e, j, np.maximum(t - (S - 1 - q), t0)), frame) for q in range(S)]
+    return np.stack(out, axis=e.ndim)
+
+
 def reward(k):
     h = sm(k ^ REW_SALT)
     return (h >> np.uint64(40)).astype(np.float64) * (2.0 ** -24)
@@ -71,14 +81,18 @@ def reward(k):
 class SynthVecEnvNP:
     """Vectorised NumPy version (all envs in one object), used as the CPU port."""
 
-    def __init__(self, num_envs, obs_shape, act_dim, ep_len, seed=0, u8=False):
+    def __init__(self, num_envs, obs_shape, act_dim, ep_len, seed=0, u8=False, frame_stack=1):
         self.num_envs, self.obs_shape, self.act_dim = num_envs, tuple(obs_shape), act_dim
         self.ep_len, self.seed, self.u8 = ep_len, seed, u8
+        self.frame_stack = frame_stack
         self.j = np.full(num_envs, -1, np.int64)
         self.t = np.zeros(num_envs, np.int64)
 
     def _obs(self, ids):
         k = key(self.seed, ids, self.j[ids], self.t[ids])
+        if self.u8 and self.frame_stack > 1:
+            t0 = np.where(self.j[ids] == 0, ids % self.ep_len, 0)
+            return u8_obs_stacked(self.seed, ids, self.j[ids], self.t[ids], t0, self.obs_shape)
         if self.u8:
             return u8_obs(k, self.obs_shape)
         return box_obs(k, int(np.prod(self.obs_shape))).reshape((len(ids),) + self.obs_shape)

@@ -1,0 +1,115 @@
+"""Atari-shaped on-policy path (BASELINE config 5 in miniature): uint8
+4x84x84 frame stacks from the device env (frame_stack=4, gymnasium FrameStack semantics),
+a save_only_last_obs / ignore_obs_next / stack_num=4 VectorReplayBuffer
+(examples/atari/atari_ppo.py:183-189), the Nature-DQN trunk shared by a logits actor and a
+critic (atari_ppo.py:104-137) and PPO with the fused Categorical loss.
+
+Parity: the buffer stores exactly the last frame of every observation (bit-exact vs the
+NumPy env restatement, oracle/synth_env.py), and the stacked observations the buffer
+rebuilds through its episode-aware prev chain are exactly the frame stacks the collector saw
+(bit-exact).  The PPO update must produce finite losses and the fused-loss learn() must
+match the torch formulation of the same update (rtol 1e-4 on the losses)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import synth_env
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    return torch.device("cuda", 0)
+
+
+def _setup(dev, E, T, L, seed=0):
+    from tianshou_amd.data import Collector, VectorReplayBuffer
+    from tianshou_amd.env import Discrete, SyntheticVectorEnv
+    from tianshou_amd.policy import PPOPolicy
+    from tianshou_amd.utils.net import ActorCritic, DiscreteActor, DiscreteCritic
+    from tianshou_amd.utils.net_atari import DQN, layer_init
+    torch.manual_seed(seed)
+    env = SyntheticVectorEnv(E, (4, 84, 84), 6, ep_len=L, seed=3, device=dev,
+                             obs_dtype=np.uint8, discrete=True, frame_stack=4)
+    net = DQN(4, 84, 84, (6,), device=dev, features_only=True, output_dim=512,
+              layer_init=layer_init).to(dev)
+    actor = DiscreteActor(net, 6, softmax_output=False, device=dev).to(dev)
+    critic = DiscreteCritic(net, device=dev).to(dev)
+    optim = torch.optim.Adam(ActorCritic(actor, critic).parameters(), lr=2.5e-4)
+    policy = PPOPolicy(actor, critic, optim,
+                       lambda p: torch.distributions.Categorical(logits=p),
+                       action_space=Discrete(6), action_scaling=False, discount_factor=0.99,
+                       gae_lambda=0.95, max_grad_norm=0.5, vf_coef=0.25, ent_coef=0.01,
+                       eps_clip=0.1, value_clip=True, advantage_normalization=False,
+                       reward_normalization=True).to(dev)
+    buf = VectorReplayBuffer(E * T, E, stack_num=4, ignore_obs_next=True,
+                             save_only_last_obs=True, device=dev)
+    return env, policy, buf, Collector(policy, env, buf, exploration_noise=True)
+
+
+def test_atari_frame_stack_collect_and_update(dev):
+    E, T, L = 8, 24, 11
+    env, policy, buf, coll = _setup(dev, E, T, L)
+    res = coll.collect(n_step=E * T)
+    assert res["n/st"] == E * T
+    assert buf.obs.shape == (buf.maxsize, 84, 84) and buf.obs.dtype == torch.uint8
+    assert "obs_next" not in buf._meta.keys()
+    # the observation stream of every env, from the NumPy env restatement
+    ref = synth_env.SynthVecEnvNP(E, (4, 84, 84), 6, L, seed=3, u8=True, frame_stack=4)
+    cur = ref.reset()
+    seen = np.zeros((E, T, 4, 84, 84), np.uint8)
+    dones = np.zeros((E, T), bool)
+    for t in range(T):
+        seen[:, t] = cur
+        nxt, _, term, trunc = ref.step()
+        done = term | trunc
+        dones[:, t] = done
+        if done.any():
+            ids = np.flatnonzero(done)
+            nxt[ids] = ref.reset(ids)
+        cur = nxt
+    stored = buf.obs.cpu().numpy().reshape(E, T, 84, 84)
+    assert np.array_equal(stored, seen[:, :, -1])
+    batch, idx = buf.sample(0)
+    assert np.array_equal(idx, np.arange(E * T))
+    assert batch.obs.shape == (E * T, 4, 84, 84)
+    assert np.array_equal(batch.obs.cpu().numpy().reshape(E, T, 4, 84, 84), seen)
+    # obs_next = get(next(idx), "obs"): the next observation inside an episode, the row's own
+    # observation where the episode (or the stored data) ends (base.py:380-381)
+    on = batch.obs_next.cpu().numpy().reshape(E, T, 4, 84, 84)
+    inner = ~dones[:, :-1]
+    assert np.array_equal(on[:, :-1][inner], seen[:, 1:][inner])
+    assert np.array_equal(on[:, :-1][~inner], seen[:, :-1][~inner])
+    assert np.array_equal(on[:, -1], seen[:, -1])
+    assert np.array_equal(batch.info.env_id.cpu().numpy()[:, -1],
+                          np.repeat(np.arange(E), T))
+    out = policy.update(0, buf, batch_size=E * T // 4, repeat=2)
+    assert len(out["loss"]) == 8 and np.all(np.isfinite(out["loss"]))
+
+
+def test_atari_fused_cat_learn_matches_torch_formulation(dev):
+    """The same collected batch and minibatch order through the fused Categorical loss and
+    through the reference's torch formulation (_learn_generic)."""
+    E, T, L = 8, 16, 7
+    _, policy, buf, coll = _setup(dev, E, T, L, seed=1)
+    coll.collect(n_step=E * T)
+    batch, idx = buf.sample(0)
+    batch = policy.process_fn(batch, buf, idx)
+    sd = {k: v.clone() for k, v in policy.state_dict().items()}
+    osd = policy.optim.state_dict()
+    results = []
+    for fused in (True, False):
+        policy.load_state_dict(sd)
+        policy.optim.load_state_dict(osd)
+        np.random.seed(4)
+        if fused:
+            r = policy.learn(batch, batch_size=E * T // 2, repeat=2)
+        else:
+            r = policy._learn_generic(batch, batch_size=E * T // 2, repeat=2)
+        results.append((r, {k: v.detach().cpu().clone() for k, v in
+                            policy.state_dict().items()}))
+    for k in ("loss", "loss/clip", "loss/vf", "loss/ent"):
+        np.testing.assert_allclose(results[0][0][k], results[1][0][k], rtol=1e-4, atol=1e-5)
+    for k, v in results[0][1].items():
+        np.testing.assert_allclose(v.numpy(), results[1][1][k].numpy(), rtol=1e-3, atol=1e-5)

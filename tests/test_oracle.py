@@ -156,3 +156,56 @@ def test_ppo_loss_oracle_matches_reference_grads(golden_dir):
     np.testing.assert_allclose(float(clip), float(z["base_loss_clip"][0]), rtol=1e-5)
     np.testing.assert_allclose(float(vf), float(z["base_loss_vf"][0]), rtol=1e-5)
     np.testing.assert_allclose(float(ent), float(z["base_loss_ent"][0]), rtol=1e-5)
+
+
+STACK_CASES = [("atari", 4, True, True, False), ("avail", 4, True, True, True),
+               ("full_obs", 3, False, False, False), ("last_next", 3, True, False, True)]
+
+
+def replay_stack_case(z, name, last_only, ign_next):
+    """Re-run the golden add sequence through the oracle's index restatement; returns the
+    index object and the stored obs / obs_next arrays (manager.py:104-161)."""
+    p = name + "_"
+    num, per = 5, 8
+    ix = ref.VecBufferIndex(num * per, num)
+    frame = z[p + "in_obs"].shape[2:] if last_only else z[p + "in_obs"].shape[1:]
+    obs = np.zeros((ix.maxsize,) + frame, np.uint8)
+    obs_next = np.zeros_like(obs)
+    o = 0
+    for step, k in enumerate(z[p + "sizes"]):
+        sl = slice(o, o + k)
+        o += k
+        ids = z[p + "ids"][sl]
+        gptr, _, _, _ = ix.add(z[p + "in_rew"][sl], z[p + "in_term"][sl], z[p + "in_trunc"][sl],
+                               ids)
+        ob, obn = z[p + "in_obs"][sl], z[p + "in_obs_next"][sl]
+        obs[gptr] = ob[:, -1] if last_only else ob
+        obs_next[gptr] = obn[:, -1] if last_only else obn
+        if step == 40:
+            ix.reset(keep_statistics=True)
+    return ix, obs, (None if ign_next else obs_next)
+
+
+@pytest.mark.parametrize("name,stack_num,last_only,ign_next,avail", STACK_CASES)
+def test_frame_stack_oracle(golden_dir, name, stack_num, last_only, ign_next, avail):
+    """oracle.stack_get / avail_indices vs the reference's VectorReplayBuffer with
+    stack_num / save_only_last_obs / ignore_obs_next / sample_avail (tools/gen_goldens.py
+    gen_stack), bit-exact."""
+    z = np.load(os.path.join(golden_dir, "stack.npz"))
+    p = name + "_"
+    ix, obs, obs_next = replay_stack_case(z, name, last_only, ign_next)
+    assert np.array_equal(obs, z[p + "stored_obs"])
+    if obs_next is not None:
+        assert np.array_equal(obs_next, z[p + "stored_obs_next"])
+    allidx = np.arange(ix.maxsize)
+    assert np.array_equal(ix.prev(allidx), z[p + "prev"])
+    assert np.array_equal(ix.next(allidx), z[p + "next"])
+    q = z[p + "q_idx"]
+    assert np.array_equal(ref.stack_get(obs, q, stack_num, ix.prev), z[p + "q_obs"])
+    want_next = ref.stack_get(obs, ix.next(q), stack_num, ix.prev) if obs_next is None else \
+        ref.stack_get(obs_next, q, stack_num, ix.prev)
+    assert np.array_equal(want_next, z[p + "q_obs_next"])
+    if avail:
+        assert np.array_equal(ref.avail_indices(ix, stack_num), z[p + "sample0"])
+    else:
+        assert np.array_equal(ix.sample_indices0(), z[p + "sample0"])

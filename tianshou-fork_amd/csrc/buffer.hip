@@ -44,14 +44,16 @@ __global__ __launch_bounds__(TPB) void buffer_add_kernel(tsrl_add_args a) {
         const int64_t b = a.ids ? a.ids[r] : r;
         const int64_t ptr = a.ptr ? a.ptr[r] : a.offset[b] + urel;
 
+        const int64_t obs_pitch = a.obs_src_pitch ? a.obs_src_pitch : a.obs_row_bytes;
+        const int64_t next_pitch = a.obs_next_src_pitch ? a.obs_next_src_pitch : a.obs_row_bytes;
         if (a.obs_src && a.obs_dst)
-            copy_row((const char*)a.obs_src + r * a.obs_row_bytes,
+            copy_row((const char*)a.obs_src + r * obs_pitch,
                      (char*)a.obs_dst + ptr * a.obs_row_bytes, a.obs_row_bytes, lane);
         if (a.act_src && a.act_dst)
             copy_row((const char*)a.act_src + r * a.act_row_bytes,
                      (char*)a.act_dst + ptr * a.act_row_bytes, a.act_row_bytes, lane);
         if (a.obs_next_src_raw && a.obs_next_dst_raw)
-            copy_row((const char*)a.obs_next_src_raw + r * a.obs_row_bytes,
+            copy_row((const char*)a.obs_next_src_raw + r * next_pitch,
                      (char*)a.obs_next_dst_raw + ptr * a.obs_row_bytes, a.obs_row_bytes, lane);
         if (a.obs_next_src && (a.obs_next_dst || a.cur_obs)) {
             const float* src = a.obs_next_src + r * a.obs_dim;

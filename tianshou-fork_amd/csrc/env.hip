@@ -156,36 +156,59 @@ __global__ __launch_bounds__(1024) void box_step_reset_kernel(
 }
 
 // u8 (Atari-shaped) observations: 4 bytes per thread-iteration, packed 32-bit stores.
-__device__ void u8_rows(const RowState* rs, int64_t r0, int64_t k, int64_t nbytes,
-                        uint8_t* obs) {
+// frame_stack S > 1 emulates gymnasium's FrameStack wrapper over a one-frame env: the
+// observation is the last S frames, frame q of the obs at episode time t is the frame of
+// time max(t - (S-1-q), t0) (t0 = the episode's first time step, whose frame a reset repeats
+// S times).  fk[r][q] holds the key of that frame; S == 1 is the plain u8 observation.
+constexpr int MAX_STACK = 8;
+
+__device__ void u8_rows(const RowState* rs, const uint64_t (*fk)[MAX_STACK], int64_t r0,
+                        int64_t k, int64_t nbytes, int S, uint8_t* obs) {
     const int nrows = (int)min((int64_t)ROWS, k - r0);
-    const int64_t nw = nbytes / 4;
+    const int64_t fbytes = nbytes / S;
     for (int r = 0; r < nrows; ++r) {
         if (!rs[r].active) continue;
-        const uint64_t key = rs[r].key;
         uint8_t* row = obs + (r0 + r) * nbytes;
-        if ((nbytes & 3) == 0 && (((uintptr_t)row) & 3) == 0) {
+        if ((fbytes & 3) == 0 && (((uintptr_t)row) & 3) == 0) {
             uint32_t* w = reinterpret_cast<uint32_t*>(row);
-            for (int64_t q = threadIdx.x; q < nw; q += TPB) {
+            for (int64_t q = threadIdx.x; q < nbytes / 4; q += TPB) {
+                const int f = (int)((4 * q) / fbytes);
+                const uint64_t key = fk[r][f];
+                const uint64_t i0 = (uint64_t)(4 * q - f * fbytes);
                 uint32_t v = 0;
 #pragma unroll
                 for (int b = 0; b < 4; ++b)
-                    v |= (uint32_t)(sm64(key + (uint64_t)(4 * q + b) * GOLD) & 0xFF) << (8 * b);
+                    v |= (uint32_t)(sm64(key + (i0 + b) * GOLD) & 0xFF) << (8 * b);
                 w[q] = v;
             }
         } else {
-            for (int64_t i = threadIdx.x; i < nbytes; i += TPB)
-                row[i] = (uint8_t)(sm64(key + (uint64_t)i * GOLD) & 0xFF);
+            for (int64_t i = threadIdx.x; i < nbytes; i += TPB) {
+                const int f = (int)(i / fbytes);
+                row[i] = (uint8_t)(sm64(fk[r][f] + (uint64_t)(i - f * fbytes) * GOLD) & 0xFF);
+            }
         }
     }
 }
 
+__device__ __forceinline__ void frame_keys(uint64_t s_seed, int64_t e, int64_t j, int64_t t,
+                                           int64_t t0, int S, uint64_t* fk) {
+    for (int q = 0; q < S; ++q) {
+        const int64_t tq = max(t - (int64_t)(S - 1 - q), t0);
+        fk[q] = env_key(s_seed, (uint64_t)e, j, tq);
+    }
+}
+
+__device__ __forceinline__ int64_t episode_t0(int64_t e, int64_t j, int64_t ep_len) {
+    return j == 0 ? e % ep_len : 0;
+}
+
 __global__ __launch_bounds__(TPB) void u8_step_kernel(const int64_t* ids, int64_t k,
-                                                      int64_t nbytes, uint64_t s_seed,
+                                                      int64_t nbytes, int S, uint64_t s_seed,
                                                       int64_t ep_len, int64_t* ep_j,
                                                       int64_t* ep_t, uint8_t* obs, double* rew,
                                                       uint8_t* term, uint8_t* trunc) {
     __shared__ RowState rs[ROWS];
+    __shared__ uint64_t fk[ROWS][MAX_STACK];
     const int64_t r0 = (int64_t)blockIdx.x * ROWS;
     if (threadIdx.x < ROWS) {
         const int64_t r = r0 + threadIdx.x;
@@ -197,6 +220,7 @@ __global__ __launch_bounds__(TPB) void u8_step_kernel(const int64_t* ids, int64_
             ep_t[e] = t;
             st.key = env_key(s_seed, (uint64_t)e, j, t);
             st.active = 1;
+            frame_keys(s_seed, e, j, t, episode_t0(e, j, ep_len), S, fk[threadIdx.x]);
             const uint64_t h = sm64(st.key ^ REW_SALT);
             rew[r] = (double)(h >> 40) * 0x1p-24;
             const bool done = t >= ep_len;
@@ -206,15 +230,16 @@ __global__ __launch_bounds__(TPB) void u8_step_kernel(const int64_t* ids, int64_
         rs[threadIdx.x] = st;
     }
     __syncthreads();
-    u8_rows(rs, r0, k, nbytes, obs);
+    u8_rows(rs, fk, r0, k, nbytes, S, obs);
 }
 
 __global__ __launch_bounds__(TPB) void u8_reset_kernel(const int64_t* ids, const uint8_t* mask,
-                                                       int64_t k, int64_t nbytes,
+                                                       int64_t k, int64_t nbytes, int S,
                                                        uint64_t s_seed, int64_t ep_len,
                                                        int64_t* ep_j, int64_t* ep_t,
                                                        uint8_t* obs) {
     __shared__ RowState rs[ROWS];
+    __shared__ uint64_t fk[ROWS][MAX_STACK];
     const int64_t r0 = (int64_t)blockIdx.x * ROWS;
     if (threadIdx.x < ROWS) {
         const int64_t r = r0 + threadIdx.x;
@@ -222,16 +247,17 @@ __global__ __launch_bounds__(TPB) void u8_reset_kernel(const int64_t* ids, const
         if (r < k && (!mask || mask[r])) {
             const int64_t e = ids ? ids[r] : r;
             const int64_t j = ep_j[e] + 1;
-            const int64_t t = (j == 0) ? (e % ep_len) : 0;
+            const int64_t t = episode_t0(e, j, ep_len);
             ep_j[e] = j;
             ep_t[e] = t;
             st.key = env_key(s_seed, (uint64_t)e, j, t);
             st.active = 1;
+            frame_keys(s_seed, e, j, t, t, S, fk[threadIdx.x]);
         }
         rs[threadIdx.x] = st;
     }
     __syncthreads();
-    u8_rows(rs, r0, k, nbytes, obs);
+    u8_rows(rs, fk, r0, k, nbytes, S, obs);
 }
 
 inline unsigned blocks_for(int64_t k) { return (unsigned)((k + ROWS - 1) / ROWS); }
@@ -297,29 +323,39 @@ extern "C" int tsrl_synth_box_reset(const int64_t* ids, const uint8_t* mask, int
 }
 
 extern "C" int tsrl_synth_u8_step(const int64_t* ids, int64_t k, int64_t obs_bytes,
-                                  uint64_t seed, int64_t ep_len, int64_t* ep_j, int64_t* ep_t,
-                                  uint8_t* obs_out, double* rew_out, uint8_t* term_out,
-                                  uint8_t* trunc_out, void* stream) {
+                                  int64_t frame_stack, uint64_t seed, int64_t ep_len,
+                                  int64_t* ep_j, int64_t* ep_t, uint8_t* obs_out,
+                                  double* rew_out, uint8_t* term_out, uint8_t* trunc_out,
+                                  void* stream) {
     TSRL_CHECK_ARG(k >= 0 && obs_bytes > 0 && ep_len > 0, "tsrl_synth_u8_step: bad sizes");
+    TSRL_CHECK_ARG(frame_stack >= 1 && frame_stack <= MAX_STACK &&
+                       obs_bytes % frame_stack == 0,
+                   "tsrl_synth_u8_step: frame_stack must be 1..%d and divide obs_bytes",
+                   MAX_STACK);
     if (k == 0) return 0;
     TSRL_CHECK_ARG(ep_j && ep_t && obs_out && rew_out && term_out && trunc_out,
                    "tsrl_synth_u8_step: null pointer");
     hipLaunchKernelGGL(u8_step_kernel, dim3(blocks_for(k)), dim3(TPB), 0, as_stream(stream), ids,
-                       k, obs_bytes, sm64(seed), ep_len, ep_j, ep_t, obs_out, rew_out, term_out,
-                       trunc_out);
+                       k, obs_bytes, (int)frame_stack, sm64(seed), ep_len, ep_j, ep_t, obs_out,
+                       rew_out, term_out, trunc_out);
     TSRL_LAUNCH_CHECK("tsrl_synth_u8_step");
     return 0;
 }
 
 extern "C" int tsrl_synth_u8_reset(const int64_t* ids, const uint8_t* mask, int64_t k,
-                                   int64_t obs_bytes, uint64_t seed, int64_t ep_len,
-                                   int64_t* ep_j, int64_t* ep_t, uint8_t* obs_out,
-                                   void* stream) {
+                                   int64_t obs_bytes, int64_t frame_stack, uint64_t seed,
+                                   int64_t ep_len, int64_t* ep_j, int64_t* ep_t,
+                                   uint8_t* obs_out, void* stream) {
     TSRL_CHECK_ARG(k >= 0 && obs_bytes > 0 && ep_len > 0, "tsrl_synth_u8_reset: bad sizes");
+    TSRL_CHECK_ARG(frame_stack >= 1 && frame_stack <= MAX_STACK &&
+                       obs_bytes % frame_stack == 0,
+                   "tsrl_synth_u8_reset: frame_stack must be 1..%d and divide obs_bytes",
+                   MAX_STACK);
     if (k == 0) return 0;
     TSRL_CHECK_ARG(ep_j && ep_t && obs_out, "tsrl_synth_u8_reset: null pointer");
     hipLaunchKernelGGL(u8_reset_kernel, dim3(blocks_for(k)), dim3(TPB), 0, as_stream(stream),
-                       ids, mask, k, obs_bytes, sm64(seed), ep_len, ep_j, ep_t, obs_out);
+                       ids, mask, k, obs_bytes, (int)frame_stack, sm64(seed), ep_len, ep_j, ep_t,
+                       obs_out);
     TSRL_LAUNCH_CHECK("tsrl_synth_u8_reset");
     return 0;
 }

@@ -1,0 +1,150 @@
+// Episode-aware index stepping and frame-stack gathers of the VectorReplayBuffer.
+//
+// ring_step : ReplayBufferManager prev/next (tianshou/data/buffer/manager.py:259-297, the
+//             numba _prev_index/_next_index).  Sub-buffer b owns storage rows
+//             [b*size, (b+1)*size) (vecbuf.py:33-37: equal sub-buffers), holds lengths[b]
+//             rows and last wrote last_index[b]; a row whose done flag is set, or the last
+//             written row, ends an episode, so prev() does not step back across it and next()
+//             does not step forward across it.
+// stack     : ReplayBuffer.get(index, key, stack_num) (base.py:317-358): frame s of output row
+//             r is the storage row prev^(stack_num-1-s)(idx[r]); with save_only_last_obs
+//             (manager.py:127-132) the storage holds one frame per row and this rebuilds the
+//             [stack_num, ...] observation (examples/atari/atari_ppo.py:183-189).  One wave
+//             per (row, frame): the wave walks its prev chain (a few done[] reads that hit
+//             L2) and copies the frame with 16-byte loads; the chain indices can be written
+//             out for the keys that are stacked with torch gathers (info / policy).
+#include "tsrl_common.h"
+
+namespace tsrl {
+namespace {
+
+constexpr int TPB = 256;
+constexpr int WPB = TPB / kWave;
+
+struct Ring {
+    const uint8_t* done;
+    const int64_t* last_index;
+    const int64_t* lengths;
+    int64_t size;     // rows per sub-buffer
+    int64_t maxsize;  // size * num
+};
+
+__device__ __forceinline__ int64_t pmod(int64_t a, int64_t m) {
+    const int64_t r = a % m;
+    return r < 0 ? r + m : r;
+}
+
+// manager.py:259-277
+__device__ __forceinline__ int64_t ring_prev(const Ring& g, int64_t i) {
+    i = pmod(i, g.maxsize);
+    const int64_t b = i / g.size;
+    const int64_t start = b * g.size;
+    const int64_t cur = max(g.lengths[b], (int64_t)1);
+    const int64_t sub = pmod(i - start - 1, cur);
+    const int64_t end = (g.done[sub + start] != 0) | (sub + start == g.last_index[b]);
+    return pmod(sub + end, cur) + start;
+}
+
+// manager.py:280-297
+__device__ __forceinline__ int64_t ring_next(const Ring& g, int64_t i) {
+    i = pmod(i, g.maxsize);
+    const int64_t b = i / g.size;
+    const int64_t start = b * g.size;
+    const int64_t cur = max(g.lengths[b], (int64_t)1);
+    const int64_t end = (g.done[i] != 0) | (i == g.last_index[b]);
+    return pmod(i - start + 1 - end, cur) + start;
+}
+
+__global__ __launch_bounds__(TPB) void ring_step_kernel(Ring g, const int64_t* idx, int64_t k,
+                                                        int steps, int64_t* out) {
+    const int64_t r = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (r >= k) return;
+    int64_t i = idx[r];
+    if (steps == 0) i = pmod(i, g.maxsize);
+    for (int s = 0; s < steps; ++s) i = ring_prev(g, i);
+    for (int s = 0; s > steps; --s) i = ring_next(g, i);
+    out[r] = i;
+}
+
+__device__ __forceinline__ void copy_frame(const char* s, char* d, int64_t bytes, int lane) {
+    if ((bytes & 15) == 0 && aligned16(s) && aligned16(d)) {
+        const int4* s4 = reinterpret_cast<const int4*>(s);
+        int4* d4 = reinterpret_cast<int4*>(d);
+        for (int64_t i = lane; i < bytes / 16; i += kWave) d4[i] = s4[i];
+    } else if ((bytes & 3) == 0 && (((uintptr_t)s | (uintptr_t)d) & 3) == 0) {
+        const int* s4 = reinterpret_cast<const int*>(s);
+        int* d4 = reinterpret_cast<int*>(d);
+        for (int64_t i = lane; i < bytes / 4; i += kWave) d4[i] = s4[i];
+    } else {
+        for (int64_t i = lane; i < bytes; i += kWave) d[i] = s[i];
+    }
+}
+
+// Output row r, frame s: wave (r * S + s) over the flattened grid.
+__global__ __launch_bounds__(TPB) void stack_gather_kernel(Ring g, const char* src,
+                                                           int64_t frame_bytes,
+                                                           const int64_t* idx, int64_t k,
+                                                           int S, char* dst, int64_t* chain) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t wv = (int64_t)blockIdx.x * WPB + threadIdx.x / kWave;
+    if (wv >= k * S) return;
+    const int64_t r = wv / S;
+    const int s = (int)(wv - r * S);
+    // base.py:344-350: the newest frame is val[index] (index as given), older ones step prev
+    int64_t i = pmod(idx[r], g.maxsize);
+    for (int q = S - 1; q > s; --q) i = ring_prev(g, i);
+    if (dst) copy_frame(src + i * frame_bytes, dst + wv * frame_bytes, frame_bytes, lane);
+    if (chain && lane == 0) chain[wv] = i;
+}
+
+}  // namespace
+}  // namespace tsrl
+
+using namespace tsrl;
+
+static int check_ring(const uint8_t* done, const int64_t* last_index, const int64_t* lengths,
+                      int64_t size, int64_t num, const char* who) {
+    TSRL_CHECK_ARG(done && last_index && lengths, "%s: null ring pointer", who);
+    TSRL_CHECK_ARG(size > 0 && num > 0, "%s: empty ring (size %lld, num %lld)", who,
+                   (long long)size, (long long)num);
+    return 0;
+}
+
+extern "C" int tsrl_ring_step_index(const int64_t* idx, int64_t k, const uint8_t* done,
+                                    const int64_t* last_index, const int64_t* lengths,
+                                    int64_t size, int64_t num, int steps, int64_t* out,
+                                    void* stream) {
+    TSRL_CHECK_ARG(k >= 0, "tsrl_ring_step_index: k < 0");
+    if (k == 0) return 0;
+    if (int rc = check_ring(done, last_index, lengths, size, num, "tsrl_ring_step_index"))
+        return rc;
+    TSRL_CHECK_ARG(idx && out, "tsrl_ring_step_index: null idx/out");
+    const Ring g = {done, last_index, lengths, size, size * num};
+    hipLaunchKernelGGL(ring_step_kernel, dim3((unsigned)((k + TPB - 1) / TPB)), dim3(TPB), 0,
+                       as_stream(stream), g, idx, k, steps, out);
+    TSRL_LAUNCH_CHECK("tsrl_ring_step_index");
+    return 0;
+}
+
+extern "C" int tsrl_stack_gather(const void* src, int64_t frame_bytes, const int64_t* idx,
+                                 int64_t k, int64_t stack_num, const uint8_t* done,
+                                 const int64_t* last_index, const int64_t* lengths,
+                                 int64_t size, int64_t num, void* dst, int64_t* chain_out,
+                                 void* stream) {
+    TSRL_CHECK_ARG(k >= 0 && stack_num >= 1 && stack_num <= 1024 && frame_bytes >= 0,
+                   "tsrl_stack_gather: bad sizes");
+    if (k == 0) return 0;
+    if (int rc = check_ring(done, last_index, lengths, size, num, "tsrl_stack_gather"))
+        return rc;
+    TSRL_CHECK_ARG(idx && (dst || chain_out), "tsrl_stack_gather: null idx or no output");
+    TSRL_CHECK_ARG(!dst || src, "tsrl_stack_gather: dst without src");
+    const Ring g = {done, last_index, lengths, size, size * num};
+    const int64_t waves = k * stack_num;
+    const int64_t grid = (waves + WPB - 1) / WPB;
+    TSRL_CHECK_ARG(grid < (1ll << 31), "tsrl_stack_gather: too many rows");
+    hipLaunchKernelGGL(stack_gather_kernel, dim3((unsigned)grid), dim3(TPB), 0,
+                       as_stream(stream), g, reinterpret_cast<const char*>(src), frame_bytes,
+                       idx, k, (int)stack_num, reinterpret_cast<char*>(dst), chain_out);
+    TSRL_LAUNCH_CHECK("tsrl_stack_gather");
+    return 0;
+}

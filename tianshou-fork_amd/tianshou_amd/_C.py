@@ -35,7 +35,7 @@ class AddArgs(ctypes.Structure):
         ("out_ep_rew", _p), ("out_ep_len", _p), ("out_ep_idx", _p),
         ("stat_rew", _p), ("stat_len", _p), ("stat_idx", _p),
         ("reset_src", _p), ("reset_mask", _p), ("reset_mean", _p), ("reset_var", _p),
-        ("rel_next", _p),
+        ("rel_next", _p), ("obs_src_pitch", _i64), ("obs_next_src_pitch", _i64),
     ]
 
 
@@ -76,14 +76,19 @@ _SIGS = {
     "tsrl_rms_merge2": ([_p, _p, _p, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p, _p],
                         ctypes.c_int),
     "tsrl_synth_box_reset": ([_p, _p, _i64, _i64, _u64, _i64, _p, _p, _p, _p, _p], ctypes.c_int),
-    "tsrl_synth_u8_step": ([_p, _i64, _i64, _u64, _i64, _p, _p, _p, _p, _p, _p, _p],
+    "tsrl_synth_u8_step": ([_p, _i64, _i64, _i64, _u64, _i64, _p, _p, _p, _p, _p, _p, _p],
                            ctypes.c_int),
-    "tsrl_synth_u8_reset": ([_p, _p, _i64, _i64, _u64, _i64, _p, _p, _p, _p], ctypes.c_int),
+    "tsrl_synth_u8_reset": ([_p, _p, _i64, _i64, _i64, _u64, _i64, _p, _p, _p, _p],
+                            ctypes.c_int),
     "tsrl_rms_merge": ([_p, _i64, _i64, _p, _i64, _p, _p, _p, _p, _p, _p], ctypes.c_int),
     "tsrl_rms_norm_rows": ([_p, _p, _i64, _i64, _p, _p, _f, _f, _p, _p], ctypes.c_int),
     "tsrl_buffer_add": ([ctypes.POINTER(AddArgs), _p], ctypes.c_int),
     "tsrl_ring_advance": ([_p, _i64, _p], ctypes.c_int),
     "tsrl_gather_rows": ([_p, _i64, _p, _i64, _p, _p], ctypes.c_int),
+    "tsrl_ring_step_index": ([_p, _i64, _p, _p, _p, _i64, _i64, ctypes.c_int, _p, _p],
+                             ctypes.c_int),
+    "tsrl_stack_gather": ([_p, _i64, _p, _i64, _i64, _p, _p, _p, _i64, _i64, _p, _p, _p],
+                          ctypes.c_int),
     "tsrl_sum_rows_workspace_bytes": ([_i64, _i64], _i64),
     "tsrl_sum_rows_f32": ([_p, _i64, _i64, _p, _p, _i64, _p], ctypes.c_int),
     "tsrl_ppo_num_partials": ([_i64], _i64),
@@ -93,6 +98,10 @@ _SIGS = {
                                 _p, _p, _p, _p], ctypes.c_int),
     "tsrl_ppo_gauss_finalize": ([_p, _i64, _p, PPOParams, _p, _p, _p], ctypes.c_int),
     "tsrl_gauss_logp": ([_p, _p, _p, _i64, _i64, _p, _p], ctypes.c_int),
+    "tsrl_ppo_cat_fwd_bwd": ([_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, ctypes.c_int, _p,
+                              PPOParams, _p, _p, _p, _p], ctypes.c_int),
+    "tsrl_ppo_cat_finalize": ([_p, PPOParams, _p, _p], ctypes.c_int),
+    "tsrl_cat_logp": ([_p, _p, _i64, _i64, ctypes.c_int, _p, _p], ctypes.c_int),
     "tsrl_mlp_l1_fwd": ([_p, _i64, _p, _i64, _i64, _p, _p, _p, _p, ctypes.c_int, _p,
                          ctypes.c_int, _p], ctypes.c_int),
     "tsrl_mlp_frag_floats": ([_i64], _i64),

@@ -115,10 +115,6 @@ class VectorReplayBuffer:
                  sample_avail: bool = False, device=None, **kwargs: Any) -> None:
         assert buffer_num > 0
         assert stack_num > 0, "stack_num should be greater than 0"
-        if stack_num != 1 or save_only_last_obs or sample_avail:
-            raise NotImplementedError(
-                "frame-stack sampling (stack_num>1 / save_only_last_obs / sample_avail) is "
-                "the next row of the scope table (SURVEY.md §8f item 2)")
         self.options = dict(stack_num=stack_num, ignore_obs_next=ignore_obs_next,
                             save_only_last_obs=save_only_last_obs, sample_avail=sample_avail)
         self.stack_num = stack_num
@@ -129,6 +125,8 @@ class VectorReplayBuffer:
         self._offset = self._ring.offset
         self._extend_offset = np.concatenate([self._offset, [self.maxsize]])
         self._save_obs_next = not ignore_obs_next
+        self._save_only_last_obs = save_only_last_obs
+        self._sample_avail = sample_avail
         self._indices = np.arange(self.maxsize)
         self.device = torch.device(device) if device is not None else None
         self._meta = Batch()
@@ -189,6 +187,8 @@ class VectorReplayBuffer:
         dev = self._ensure_device()
         self._alloc_state()
         m = self.maxsize
+        if self._save_only_last_obs:  # manager.py:127-132: one frame per stored row
+            obs_shape = tuple(obs_shape)[1:]
         meta = Batch(
             obs=torch.zeros((m,) + tuple(obs_shape), dtype=obs_dtype, device=dev),
             act=torch.zeros((m,) + tuple(act_shape), dtype=act_dtype, device=dev),
@@ -251,6 +251,8 @@ class VectorReplayBuffer:
         if obs.dim() == 1:
             obs = obs.reshape(k)
         self._alloc_storage(obs.shape[1:], obs.dtype, act.shape[1:], act.dtype)
+        if self._save_only_last_obs:  # manager.py:127-132
+            obs = obs[:, -1].contiguous()
         rew = self._to_dev(batch.rew, torch.float64).reshape(k)
         term = self._to_dev(batch.terminated).reshape(k).bool()
         trunc = self._to_dev(batch.truncated).reshape(k).bool()
@@ -258,6 +260,8 @@ class VectorReplayBuffer:
         if self._save_obs_next and "obs_next" in batch.keys() and \
                 not (isinstance(batch.obs_next, Batch) and batch.obs_next.is_empty()):
             obs_next = self._to_dev(batch.obs_next).to(self._meta.obs_next.dtype)
+            if self._save_only_last_obs:
+                obs_next = obs_next[:, -1].contiguous()
         ptr, next_rel = self._ring.advance(ids)
         out_rew = torch.empty(k, dtype=torch.float64, device=self.device)
         out_len = torch.empty(k, dtype=torch.int64, device=self.device)
@@ -283,8 +287,6 @@ class VectorReplayBuffer:
         for k, v in value.items():
             if isinstance(v, Batch):
                 continue
-            if k == "env_id" and key == "info":
-                continue  # written by the kernel
             t = self._to_dev(v)
             if k not in dst.keys():
                 dst.__dict__[k] = torch.zeros((self.maxsize,) + tuple(t.shape[1:]),
@@ -309,10 +311,10 @@ class VectorReplayBuffer:
         a.uniform_next = uniform_next
         a.rel_dev = _C.ptr(rel_dev)
         a.ring_size = self._ring.size
-        if obs is not None:
-            a.obs_src = _C.ptr(obs)
-            a.obs_dst = _C.ptr(m.obs)
         a.obs_row_bytes = m.obs.element_size() * int(np.prod(m.obs.shape[1:]))
+        if obs is not None:
+            a.obs_src, a.obs_src_pitch = self._frame_src(obs, a.obs_row_bytes)
+            a.obs_dst = _C.ptr(m.obs)
         has_next = self._save_obs_next and "obs_next" in m.keys()
         if obs_next is not None:  # f32 rows, optionally normalised in-kernel
             a.obs_next_src = _C.ptr(obs_next)
@@ -335,7 +337,8 @@ class VectorReplayBuffer:
                     a.norm_clip = float(reset_norm.clip_max or 0.0)
         a.rel_next = _C.ptr(rel_next)
         if obs_next_raw is not None and has_next:
-            a.obs_next_src_raw = _C.ptr(obs_next_raw)
+            a.obs_next_src_raw, a.obs_next_src_pitch = self._frame_src(obs_next_raw,
+                                                                       a.obs_row_bytes)
             a.obs_next_dst_raw = _C.ptr(m.obs_next)
         if act is not None:
             a.act_src = _C.ptr(act)
@@ -360,11 +363,27 @@ class VectorReplayBuffer:
             a.stat_idx = _C.ptr(d["stat_idx"])
         _C.check(_C.lib().tsrl_buffer_add(a, _C.stream_ptr(self.device)), "tsrl_buffer_add")
 
+    def _frame_src(self, x: torch.Tensor, row_bytes: int):
+        """(source pointer, row pitch) for a source of stored-row payloads: a plain
+        [k, ...] tensor (pitch 0 = row_bytes), or with save_only_last_obs a stacked
+        [k, stack, ...] tensor whose LAST frame is stored (manager.py:127-132)."""
+        full = x.element_size() * (x[0].numel() if x.shape[0] else 0)
+        if not self._save_only_last_obs or full == row_bytes or x.shape[0] == 0:
+            return _C.ptr(x), 0
+        assert x.is_contiguous() and full == row_bytes * x.shape[1], \
+            "save_only_last_obs expects [k, stack, *frame] rows"
+        return _C.ptr(x) + (x.shape[1] - 1) * row_bytes, full
+
     # -- sampling -------------------------------------------------------------------------------
     def sample_indices(self, batch_size: int) -> np.ndarray:
         """manager.py:163-192 (host RNG: the same np.random calls as the reference)."""
         if batch_size < 0:
             return np.array([], int)
+        if self._sample_avail and self.stack_num > 1:
+            all_indices = self._avail_indices()
+            if batch_size == 0:
+                return all_indices
+            return np.random.choice(all_indices, batch_size)
         if batch_size == 0:
             idx = self._ring.sample0()
             self._last_sample0 = idx  # lets process_fn recognise the sample(0) layout
@@ -391,6 +410,8 @@ class VectorReplayBuffer:
         return self[indices], indices
 
     def __getitem__(self, index) -> Batch:
+        """base.py:360-389.  With stack_num > 1, obs / obs_next / info / policy come back
+        stacked [k, stack_num, ...] through the device prev chain (tsrl_stack_gather)."""
         if isinstance(index, slice):
             indices = self.sample_indices(0) if index == slice(None) \
                 else self._indices[:len(self)][index]
@@ -399,6 +420,8 @@ class VectorReplayBuffer:
         m = self._meta
         if m.is_empty():
             return Batch()
+        if self.stack_num > 1:
+            return self._getitem_stacked(indices)
         if isinstance(index, np.ndarray) and len(indices) == self.maxsize and \
                 self._ring.is_identity() and np.array_equal(indices[:1], [0]) and \
                 indices[-1] == self.maxsize - 1:
@@ -407,15 +430,16 @@ class VectorReplayBuffer:
             view = False
         if view:
             obs = m.obs
-            obs_next = m.obs_next if self._save_obs_next else gather_rows(m.obs, self.next(indices))
+            obs_next = m.obs_next if self._save_obs_next else \
+                gather_rows(m.obs, self._step_dev(self._index_tensor(indices), -1))
             return Batch(obs=obs, act=m.act, rew=m.rew, terminated=m.terminated,
                          truncated=m.truncated, done=m.done, obs_next=obs_next,
                          info=Batch(env_id=m.info.env_id), policy=m.get("policy", Batch()))
-        it = torch.as_tensor(np.asarray(indices, np.int64).reshape(-1), device=self.device)
+        it = self._index_tensor(indices)
         if self._save_obs_next:
             obs_next = gather_rows(m.obs_next, it)
         else:
-            obs_next = gather_rows(m.obs, self.next(indices))
+            obs_next = gather_rows(m.obs, self._step_dev(it, -1))
         info = Batch({k: gather_rows(v, it) for k, v in m.info.items()
                       if isinstance(v, torch.Tensor)})
         pol = m.get("policy", Batch())
@@ -426,7 +450,114 @@ class VectorReplayBuffer:
                      truncated=gather_rows(m.truncated, it), done=gather_rows(m.done, it),
                      obs_next=obs_next, info=info, policy=policy)
 
-    # -- episode-aware index stepping (device done flags; returns NumPy) ----------------------
+    def _index_tensor(self, indices) -> torch.Tensor:
+        """Device int64 index tensor; NumPy semantics for the range (IndexError past the end,
+        negative indices count from the end)."""
+        idx = np.asarray(indices, np.int64).reshape(-1)
+        if len(idx) and (idx.max() >= self.maxsize or idx.min() < -self.maxsize):
+            raise IndexError(f"index out of range for buffer of maxsize {self.maxsize}")
+        return torch.as_tensor(idx % self.maxsize if len(idx) else idx, device=self.device)
+
+    # -- episode-aware index stepping and frame stacking (device) -----------------------------
+    def _ring_dev(self):
+        dev = self.device
+        return (self._meta.done, torch.as_tensor(self._ring.last_index, device=dev),
+                torch.as_tensor(self._ring.lengths, device=dev))
+
+    def _step_dev(self, it: torch.Tensor, steps: int) -> torch.Tensor:
+        """prev^steps (steps > 0) / next^-steps (steps < 0) of device indices
+        (manager.py:259-297) via tsrl_ring_step_index."""
+        out = torch.empty_like(it)
+        if it.numel() == 0:
+            return out
+        done, last, lengths = self._ring_dev()
+        _C.check(_C.lib().tsrl_ring_step_index(
+            _C.ptr(it), it.numel(), _C.ptr(done), _C.ptr(last), _C.ptr(lengths),
+            self._ring.size, self.buffer_num, int(steps), _C.ptr(out),
+            _C.stream_ptr(self.device)), "tsrl_ring_step_index")
+        return out
+
+    def _stack_dev(self, val: torch.Tensor, it: torch.Tensor, stack_num: int,
+                   want_chain: bool = False):
+        """get(index, key, stack_num) for one stored tensor: [k, stack_num, *row]."""
+        k = it.numel()
+        out = torch.empty((k, stack_num) + tuple(val.shape[1:]), dtype=val.dtype,
+                          device=val.device)
+        chain = torch.empty((k, stack_num), dtype=torch.int64, device=val.device) \
+            if want_chain else None
+        if k == 0:
+            return out, chain
+        done, last, lengths = self._ring_dev()
+        row_bytes = val.element_size() * int(np.prod(val.shape[1:]))
+        _C.check(_C.lib().tsrl_stack_gather(
+            _C.ptr(val), row_bytes, _C.ptr(it), k, stack_num, _C.ptr(done), _C.ptr(last),
+            _C.ptr(lengths), self._ring.size, self.buffer_num, _C.ptr(out), _C.ptr(chain),
+            _C.stream_ptr(self.device)), "tsrl_stack_gather")
+        return out, chain
+
+    def _chain_dev(self, it: torch.Tensor, stack_num: int) -> torch.Tensor:
+        chain = torch.empty((it.numel(), stack_num), dtype=torch.int64, device=self.device)
+        if it.numel():
+            done, last, lengths = self._ring_dev()
+            _C.check(_C.lib().tsrl_stack_gather(
+                None, 0, _C.ptr(it), it.numel(), stack_num, _C.ptr(done), _C.ptr(last),
+                _C.ptr(lengths), self._ring.size, self.buffer_num, None, _C.ptr(chain),
+                _C.stream_ptr(self.device)), "tsrl_stack_gather")
+        return chain
+
+    def get(self, index, key: str, default_value: Any = None,
+            stack_num: Optional[int] = None):
+        """base.py:317-358: ``self.key[index]`` stacked over ``stack_num`` frames through
+        prev (the newest frame last)."""
+        if key not in self._meta.keys() and default_value is not None:
+            return default_value
+        val = self._meta[key]
+        if stack_num is None:
+            stack_num = self.stack_num
+        it = self._index_tensor(index)
+        if stack_num == 1:
+            if isinstance(val, Batch):
+                return Batch({k: gather_rows(v, it) for k, v in val.items()
+                              if isinstance(v, torch.Tensor)})
+            return gather_rows(val, it)
+        if isinstance(val, Batch):
+            if val.is_empty():
+                return Batch()
+            chain = self._chain_dev(it, stack_num)
+            return Batch({k: v[chain] for k, v in val.items() if isinstance(v, torch.Tensor)})
+        out, _ = self._stack_dev(val, it, stack_num)
+        return out
+
+    def _getitem_stacked(self, indices) -> Batch:
+        m = self._meta
+        it = self._index_tensor(indices)
+        S = self.stack_num
+        obs, chain = self._stack_dev(m.obs, it, S, want_chain=True)
+        if self._save_obs_next:
+            obs_next, _ = self._stack_dev(m.obs_next, it, S)
+        else:  # base.py:380-381: get(next(indices), "obs")
+            obs_next, _ = self._stack_dev(m.obs, self._step_dev(it, -1), S)
+        info = Batch({k: v[chain] for k, v in m.info.items() if isinstance(v, torch.Tensor)})
+        pol = m.get("policy", Batch())
+        policy = Batch({k: v[chain] for k, v in pol.items() if isinstance(v, torch.Tensor)}) \
+            if not pol.is_empty() else Batch()
+        return Batch(obs=obs, act=gather_rows(m.act, it), rew=gather_rows(m.rew, it),
+                     terminated=gather_rows(m.terminated, it),
+                     truncated=gather_rows(m.truncated, it), done=gather_rows(m.done, it),
+                     obs_next=obs_next, info=info, policy=policy)
+
+    def _avail_indices(self) -> np.ndarray:
+        """manager.py:165-171 + base.py:291-303: per sub-buffer, the sample(0) rows whose
+        stack_num-1 predecessors lie in the same episode."""
+        idx = self._ring.sample0()
+        if len(idx) == 0 or self._meta.is_empty():
+            return np.asarray(idx, np.int64)
+        it = torch.as_tensor(np.asarray(idx, np.int64), device=self.device)
+        p = self._step_dev(it, max(self.stack_num - 2, 0))
+        keep = (p != self._step_dev(p, 1)).cpu().numpy()
+        return np.asarray(idx, np.int64)[keep]
+
+    # -- episode-aware index stepping (host API; device done flags) ----------------------------
     def _done_at(self, pos: np.ndarray) -> np.ndarray:
         if self._meta.is_empty():
             return np.zeros(len(pos), bool)
@@ -503,6 +634,12 @@ class ReplayBuffer(VectorReplayBuffer):
         return int(self._ring.index[0])
 
     def sample_indices(self, batch_size: int) -> np.ndarray:
+        """base.py:276-305."""
+        if self._sample_avail and self.stack_num > 1:
+            if batch_size < 0:
+                return np.array([], int)
+            all_indices = self._avail_indices()
+            return all_indices if batch_size == 0 else np.random.choice(all_indices, batch_size)
         if batch_size > 0:
             return np.random.choice(self._size, batch_size)
         if batch_size == 0:

@@ -36,11 +36,18 @@ class SyntheticVectorEnv(DeviceVectorEnv):
     episode length ``ep_len``; even envs terminate, odd envs truncate; actions are ignored."""
 
     def __init__(self, num_envs: int, obs_shape, act_dim: int = 1, ep_len: int = 1000,
-                 seed: int = 0, device=None, obs_dtype=np.float32, discrete: bool = False):
+                 seed: int = 0, device=None, obs_dtype=np.float32, discrete: bool = False,
+                 frame_stack: int = 1):
+        """``frame_stack`` S > 1 (u8 only): obs_shape = (S, *frame) holds the last S frames
+        like gymnasium's FrameStack wrapper (the Atari setup of
+        examples/atari/atari_wrapper.py), so a save_only_last_obs buffer rebuilds it."""
         self.env_num = int(num_envs)
         self.obs_shape = tuple(np.atleast_1d(obs_shape).tolist())
         self.obs_numel = int(np.prod(self.obs_shape))
         self.u8 = np.dtype(obs_dtype) == np.uint8
+        self.frame_stack = int(frame_stack)
+        assert self.frame_stack == 1 or (self.u8 and self.obs_shape[0] == self.frame_stack), \
+            "frame_stack needs u8 observations of shape (frame_stack, ...)"
         self.ep_len, self.seed_ = int(ep_len), int(seed)
         self.device = torch.device(device) if device is not None else \
             torch.device("cuda", torch.cuda.current_device())
@@ -72,7 +79,8 @@ class SyntheticVectorEnv(DeviceVectorEnv):
         L = _C.lib()
         s = _C.stream_ptr(self.device)
         if self.u8:
-            _C.check(L.tsrl_synth_u8_step(_C.ptr(ids), k, self.obs_numel, self.seed_,
+            _C.check(L.tsrl_synth_u8_step(_C.ptr(ids), k, self.obs_numel, self.frame_stack,
+                                          self.seed_,
                                           self.ep_len, _C.ptr(self.ep_j), _C.ptr(self.ep_t),
                                           _C.ptr(obs_out), _C.ptr(rew_out), _C.ptr(term_out),
                                           _C.ptr(trunc_out), s), "tsrl_synth_u8_step")
@@ -102,7 +110,7 @@ class SyntheticVectorEnv(DeviceVectorEnv):
         s = _C.stream_ptr(self.device)
         if self.u8:
             _C.check(L.tsrl_synth_u8_reset(_C.ptr(ids), _C.ptr(mask), k, self.obs_numel,
-                                           self.seed_, self.ep_len, _C.ptr(self.ep_j),
+                                           self.frame_stack, self.seed_, self.ep_len, _C.ptr(self.ep_j),
                                            _C.ptr(self.ep_t), _C.ptr(obs_out), s),
                      "tsrl_synth_u8_reset")
         else:

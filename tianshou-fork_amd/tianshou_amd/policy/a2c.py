@@ -41,14 +41,16 @@ class A2CPolicy(PGPolicy):
         batch.act = torch.as_tensor(batch.act, device=batch.v_s.device).to(batch.v_s.dtype)
         return batch
 
-    def _chunks(self, n: int):
-        c = max(self._batch, EVAL_CHUNK)
+    def _chunks(self, n: int, row_numel: int = 1):
+        """Evaluation chunks: at most EVAL_CHUNK rows and 2**30 input elements per chunk (a
+        conv trunk's activations are ~2x its uint8 frame stack per row in f32)."""
+        c = max(self._batch, min(EVAL_CHUNK, (1 << 30) // max(int(row_numel), 1)))
         return [(s, min(s + c, n)) for s in range(0, n, c)]
 
     def _values(self, obs: torch.Tensor) -> torch.Tensor:
         n = len(obs)
         out = torch.empty(n, dtype=torch.float32, device=obs.device)
-        for s, e in self._chunks(n):
+        for s, e in self._chunks(n, obs[0].numel() if n else 1):
             out[s:e] = self.critic(obs[s:e]).flatten()
         return out
 

@@ -32,6 +32,22 @@ def _is_fixed_std_normal(dist_fn) -> bool:
         d.reinterpreted_batch_ndims == 1
 
 
+def cat_mode(dist_fn) -> Optional[int]:
+    """0 when dist_fn(x) is Categorical(logits=x), 1 when Categorical(probs=x), else None."""
+    x = torch.tensor([[0.2, 0.6, 0.2]])
+    try:
+        d = dist_fn(x)
+    except Exception:
+        return None
+    if not isinstance(d, torch.distributions.Categorical):
+        return None
+    if torch.allclose(d.probs, x / x.sum(-1, keepdim=True)):
+        return 1
+    if torch.allclose(d.probs, torch.softmax(x, -1)):
+        return 0
+    return None
+
+
 def split_bounds(length: int, size: int, merge_last: bool):
     """[start, end) of every Batch.split chunk (batch.py:896-912)."""
     if size == -1:
@@ -101,6 +117,64 @@ class _GaussPPOLoss(torch.autograd.Function):
                 grad_value * g_loss, None)
 
 
+class _CatPPOLoss(torch.autograd.Function):
+    """Fused forward+backward of the Categorical PPO loss (tsrl_ppo_cat_*): x is the dist_fn
+    input (logits or probs) of the minibatch rows."""
+
+    @staticmethod
+    def forward(ctx, x, value, ctx_args):
+        (act, logp_old, adv, ret, v_s, idx, params, dp, mode) = ctx_args
+        L = _C.lib()
+        s = _C.stream_ptr(x.device)
+        x = x.detach().float().contiguous()
+        value = value.detach().contiguous()
+        B, A = x.shape
+        nblk = int(L.tsrl_ppo_num_partials(B))
+        dev = x.device
+        adv_sums = None
+        if params.norm_adv:
+            pa = torch.empty(nblk * 2, dtype=torch.float64, device=dev)
+            _C.check(L.tsrl_adv_moments(_C.ptr(adv), _C.ptr(idx), B, _C.ptr(pa), s),
+                     "tsrl_adv_moments")
+            adv_sums = torch.empty(2, dtype=torch.float64, device=dev)
+            _C.check(L.tsrl_reduce_partials(_C.ptr(pa), nblk, 2, _C.ptr(adv_sums), s),
+                     "tsrl_reduce_partials")
+            dp.all_reduce_(adv_sums)
+        grad_x = torch.empty_like(x)
+        grad_value = torch.empty_like(value)
+        partials = torch.empty(nblk * 4, dtype=torch.float64, device=dev)
+        _C.check(L.tsrl_ppo_cat_fwd_bwd(
+            _C.ptr(x), _C.ptr(value), _C.ptr(act), _C.ptr(logp_old), _C.ptr(adv), _C.ptr(ret),
+            _C.ptr(v_s), _C.ptr(idx), B, A, int(mode), _C.ptr(adv_sums), params,
+            _C.ptr(grad_x), _C.ptr(grad_value), _C.ptr(partials), s), "tsrl_ppo_cat_fwd_bwd")
+        sums = torch.empty(4, dtype=torch.float64, device=dev)
+        _C.check(L.tsrl_reduce_partials(_C.ptr(partials), nblk, 4, _C.ptr(sums), s),
+                 "tsrl_reduce_partials")
+        dp.all_reduce_(sums)
+        terms = torch.empty(4, dtype=torch.float32, device=dev)
+        _C.check(L.tsrl_ppo_cat_finalize(_C.ptr(sums), params, _C.ptr(terms), s),
+                 "tsrl_ppo_cat_finalize")
+        ctx.save_for_backward(grad_x, grad_value)
+        loss = terms[0].clone()
+        ctx.mark_non_differentiable(terms)
+        return loss, terms
+
+    @staticmethod
+    def backward(ctx, g_loss, g_terms):
+        grad_x, grad_value = ctx.saved_tensors
+        return grad_x * g_loss, grad_value * g_loss, None
+
+
+def cat_logp(x: torch.Tensor, act: torch.Tensor, mode: int) -> torch.Tensor:
+    """Categorical(...).log_prob(act) of dist_fn input rows x (tsrl_cat_logp)."""
+    x = x.detach().float().contiguous()
+    act = act.reshape(-1).to(torch.int64).contiguous()
+    out = torch.empty(x.shape[0], dtype=torch.float32, device=x.device)
+    _C.check(_C.lib().tsrl_cat_logp(_C.ptr(x), _C.ptr(act), x.shape[0], x.shape[1], int(mode),
+                                    _C.ptr(out), _C.stream_ptr(x.device)), "tsrl_cat_logp")
+    return out
+
+
 class PPOPolicy(A2CPolicy):
     def __init__(self, actor: torch.nn.Module, critic: torch.nn.Module,
                  optim: torch.optim.Optimizer, dist_fn: Callable, eps_clip: float = 0.2,
@@ -121,6 +195,8 @@ class PPOPolicy(A2CPolicy):
         self._fused = isinstance(actor, ActorProb) and not actor._c_sigma and \
             _is_fixed_std_normal(dist_fn)
         self._gauss_dist = self._fused
+        # Categorical policies: the fused loss kernel (tsrl_ppo_cat_*), torch actor/critic
+        self._cat = cat_mode(dist_fn) if not self._fused else None
         # the whole minibatch (MLP forward, loss, backward) as three HIP kernels when the
         # networks have the get_actor_critic shape (policy/fused_mlp.py); fused_mlp=False
         # keeps the torch layers + fused loss kernel.
@@ -158,6 +234,9 @@ class PPOPolicy(A2CPolicy):
                 batch.logp_old = self._pending_logp
             elif self._fused:
                 batch.logp_old = self._logp_fused(batch.obs, batch.act)
+            elif self._cat is not None and isinstance(batch.obs, torch.Tensor) and \
+                    batch.obs.is_cuda:
+                batch.logp_old = self._logp_cat(batch.obs, batch.act)
             else:
                 batch.logp_old = self(batch).dist.log_prob(batch.act)
         self._pending_logp = None
@@ -205,6 +284,15 @@ class PPOPolicy(A2CPolicy):
                                        _C.ptr(out[s:e]), _C.stream_ptr(dev)), "tsrl_gauss_logp")
         return out
 
+    def _logp_cat(self, obs: torch.Tensor, act: torch.Tensor) -> torch.Tensor:
+        n = obs.shape[0]
+        out = torch.empty(n, dtype=torch.float32, device=obs.device)
+        act = torch.as_tensor(act, device=obs.device).reshape(n)
+        for s, e in self._chunks(n, obs[0].numel() if n else 1):
+            x, _ = self.actor(obs[s:e])
+            out[s:e] = cat_logp(x, act[s:e], self._cat)
+        return out
+
     # -- learn ----------------------------------------------------------------------------------
     def _permutation(self, n: int, dev):
         if self.perm_device:
@@ -214,6 +302,9 @@ class PPOPolicy(A2CPolicy):
     def learn(self, batch: Batch, batch_size: int, repeat: int, **kwargs: Any
               ) -> Dict[str, List[float]]:
         if not self._fused:
+            if self._cat is not None and isinstance(batch.obs, torch.Tensor) and \
+                    batch.obs.is_cuda:
+                return self._learn_cat(batch, batch_size, repeat)
             return self._learn_generic(batch, batch_size, repeat)
         dev = batch.v_s.device
         n = len(batch.v_s)
@@ -319,6 +410,45 @@ class PPOPolicy(A2CPolicy):
         st["perm"].copy_(perm)
         st["graph"].replay()
         return st["terms"].clone()
+
+    def _learn_cat(self, batch: Batch, batch_size: int, repeat: int
+                   ) -> Dict[str, List[float]]:
+        """ppo.py:99-162 for Categorical policies: torch actor/critic (MLP or conv trunk on
+        MIOpen/hipBLASLt), minibatch rows gathered once through the permutation, the loss and
+        its gradient w.r.t. the dist_fn input from the fused tsrl_ppo_cat kernel."""
+        dev = batch.v_s.device
+        n = len(batch.v_s)
+        terms = []
+        f32 = dict(device=dev, dtype=torch.float32)
+        for step in range(repeat):
+            if self._recompute_adv and step > 0:
+                batch = self._compute_returns(batch, self._buffer, self._indices)
+            act = torch.as_tensor(batch.act, device=dev).reshape(n).to(torch.int64).contiguous()
+            logp_old = batch.logp_old.reshape(-1).to(**f32).contiguous()
+            adv = batch.adv.reshape(-1).to(**f32).contiguous()
+            ret = batch.returns.reshape(-1).to(**f32).contiguous()
+            v_s = batch.v_s.reshape(-1).to(**f32).contiguous()
+            perm = self._permutation(n, dev)
+            for s, e in split_bounds(n, batch_size, merge_last=True):
+                idx = perm[s:e]
+                obs_mb = gather_rows(batch.obs, idx)
+                x, _ = self.actor(obs_mb)
+                value = self.critic(obs_mb).flatten()
+                params = self._params((e - s) * self.dp.world)
+                loss, t = _CatPPOLoss.apply(x, value, (act, logp_old, adv, ret, v_s, idx, params,
+                                                       self.dp, self._cat))
+                self.optim.zero_grad()
+                loss.backward()
+                self.dp.all_reduce_grads_(self._actor_critic.parameters())
+                if self._grad_norm:
+                    nn.utils.clip_grad_norm_(self._actor_critic.parameters(),
+                                             max_norm=self._grad_norm)
+                self.optim.step()
+                terms.append(t)
+        vals = torch.cat([t.reshape(-1, 4) for t in terms]).cpu().numpy() if terms else \
+            np.zeros((0, 4), np.float32)
+        return {"loss": vals[:, 0].tolist(), "loss/clip": vals[:, 1].tolist(),
+                "loss/vf": vals[:, 2].tolist(), "loss/ent": vals[:, 3].tolist()}
 
     def _learn_generic(self, batch: Batch, batch_size: int, repeat: int
                        ) -> Dict[str, List[float]]:

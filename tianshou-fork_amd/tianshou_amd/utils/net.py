@@ -225,12 +225,16 @@ class Critic(_PreprocessWrapper):
         return self.last(logits)
 
 
-class DiscreteActor(_PreprocessWrapper):
-    """Softmax actor (discrete.py:12-71); outputs probabilities unless softmax_output=False."""
+class DiscreteActor(nn.Module):
+    """Softmax actor (utils/net/discrete.py:12-71): preprocess -> MLP -> softmax unless
+    softmax_output=False.  Module layout (``preprocess``, ``last``) as the reference's, so
+    state_dicts interchange."""
 
     def __init__(self, preprocess_net, action_shape, hidden_sizes=(), softmax_output=True,
                  preprocess_net_output_dim=None, device="cpu"):
-        super().__init__(preprocess_net, device=device)
+        super().__init__()
+        self.device = device
+        self.preprocess = preprocess_net
         self.output_dim = int(np.prod(action_shape))
         input_dim = getattr(preprocess_net, "output_dim", preprocess_net_output_dim)
         self.last = MLP(input_dim, self.output_dim, hidden_sizes, device=self.device)
@@ -244,8 +248,22 @@ class DiscreteActor(_PreprocessWrapper):
         return logits, hidden
 
 
-class DiscreteCritic(Critic):
-    pass
+class DiscreteCritic(nn.Module):
+    """V(s) head of discrete-action policies (utils/net/discrete.py:74-121): the observation
+    goes to the preprocess net unchanged (a conv trunk sees its frame stack)."""
+
+    def __init__(self, preprocess_net, hidden_sizes=(), last_size: int = 1,
+                 preprocess_net_output_dim=None, device="cpu"):
+        super().__init__()
+        self.device = device
+        self.preprocess = preprocess_net
+        self.output_dim = last_size
+        input_dim = getattr(preprocess_net, "output_dim", preprocess_net_output_dim)
+        self.last = MLP(input_dim, last_size, hidden_sizes, device=self.device)
+
+    def forward(self, obs, **kwargs: Any):
+        logits, _ = self.preprocess(obs, state=kwargs.get("state", None))
+        return self.last(logits)
 
 
 class ActorCritic(nn.Module):

@@ -1,0 +1,55 @@
+"""Atari network of the reference's PPO example (examples/atari/atari_network.py:10-80):
+the Nature-DQN conv trunk over a uint8 4x84x84 frame stack scaled by 1/255
+(``scale_obs``, :18-30) with orthogonal ``layer_init`` (:10-15), used as the shared
+``features_only`` trunk of the actor and critic (examples/atari/atari_ppo.py:104-125).
+
+The convolutions and the two linear layers run on MIOpen / hipBLASLt through PyTorch-ROCm
+(the conv trunk is MFMA-bound library work); the PPO loss around it is the
+fused tsrl_ppo_cat kernel (policy/ppo.py)."""
+from typing import Any, Dict, Optional, Sequence
+
+import numpy as np
+import torch
+from torch import nn
+
+
+def layer_init(layer: nn.Module, std: float = np.sqrt(2), bias_const: float = 0.0):
+    torch.nn.init.orthogonal_(layer.weight, std)
+    torch.nn.init.constant_(layer.bias, bias_const)
+    return layer
+
+
+class DQN(nn.Module):
+    """Conv(c,32,8,4)-ReLU-Conv(32,64,4,2)-ReLU-Conv(64,64,3,1)-ReLU-Flatten, then either the
+    Q head (Linear 512 - ReLU - Linear A) or, with ``features_only``, an optional
+    Linear(., output_dim)-ReLU projection."""
+
+    def __init__(self, c: int, h: int, w: int, action_shape: Sequence[int], device="cpu",
+                 features_only: bool = False, output_dim: Optional[int] = None,
+                 layer_init=lambda x: x, scale: float = 255.0) -> None:
+        super().__init__()
+        self.device = device
+        self.scale = scale
+        self.net = nn.Sequential(
+            layer_init(nn.Conv2d(c, 32, kernel_size=8, stride=4)), nn.ReLU(inplace=True),
+            layer_init(nn.Conv2d(32, 64, kernel_size=4, stride=2)), nn.ReLU(inplace=True),
+            layer_init(nn.Conv2d(64, 64, kernel_size=3, stride=1)), nn.ReLU(inplace=True),
+            nn.Flatten())
+        with torch.no_grad():
+            self.output_dim = int(np.prod(self.net(torch.zeros(1, c, h, w)).shape[1:]))
+        if not features_only:
+            self.net = nn.Sequential(self.net, layer_init(nn.Linear(self.output_dim, 512)),
+                                     nn.ReLU(inplace=True),
+                                     layer_init(nn.Linear(512, int(np.prod(action_shape)))))
+            self.output_dim = int(np.prod(action_shape))
+        elif output_dim is not None:
+            self.net = nn.Sequential(self.net, layer_init(nn.Linear(self.output_dim, output_dim)),
+                                     nn.ReLU(inplace=True))
+            self.output_dim = output_dim
+
+    def forward(self, obs, state: Any = None, info: Dict[str, Any] = {}):
+        obs = torch.as_tensor(obs, device=self.device)
+        x = obs.to(torch.float32)
+        if self.scale:
+            x = x / self.scale  # scale_obs (atari_network.py:18-30)
+        return self.net(x), state

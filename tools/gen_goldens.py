@@ -345,6 +345,69 @@ def gen_ppo():
 
 
 # --------------------------------------------------------------------------------------
+# 6b. PPO learn with Categorical policies (discrete actions): test/discrete/test_ppo.py:80-
+#     110 (Net trunks, softmax Actor, Critic, dist = Categorical -> Categorical(probs)) and
+#     the Atari form (examples/atari/atari_ppo.py:118-137: Actor(softmax_output=False),
+#     Categorical(logits=p)) on an MLP trunk.
+# --------------------------------------------------------------------------------------
+def gen_ppo_discrete():
+    from tianshou.utils.net.common import ActorCritic, Net
+    from tianshou.utils.net.discrete import Actor, Critic
+    out = {}
+    variants = {
+        "probs": dict(obs=4, act=2, n=96, batch_size=32, repeat=2, softmax=True,
+                      kw=dict(ent_coef=0.0)),
+        "logits": dict(obs=12, act=6, n=80, batch_size=80, repeat=1, softmax=False,
+                       kw=dict(ent_coef=0.01, value_clip=True, dual_clip=3.0)),
+        "logits_multi": dict(obs=12, act=6, n=100, batch_size=24, repeat=2, softmax=False,
+                             kw=dict(ent_coef=0.02, advantage_normalization=False)),
+    }
+    for tag, v in variants.items():
+        torch.manual_seed(7)
+        net = Net(v["obs"], hidden_sizes=(64, 64))
+        actor = Actor(net, v["act"], softmax_output=v["softmax"])
+        critic = Critic(Net(v["obs"], hidden_sizes=(64, 64)))
+        ac = ActorCritic(actor, critic)
+        optim = torch.optim.Adam(ac.parameters(), lr=1e-3)
+        dist = torch.distributions.Categorical if v["softmax"] else \
+            (lambda p: torch.distributions.Categorical(logits=p))
+        args = dict(discount_factor=0.99, gae_lambda=0.95, max_grad_norm=0.5, vf_coef=0.5,
+                    eps_clip=0.2, advantage_normalization=True, action_scaling=False)
+        args.update(v["kw"])
+        policy = PPOPolicy(actor, critic, optim, dist,
+                           action_space=gym.spaces.Discrete(v["act"]), **args)
+        rng = np.random.default_rng(123)
+        n = v["n"]
+        obs = rng.standard_normal((n, v["obs"])).astype(np.float32)
+        act = rng.integers(0, v["act"], n).astype(np.int64)
+        with torch.no_grad():
+            d = policy(Batch(obs=obs, info={})).dist
+            logp_old = d.log_prob(torch.as_tensor(act)).numpy()
+        out[tag + "_logp_fresh"] = logp_old.copy()
+        logp_old = (logp_old + rng.normal(0, 0.3, n)).astype(np.float32)
+        adv = (rng.standard_normal(n) * 2 + 0.3).astype(np.float32)
+        ret = rng.standard_normal(n).astype(np.float32)
+        v_s = (ret + rng.normal(0, 0.3, n)).astype(np.float32)
+        p = tag + "_"
+        out.update(_sd_arrays(p + "init_", policy))
+        batch = Batch(obs=obs, act=torch.as_tensor(act), logp_old=torch.as_tensor(logp_old),
+                      adv=torch.as_tensor(adv), returns=torch.as_tensor(ret),
+                      v_s=torch.as_tensor(v_s), info={})
+        np.random.seed(21)
+        res = policy.learn(batch, batch_size=v["batch_size"], repeat=v["repeat"])
+        for k in ("loss", "loss/clip", "loss/vf", "loss/ent"):
+            out[p + k.replace("/", "_")] = np.array(res[k])
+        out.update(_sd_arrays(p + "final_", policy))
+        out[p + "obs"], out[p + "act"], out[p + "logp_old"] = obs, act, logp_old
+        out[p + "adv"], out[p + "returns"], out[p + "v_s"] = adv, ret, v_s
+        out[p + "cfg"] = np.array(json.dumps(dict(n=n, batch_size=v["batch_size"],
+                                                   repeat=v["repeat"], obs=v["obs"],
+                                                   act=v["act"], softmax=v["softmax"],
+                                                   **v["kw"])))
+    _save("ppo_discrete.npz", **out)
+
+
+# --------------------------------------------------------------------------------------
 # 7. Collector + VectorEnvNormObs + VectorReplayBuffer + PPO process_fn/learn on the
 #    synthetic env (tianshou/data/collector.py:184-402, policy/modelfree/ppo.py:87-162).
 # --------------------------------------------------------------------------------------
@@ -445,10 +508,80 @@ def gen_collector():
     _save("collector.npz", **out)
 
 
+# --------------------------------------------------------------------------------------
+# 8. Frame-stack storage: VectorReplayBuffer(stack_num, save_only_last_obs,
+#    ignore_obs_next, sample_avail) -- manager.py:104-161 (last-frame store),
+#    base.py:317-358 (get with stack_num through prev), base.py:360-389 (__getitem__,
+#    obs_next = get(next(idx), "obs") when obs_next is not stored), manager.py:163-175 +
+#    base.py:291-305 (sample_avail).  Ragged adds of random uint8 "frames" [S, 3, 2].
+# --------------------------------------------------------------------------------------
+STACK_CASES = [
+    # name, stack_num, save_only_last_obs, ignore_obs_next, sample_avail
+    ("atari", 4, True, True, False),
+    ("avail", 4, True, True, True),
+    ("full_obs", 3, False, False, False),
+    ("last_next", 3, True, False, True),
+]
+
+
+def gen_stack():
+    out = {}
+    num, per, steps, S = 5, 8, 70, 4
+    for name, stack_num, last_only, ign_next, avail in STACK_CASES:
+        rng = np.random.default_rng(11)
+        buf = VectorReplayBuffer(num * per, num, stack_num=stack_num,
+                                 save_only_last_obs=last_only, ignore_obs_next=ign_next,
+                                 sample_avail=avail)
+        adds = []
+        for step in range(steps):
+            k = int(rng.integers(1, num + 1))
+            ids = np.sort(rng.choice(num, size=k, replace=False))
+            term = (rng.random(k) < 0.12)
+            trunc = (rng.random(k) < 0.08) & ~term
+            obs = rng.integers(0, 256, (k, S, 3, 2), dtype=np.uint8)
+            obs_next = rng.integers(0, 256, (k, S, 3, 2), dtype=np.uint8)
+            rew = np.round(rng.random(k) * 8) / 4.0
+            env_id = ids.astype(np.int64) + 100
+            buf.add(Batch(obs=obs, act=ids.astype(np.int64), rew=rew, terminated=term,
+                          truncated=trunc, obs_next=obs_next, info=Batch(env_id=env_id)),
+                    buffer_ids=ids)
+            adds.append((ids, obs, obs_next, rew, term, trunc))
+            if step == 40:
+                buf.reset(keep_statistics=True)
+        p = f"{name}_"
+        out[p + "ids"] = np.concatenate([a[0] for a in adds])
+        out[p + "sizes"] = np.array([len(a[0]) for a in adds])
+        for j, key in enumerate(("obs", "obs_next", "rew", "term", "trunc"), start=1):
+            out[p + "in_" + key] = np.concatenate([a[j] for a in adds])
+        out[p + "stored_obs"] = np.asarray(buf.obs)
+        if not ign_next:
+            out[p + "stored_obs_next"] = np.asarray(buf.obs_next)
+        idx0 = buf.sample_indices(0)
+        out[p + "sample0"] = idx0
+        qidx = np.concatenate([np.arange(buf.maxsize), rng.integers(0, buf.maxsize, 17)])
+        b = buf[qidx]
+        out[p + "q_idx"] = qidx
+        out[p + "q_obs"] = np.asarray(b.obs)
+        out[p + "q_obs_next"] = np.asarray(b.obs_next)
+        out[p + "q_env_id"] = np.asarray(b.info.env_id)
+        out[p + "q_act"] = np.asarray(b.act)
+        out[p + "prev"] = buf.prev(np.arange(buf.maxsize))
+        out[p + "next"] = buf.next(np.arange(buf.maxsize))
+        out[p + "done"] = np.asarray(buf.done)
+        out[p + "lengths"] = np.asarray(buf._lengths)
+        out[p + "last_index"] = np.asarray(buf.last_index)
+        if avail:
+            np.random.seed(3)
+            out[p + "sample7"] = buf.sample_indices(7)
+    _save("stack.npz", **out)
+
+
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
-    which = sys.argv[1:] or ["returns", "gae", "buffer", "split", "rms", "ppo", "collector"]
+    which = sys.argv[1:] or ["returns", "gae", "buffer", "split", "rms", "ppo", "collector",
+                             "stack", "ppo_discrete"]
     table = dict(returns=gen_returns_known, gae=gen_gae_random, buffer=gen_buffer_traces,
-                 split=gen_split, rms=gen_rms, ppo=gen_ppo, collector=gen_collector)
+                 split=gen_split, rms=gen_rms, ppo=gen_ppo, collector=gen_collector,
+                 stack=gen_stack, ppo_discrete=gen_ppo_discrete)
     for w in which:
         table[w]()
