@@ -36,23 +36,40 @@ SPIN_CYCLES = 100_000          # device spin ahead of the GAE start event (see G
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--workload", choices=["humanoid", "small", "atari"], default="humanoid",
+                    help="humanoid: BASELINE config 3 (the headline line); small: config 2 "
+                         "(Box 17/6, 512 envs x 128 steps); atari: config 5 (u8 4x84x84 frame "
+                         "stacks, Discrete(6), Nature-DQN trunk, 1024 envs x 256 steps)")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--envs", type=int, default=4096)
-    ap.add_argument("--T", type=int, default=2048)
-    ap.add_argument("--obs", type=int, default=376)
-    ap.add_argument("--act", type=int, default=17)
+    ap.add_argument("--envs", type=int, default=None)
+    ap.add_argument("--T", type=int, default=None)
+    ap.add_argument("--obs", type=int, default=None)
+    ap.add_argument("--act", type=int, default=None)
     ap.add_argument("--repeat", type=int, default=4)
     ap.add_argument("--minibatches", type=int, default=32)
-    ap.add_argument("--ep-len", type=int, default=1000)
+    ap.add_argument("--ep-len", type=int, default=None)
     ap.add_argument("--perm", choices=["numpy", "device"], default="device")
-    ap.add_argument("--cpu-steps", type=int, default=256,
+    ap.add_argument("--cpu-steps", type=int, default=None,
                     help="T' of the bounded CPU-baseline sample (envs x T')")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--force-dp", action="store_true",
+                    help="diagnostic: under torch.distributed.run with ONE rank, run the "
+                         "data-parallel code path (RCCL collectives over a one-rank "
+                         "communicator) -- rehearses the N>1 path on a one-GPU box")
     ap.add_argument("--eager-learn", action="store_true",
                     help="diagnostic: run learn() eagerly (no HIP-graph epoch replay), as the "
                          "data-parallel (N>1) path does")
-    return ap.parse_args()
+    a = ap.parse_args()
+    defaults = dict(humanoid=(4096, 2048, 376, 17, 256, 1000),
+                    small=(512, 128, 17, 6, 128, 1000),
+                    atari=(1024, 256, 0, 6, 16, 256))[a.workload]
+    for k, v in zip(("envs", "T", "obs", "act", "cpu_steps", "ep_len"), defaults):
+        if getattr(a, k) is None:
+            setattr(a, k, v)
+    if a.workload == "atari":
+        a.no_cpu_baseline = True  # the CPU port covers the Box workloads only
+    return a
 
 
 class GaeTimer:
@@ -86,6 +103,36 @@ class GaeTimer:
         return float(np.mean(ts)) if ts else float("nan")
 
 
+def build_atari(args, dev, rank):
+    """BASELINE config 5: examples/atari/atari_ppo.py's PPO (shared Nature-DQN trunk,
+    Categorical(logits), frame-stack buffer with save_only_last_obs / ignore_obs_next) on the
+    device u8 env with FrameStack semantics; no obs normalisation (the net scales by 1/255)."""
+    from tianshou_amd.data import Collector, VectorReplayBuffer
+    from tianshou_amd.env import Discrete, SyntheticVectorEnv
+    from tianshou_amd.policy import PPOPolicy
+    from tianshou_amd.utils.net import ActorCritic, DiscreteActor, DiscreteCritic
+    from tianshou_amd.utils.net_atari import DQN, layer_init
+    E, T, A = args.envs, args.T, args.act
+    env = SyntheticVectorEnv(E, (4, 84, 84), A, ep_len=args.ep_len, seed=rank, device=dev,
+                             obs_dtype=np.uint8, discrete=True, frame_stack=4)
+    net = DQN(4, 84, 84, (A,), device=dev, features_only=True, output_dim=512,
+              layer_init=layer_init).to(dev)
+    actor = DiscreteActor(net, A, softmax_output=False, device=dev).to(dev)
+    critic = DiscreteCritic(net, device=dev).to(dev)
+    optim = torch.optim.Adam(ActorCritic(actor, critic).parameters(), lr=2.5e-4, eps=1e-5)
+    policy = PPOPolicy(actor, critic, optim,
+                       lambda p: torch.distributions.Categorical(logits=p),
+                       action_space=Discrete(A), action_scaling=False, discount_factor=0.99,
+                       gae_lambda=0.95, max_grad_norm=0.5, vf_coef=0.25, ent_coef=0.01,
+                       eps_clip=0.1, value_clip=True, dual_clip=None,
+                       advantage_normalization=False, recompute_advantage=False,
+                       reward_normalization=False,
+                       perm_device=(args.perm == "device")).to(dev)
+    buf = VectorReplayBuffer(E * T, E, stack_num=4, ignore_obs_next=True,
+                             save_only_last_obs=True, device=dev)
+    return Collector(policy, env, buf, exploration_noise=True), policy, buf
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -93,10 +140,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    distributed = world > 1 or (args.force_dp and "WORLD_SIZE" in os.environ)
+    if distributed:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=dev)
+        if args.force_dp:
+            from tianshou_amd.dist import DataParallel
+            DataParallel.force = True
 
     from tianshou_amd.data import Collector, VectorReplayBuffer
     from tianshou_amd.env import SyntheticVectorEnv, VectorEnvNormObs
@@ -107,20 +158,26 @@ def main():
     np.random.seed(rank)
     E, T, D, A = args.envs, args.T, args.obs, args.act
     n = E * T
-    env = VectorEnvNormObs(SyntheticVectorEnv(E, (D,), A, ep_len=args.ep_len, seed=rank,
-                                              device=dev))
-    actor, critic = get_actor_critic((D,), (64, 64), (A,), dev)
-    actor, critic = actor.to(dev), critic.to(dev)  # before the optimiser: fused + capturable Adam
-    optim = init_and_get_optim(actor, critic, 3e-4)
-    policy = PPOPolicy(actor, critic, optim, fixed_std_normal, action_space=env.action_space,
-                       discount_factor=0.99, gae_lambda=0.95, max_grad_norm=0.5, vf_coef=0.25,
-                       ent_coef=0.0, reward_normalization=True, advantage_normalization=True,
-                       recompute_advantage=False, eps_clip=0.2, value_clip=False,
-                       dual_clip=None, action_bound_method="clip",
-                       perm_device=(args.perm == "device")).to(dev)
+    if args.workload == "atari":
+        coll, policy, buf = build_atari(args, dev, rank)
+        D = "4x84x84 u8"
+    else:
+        env = VectorEnvNormObs(SyntheticVectorEnv(E, (D,), A, ep_len=args.ep_len, seed=rank,
+                                                  device=dev))
+        actor, critic = get_actor_critic((D,), (64, 64), (A,), dev)
+        # to the device before the optimiser: fused + capturable Adam
+        actor, critic = actor.to(dev), critic.to(dev)
+        optim = init_and_get_optim(actor, critic, 3e-4)
+        policy = PPOPolicy(actor, critic, optim, fixed_std_normal,
+                           action_space=env.action_space, discount_factor=0.99,
+                           gae_lambda=0.95, max_grad_norm=0.5, vf_coef=0.25, ent_coef=0.0,
+                           reward_normalization=True, advantage_normalization=True,
+                           recompute_advantage=False, eps_clip=0.2, value_clip=False,
+                           dual_clip=None, action_bound_method="clip",
+                           perm_device=(args.perm == "device")).to(dev)
+        buf = VectorReplayBuffer(n, E, device=dev)
+        coll = Collector(policy, env, buf)
     policy.graph_learn = not args.eager_learn
-    buf = VectorReplayBuffer(n, E, device=dev)
-    coll = Collector(policy, env, buf)
     timer = GaeTimer()
     pbase.GAE_HOOK = timer
     phase = {"collect": 0.0, "update": 0.0}
@@ -137,7 +194,7 @@ def main():
         phase["update"] += time.perf_counter() - t1
 
     def barrier():
-        if world > 1:
+        if distributed:
             import torch.distributed as dist
             dist.barrier()
         torch.cuda.synchronize()
@@ -156,7 +213,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     timer.on = False
-    if world > 1:
+    if distributed:
         import torch.distributed as dist
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -193,9 +250,11 @@ def main():
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f32 (GAE scan f64)", "data": "synthetic",
-            "config": {"workload": f"Synthetic Box(obs={D}, act={A}), {E} envs x {T} steps "
+            "config": {"workload": f"Synthetic {'Discrete' if args.workload == 'atari' else 'Box'}"
+                                   f"(obs={D}, act={A}), {E} envs x {T} steps "
                                    f"per GPU, GAE+PPO (repeat {args.repeat}, "
                                    f"{args.minibatches} minibatches)",
+                       "baseline_config": dict(humanoid=3, small=2, atari=5)[args.workload],
                        "envs_per_gpu": E, "steps_per_env": T, "global_batch": n * world,
                        "minibatch": n // args.minibatches * world,
                        "parallelism": f"env-sharded dp{world}",
@@ -210,7 +269,7 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if distributed:
         import torch.distributed as dist
         dist.destroy_process_group()
 

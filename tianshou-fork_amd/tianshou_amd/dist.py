@@ -14,6 +14,11 @@ import torch.distributed as dist
 
 
 class DataParallel:
+    # True: run the collective code path even with a single rank (all-reduces over a
+    # one-rank RCCL communicator are identities) -- bench.py --force-dp, used by the GPU test
+    # that rehearses the N>1 path on a one-GPU box.
+    force = False
+
     def __init__(self, group=None) -> None:
         self.group = group
         self.enabled = dist.is_available() and dist.is_initialized()
@@ -23,7 +28,7 @@ class DataParallel:
 
     @property
     def active(self) -> bool:
-        return self.enabled and self.world > 1
+        return self.enabled and (self.world > 1 or DataParallel.force)
 
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         if self.active:
