@@ -320,6 +320,16 @@ int tsrl_mlp_l1_fwd(const float* X, int64_t ldx, const int64_t* idx, int64_t n, 
                     const float* Wa, const float* ba, const float* Wc, const float* bc,
                     int act_tanh, float* out, int frag_out, void* stream);
 int64_t tsrl_mlp_frag_floats(int64_t n);
+/* The same first layer on the bf16 matrix cores with an exact three-way bf16 split of every
+ * f32 operand and the six products of order <= 2 accumulated in f32 ("bf16x6": f32-level
+ * error, 2.7x the f32-input MFMA rate; csrc/mlp_x6.hip).  wsplit holds the split stacked
+ * weight (tsrl_mlp_split_bytes(D) bytes, 16-byte aligned), refreshed by tsrl_mlp_split_w after
+ * every parameter update.  Output layouts as tsrl_mlp_l1_fwd. */
+int64_t tsrl_mlp_split_bytes(int64_t D);
+int tsrl_mlp_split_w(const float* Wa, const float* Wc, int64_t D, void* wsplit, void* stream);
+int tsrl_mlp_l1_fwd_x6(const float* X, int64_t ldx, const int64_t* idx, int64_t n, int64_t D,
+                       const void* wsplit, const float* ba, const float* bc, int act_tanh,
+                       float* out, int frag_out, void* stream);
 int64_t tsrl_ppo_tail_workspace_bytes(int64_t n);
 int tsrl_ppo_tail(const float* h1frag, int64_t n, const int64_t* idx,
                   const tsrl_tail_weights* w, int64_t act_dim, const float* act,

@@ -54,6 +54,55 @@ def _nets(D, A, dev, seed):
     return actor, critic
 
 
+@pytest.mark.parametrize("D,n", [(376, 1000), (24, 4096), (8, 33), (128, 128), (376, 262144)])
+def test_l1_fwd_x6_f32_accuracy(dev, D, n):
+    """tsrl_mlp_l1_fwd_x6 (exact 3-way bf16 split, six bf16 products, f32 accumulation) is an
+    f32 GEMM: against an fp64 product of the same f32 operands its error must be within 2x of
+    the error of torch's own f32 GEMM (hipBLASLt, f32-input MFMA) and of the f32-input MFMA
+    kernel, elementwise bounded by 1e-6 * sum|w x| + 1e-7, and the outputs (both layouts,
+    tanh) must match torch fp32 at rtol 1e-5 / atol 1e-5 like the f32 kernel's."""
+    from tianshou_amd import _C
+    g = torch.Generator().manual_seed(D + n + 1)
+    N = n + 50
+    X = (torch.randn(N, D, generator=g) * 2).to(dev)
+    idx = torch.randperm(N, generator=g)[:n].to(dev)
+    Wa, Wc = torch.randn(64, D, generator=g).to(dev) * 0.1, torch.randn(64, D, generator=g).to(dev) * 0.1
+    ba, bc = torch.randn(64, generator=g).to(dev), torch.randn(64, generator=g).to(dev)
+    L = _C.lib()
+    s = _C.stream_ptr(dev)
+    ws = torch.empty((int(L.tsrl_mlp_split_bytes(D)) + 3) // 4, device=dev)
+    _C.check(L.tsrl_mlp_split_w(_C.ptr(Wa), _C.ptr(Wc), D, _C.ptr(ws), s))
+    W = torch.cat([Wa, Wc])
+    Xi = X[idx]
+    lin = torch.empty(n, 128, device=dev)
+    _C.check(L.tsrl_mlp_l1_fwd_x6(_C.ptr(X), D, _C.ptr(idx), n, D, _C.ptr(ws), _C.ptr(ba),
+                                  _C.ptr(bc), 0, _C.ptr(lin), 0, s))
+    lin32 = torch.empty(n, 128, device=dev)
+    _C.check(L.tsrl_mlp_l1_fwd(_C.ptr(X), D, _C.ptr(idx), n, D, _C.ptr(Wa), _C.ptr(ba),
+                               _C.ptr(Wc), _C.ptr(bc), 0, _C.ptr(lin32), 0, s))
+    b = torch.cat([ba, bc])
+    ref64 = Xi.double() @ W.double().T + b.double()
+    torch_f32 = Xi @ W.T + b
+    mag = Xi.double().abs() @ W.double().abs().T + b.double().abs()
+    err = (lin.double() - ref64).abs()
+    err_t = (torch_f32.double() - ref64).abs()
+    err_k = (lin32.double() - ref64).abs()
+    assert float((err - (1e-6 * mag + 1e-7)).max()) <= 0.0
+    assert float(err.pow(2).mean().sqrt()) <= 2.0 * max(float(err_t.pow(2).mean().sqrt()),
+                                                       float(err_k.pow(2).mean().sqrt()))
+    want = torch.tanh(torch_f32)
+    rows = torch.empty(n, 128, device=dev)
+    _C.check(L.tsrl_mlp_l1_fwd_x6(_C.ptr(X), D, _C.ptr(idx), n, D, _C.ptr(ws), _C.ptr(ba),
+                                  _C.ptr(bc), 1, _C.ptr(rows), 0, s))
+    frag = torch.empty(int(L.tsrl_mlp_frag_floats(n)), device=dev)
+    _C.check(L.tsrl_mlp_l1_fwd_x6(_C.ptr(X), D, _C.ptr(idx), n, D, _C.ptr(ws), _C.ptr(ba),
+                                  _C.ptr(bc), 1, _C.ptr(frag), 1, s))
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(rows.cpu(), want.cpu(), rtol=1e-5, atol=1e-5)
+    if n <= 4096:
+        np.testing.assert_allclose(frag_to_rows(frag, n), want.cpu(), rtol=1e-5, atol=1e-5)
+
+
 @pytest.mark.parametrize("D,n", [(376, 1000), (24, 4096), (8, 33), (128, 128)])
 def test_l1_fwd_matches_torch(dev, D, n):
     from tianshou_amd import _C

@@ -240,6 +240,27 @@ __device__ Welford block_welford(Welford v, double* sh /*[3*TPB]*/) {
     return r;
 }
 
+// Block-wide Chan merge with wave shuffles (xor butterfly inside each wave, then the 4 wave
+// results folded in wave order by thread 0): fixed order -> deterministic; result valid in
+// thread 0.  `sh` holds NWAVE entries.
+__device__ __forceinline__ Welford block_welford_fast(Welford v, Welford* sh) {
+#pragma unroll
+    for (int off = kWave / 2; off > 0; off >>= 1) {
+        Welford o;
+        o.n = __shfl_xor(v.n, off, kWave);
+        o.mean = __shfl_xor(v.mean, off, kWave);
+        o.m2 = __shfl_xor(v.m2, off, kWave);
+        v = chan(v, o);
+    }
+    const int w = threadIdx.x / kWave;
+    if ((threadIdx.x & (kWave - 1)) == 0) sh[w] = v;
+    __syncthreads();
+    Welford r = sh[0];
+#pragma unroll
+    for (int i = 1; i < NWAVE; ++i) r = chan(r, sh[i]);
+    return r;
+}
+
 // One tile [tb, te) with carry-in `carry` (= adv at te, 0 beyond a segment end).
 // Returns the carry for the tile to its left (adv at tb).
 template <bool F64V, bool VEC>
@@ -314,7 +335,7 @@ __device__ double gae_tile(const GaeArgs& p, int64_t tb, int64_t te, double carr
             for (int k = 0; k < EPT; ++k)
                 if (e.validb & (1u << k)) { const double dv = ret[k] - w.mean; w.m2 += dv * dv; }
         }
-        Welford t = block_welford(w, wsh);
+        Welford t = block_welford_fast(w, reinterpret_cast<Welford*>(wsh));
         if (threadIdx.x == 0) *acc = chan(t, *acc);
     }
     __syncthreads();  // lds reuse by the next tile

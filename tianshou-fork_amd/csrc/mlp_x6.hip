@@ -1,0 +1,311 @@
+// First-layer GEMMs of the fused PPO MLP (mlp.hip) on the bf16 matrix cores with an exact
+// three-way split of every f32 operand ("bf16x6" f32 emulation).
+//
+// An f32 x is split exactly into x = x0 + x1 + x2 with x0 = bf16(x), x1 = bf16(x - x0),
+// x2 = bf16(x - x0 - x1) (round-to-nearest each time; the residuals are exact in f32 and the
+// third piece holds the last 8 bits, so the split loses nothing).  A product a.b is
+// accumulated as the six bf16 products of order <= 2,
+//     a0b0 + (a0b1 + a1b0) + (a0b2 + a1b1 + a2b0),
+// each exact in the f32 MFMA accumulator; the dropped terms (a1b2, a2b1, a2b2) are below
+// 2^-24 |ab|, i.e. at the f32 rounding level of one product.  The sums accumulate in f32 as
+// the f32-input MFMA path does, so the result carries f32 GEMM error (tests/test_gpu_mlp.py
+// measures it against an fp64 product next to torch's own f32 GEMM).  Six bf16 MFMAs
+// (v_mfma_f32_32x32x16_bf16, 32 cycles for 32x32x16) replace eight f32 ones
+// (v_mfma_f32_32x32x2_f32, 64 cycles for 32x32x2): 2.7x the f32 matrix rate.
+//
+// l1_fwd_x6: H1^T = act(W1cat . X[idx]^T + b1) exactly as tsrl_mlp_l1_fwd (same output
+// layouts); the weights are split once per parameter update (tsrl_mlp_split_w), the
+// observation rows are staged as f32 and split by the wave that owns them, right before
+// their MFMAs (each element is split once).  Measured (tools/mlp_kernel_bench.py, 262144
+// gathered rows x 376): 250 us vs 336 us for the f32-input kernel.
+#include "tsrl_common.h"
+
+namespace tsrl {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int H = 64;
+constexpr int HC = 2 * H;   // actor + critic first-layer features
+constexpr int NT = HC / 32;
+constexpr int XR = 128;     // minibatch rows per workgroup
+constexpr int KC = 32;      // k per staged chunk (two 16-k MFMA steps)
+constexpr int NPL = 3;      // split planes
+constexpr int ROWB = KC * 2;  // bytes per LDS row of one plane (32 bf16)
+
+__device__ __forceinline__ int rho(int r) { return (r & 3) + 8 * (r >> 2); }
+
+// Byte offset of 16-byte chunk q (0..3) of LDS row `row`: chunks XOR-swizzled by row bits 2-3
+// so that the 16 lanes of a ds_read_b128 phase (rows c..c+15, one chunk) hit all 64 banks.
+__device__ __forceinline__ int sw_off(int row, int q) {
+    return row * ROWB + 16 * (q ^ ((row >> 2) & 3));
+}
+
+// f32 rows of KC floats (128 B, chunks q = 0..7): chunk index XOR row bits 1-3, so the
+// 16-lane phases of a ds_read_b128 (rows r..r+15, one chunk) cover all banks.
+constexpr int XROWB = KC * 4;
+__device__ __forceinline__ int swf_off(int row, int q) {
+    return row * XROWB + 16 * (q ^ ((row >> 1) & 7));
+}
+
+// One f32 split exactly into three bf16 pieces.
+__device__ __forceinline__ void split1(float x, __bf16& a0, __bf16& a1, __bf16& a2) {
+    a0 = (__bf16)x;
+    const float r1 = x - (float)a0;
+    a1 = (__bf16)r1;
+    a2 = (__bf16)(r1 - (float)a1);
+}
+
+// Elements o..o+3 of the three split planes from one float4.
+__device__ __forceinline__ void split4(float4 v, bf16x8& p0, bf16x8& p1, bf16x8& p2, int o) {
+    __bf16 a, b, c;
+    split1(v.x, a, b, c);
+    p0[o] = a, p1[o] = b, p2[o] = c;
+    split1(v.y, a, b, c);
+    p0[o + 1] = a, p1[o + 1] = b, p2[o + 1] = c;
+    split1(v.z, a, b, c);
+    p0[o + 2] = a, p1[o + 2] = b, p2[o + 2] = c;
+    split1(v.w, a, b, c);
+    p0[o + 3] = a, p1[o + 3] = b, p2[o + 3] = c;
+}
+
+__device__ __forceinline__ f32x16 mfma6(const bf16x8 (&a)[NPL], const bf16x8 (&b)[NPL],
+                                        f32x16 acc) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], acc, 0, 0, 0);
+    return acc;
+}
+
+// Split planes of the stacked first-layer weight: out[p][f][k] (f < 64 actor, >= 64 critic;
+// k padded with zeros to Kp = roundup(D, 32)).
+__global__ void split_w_kernel(const float* __restrict__ Wa, const float* __restrict__ Wc,
+                               int64_t D, int64_t Kp, __bf16* __restrict__ out) {
+    const int64_t total = (int64_t)HC * Kp;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t f = i / Kp, k = i - f * Kp;
+        float x = 0.0f;
+        if (k < D) x = f < H ? Wa[f * D + k] : Wc[(f - H) * D + k];
+        const __bf16 a0 = (__bf16)x;
+        const float r1 = x - (float)a0;
+        const __bf16 a1 = (__bf16)r1;
+        out[i] = a0;
+        out[total + i] = a1;
+        out[2 * total + i] = (__bf16)(r1 - (float)a1);
+    }
+}
+
+// Workgroup = 128 minibatch rows x 128 features, 4 waves; wave w owns rows [32w, 32w+32) and
+// the 4 feature tiles.  K is staged 32 at a time: every thread loads 16 floats of one row
+// (two threads per row, 128-byte row segments) and 16 pre-split weights per plane, both held
+// in registers one chunk ahead and stored into the single-buffered LDS tiles after the
+// chunk's MFMAs.  X6_IL interleaves the six products of two feature tiles; X6_OCC is the
+// workgroups-per-CU bound (variants measured equal within 2 %, 2/1 kept).
+#ifndef X6_IL
+#define X6_IL 1
+#endif
+#ifndef X6_OCC
+#define X6_OCC 2
+#endif
+__global__ __launch_bounds__(256, X6_OCC) void l1_fwd_x6_kernel(
+    const float* __restrict__ X, int64_t ldx, const int64_t* __restrict__ idx, int64_t n,
+    int D, int Kp, const __bf16* __restrict__ wsp, const float* __restrict__ ba,
+    const float* __restrict__ bc, int act_tanh, float* __restrict__ out, int frag_out) {
+    __shared__ __attribute__((aligned(16))) char Xs[XR * XROWB];  // f32 rows
+    __shared__ __attribute__((aligned(16))) char Ws[NPL][HC * ROWB];
+    __shared__ float sb[HC];
+    const int t = threadIdx.x;
+    const int w = t >> 6, l = t & 63, h = l >> 5, c = l & 31;
+    const int64_t row0 = (int64_t)blockIdx.x * XR;
+    if (t < HC) sb[t] = t < H ? ba[t] : bc[t - H];
+    const int srow = t >> 1, sq = 2 * (t & 1);
+    const int64_t gr = row0 + srow;
+    const bool live = gr < n;
+    const float* xsrc = X + (live ? (idx ? idx[gr] : gr) : 0) * ldx;
+    const int64_t plane = (int64_t)HC * Kp;
+    const __bf16* wsrc = wsp + (int64_t)srow * Kp + 8 * sq;
+    const int nch = Kp / KC;
+    // registers one chunk ahead: 16 floats of the row, 2 x 16 B per weight plane.  Loads are
+    // branch-free (an out-of-range float4 reads k = 0 and is zeroed by a select: a load under
+    // a runtime condition makes hipcc branch around it and drain vmcnt per element), and all
+    // staging values are named scalars (no arrays or lambdas that end up in scratch).
+    float4 x0, x1, x2, x3;
+    uint4 w00, w01, w10, w11, w20, w21;
+#define X6_LOAD(kc)                                                                         \
+    {                                                                                       \
+        const int k_ = (kc) * KC + 8 * sq;                                                  \
+        const bool i0_ = live && k_ < D, i1_ = live && k_ + 4 < D;                          \
+        const bool i2_ = live && k_ + 8 < D, i3_ = live && k_ + 12 < D;                     \
+        x0 = *reinterpret_cast<const float4*>(xsrc + (i0_ ? k_ : 0));                       \
+        x1 = *reinterpret_cast<const float4*>(xsrc + (i1_ ? k_ + 4 : 0));                   \
+        x2 = *reinterpret_cast<const float4*>(xsrc + (i2_ ? k_ + 8 : 0));                   \
+        x3 = *reinterpret_cast<const float4*>(xsrc + (i3_ ? k_ + 12 : 0));                  \
+        if (!i0_) x0 = make_float4(0.f, 0.f, 0.f, 0.f);                                     \
+        if (!i1_) x1 = make_float4(0.f, 0.f, 0.f, 0.f);                                     \
+        if (!i2_) x2 = make_float4(0.f, 0.f, 0.f, 0.f);                                     \
+        if (!i3_) x3 = make_float4(0.f, 0.f, 0.f, 0.f);                                     \
+        const __bf16* wk_ = wsrc + (kc) * KC;                                                \
+        w00 = *reinterpret_cast<const uint4*>(wk_);                                         \
+        w01 = *reinterpret_cast<const uint4*>(wk_ + 8);                                     \
+        w10 = *reinterpret_cast<const uint4*>(wk_ + plane);                                 \
+        w11 = *reinterpret_cast<const uint4*>(wk_ + plane + 8);                             \
+        w20 = *reinterpret_cast<const uint4*>(wk_ + 2 * plane);                             \
+        w21 = *reinterpret_cast<const uint4*>(wk_ + 2 * plane + 8);                         \
+    }
+    const int off0 = sw_off(srow, sq), off1 = sw_off(srow, sq + 1);
+    // f32 X rows, 16-B chunk qc = 4 * (t & 1) + i of row srow
+    const int xo0 = swf_off(srow, 2 * sq), xo1 = swf_off(srow, 2 * sq + 1);
+    const int xo2 = swf_off(srow, 2 * sq + 2), xo3 = swf_off(srow, 2 * sq + 3);
+#define X6_STORE()                                                                          \
+    {                                                                                       \
+        *reinterpret_cast<float4*>(&Xs[xo0]) = x0;                                          \
+        *reinterpret_cast<float4*>(&Xs[xo1]) = x1;                                          \
+        *reinterpret_cast<float4*>(&Xs[xo2]) = x2;                                          \
+        *reinterpret_cast<float4*>(&Xs[xo3]) = x3;                                          \
+        *reinterpret_cast<uint4*>(&Ws[0][off0]) = w00;                                      \
+        *reinterpret_cast<uint4*>(&Ws[0][off1]) = w01;                                      \
+        *reinterpret_cast<uint4*>(&Ws[1][off0]) = w10;                                      \
+        *reinterpret_cast<uint4*>(&Ws[1][off1]) = w11;                                      \
+        *reinterpret_cast<uint4*>(&Ws[2][off0]) = w20;                                      \
+        *reinterpret_cast<uint4*>(&Ws[2][off1]) = w21;                                      \
+    }
+    f32x16 acc[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][r] = 0.0f;
+    X6_LOAD(0)
+    X6_STORE()
+    __syncthreads();
+    for (int kc = 0; kc < nch; ++kc) {
+        if (kc + 1 < nch) X6_LOAD(kc + 1)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            // this lane's 8 k of its row (f32), split here: every X element belongs to exactly
+            // one wave's rows, so each is split once
+            bf16x8 b[NPL];
+            {
+                const int xr = 32 * w + c;
+                const float4 u = *reinterpret_cast<const float4*>(&Xs[swf_off(xr, 4 * s + 2 * h)]);
+                const float4 v = *reinterpret_cast<const float4*>(
+                    &Xs[swf_off(xr, 4 * s + 2 * h + 1)]);
+                split4(u, b[0], b[1], b[2], 0);
+                split4(v, b[0], b[1], b[2], 4);
+            }
+#if X6_IL
+            // two feature tiles at a time, their six products interleaved (two independent
+            // accumulation chains in flight)
+#pragma unroll
+            for (int ip = 0; ip < NT; ip += 2) {
+                bf16x8 a0[NPL], a1[NPL];
+                const int ao0 = sw_off(32 * ip + c, 2 * s + h);
+                const int ao1 = sw_off(32 * (ip + 1) + c, 2 * s + h);
+#pragma unroll
+                for (int p = 0; p < NPL; ++p) {
+                    a0[p] = *reinterpret_cast<const bf16x8*>(&Ws[p][ao0]);
+                    a1[p] = *reinterpret_cast<const bf16x8*>(&Ws[p][ao1]);
+                }
+#define X6_PAIR(pa, pb)                                                                     \
+    acc[ip] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[pa], b[pb], acc[ip], 0, 0, 0);     \
+    acc[ip + 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[pa], b[pb], acc[ip + 1], 0, 0, 0);
+                X6_PAIR(0, 0)
+                X6_PAIR(0, 1)
+                X6_PAIR(1, 0)
+                X6_PAIR(0, 2)
+                X6_PAIR(1, 1)
+                X6_PAIR(2, 0)
+#undef X6_PAIR
+            }
+#else
+#pragma unroll
+            for (int i = 0; i < NT; ++i) {
+                bf16x8 a[NPL];
+                const int aoff = sw_off(32 * i + c, 2 * s + h);
+#pragma unroll
+                for (int p = 0; p < NPL; ++p)
+                    a[p] = *reinterpret_cast<const bf16x8*>(&Ws[p][aoff]);
+                acc[i] = mfma6(a, b, acc[i]);
+            }
+#endif
+        }
+        if (kc + 1 < nch) {
+            __syncthreads();
+            X6_STORE()
+            __syncthreads();
+        }
+    }
+#undef X6_LOAD
+#undef X6_STORE
+    // epilogue: bias + tanh; frag layout [row tile][feature tile][lane][16] or row-major
+    const int64_t bt = (row0 >> 5) + w;
+    const int64_t brow = row0 + 32 * w + c;
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+        float v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int f = 32 * i + rho(r) + 4 * h;
+            const float z = acc[i][r] + sb[f];
+            v[r] = act_tanh ? tanh_nb(z) : z;
+        }
+        if (frag_out) {
+            float4* o = reinterpret_cast<float4*>(out + ((bt * NT + i) * 64 + l) * 16);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                o[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+        } else if (brow < n) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                *reinterpret_cast<float4*>(out + brow * HC + 32 * i + 8 * q + 4 * h) =
+                    make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+        }
+    }
+}
+
+inline int64_t kpad32(int64_t D) { return (D + KC - 1) / KC * KC; }
+
+}  // namespace
+}  // namespace tsrl
+
+using namespace tsrl;
+
+extern "C" int64_t tsrl_mlp_split_bytes(int64_t D) {
+    return D > 0 ? (int64_t)NPL * HC * kpad32(D) * 2 : 0;
+}
+
+extern "C" int tsrl_mlp_split_w(const float* Wa, const float* Wc, int64_t D, void* wsplit,
+                                void* stream) {
+    TSRL_CHECK_ARG(D > 0, "tsrl_mlp_split_w: D <= 0");
+    TSRL_CHECK_ARG(Wa && Wc && wsplit, "tsrl_mlp_split_w: null pointer");
+    const int64_t total = (int64_t)HC * kpad32(D);
+    const unsigned g = (unsigned)std::min<int64_t>((total + 255) / 256, 1024);
+    hipLaunchKernelGGL(split_w_kernel, dim3(g), dim3(256), 0, as_stream(stream), Wa, Wc, D,
+                       kpad32(D), reinterpret_cast<__bf16*>(wsplit));
+    TSRL_LAUNCH_CHECK("tsrl_mlp_split_w");
+    return 0;
+}
+
+extern "C" int tsrl_mlp_l1_fwd_x6(const float* X, int64_t ldx, const int64_t* idx, int64_t n,
+                                  int64_t D, const void* wsplit, const float* ba,
+                                  const float* bc, int act_tanh, float* out, int frag_out,
+                                  void* stream) {
+    TSRL_CHECK_ARG(n >= 0 && D > 0 && ldx >= D, "tsrl_mlp_l1_fwd_x6: bad sizes");
+    if (n == 0) return 0;
+    TSRL_CHECK_ARG(X && wsplit && ba && bc && out, "tsrl_mlp_l1_fwd_x6: null pointer");
+    TSRL_CHECK_ARG(aligned16(X) && ldx % 4 == 0 && D % 4 == 0 && aligned16(out) &&
+                       aligned16(wsplit),
+                   "tsrl_mlp_l1_fwd_x6: X/out/wsplit must be 16-byte aligned, D and ldx "
+                   "multiples of 4");
+    const unsigned grid = (unsigned)((n + XR - 1) / XR);
+    hipLaunchKernelGGL(l1_fwd_x6_kernel, dim3(grid), dim3(256), 0, as_stream(stream), X, ldx,
+                       idx, n, (int)D, (int)kpad32(D),
+                       reinterpret_cast<const __bf16*>(wsplit), ba, bc, act_tanh, out,
+                       frag_out);
+    TSRL_LAUNCH_CHECK("tsrl_mlp_l1_fwd_x6");
+    return 0;
+}

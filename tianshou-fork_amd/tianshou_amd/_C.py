@@ -8,7 +8,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libtsrl.so")
+# TSRL_LIB_PATH: load another build of the same library (kernel-variant experiments, tools/)
+LIB_PATH = os.environ.get("TSRL_LIB_PATH") or os.path.join(_HERE, "lib", "libtsrl.so")
 
 _i64 = ctypes.c_int64
 _u64 = ctypes.c_uint64
@@ -105,6 +106,10 @@ _SIGS = {
     "tsrl_mlp_l1_fwd": ([_p, _i64, _p, _i64, _i64, _p, _p, _p, _p, ctypes.c_int, _p,
                          ctypes.c_int, _p], ctypes.c_int),
     "tsrl_mlp_frag_floats": ([_i64], _i64),
+    "tsrl_mlp_split_bytes": ([_i64], _i64),
+    "tsrl_mlp_split_w": ([_p, _p, _i64, _p, _p], ctypes.c_int),
+    "tsrl_mlp_l1_fwd_x6": ([_p, _i64, _p, _i64, _i64, _p, _p, _p, ctypes.c_int, _p,
+                            ctypes.c_int, _p], ctypes.c_int),
     "tsrl_ppo_tail_workspace_bytes": ([_i64], _i64),
     "tsrl_ppo_tail": ([_p, _i64, _p, ctypes.POINTER(TailWeights), _i64, _p, _p, _p, _p, _p, _p,
                        PPOParams, _p, ctypes.POINTER(TailGrads), _p, _p, _i64, _p],

@@ -23,6 +23,9 @@ from tianshou_amd import _C
 
 HIDDEN = 64
 MAX_ACT = 32
+# first-layer forward on the bf16 matrix cores with the exact 3-way operand split
+# (tsrl_mlp_l1_fwd_x6, f32-level error); False: the f32-input MFMA kernel (tsrl_mlp_l1_fwd)
+L1_X6 = True
 
 
 def _seq(mlp) -> Optional[list]:
@@ -121,6 +124,25 @@ class FusedActorCritic:
             _C.ptr(L["w3c"].weight.detach()), _C.ptr(L["w3c"].bias.detach()),
             _C.ptr(L["sigma"].detach()))
 
+    def _l1_fwd(self, xp, ldx, ip, m, out, frag_out: int, split: bool = True) -> None:
+        """Layer 1 of both nets for m rows (X at xp, rows through ip when given)."""
+        L, lib = self.L, _C.lib()
+        s = _C.stream_ptr(self.params[0].device)
+        D = self.D
+        if L1_X6:
+            ws = self._buf("w1split", (int(lib.tsrl_mlp_split_bytes(D)) + 3) // 4)
+            if split:
+                _C.check(lib.tsrl_mlp_split_w(_C.ptr(L["w1a"].weight), _C.ptr(L["w1c"].weight),
+                                              D, _C.ptr(ws), s), "tsrl_mlp_split_w")
+            _C.check(lib.tsrl_mlp_l1_fwd_x6(xp, ldx, ip, m, D, _C.ptr(ws),
+                                            _C.ptr(L["w1a"].bias), _C.ptr(L["w1c"].bias), 1,
+                                            out, frag_out, s), "tsrl_mlp_l1_fwd_x6")
+            return
+        _C.check(lib.tsrl_mlp_l1_fwd(xp, ldx, ip, m, D, _C.ptr(L["w1a"].weight),
+                                     _C.ptr(L["w1a"].bias), _C.ptr(L["w1c"].weight),
+                                     _C.ptr(L["w1c"].bias), 1, out, frag_out, s),
+                 "tsrl_mlp_l1_fwd")
+
     # -- forward-only evaluation (process_fn) ---------------------------------------------------
     EVAL_CHUNK = 1 << 21
 
@@ -138,8 +160,6 @@ class FusedActorCritic:
         values = torch.empty(n, dtype=torch.float32, device=dev)
         logp = torch.empty(n, dtype=torch.float32, device=dev) if act is not None else None
         w = self._weights()
-        W = [L["w1a"].weight.detach(), L["w1a"].bias.detach(), L["w1c"].weight.detach(),
-             L["w1c"].bias.detach()]
         for s0 in range(0, n, self.EVAL_CHUNK):
             e0 = min(n, s0 + self.EVAL_CHUNK)
             m = e0 - s0
@@ -148,8 +168,7 @@ class FusedActorCritic:
                 xp, ip = obs.data_ptr() + s0 * D * 4, None
             else:
                 xp, ip = obs.data_ptr(), idx.data_ptr() + s0 * 8
-            _C.check(lib.tsrl_mlp_l1_fwd(xp, D, ip, m, D, *(_C.ptr(t) for t in W), 1,
-                                         _C.ptr(h1), 1, s), "tsrl_mlp_l1_fwd")
+            self._l1_fwd(xp, D, ip, m, _C.ptr(h1), 1, split=(s0 == 0))
             ap = None
             if act is not None:
                 ap = act.data_ptr() + s0 * A * 4
@@ -195,10 +214,7 @@ class FusedActorCritic:
                      "tsrl_reduce_partials")
             dp.all_reduce_(adv_sums)
         h1 = self._buf("h1", int(lib.tsrl_mlp_frag_floats(b)))
-        _C.check(lib.tsrl_mlp_l1_fwd(
-            _C.ptr(obs), D, ip, b, D, _C.ptr(L["w1a"].weight), _C.ptr(L["w1a"].bias),
-            _C.ptr(L["w1c"].weight), _C.ptr(L["w1c"].bias), 1, _C.ptr(h1), 1, s),
-            "tsrl_mlp_l1_fwd")
+        self._l1_fwd(_C.ptr(obs), D, ip, b, _C.ptr(h1), 1)
         dz1 = self._buf("dz1", b * 2 * 64)
         sums = self._buf("sums", 4 + A, torch.float64)[:4 + A]
         wsb = int(lib.tsrl_ppo_tail_workspace_bytes(b))

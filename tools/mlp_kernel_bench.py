@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--D", type=int, default=376)
     ap.add_argument("--A", type=int, default=17)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--contig", action="store_true",
+                    help="minibatch rows contiguous (no permutation gather)")
     a = ap.parse_args()
     from tianshou_amd import _C
     from tianshou_amd.dist import DataParallel
@@ -39,7 +41,7 @@ def main():
     adv = torch.randn(N, device=dev)
     ret = torch.randn(N, device=dev)
     v_s = torch.randn(N, device=dev)
-    idx = torch.randperm(N, device=dev)[:B]
+    idx = None if a.contig else torch.randperm(N, device=dev)[:B]
     p = _C.PPOParams()
     p.eps_clip, p.dual_clip, p.vf_coef, p.ent_coef, p.adv_eps = 0.2, 0.0, 0.25, 0.0, 1e-8
     p.b_global, p.value_clip, p.norm_adv = float(B), 0, 1
@@ -63,6 +65,15 @@ def main():
                                    _C.ptr(W["w1a"].bias), _C.ptr(W["w1c"].weight),
                                    _C.ptr(W["w1c"].bias), 1, _C.ptr(h1), 1, s))
 
+    wsx = torch.empty((int(L.tsrl_mlp_split_bytes(D)) + 3) // 4, device=dev)
+
+    def l1x6():
+        _C.check(L.tsrl_mlp_split_w(_C.ptr(W["w1a"].weight), _C.ptr(W["w1c"].weight), D,
+                                    _C.ptr(wsx), s))
+        _C.check(L.tsrl_mlp_l1_fwd_x6(_C.ptr(obs), D, _C.ptr(idx), B, D, _C.ptr(wsx),
+                                      _C.ptr(W["w1a"].bias), _C.ptr(W["w1c"].bias), 1,
+                                      _C.ptr(h1), 1, s))
+
     def tail():
         _C.check(L.tsrl_ppo_tail(_C.ptr(h1), B, _C.ptr(idx), fm._tail_w, A, _C.ptr(act),
                                  _C.ptr(logp_old), _C.ptr(adv), _C.ptr(ret), _C.ptr(v_s),
@@ -78,7 +89,8 @@ def main():
     def whole():
         fm.minibatch(obs, idx, B, act, logp_old, adv, ret, v_s, p, dp)
 
-    for name, fn, flop in (("l1_fwd", l1, flop_l1), ("tail(+reduce)", tail, flop_tail),
+    for name, fn, flop in (("l1_fwd", l1, flop_l1), ("l1_fwd_x6(+split)", l1x6, flop_l1),
+                           ("tail(+reduce)", tail, flop_tail),
                            ("dw(+reduce)", dw, flop_l1), ("minibatch", whole, None)):
         fn()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
