@@ -837,7 +837,9 @@ __global__ __launch_bounds__(256, 2) void dw_kernel(
     // index of chunk ch+1 is loaded one chunk ahead (no dependent-load stall per chunk).
     const int sc = 4 * (t & 31);
     const int k = col0 + sc;
-    const bool kin = k + 3 < D;  // whole float4 inside the row (D % 4 == 0)
+    // the float4 at column k starts inside the row; its columns >= D are the caller's zero
+    // padding (ldx >= roundup(D, 4)) and are masked per element below
+    const bool kin = k < D;
     float4 zr[4], xr[4];
     int64_t rid[4];       // gather rows of the NEXT chunk to load (raw index values)
     bool live_ld[4];      // row liveness of the chunk whose loads are in flight
@@ -861,9 +863,10 @@ __global__ __launch_bounds__(256, 2) void dw_kernel(
     };
     auto store = [&](int buf) {
         const int i = sc >> 5, c0 = sc & 31;
-        // ones column (db) at k == D
+        // ones column (db) at k == D; data columns k + e < D
         const float o0 = k == D ? 1.f : 0.f, o1 = k + 1 == D ? 1.f : 0.f,
                     o2 = k + 2 == D ? 1.f : 0.f, o3 = k + 3 == D ? 1.f : 0.f;
+        const bool d0 = k < D, d1 = k + 1 < D, d2 = k + 2 < D, d3 = k + 3 < D;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const bool lv = live_ld[q];
@@ -873,8 +876,8 @@ __global__ __launch_bounds__(256, 2) void dw_kernel(
             zd[(c0 + 2) * 4 + i] = lv ? zr[q].z : 0.f;
             zd[(c0 + 3) * 4 + i] = lv ? zr[q].w : 0.f;
             *reinterpret_cast<float4*>(&Xs[buf][(t >> 5) + 8 * q][sc]) =
-                make_float4(lv ? (kin ? xr[q].x : o0) : 0.f, lv ? (kin ? xr[q].y : o1) : 0.f,
-                            lv ? (kin ? xr[q].z : o2) : 0.f, lv ? (kin ? xr[q].w : o3) : 0.f);
+                make_float4(lv ? (d0 ? xr[q].x : o0) : 0.f, lv ? (d1 ? xr[q].y : o1) : 0.f,
+                            lv ? (d2 ? xr[q].z : o2) : 0.f, lv ? (d3 ? xr[q].w : o3) : 0.f);
         }
     };
     f32x16 acc[NT];
@@ -1044,8 +1047,9 @@ extern "C" int tsrl_mlp_dw(const float* dz1, const float* X, int64_t ldx, const 
                            void* workspace, int64_t ws_bytes, void* stream) {
     TSRL_CHECK_ARG(n > 0 && D > 0 && ldx >= D, "tsrl_mlp_dw: bad sizes");
     TSRL_CHECK_ARG(dz1 && X && gWa && gba && gWc && gbc && workspace, "tsrl_mlp_dw: null pointer");
-    TSRL_CHECK_ARG(aligned16(dz1) && aligned16(X) && ldx % 4 == 0,
-                   "tsrl_mlp_dw: dz1/X must be 16-byte aligned, ldx a multiple of 4");
+    TSRL_CHECK_ARG(aligned16(dz1) && aligned16(X) && ldx % 4 == 0 && ldx >= (D + 3) / 4 * 4,
+                   "tsrl_mlp_dw: dz1/X must be 16-byte aligned, ldx a multiple of 4 and >= "
+                   "roundup(D, 4) (columns D.. of the padding read as data-free)");
     TSRL_CHECK_ARG(ws_bytes >= tsrl_mlp_dw_workspace_bytes(n, D), "tsrl_mlp_dw: workspace too small");
     const int ncolt = (int)((D + 1 + DW_COLS - 1) / DW_COLS);
     const int ncolpad = ncolt * DW_COLS;

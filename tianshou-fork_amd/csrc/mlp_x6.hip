@@ -139,6 +139,8 @@ __global__ __launch_bounds__(256, X6_OCC) void l1_fwd_x6_kernel(
 #define X6_LOAD(kc)                                                                         \
     {                                                                                       \
         const int k_ = (kc) * KC + 8 * sq;                                                  \
+        /* a float4 that starts inside the row is read whole: its columns >= D are the */    \
+        /* caller's finite padding and meet zero weights (split_w pads W with zeros)  */    \
         const bool i0_ = live && k_ < D, i1_ = live && k_ + 4 < D;                          \
         const bool i2_ = live && k_ + 8 < D, i3_ = live && k_ + 12 < D;                     \
         x0 = *reinterpret_cast<const float4*>(xsrc + (i0_ ? k_ : 0));                       \
@@ -297,10 +299,10 @@ extern "C" int tsrl_mlp_l1_fwd_x6(const float* X, int64_t ldx, const int64_t* id
     TSRL_CHECK_ARG(n >= 0 && D > 0 && ldx >= D, "tsrl_mlp_l1_fwd_x6: bad sizes");
     if (n == 0) return 0;
     TSRL_CHECK_ARG(X && wsplit && ba && bc && out, "tsrl_mlp_l1_fwd_x6: null pointer");
-    TSRL_CHECK_ARG(aligned16(X) && ldx % 4 == 0 && D % 4 == 0 && aligned16(out) &&
+    TSRL_CHECK_ARG(aligned16(X) && ldx % 4 == 0 && ldx >= (D + 3) / 4 * 4 && aligned16(out) &&
                        aligned16(wsplit),
-                   "tsrl_mlp_l1_fwd_x6: X/out/wsplit must be 16-byte aligned, D and ldx "
-                   "multiples of 4");
+                   "tsrl_mlp_l1_fwd_x6: X/out/wsplit must be 16-byte aligned, ldx a multiple "
+                   "of 4 and >= roundup(D, 4) (X columns D..roundup(D,4) finite: zero padding)");
     const unsigned grid = (unsigned)((n + XR - 1) / XR);
     hipLaunchKernelGGL(l1_fwd_x6_kernel, dim3(grid), dim3(256), 0, as_stream(stream), X, ldx,
                        idx, n, (int)D, (int)kpad32(D),

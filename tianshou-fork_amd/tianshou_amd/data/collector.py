@@ -52,7 +52,7 @@ class Collector:
         self._scratch = None
         # vector steps per captured HIP graph (0 disables graph replay of the fused step)
         self.graph_steps = 64
-        self._graph = None
+        self._graphs = {}  # captured collect graphs by step count
         # run the policy step as the fused HIP kernel when the policy offers one
         self.use_fused_act = True
         self._fused_act_on = False
@@ -298,33 +298,38 @@ class Collector:
                 tuple(ptrs))
 
     def _replay_steps(self, no_grad, n_steps: int, written: list) -> int:
-        """Run up to n_steps uniform steps as replays of a captured G-step HIP graph; returns
-        the number of steps done (the rest is left to the eager loop)."""
-        G = self.graph_steps
-        if n_steps < G:
+        """Run up to n_steps uniform steps as replays of captured HIP graphs of G steps
+        (graph_steps, then one shorter even-length graph for the remainder, each captured
+        once per shape); returns the number of steps done (the rest, at most one step, is
+        left to the eager loop)."""
+        Gmax = self.graph_steps
+        assert Gmax % 2 == 0, "graph_steps must be even (ping-pong step counters)"
+        if n_steps < 2:
             return 0
-        assert G % 2 == 0, "graph_steps must be even (ping-pong step counters)"
-        buf, dev = self.buffer, self._base.device
+        buf = self.buffer
         sc = self._scratch["step_ctr"]
         if self._parity:  # the live counters sit in slot 1: the graph starts from slot 0
             sc[0].copy_(sc[1])
             self._parity = 0
-        key = self._graph_key(G)
-        if getattr(self, "_graph", None) is None or self._graph[0] != key:
-            graph = torch.cuda.CUDAGraph()
-            torch.cuda.synchronize()
-            with torch.cuda.graph(graph):
-                for i in range(G):
-                    self._device_step(self._scratch["cur"], self.env_num, None, False, no_grad,
-                                      dict(rel_dev=sc[i % 2, 0:1],
-                                           rel_next=sc[(i + 1) % 2, 0:1]))
-            self._graph = (key, graph)
-            self._parity = 0
-        _, graph = self._graph
+        if getattr(self, "_graphs", None) is None:
+            self._graphs = {}
         sc[0, 0].fill_(int(buf._ring.index[0]))
         done = 0
-        while n_steps - done >= G:
-            graph.replay()
+        while n_steps - done >= 2:
+            G = min(Gmax, (n_steps - done) // 2 * 2)
+            key = self._graph_key(G)
+            graph = self._graphs.get(G)
+            if graph is None or graph[0] != key:
+                g = torch.cuda.CUDAGraph()
+                torch.cuda.synchronize()
+                with torch.cuda.graph(g):
+                    for i in range(G):
+                        self._device_step(self._scratch["cur"], self.env_num, None, False,
+                                          no_grad, dict(rel_dev=sc[i % 2, 0:1],
+                                                        rel_next=sc[(i + 1) % 2, 0:1]))
+                self._graphs[G] = graph = (key, g)
+                self._parity = 0
+            graph[1].replay()
             for _ in range(G):
                 written.append(int(buf._ring.index[0]))
                 buf._ring.advance(None)

@@ -59,8 +59,8 @@ def match(actor, critic) -> Optional[Dict[str, nn.Linear]]:
         return None
     l1 = getattr(actor.preprocess, "model", None)
     D = getattr(getattr(l1, "model", [None])[0], "in_features", None) if l1 is not None else None
-    if not isinstance(D, int) or D % 4 != 0:
-        return None
+    if not isinstance(D, int) or (D % 4 != 0 and not L1_X6):
+        return None  # D % 4 != 0 runs on zero-padded rows (FusedActorCritic.rows), x6 only
     ta, tc = _trunk(actor.preprocess, D), _trunk(critic.preprocess, D)
     mu, last = _seq(actor.mu), _seq(critic.last)
     if ta is None or tc is None or mu is None or last is None or len(mu) != 1 or len(last) != 1:
@@ -82,6 +82,7 @@ class FusedActorCritic:
     def __init__(self, layers: Dict, params) -> None:
         self.L = layers
         self.D = layers["D"]
+        self.Dp = (self.D + 3) // 4 * 4  # row stride the kernels read (16-byte rows)
         self.A = layers["A"]
         self.params = [p for p in params]
         self._flat = None
@@ -143,6 +144,18 @@ class FusedActorCritic:
                                      _C.ptr(L["w1c"].bias), 1, out, frag_out, s),
                  "tsrl_mlp_l1_fwd")
 
+    def rows(self, obs: torch.Tensor, key: str = "xpad") -> torch.Tensor:
+        """The observation rows as the kernels read them: obs itself when D % 4 == 0, else a
+        zero-padded [n, roundup(D, 4)] copy in a persistent buffer (stable address: the
+        captured learn graph reads it)."""
+        if self.Dp == self.D:
+            return obs.contiguous()
+        n = obs.shape[0]
+        b = self._buf(key, n * self.Dp)[:n * self.Dp].view(n, self.Dp)
+        b[:, self.D:].zero_()
+        b[:, :self.D].copy_(obs)
+        return b
+
     # -- forward-only evaluation (process_fn) ---------------------------------------------------
     EVAL_CHUNK = 1 << 21
 
@@ -155,7 +168,9 @@ class FusedActorCritic:
         dev = obs.device
         s = _C.stream_ptr(dev)
         D, A = self.D, self.A
-        assert obs.dim() == 2 and obs.shape[1] == D and obs.is_contiguous()
+        assert obs.dim() == 2 and obs.shape[1] == D
+        obs = self.rows(obs, "xpad_eval")
+        ldx = obs.shape[1]
         n = obs.shape[0] if idx is None else idx.numel()
         values = torch.empty(n, dtype=torch.float32, device=dev)
         logp = torch.empty(n, dtype=torch.float32, device=dev) if act is not None else None
@@ -165,10 +180,10 @@ class FusedActorCritic:
             m = e0 - s0
             h1 = self._buf("eval_h1", int(lib.tsrl_mlp_frag_floats(m)))
             if idx is None:
-                xp, ip = obs.data_ptr() + s0 * D * 4, None
+                xp, ip = obs.data_ptr() + s0 * ldx * 4, None
             else:
                 xp, ip = obs.data_ptr(), idx.data_ptr() + s0 * 8
-            self._l1_fwd(xp, D, ip, m, _C.ptr(h1), 1, split=(s0 == 0))
+            self._l1_fwd(xp, ldx, ip, m, _C.ptr(h1), 1, split=(s0 == 0))
             ap = None
             if act is not None:
                 ap = act.data_ptr() + s0 * A * 4
@@ -194,13 +209,14 @@ class FusedActorCritic:
                   ret: torch.Tensor, v_s: torch.Tensor, params: "_C.PPOParams", dp
                   ) -> torch.Tensor:
         """Gradients of the minibatch loss into the parameters' .grad; returns the device
-        tensor [loss, clip, vf, ent] (ppo.py:140-142)."""
+        tensor [loss, clip, vf, ent] (ppo.py:140-142).  ``obs`` are the rows of ``rows()``."""
         self.bind_grads()
         L, lib = self.L, _C.lib()
         dev = obs.device
         s = _C.stream_ptr(dev)
         D, A = self.D, self.A
-        assert obs.dim() == 2 and obs.shape[1] == D and obs.is_contiguous()
+        assert obs.dim() == 2 and obs.shape[1] == self.Dp and obs.is_contiguous()
+        ldx = self.Dp
         assert act.shape[-1] == A and act.is_contiguous()
         ip = _C.ptr(idx) if idx is not None else None
         # advantage moments of the (global) minibatch
@@ -214,7 +230,7 @@ class FusedActorCritic:
                      "tsrl_reduce_partials")
             dp.all_reduce_(adv_sums)
         h1 = self._buf("h1", int(lib.tsrl_mlp_frag_floats(b)))
-        self._l1_fwd(_C.ptr(obs), D, ip, b, _C.ptr(h1), 1)
+        self._l1_fwd(_C.ptr(obs), ldx, ip, b, _C.ptr(h1), 1)
         dz1 = self._buf("dz1", b * 2 * 64)
         sums = self._buf("sums", 4 + A, torch.float64)[:4 + A]
         wsb = int(lib.tsrl_ppo_tail_workspace_bytes(b))
@@ -227,7 +243,7 @@ class FusedActorCritic:
         wsb2 = int(lib.tsrl_mlp_dw_workspace_bytes(b, D))
         ws2 = self._buf("dw_ws", wsb2, torch.uint8)
         _C.check(lib.tsrl_mlp_dw(
-            _C.ptr(dz1), _C.ptr(obs), D, ip, b, D, _C.ptr(L["w1a"].weight.grad),
+            _C.ptr(dz1), _C.ptr(obs), ldx, ip, b, D, _C.ptr(L["w1a"].weight.grad),
             _C.ptr(L["w1a"].bias.grad), _C.ptr(L["w1c"].weight.grad),
             _C.ptr(L["w1c"].bias.grad), _C.ptr(ws2), wsb2, s), "tsrl_mlp_dw")
         dp.all_reduce_(self._flat)

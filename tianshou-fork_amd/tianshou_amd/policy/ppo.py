@@ -321,7 +321,7 @@ class PPOPolicy(A2CPolicy):
             perm = self._permutation(n, dev)
             mlp_ok = self._mlp is not None and batch.obs.is_cuda and \
                 batch.obs.dtype == torch.float32 and batch.obs.dim() == 2
-            obs_all = batch.obs.contiguous() if mlp_ok else None
+            obs_all = self._mlp.rows(batch.obs) if mlp_ok else None
             if mlp_ok and self._graph_ready():
                 terms.append(self._epoch_graph(obs_all, (act, logp_old, adv, ret, v_s), perm, n,
                                                batch_size, first=(step == 0)))
