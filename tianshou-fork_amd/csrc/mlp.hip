@@ -175,7 +175,6 @@ struct TailParams {
 };
 
 constexpr int WS2 = 65;   // LDS row stride of the staged weights (odd: conflict-free reads)
-constexpr int SS = 34;    // LDS row stride of the per-wave transpose scratch
 // per-workgroup slab of weight-gradient partial sums (floats) and loss partial sums (doubles)
 constexpr int SL_W2A = 0, SL_B2A = SL_W2A + H * H, SL_W2C = SL_B2A + H, SL_B2C = SL_W2C + H * H,
               SL_W3A = SL_B2C + H, SL_B3A = SL_W3A + AMAX * H, SL_W3C = SL_B3A + AMAX,

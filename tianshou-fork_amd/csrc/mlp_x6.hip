@@ -17,7 +17,12 @@
 // layouts); the weights are split once per parameter update (tsrl_mlp_split_w), the
 // observation rows are staged as f32 and split by the wave that owns them, right before
 // their MFMAs (each element is split once).  Measured (tools/mlp_kernel_bench.py, 262144
-// gathered rows x 376): 250 us vs 336 us for the f32-input kernel.
+// gathered rows x 376): 250 us vs 336 us for the f32-input kernel.  Where the time goes
+// (build variants timed on MI355X, since removed): without the global loads after chunk 0
+// 171 us, without the MFMAs 223 us, X-row loads only 243 us, weight loads only 187 us; the
+// matrix cores are 28 % busy (SQ_VALU_MFMA_BUSY_CYCLES).  The gathered X rows and the
+// single-buffered chunk loop (two barriers per 32 k) bound it, not the MFMA rate; reading all
+// of a step's LDS operands ahead of its MFMAs (sched_barrier) measured 6 % slower.
 #include "tsrl_common.h"
 
 namespace tsrl {
@@ -47,6 +52,11 @@ __device__ __forceinline__ int sw_off(int row, int q) {
 constexpr int XROWB = KC * 4;
 __device__ __forceinline__ int swf_off(int row, int q) {
     return row * XROWB + 16 * (q ^ ((row >> 1) & 7));
+}
+
+// v if keep else 0, per component (a whole-vector ternary becomes a scratch-indexed select)
+__device__ __forceinline__ float4 keep4(bool keep, float4 v) {
+    return make_float4(keep ? v.x : 0.f, keep ? v.y : 0.f, keep ? v.z : 0.f, keep ? v.w : 0.f);
 }
 
 // One f32 split exactly into three bf16 pieces.
@@ -147,10 +157,6 @@ __global__ __launch_bounds__(256, X6_OCC) void l1_fwd_x6_kernel(
         x1 = *reinterpret_cast<const float4*>(xsrc + (i1_ ? k_ + 4 : 0));                   \
         x2 = *reinterpret_cast<const float4*>(xsrc + (i2_ ? k_ + 8 : 0));                   \
         x3 = *reinterpret_cast<const float4*>(xsrc + (i3_ ? k_ + 12 : 0));                  \
-        if (!i0_) x0 = make_float4(0.f, 0.f, 0.f, 0.f);                                     \
-        if (!i1_) x1 = make_float4(0.f, 0.f, 0.f, 0.f);                                     \
-        if (!i2_) x2 = make_float4(0.f, 0.f, 0.f, 0.f);                                     \
-        if (!i3_) x3 = make_float4(0.f, 0.f, 0.f, 0.f);                                     \
         const __bf16* wk_ = wsrc + (kc) * KC;                                                \
         w00 = *reinterpret_cast<const uint4*>(wk_);                                         \
         w01 = *reinterpret_cast<const uint4*>(wk_ + 8);                                     \
@@ -163,12 +169,16 @@ __global__ __launch_bounds__(256, X6_OCC) void l1_fwd_x6_kernel(
     // f32 X rows, 16-B chunk qc = 4 * (t & 1) + i of row srow
     const int xo0 = swf_off(srow, 2 * sq), xo1 = swf_off(srow, 2 * sq + 1);
     const int xo2 = swf_off(srow, 2 * sq + 2), xo3 = swf_off(srow, 2 * sq + 3);
-#define X6_STORE()                                                                          \
+// The out-of-range float4s are zeroed here, at the LDS store, not right after their loads:
+// a select next to the load makes the wave wait for the data before the chunk's MFMAs (the
+// whole fetch latency exposed once per chunk).
+#define X6_STORE(kc)                                                                        \
     {                                                                                       \
-        *reinterpret_cast<float4*>(&Xs[xo0]) = x0;                                          \
-        *reinterpret_cast<float4*>(&Xs[xo1]) = x1;                                          \
-        *reinterpret_cast<float4*>(&Xs[xo2]) = x2;                                          \
-        *reinterpret_cast<float4*>(&Xs[xo3]) = x3;                                          \
+        const int k_ = (kc) * KC + 8 * sq;                                                  \
+        *reinterpret_cast<float4*>(&Xs[xo0]) = keep4(live && k_ < D, x0);                   \
+        *reinterpret_cast<float4*>(&Xs[xo1]) = keep4(live && k_ + 4 < D, x1);               \
+        *reinterpret_cast<float4*>(&Xs[xo2]) = keep4(live && k_ + 8 < D, x2);               \
+        *reinterpret_cast<float4*>(&Xs[xo3]) = keep4(live && k_ + 12 < D, x3);              \
         *reinterpret_cast<uint4*>(&Ws[0][off0]) = w00;                                      \
         *reinterpret_cast<uint4*>(&Ws[0][off1]) = w01;                                      \
         *reinterpret_cast<uint4*>(&Ws[1][off0]) = w10;                                      \
@@ -182,7 +192,7 @@ __global__ __launch_bounds__(256, X6_OCC) void l1_fwd_x6_kernel(
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][r] = 0.0f;
     X6_LOAD(0)
-    X6_STORE()
+    X6_STORE(0)
     __syncthreads();
     for (int kc = 0; kc < nch; ++kc) {
         if (kc + 1 < nch) X6_LOAD(kc + 1)
@@ -237,7 +247,7 @@ __global__ __launch_bounds__(256, X6_OCC) void l1_fwd_x6_kernel(
         }
         if (kc + 1 < nch) {
             __syncthreads();
-            X6_STORE()
+            X6_STORE(kc + 1)
             __syncthreads();
         }
     }

@@ -4,11 +4,12 @@
 //   mu  = Linear(64,A)(tanh(Linear(64,64)(tanh(Linear(D,64)(obs)))))   (unbounded)
 //   act = eps * exp(log_std) + mu        (dist.sample() = torch.normal(mu, sigma))
 //   act_remap = scale(bound(act))         (clip / tanh to [-1,1], then to [low, high])
-// One workgroup = 32 env rows.  The first layer's K (= obs dim) is split over the 4 waves
+// One workgroup = 32 env rows.  The first layer's K (= obs dim) is split over the 8 waves
 // (f32 MFMA 32x32x2, batch rows on lanes, features on accumulator registers as in
-// mlp.hip); wave 0 folds the partials in fixed order and runs layer 2, the mu head and the
-// sampling/mapping epilogue.  The first-layer weight is pre-packed once per collect into the
-// per-lane fragment order so every weight load is a contiguous 1 KB wave access.
+// mlp.hip); layer 2 and the mu head are split over the 8 waves too (K quarters / eighths),
+// every partial folded in fixed order through LDS.  The first-layer weight is pre-packed
+// once per collect into the per-lane fragment order so every weight load is a contiguous
+// 1 KB wave access.
 #include "tsrl_common.h"
 
 namespace tsrl {
@@ -82,7 +83,8 @@ __global__ __launch_bounds__(ANW * 64) void gauss_act_kernel(
     __shared__ float sW2[H * WS], sW3[AMAX * WS];
     __shared__ float sb1[H], sb2[H], sb3[AMAX], ssig[AMAX], slo[AMAX], shi[AMAX];
     __shared__ float seps[32][AMAX + 1];
-    __shared__ float red[ANW / 2][2][16][64];
+    __shared__ float red[ANW][2][16][64];
+    __shared__ float sH[H * 32];  // h1, then h2: [feature][row]
     const int t = threadIdx.x;
     const int w = t >> 6, l = t & 63, h = l >> 5, c = l & 31;
     const int A = p.A;
@@ -190,59 +192,74 @@ __global__ __launch_bounds__(ANW * 64) void gauss_act_kernel(
     }
     // next step's noise counter into the other slot of a ping-pong pair (no atomics)
     if (rng_next && blockIdx.x == 0 && t == 0) *rng_next = rng_step + 1;
-    // fixed-order tree over the 8 waves' layer-1 partials
-#pragma unroll
-    for (int half = ANW / 2; half >= 1; half >>= 1) {
-        if (w >= half && w < 2 * half) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                red[w - half][0][r][l] = acc0[r];
-                red[w - half][1][r][l] = acc1[r];
-            }
-        }
-        __syncthreads();
-        if (w < half) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                acc0[r] += red[w][0][r][l];
-                acc1[r] += red[w][1][r][l];
-            }
-        }
-        if (half > 1) __syncthreads();
-    }
-    if (w != 0) return;
-    float h1[2][16];
+    // Every later stage is spread over all 8 waves (a serial chain of 96 dependent MFMAs in
+    // one wave cost ~8 us of the ~17 us kernel).  Register slot j of the 32x64 C tile
+    // (ot = j >> 4, r = j & 15) holds feature 32*ot + rho(r) + 4h of row c.
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-        h1[0][r] = tanh_nb(acc0[r] + sb1[rho(r) + 4 * h]);
-        h1[1][r] = tanh_nb(acc1[r] + sb1[32 + rho(r) + 4 * h]);
+        red[w][0][r][l] = acc0[r];
+        red[w][1][r][l] = acc1[r];
     }
-    float h2[2][16];
+    __syncthreads();
+    // layer-1 partials summed over the waves in fixed order; h1 -> sH[feature][row]
 #pragma unroll
-    for (int ot = 0; ot < 2; ++ot) {
-        f32x16 z = zero16();
-        const float* wa = sW2 + (32 * ot + c) * WS + 4 * h;
+    for (int q = 0; q < 4; ++q) {
+        const int j = 4 * w + q, ot = j >> 4, r = j & 15;
+        float z = red[0][ot][r][l];
 #pragma unroll
-        for (int it = 0; it < 2; ++it)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) z = mfma(wa[32 * it + rho(r)], h1[it][r], z);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) h2[ot][r] = tanh_nb(z[r] + sb2[32 * ot + rho(r) + 4 * h]);
+        for (int v = 1; v < ANW; ++v) z += red[v][ot][r][l];
+        const int f = 32 * ot + rho(r) + 4 * h;
+        sH[f * 32 + c] = tanh_nb(z + sb1[f]);
     }
-    f32x16 mu = zero16();
+    __syncthreads();
+    // layer 2: wave w -> output tile ot = w & 1 over k quarter kq = w >> 1 (16 k, 8 steps)
     {
-        const float* wa = sW3 + c * WS + 4 * h;
+        const int ot = w & 1, kq = w >> 1;
+        f32x16 z = zero16();
+        const float* wa = sW2 + (32 * ot + c) * WS + 16 * kq + h;
+        const float* hb = sH + (16 * kq + h) * 32 + c;
 #pragma unroll
-        for (int it = 0; it < 2; ++it)
+        for (int st = 0; st < 8; ++st) z = mfma(wa[2 * st], hb[64 * st], z);
+        float* rp = &red[0][0][0][0] + w * 16 * 64;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) mu = mfma(wa[32 * it + rho(r)], h2[it][r], mu);
+        for (int r = 0; r < 16; ++r) rp[r * 64 + l] = z[r];
     }
+    __syncthreads();
+    // h2 = tanh(sum of the 4 k quarters + b2) -> sH (h1 is dead)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int j = 4 * w + q, ot = j >> 4, r = j & 15;
+        const float* rp = &red[0][0][0][0] + ot * 16 * 64 + r * 64 + l;
+        float z = rp[0];
+#pragma unroll
+        for (int kq = 1; kq < 4; ++kq) z += rp[2 * kq * 16 * 64];
+        const int f = 32 * ot + rho(r) + 4 * h;
+        sH[f * 32 + c] = tanh_nb(z + sb2[f]);
+    }
+    __syncthreads();
+    // mu head: wave w -> k eighth (8 k, 4 steps); rows of sW3 beyond A are zero
+    {
+        f32x16 z = zero16();
+        const float* wa = sW3 + c * WS + 8 * w + h;
+        const float* hb = sH + (8 * w + h) * 32 + c;
+#pragma unroll
+        for (int st = 0; st < 4; ++st) z = mfma(wa[2 * st], hb[64 * st], z);
+        float* rp = &red[0][0][0][0] + w * 16 * 64;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) rp[r * 64 + l] = z[r];
+    }
+    __syncthreads();
     if (!live) return;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
+    for (int q = 0; q < 2; ++q) {
+        const int r = 2 * w + q;
         const int a = rho(r) + 4 * h;
         if (a >= A) continue;
-        const float m = mu[r] + sb3[a];
+        const float* rp = &red[0][0][0][0] + r * 64 + l;
+        float mu = rp[0];
+#pragma unroll
+        for (int v = 1; v < ANW; ++v) mu += rp[v * 16 * 64];
+        const float m = mu + sb3[a];
         float x = m;
         // randn * sigma + mu (two roundings, as torch's mul_ then add_)
         if (p.sample) x = __fadd_rn(__fmul_rn(seps[c][a], ssig[a]), m);

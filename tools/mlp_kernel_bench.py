@@ -1,7 +1,7 @@
 """Time the fused MLP kernels of one PPO minibatch at the benchmark shape (262144 rows,
 Box(376)/Box(17), 64-64 tanh nets) with HIP events, and report achieved f32 MFMA TFLOP/s.
 
-    python tools/mlp_kernel_bench.py [--rows 262144] [--D 376] [--A 17] [--iters 20]
+    python tools/mlp_kernel_bench.py [--rows 262144] [--D 376] [--A 17] [--iters 20] [--only NAME]
 """
 import argparse
 import os
@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--D", type=int, default=376)
     ap.add_argument("--A", type=int, default=17)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--only", default=None,
+                    help="time one kernel only (l1_fwd, l1_fwd_x6, tail, dw, minibatch): PMC passes")
     ap.add_argument("--contig", action="store_true",
                     help="minibatch rows contiguous (no permutation gather)")
     a = ap.parse_args()
@@ -92,6 +94,8 @@ def main():
     for name, fn, flop in (("l1_fwd", l1, flop_l1), ("l1_fwd_x6(+split)", l1x6, flop_l1),
                            ("tail(+reduce)", tail, flop_tail),
                            ("dw(+reduce)", dw, flop_l1), ("minibatch", whole, None)):
+        if a.only and not name.startswith(a.only):
+            continue
         fn()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
