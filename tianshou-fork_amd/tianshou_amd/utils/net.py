@@ -53,6 +53,16 @@ class _LinearFn(torch.autograd.Function):
     def backward(ctx, gy):
         x, weight = ctx.saved_tensors
         gx = gw = gb = None
+        if torch.is_grad_enabled():
+            # backward of a create_graph pass (NPG/TRPO's KL Hessian-vector products): only
+            # differentiable torch ops, so the double backward sees the whole graph
+            if ctx.needs_input_grad[0]:
+                gx = gy @ weight
+            if ctx.needs_input_grad[1]:
+                gw = gy.t() @ x
+            if ctx.has_bias and ctx.needs_input_grad[2]:
+                gb = gy.sum(0)
+            return gx, gw, gb
         if ctx.needs_input_grad[0]:
             gx = gy @ weight
         if ctx.needs_input_grad[1]:

@@ -576,12 +576,69 @@ def gen_stack():
     _save("stack.npz", **out)
 
 
+# --------------------------------------------------------------------------------------
+# 9. NPG / TRPO: npg.py:68-79 process_fn (A2C returns + logp_old +
+#    whole-batch adv normalisation) and npg.py:81-130 / trpo.py:74-160 learn (CG on the KL
+#    Hessian, natural step or KL-bounded line search, critic iterations) on the collector
+#    rollout of gen_collector's env; critic-only Adam as in examples/mujoco/mujoco_npg.py.
+# --------------------------------------------------------------------------------------
+NPG_CASES = [
+    # tag, class name, kwargs
+    ("npg", "NPGPolicy", dict(actor_step_size=0.1)),
+    ("trpo", "TRPOPolicy", dict(max_kl=0.01)),
+    ("trpo_nonorm", "TRPOPolicy", dict(max_kl=0.005, advantage_normalization=False,
+                                       reward_normalization=False, optim_critic_iters=3)),
+]
+
+
+def gen_npg():
+    import warnings
+    from tianshou import policy as tpol
+    from tianshou.utils.models import init_actor_critic
+    E, D, A, L, T = 8, 5, 2, 7, 20
+    out = dict(E=np.array(E), D=np.array(D), A=np.array(A), L=np.array(L), T=np.array(T))
+    for tag, cls_name, kw in NPG_CASES:
+        p = tag + "_"
+        venv = VectorEnvNormObs(DummyVectorEnv(
+            [lambda e=e: SynthGymEnv(e, D, A, L) for e in range(E)]))
+        torch.manual_seed(3)
+        actor, critic = get_actor_critic((D,), (64, 64), (A,), "cpu")
+        init_actor_critic(actor, critic)
+        optim = torch.optim.Adam(critic.parameters(), lr=1e-3)
+        args = dict(discount_factor=0.99, gae_lambda=0.95, reward_normalization=True,
+                    advantage_normalization=True, optim_critic_iters=5,
+                    action_bound_method="clip", action_scaling=True)
+        args.update(kw)
+        policy = getattr(tpol, cls_name)(actor, critic, optim, dist_fn=fixed_std_normal,
+                                         action_space=gym.spaces.Box(-1.0, 1.0, (A,)), **args)
+        out.update(_sd_arrays(p + "init_", policy))
+        buf = VectorReplayBuffer(E * T, E)
+        torch.manual_seed(0)
+        np.random.seed(0)
+        Collector(policy, venv, buf).collect(n_step=E * T)
+        out.update(_buf_arrays(p + "buf_", buf))
+        batch, idx = buf.sample(0)
+        out[p + "indices"] = idx
+        batch = policy.process_fn(batch, buf, idx)
+        for k in ("v_s", "returns", "adv", "logp_old"):
+            out[p + "pf_" + k] = batch[k].detach().numpy()
+        np.random.seed(5)
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            res = policy.learn(batch, batch_size=E * T // 4, repeat=2)
+        for k, v in res.items():
+            out[p + "learn_" + k.replace("/", "_")] = np.array(v)
+        out.update(_sd_arrays(p + "final_", policy))
+        out[p + "cfg"] = np.array(json.dumps(dict(cls=cls_name, **kw)))
+    _save("npg.npz", **out)
+
+
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     which = sys.argv[1:] or ["returns", "gae", "buffer", "split", "rms", "ppo", "collector",
-                             "stack", "ppo_discrete"]
+                             "stack", "ppo_discrete", "npg"]
     table = dict(returns=gen_returns_known, gae=gen_gae_random, buffer=gen_buffer_traces,
                  split=gen_split, rms=gen_rms, ppo=gen_ppo, collector=gen_collector,
-                 stack=gen_stack, ppo_discrete=gen_ppo_discrete)
+                 stack=gen_stack, ppo_discrete=gen_ppo_discrete, npg=gen_npg)
     for w in which:
         table[w]()
