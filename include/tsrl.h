@@ -376,6 +376,35 @@ int tsrl_gauss_policy_act_rng(const float* obs, int64_t ldx, int64_t n, int64_t 
                               const float* low, const float* high, float* act,
                               float* act_remap, void* stream);
 
+/* ---------------------------------------------------------------------------------
+ * Off-policy neighbours.
+ * tsrl_nstep_return: BasePolicy.compute_nstep_return + _nstep_return (policy/base.py:386-440,
+ *   500-524) over a VectorReplayBuffer ring (done / last_index / lengths as for
+ *   tsrl_ring_step_index): for every sampled row idx[b] the next() chain of n_step rows,
+ *   episode ends = done or the unfinished last row, out[b][x] = target_q[b][x] *
+ *   !terminated[chain[n_step-1]] * gamma^gammas + G_b in f64 (reference operation order),
+ *   rounded to the target dtype (f64 != 0: double target_q/out, else float).
+ *   1 <= n_step <= 64; target_q holds Q_target(s_{t+n}) at the chain's last row.
+ * Sum tree of SegmentTree (data/utils/segtree.py:7-137): tree = f64[2*bound], bound a power of
+ *   two, leaves at [bound, bound + size).
+ * tsrl_segtree_set: _setitem (:98-104): tree[bound + idx[j]] = values[j * value_stride]
+ *   (value_stride 0 broadcasts values[0]; duplicate indices: the last occurrence wins), then
+ *   every ancestor = left + right.  win: int32 workspace of size entries, all -1 (restored).
+ * tsrl_segtree_reduce: _reduce (:107-119) over leaves [start, end) -> *out (device f64).
+ * tsrl_segtree_prefix_idx: _get_prefix_sum_idx (:122-137) for k query values (f64 or f32).
+ * ------------------------------------------------------------------------------- */
+int tsrl_nstep_return(const double* rew, const uint8_t* done, const uint8_t* terminated,
+                      const int64_t* last_index, const int64_t* lengths, int64_t size,
+                      int64_t num, const int64_t* idx, int64_t bsz, int64_t n_step,
+                      double gamma, const void* target_q, int64_t X, int f64, void* out,
+                      void* stream);
+int tsrl_segtree_set(double* tree, int64_t bound, const int64_t* idx, const double* values,
+                     int64_t value_stride, int64_t k, int* win, void* stream);
+int tsrl_segtree_reduce(const double* tree, int64_t bound, int64_t start, int64_t end,
+                        double* out, void* stream);
+int tsrl_segtree_prefix_idx(const double* tree, int64_t bound, const void* values, int f64,
+                            int64_t k, int64_t* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -322,3 +322,80 @@ def ppo_categorical_loss_torch(x, value, act, logp_old, adv, returns, v_s, mode,
     loss.backward()
     return (loss.detach(), clip_loss.detach(), vf_loss.detach(), ent_loss.detach(),
             dict(x=x.grad, value=value.grad))
+
+
+def nstep_return(vb, terminated, indices, target_q, gamma, n_step):
+    """compute_nstep_return + _nstep_return (policy/base.py:417-440, 500-524) over a
+    VecBufferIndex ``vb`` (done / rew / ring state) and the per-row terminated flags; target_q
+    is Q_target at the terminal rows, [bsz] or [bsz, X].  Returns (returns [bsz, X] in the
+    target dtype, terminal indices)."""
+    indices = np.asarray(indices, np.int64)
+    bsz = len(indices)
+    chain = [indices % vb.maxsize]
+    for _ in range(n_step - 1):
+        chain.append(vb.next(chain[-1]))
+    chain = np.stack(chain)
+    terminal = chain[-1]
+    tq = np.asarray(target_q).reshape(bsz, -1)
+    out_dtype = tq.dtype
+    tq = tq * (~np.asarray(terminated, bool)[terminal]).reshape(-1, 1)
+    end_flag = vb.done.copy()
+    end_flag[vb.unfinished_index()] = True
+    gamma_buffer = np.ones(n_step + 1)
+    for i in range(1, n_step + 1):
+        gamma_buffer[i] = gamma_buffer[i - 1] * gamma
+    returns = np.zeros(tq.shape)
+    gammas = np.full(bsz, n_step)
+    for n in range(n_step - 1, -1, -1):
+        now = chain[n]
+        gammas[end_flag[now] > 0] = n + 1
+        returns[end_flag[now] > 0] = 0.0
+        returns = vb.rew[now].reshape(bsz, 1) + gamma * returns
+    return (tq * gamma_buffer[gammas].reshape(bsz, 1) + returns).astype(out_dtype), terminal
+
+
+class SegTree:
+    """SegmentTree (data/utils/segtree.py:7-137): f64 binary-heap sum tree."""
+
+    def __init__(self, size):
+        bound = 1
+        while bound < size:
+            bound *= 2
+        self.size, self.bound = size, bound
+        self.value = np.zeros(2 * bound)
+
+    def set(self, index, value):                                # :98-104
+        index = np.asarray(index, np.int64) + self.bound
+        self.value[index] = value
+        while index[0] > 1:
+            index = index // 2
+            self.value[index] = self.value[index * 2] + self.value[index * 2 + 1]
+
+    def reduce(self, start=0, end=None):                        # :56-64, 107-119
+        if start == 0 and end is None:
+            return self.value[1]
+        if end is None:
+            end = self.size
+        if end < 0:
+            end += self.size
+        start, end = start + self.bound - 1, end + self.bound
+        result = 0.0
+        while end - start > 1:
+            if start % 2 == 0:
+                result += self.value[start + 1]
+            start //= 2
+            if end % 2 == 1:
+                result += self.value[end - 1]
+            end //= 2
+        return result
+
+    def prefix_idx(self, value):                                # :122-137
+        value = np.array(value, copy=True)
+        index = np.ones(value.shape, dtype=np.int64)
+        while index[0] < self.bound:
+            index *= 2
+            lsons = self.value[index]
+            direct = lsons < value
+            value -= lsons * direct
+            index += direct
+        return index - self.bound

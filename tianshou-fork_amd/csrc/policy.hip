@@ -262,14 +262,14 @@ __global__ __launch_bounds__(ANW * 64) void gauss_act_kernel(
         const float m = mu + sb3[a];
         float x = m;
         // randn * sigma + mu (two roundings, as torch's mul_ then add_)
-        if (p.sample) x = __fadd_rn(__fmul_rn(seps[c][a], ssig[a]), m);
+        if (p.sample) x = seps[c][a] * ssig[a] + m;  // contract(off): two roundings
         act[row * A + a] = x;
         float y = x;
         if (p.bound == 1) y = y < -1.0f ? -1.0f : (y > 1.0f ? 1.0f : y);  // clamp, NaN passes
         else if (p.bound == 2) y = tanh_nb(y);
         if (p.scale) {
             const float lo = slo[a], hi = shi[a];
-            y = __fadd_rn(lo, __fdiv_rn(__fmul_rn(__fsub_rn(hi, lo), __fadd_rn(y, 1.0f)), 2.0f));
+            y = lo + (hi - lo) * (y + 1.0f) / 2.0f;
         }
         act_remap[row * A + a] = y;
     }

@@ -1,11 +1,7 @@
 // Episode-aware index stepping and frame-stack gathers of the VectorReplayBuffer.
 //
 // ring_step : ReplayBufferManager prev/next (tianshou/data/buffer/manager.py:259-297, the
-//             numba _prev_index/_next_index).  Sub-buffer b owns storage rows
-//             [b*size, (b+1)*size) (vecbuf.py:33-37: equal sub-buffers), holds lengths[b]
-//             rows and last wrote last_index[b]; a row whose done flag is set, or the last
-//             written row, ends an episode, so prev() does not step back across it and next()
-//             does not step forward across it.
+//             numba _prev_index/_next_index; the ring arithmetic is in ring.h).
 // stack     : ReplayBuffer.get(index, key, stack_num) (base.py:317-358): frame s of output row
 //             r is the storage row prev^(stack_num-1-s)(idx[r]); with save_only_last_obs
 //             (manager.py:127-132) the storage holds one frame per row and this rebuilds the
@@ -13,47 +9,13 @@
 //             per (row, frame): the wave walks its prev chain (a few done[] reads that hit
 //             L2) and copies the frame with 16-byte loads; the chain indices can be written
 //             out for the keys that are stacked with torch gathers (info / policy).
-#include "tsrl_common.h"
+#include "ring.h"
 
 namespace tsrl {
 namespace {
 
 constexpr int TPB = 256;
 constexpr int WPB = TPB / kWave;
-
-struct Ring {
-    const uint8_t* done;
-    const int64_t* last_index;
-    const int64_t* lengths;
-    int64_t size;     // rows per sub-buffer
-    int64_t maxsize;  // size * num
-};
-
-__device__ __forceinline__ int64_t pmod(int64_t a, int64_t m) {
-    const int64_t r = a % m;
-    return r < 0 ? r + m : r;
-}
-
-// manager.py:259-277
-__device__ __forceinline__ int64_t ring_prev(const Ring& g, int64_t i) {
-    i = pmod(i, g.maxsize);
-    const int64_t b = i / g.size;
-    const int64_t start = b * g.size;
-    const int64_t cur = max(g.lengths[b], (int64_t)1);
-    const int64_t sub = pmod(i - start - 1, cur);
-    const int64_t end = (g.done[sub + start] != 0) | (sub + start == g.last_index[b]);
-    return pmod(sub + end, cur) + start;
-}
-
-// manager.py:280-297
-__device__ __forceinline__ int64_t ring_next(const Ring& g, int64_t i) {
-    i = pmod(i, g.maxsize);
-    const int64_t b = i / g.size;
-    const int64_t start = b * g.size;
-    const int64_t cur = max(g.lengths[b], (int64_t)1);
-    const int64_t end = (g.done[i] != 0) | (i == g.last_index[b]);
-    return pmod(i - start + 1 - end, cur) + start;
-}
 
 __global__ __launch_bounds__(TPB) void ring_step_kernel(Ring g, const int64_t* idx, int64_t k,
                                                         int steps, int64_t* out) {

@@ -49,6 +49,10 @@ class Collector:
         self._fused = isinstance(self._base, DeviceVectorEnv) and preprocess_fn is None
         self.device = getattr(self._base, "device", None)
         self._assign_buffer(buffer)
+        if getattr(self.buffer, "_prioritized", False):
+            # prioritized buffers initialise a priority per added row (prio.py:50-57): the
+            # generic path's buffer.add does that; the fused step writes rows directly
+            self._fused = False
         self._scratch = None
         # vector steps per captured HIP graph (0 disables graph replay of the fused step)
         self.graph_steps = 64

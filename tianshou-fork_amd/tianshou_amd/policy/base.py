@@ -231,3 +231,38 @@ class BasePolicy(nn.Module):
         if numpy_out:
             return ret.cpu().numpy(), adv.cpu().numpy()
         return ret, adv
+
+    @staticmethod
+    def compute_nstep_return(batch: Batch, buffer, indice: np.ndarray, target_q_fn,
+                             gamma: float = 0.99, n_step: int = 1, rew_norm: bool = False
+                             ) -> Batch:
+        """base.py:386-440 with _nstep_return (base.py:500-524) as tsrl_nstep_return: the
+        terminal rows next^(n_step-1)(indice) come from tsrl_ring_step_index on device (one
+        host copy for ``target_q_fn``, which takes NumPy indices as in the reference); the
+        discounted n-step sum, the episode-end truncation, the value mask and the
+        gamma^k bootstrap run in one kernel in the reference's f64 operation order."""
+        assert not rew_norm, \
+            "Reward normalization in computing n-step returns is unsupported now."
+        bsz = len(indice)
+        dev = buffer._ensure_device()
+        it = buffer._index_tensor(indice)
+        terminal = buffer._step_dev(it, -(n_step - 1)) if n_step > 1 else \
+            buffer._step_dev(it, 0)
+        with torch.no_grad():
+            target_q_torch = target_q_fn(buffer, terminal.cpu().numpy())  # (bsz, ?)
+        tq = target_q_torch.reshape(bsz, -1)
+        f64 = tq.dtype == torch.float64
+        tq_dev = tq.to(device=dev, dtype=torch.float64 if f64 else torch.float32).contiguous()
+        out = torch.empty_like(tq_dev)
+        m = buffer._meta
+        done, last, lengths = buffer._ring_dev()
+        _C.check(_C.lib().tsrl_nstep_return(
+            _C.ptr(m.rew), _C.ptr(done), _C.ptr(m.terminated), _C.ptr(last), _C.ptr(lengths),
+            buffer._ring.size, buffer.buffer_num, _C.ptr(it), bsz, int(n_step), float(gamma),
+            _C.ptr(tq_dev), tq_dev.shape[1] if bsz else 1, int(f64), _C.ptr(out),
+            _C.stream_ptr(dev)), "tsrl_nstep_return")
+        batch.returns = out.to(device=target_q_torch.device, dtype=target_q_torch.dtype)
+        if hasattr(batch, "weight"):  # prio buffer update
+            batch.weight = torch.as_tensor(batch.weight).to(device=target_q_torch.device,
+                                                            dtype=target_q_torch.dtype)
+        return batch

@@ -633,12 +633,155 @@ def gen_npg():
     _save("npg.npz", **out)
 
 
+# --------------------------------------------------------------------------------------
+# 10. Off-policy neighbours: SegmentTree (data/utils/segtree.py:
+#     7-137), compute_nstep_return / _nstep_return (policy/base.py:386-440, 500-524) and the
+#     prioritized buffers (buffer/prio.py:9-105, manager.py:195-214).
+# --------------------------------------------------------------------------------------
+SEG_SIZES = (1, 8, 10, 1000, 16384)
+
+
+def _table_q_fn(table):
+    def fn(buffer, indices):
+        return torch.as_tensor(table[np.asarray(indices)])
+    return fn
+
+
+def _next_rew_q_fn(buffer, indices):  # test/base/test_returns.py:137-140
+    indices = buffer.next(indices)
+    return torch.tensor(-buffer.rew[indices], dtype=torch.float32)
+
+
+def gen_replay():
+    from tianshou.data import (PrioritizedReplayBuffer, PrioritizedVectorReplayBuffer,
+                               SegmentTree)
+    out = {}
+    rng = np.random.default_rng(7)
+    # (a) sum tree: batch updates with duplicate indices, reduce over ranges, prefix queries
+    for size in SEG_SIZES:
+        p = f"seg{size}_"
+        tree = SegmentTree(size)
+        lens, idxs, vals = [], [], []
+        for u in range(12):
+            k = int(rng.integers(1, 2 * size + 2)) if size < 64 else int(rng.integers(1, 300))
+            idx = rng.integers(0, size, k)
+            val = rng.random(k) * (1e-3 if u % 4 == 3 else 1.0)
+            tree[idx] = val
+            lens.append(k)
+            idxs.append(idx)
+            vals.append(val)
+        out[p + "upd_len"] = np.array(lens)
+        out[p + "upd_idx"] = np.concatenate(idxs).astype(np.int64)
+        out[p + "upd_val"] = np.concatenate(vals)
+        out[p + "tree"] = tree._value.copy()
+        st = rng.integers(0, size, 40)
+        en = np.array([rng.integers(s + 1, size + 1) for s in st])
+        out[p + "red_start"], out[p + "red_end"] = st, en
+        out[p + "red"] = np.array([tree.reduce(int(a), int(b)) for a, b in zip(st, en)])
+        out[p + "root"] = np.array(tree.reduce())
+        total = tree.reduce()
+        q64 = rng.random(300) * total
+        q32 = (rng.random(300) * total).astype(np.float32)
+        q32 = q32[q32 < total]
+        out[p + "q64"], out[p + "i64"] = q64, tree.get_prefix_sum_idx(q64.copy())
+        out[p + "q32"], out[p + "i32"] = q32, tree.get_prefix_sum_idx(q32.copy())
+    tree = SegmentTree(10)  # test_buffer.py:561-565
+    tree[np.arange(3)] = np.array([0.1, 0, 0.1])
+    out["seg_corner_i"] = tree.get_prefix_sum_idx(np.array([0, .1, .1 + 1e-6, .2 - 1e-6]))
+    # (b) n-step returns on the reference's own test buffers (test_returns.py:170-296) ...
+    for tl in (0, 1):
+        buf = ReplayBuffer(10)
+        for i in range(12):
+            if tl:
+                buf.add(Batch(obs=0, act=0, rew=i + 1, terminated=i % 4 == 3 and i != 3,
+                              truncated=i == 3, info={"TimeLimit.truncated": i == 3}))
+            else:
+                buf.add(Batch(obs=0, act=0, rew=i + 1, terminated=i % 4 == 3,
+                              truncated=False))
+        batch, indices = buf.sample(0)
+        out[f"ns_tl{tl}_indices"] = indices
+        for n in (1, 2, 10):
+            r = BasePolicy.compute_nstep_return(batch, buf, indices, _next_rew_q_fn, gamma=.1,
+                                                n_step=n)
+            out[f"ns_tl{tl}_n{n}"] = r.pop("returns").numpy()
+    # ... and on a ragged VectorReplayBuffer (random flags, table-valued targets, f32 and f64)
+    E, S = 6, 40
+    vb = VectorReplayBuffer(E * S, E)
+    lens, ids_l, rew_l, term_l, trunc_l = [], [], [], [], []
+    for t in range(130):
+        ids = np.sort(rng.choice(E, size=int(rng.integers(1, E + 1)), replace=False))
+        k = len(ids)
+        rew, term, trunc = rng.random(k), rng.random(k) < 0.06, rng.random(k) < 0.04
+        vb.add(Batch(obs=np.zeros((k, 2), np.float32), act=np.zeros(k, np.int64), rew=rew,
+                     terminated=term, truncated=trunc, obs_next=np.zeros((k, 2), np.float32),
+                     info={}), buffer_ids=ids)
+        lens.append(k)
+        ids_l.append(ids)
+        rew_l.append(rew)
+        term_l.append(term)
+        trunc_l.append(trunc)
+    out["nsv_add_len"] = np.array(lens)
+    out["nsv_add_ids"] = np.concatenate(ids_l).astype(np.int64)
+    out["nsv_add_rew"] = np.concatenate(rew_l)
+    out["nsv_add_term"] = np.concatenate(term_l)
+    out["nsv_add_trunc"] = np.concatenate(trunc_l)
+    out["nsv_lengths"] = np.asarray(vb._lengths).copy()
+    out["nsv_last_index"] = np.asarray(vb.last_index).copy()
+    np.random.seed(3)
+    idx = np.concatenate([vb.sample_indices(200), vb.unfinished_index(),
+                          vb.sample_indices(0)[:30]]).astype(np.int64)
+    out["nsv_indices"] = idx
+    table = rng.standard_normal((vb.maxsize, 3)).astype(np.float32)
+    table64 = rng.standard_normal((vb.maxsize, 2))
+    out["nsv_table"], out["nsv_table64"] = table, table64
+    for n in (1, 3, 5, 12):
+        for tag, tab in (("x1", table[:, 0].copy()), ("x3", table), ("f64", table64)):
+            r = BasePolicy.compute_nstep_return(Batch(), vb, idx, _table_q_fn(tab), gamma=0.97,
+                                                n_step=n)
+            out[f"nsv_n{n}_{tag}"] = r.returns.numpy()
+    # (c) prioritized buffers: adds, sample(16) -> weights -> update_weight(f32 TD errors)
+    for alpha in (1.0, 0.6):
+        for kind in ("vec", "single"):
+            p = f"per_{kind}_a{int(alpha * 10)}_"
+            pb = PrioritizedVectorReplayBuffer(60, buffer_num=3, alpha=alpha, beta=0.4) \
+                if kind == "vec" else PrioritizedReplayBuffer(20, alpha=alpha, beta=0.4)
+            nenv = 3 if kind == "vec" else 1
+            obs_l, rew_l, term_l = [], [], []
+            for t in range(27):
+                obs = rng.random((nenv, 2)).astype(np.float32)
+                rew = rng.random(nenv)
+                term = rng.random(nenv) < 0.1
+                pb.add(Batch(obs=obs, act=np.zeros(nenv, np.int64), rew=rew, terminated=term,
+                             truncated=np.zeros(nenv, bool), obs_next=obs, info={}),
+                       buffer_ids=list(range(nenv)))
+                obs_l.append(obs)
+                rew_l.append(rew)
+                term_l.append(term)
+            out[p + "obs"], out[p + "rew"] = np.stack(obs_l), np.stack(rew_l)
+            out[p + "term"] = np.stack(term_l)
+            out[p + "tree0"] = pb.weight._value.copy()
+            np.random.seed(12)
+            sidx, sw, tds, trees = [], [], [], []
+            for rnd in range(6):
+                batch, sidx_r = pb.sample(16)
+                td = torch.as_tensor(rng.standard_normal(16).astype(np.float32))
+                pb.update_weight(sidx_r, td)
+                sidx.append(sidx_r)
+                sw.append(np.asarray(batch.weight))
+                tds.append(td.numpy())
+                trees.append(pb.weight._value.copy())
+            out[p + "sidx"], out[p + "sw"] = np.stack(sidx), np.stack(sw)
+            out[p + "td"], out[p + "trees"] = np.stack(tds), np.stack(trees)
+            out[p + "prio"] = np.array([float(pb._max_prio), float(pb._min_prio)])
+    _save("replay.npz", **out)
+
+
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     which = sys.argv[1:] or ["returns", "gae", "buffer", "split", "rms", "ppo", "collector",
-                             "stack", "ppo_discrete", "npg"]
+                             "stack", "ppo_discrete", "npg", "replay"]
     table = dict(returns=gen_returns_known, gae=gen_gae_random, buffer=gen_buffer_traces,
                  split=gen_split, rms=gen_rms, ppo=gen_ppo, collector=gen_collector,
-                 stack=gen_stack, ppo_discrete=gen_ppo_discrete, npg=gen_npg)
+                 stack=gen_stack, ppo_discrete=gen_ppo_discrete, npg=gen_npg, replay=gen_replay)
     for w in which:
         table[w]()
