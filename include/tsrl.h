@@ -405,6 +405,18 @@ int tsrl_segtree_reduce(const double* tree, int64_t bound, int64_t start, int64_
 int tsrl_segtree_prefix_idx(const double* tree, int64_t bound, const void* values, int f64,
                             int64_t k, int64_t* out, void* stream);
 
+/* torch.nn.utils.clip_grad_norm_(max_norm) + torch.optim.Adam.step() (ppo.py:143-151) over
+ * flat f32 parameter / gradient / moment buffers of n elements: partials (f64,
+ * tsrl_clip_adam_partials(n) entries) receive slice norms, norm_out[0] = gradient norm,
+ * norm_out[1] = clip coefficient (max_norm <= 0: no clipping, partials / norm_out may be
+ * NULL); the gradient is left scaled in place; step[0..nstep) (device f32 step counters, all
+ * equal) is advanced by one.  ticket: one device uint32, zero-initialised, kept zero. */
+int64_t tsrl_clip_adam_partials(int64_t n);
+int tsrl_clip_adam(float* param, float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                   float* step, int64_t nstep, float lr, float beta1, float beta2, float eps,
+                   float max_norm, double* partials, float* norm_out, unsigned int* ticket,
+                   void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,57 @@
+"""tsrl_clip_adam (csrc/optim.hip) vs torch.nn.utils.clip_grad_norm_ + torch.optim.Adam on
+the get_actor_critic parameters: 6 steps of random gradients (some clipped, some not), flat
+storage bound through FusedActorCritic.bind_adam.  Tolerance rtol 1e-5 / atol 1e-7 (the
+norm is summed in f64 here, in f32 partial norms by torch)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("max_norm", [0.5, None, 1e3])
+def test_clip_adam_matches_torch(max_norm):
+    from tianshou_amd.policy import fused_mlp
+    from tianshou_amd.utils.models import get_actor_critic, init_actor_critic
+    from tianshou_amd.utils.net import ActorCritic
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    nets = []
+    for _ in range(2):
+        a, c = get_actor_critic((24,), (64, 64), (5,), dev)
+        a, c = a.to(dev), c.to(dev)
+        nets.append((a, c))
+    init_actor_critic(*nets[0])
+    ac0, ac1 = ActorCritic(*nets[0]), ActorCritic(*nets[1])
+    ac1.load_state_dict(ac0.state_dict())
+    opt_ref = torch.optim.Adam(ac0.parameters(), lr=3e-4)
+    opt = torch.optim.Adam(ac1.parameters(), lr=3e-4)
+    fm = fused_mlp.FusedActorCritic(fused_mlp.match(*nets[1]), ac1.parameters())
+    assert fm.bind_adam(opt) and fm.adam_bound(opt)
+    g = torch.Generator(device=dev).manual_seed(1)
+    for step in range(6):
+        scale = 10.0 ** (step % 3 - 1)
+        grads = [torch.randn(p.shape, device=dev, generator=g) * scale for p in ac0.parameters()]
+        for p, gr in zip(ac0.parameters(), grads):
+            p.grad = gr.clone()
+        if max_norm:
+            torch.nn.utils.clip_grad_norm_(ac0.parameters(), max_norm=max_norm)
+        opt_ref.step()
+        fm.bind_grads()
+        for p, gr in zip(ac1.parameters(), grads):
+            p.grad.copy_(gr)
+        fm.clip_adam(max_norm)
+        torch.cuda.synchronize()
+        for (n0, p0), p1 in zip(ac0.named_parameters(), ac1.parameters()):
+            np.testing.assert_allclose(p1.detach().cpu().numpy(), p0.detach().cpu().numpy(),
+                                       rtol=1e-5, atol=1e-7, err_msg=f"step {step} {n0}")
+            np.testing.assert_allclose(p1.grad.cpu().numpy(), p0.grad.cpu().numpy(), rtol=1e-5,
+                                       atol=1e-9, err_msg=f"grad step {step} {n0}")
+    for p0, p1 in zip(ac0.parameters(), ac1.parameters()):
+        s0, s1 = opt_ref.state[p0], opt.state[p1]
+        assert float(s1["step"]) == float(s0["step"]) == 6.0
+        np.testing.assert_allclose(s1["exp_avg_sq"].cpu().numpy(), s0["exp_avg_sq"].cpu().numpy(),
+                                   rtol=5e-5, atol=1e-12)
+    # the state dict round-trips through torch
+    sd = opt.state_dict()
+    assert len(sd["state"]) == len(list(ac1.parameters()))

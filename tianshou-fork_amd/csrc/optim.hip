@@ -1,0 +1,154 @@
+// torch.nn.utils.clip_grad_norm_ + torch.optim.Adam.step of the fused PPO minibatch
+// (tianshou/policy/modelfree/ppo.py:143-151) as ONE launch over flat f32 storage: the fused
+// MLP keeps every parameter, gradient and Adam moment of the actor-critic in flat buffers
+// (policy/fused_mlp.py bind_adam), so torch's per-tensor foreach norm, scale and fused Adam
+// kernels (~50-60 us per minibatch, launch- and latency-bound on 57 763 parameters) become
+// three short launches: per-slice squared norms, Adam over 2048-element slices, and the
+// in-place gradient scaling.
+//
+//   norm  = ||g||_2 (f64 sum of squares), coef = max_norm / (norm + 1e-6) clamped at 1,
+//   g    *= coef                                   (clip_grad_norm_, torch/nn/utils/clip_grad.py)
+//   t    += 1
+//   m     = beta1 m + (1 - beta1) g,  v = beta2 v + (1 - beta2) g^2
+//   p    -= lr / (1 - beta1^t) * m / (sqrt(v) / sqrt(1 - beta2^t) + eps)
+// (torch's fused Adam formula, amsgrad / weight_decay / maximize off).  The step counter
+// lives on device, so HIP-graph replays of whole epochs advance it.
+#include "tsrl_common.h"
+
+namespace tsrl {
+namespace {
+
+constexpr int OTPB = 256;
+constexpr int OCHUNK = 2048;  // elements updated per workgroup
+
+struct AdamArgs {
+    float lr, beta1, beta2, eps, max_norm;
+};
+
+// Sum of squares of each 2048-element gradient slice (f64), one workgroup per slice.
+__global__ __launch_bounds__(OTPB) void norm_partials_kernel(const float* __restrict__ g,
+                                                             int64_t n, double* partials) {
+    __shared__ double red[OTPB / kWave];
+    const int t = threadIdx.x;
+    const int64_t i0 = (int64_t)blockIdx.x * OCHUNK;
+    double ss = 0.0;
+#pragma unroll
+    for (int q = 0; q < OCHUNK / OTPB; ++q) {  // independent loads, all in flight together
+        const int64_t i = i0 + q * OTPB + t;
+        const double x = i < n ? (double)g[i] : 0.0;
+        ss += x * x;
+    }
+    ss = wave_sum(ss);
+    if ((t & (kWave - 1)) == 0) red[t / kWave] = ss;
+    __syncthreads();
+    if (t == 0) {
+        double tot = 0.0;
+        for (int w = 0; w < OTPB / kWave; ++w) tot += red[w];
+        partials[blockIdx.x] = tot;
+    }
+}
+
+// Each workgroup updates its own 2048-element slice with the clip coefficient of the
+// partial norms; the last workgroup to finish (agent-scope ticket, as rms.hip) advances the
+// device step counter.
+__global__ __launch_bounds__(OTPB) void clip_adam_kernel(float* __restrict__ p,
+                                                         float* __restrict__ g,
+                                                         float* __restrict__ m,
+                                                         float* __restrict__ v, int64_t n,
+                                                         float* __restrict__ step, int64_t nstep,
+                                                         AdamArgs a, const double* __restrict__ partials,
+                                                         float* __restrict__ norm_out,
+                                                         unsigned int* ticket) {
+    __shared__ float s_scale;
+    const int t = threadIdx.x;
+    const bool clip = a.max_norm > 0.0f;
+    const float st = step[0] + 1.0f;
+    if (clip) {
+        // the per-slice sums of squares of norm_partials_kernel, folded by wave 0 in the same
+        // fixed order in every workgroup (so every workgroup gets the identical coefficient)
+        if (t < kWave) {
+            double ss = 0.0;
+            for (int64_t b = t; b < gridDim.x; b += kWave) ss += partials[b];
+            ss = wave_sum(ss);
+            if (t == 0) {
+                const float norm = (float)sqrt(ss);
+                s_scale = fminf(a.max_norm / (norm + 1e-6f), 1.0f);
+                if (blockIdx.x == 0) {
+                    norm_out[0] = norm;
+                    norm_out[1] = s_scale;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    const float scale = clip ? s_scale : 1.0f;
+    const float bc1 = 1.0f - powf(a.beta1, st);
+    const float bc2_sqrt = sqrtf(1.0f - powf(a.beta2, st));
+    const float step_size = a.lr / bc1;
+    const int64_t i0 = (int64_t)blockIdx.x * OCHUNK;
+    const int64_t i1 = min(n, i0 + OCHUNK);
+    // g is only read here (other workgroups are still summing it); the clipped gradient is
+    // written back by clip_scale_kernel, the next launch on the stream
+    for (int64_t i = i0 + t; i < i1; i += OTPB) {
+        const float gi = g[i] * scale;
+        const float mi = a.beta1 * m[i] + (1.0f - a.beta1) * gi;
+        const float vi = a.beta2 * v[i] + (1.0f - a.beta2) * gi * gi;
+        m[i] = mi;
+        v[i] = vi;
+        p[i] -= step_size * mi / (sqrtf(vi) / bc2_sqrt + a.eps);
+    }
+    if (t == 0) {
+        const unsigned int done = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL,
+                                                         __HIP_MEMORY_SCOPE_AGENT);
+        if (done == gridDim.x - 1) {  // every workgroup has read step[0] and the gradients
+            for (int64_t i = 0; i < nstep; ++i) step[i] = st;
+            __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+// clip_grad_norm_'s in-place scaling of the gradients (what p.grad holds after the step)
+__global__ __launch_bounds__(OTPB) void clip_scale_kernel(float* __restrict__ g, int64_t n,
+                                                          const float* __restrict__ norm_scale) {
+    const float s = norm_scale[1];
+    for (int64_t i = (int64_t)blockIdx.x * OTPB + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * OTPB)
+        g[i] *= s;
+}
+
+}  // namespace
+}  // namespace tsrl
+
+using namespace tsrl;
+
+extern "C" int64_t tsrl_clip_adam_partials(int64_t n) { return (n + OCHUNK - 1) / OCHUNK; }
+
+extern "C" int tsrl_clip_adam(float* param, float* grad, float* exp_avg, float* exp_avg_sq,
+                              int64_t n, float* step, int64_t nstep, float lr, float beta1,
+                              float beta2, float eps, float max_norm, double* partials,
+                              float* norm_out, unsigned int* ticket, void* stream) {
+    TSRL_CHECK_ARG(n >= 0 && nstep >= 1, "tsrl_clip_adam: bad sizes");
+    if (n == 0) return 0;
+    TSRL_CHECK_ARG(param && grad && exp_avg && exp_avg_sq && step && ticket,
+                   "tsrl_clip_adam: null pointer");
+    const int64_t grid = (n + OCHUNK - 1) / OCHUNK;
+    TSRL_CHECK_ARG(max_norm <= 0.0f || (norm_out && partials),
+                   "tsrl_clip_adam: clipping needs partials and norm_out[2]");
+    if (max_norm > 0.0f) {
+        hipLaunchKernelGGL(norm_partials_kernel, dim3((unsigned)grid), dim3(OTPB), 0,
+                           as_stream(stream), grad, n, partials);
+        TSRL_LAUNCH_CHECK("tsrl_clip_adam (norm)");
+    }
+    const AdamArgs a{lr, beta1, beta2, eps, max_norm};
+    hipLaunchKernelGGL(clip_adam_kernel, dim3((unsigned)grid), dim3(OTPB), 0,
+                       as_stream(stream), param, grad, exp_avg, exp_avg_sq, n, step, nstep, a,
+                       partials, norm_out, ticket);
+    TSRL_LAUNCH_CHECK("tsrl_clip_adam");
+    if (max_norm > 0.0f) {
+        const unsigned g2 = (unsigned)std::min<int64_t>((n + OTPB - 1) / OTPB, 1024);
+        hipLaunchKernelGGL(clip_scale_kernel, dim3(g2), dim3(OTPB), 0, as_stream(stream), grad,
+                           n, norm_out);
+        TSRL_LAUNCH_CHECK("tsrl_clip_adam (scale)");
+    }
+    return 0;
+}

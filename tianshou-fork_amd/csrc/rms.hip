@@ -96,82 +96,97 @@ __global__ __launch_bounds__(MCOLS * MLANES) void rms_merge_kernel(
 // P2 the rows counted in blk_done (blocks with none are skipped).  The state after the first
 // update (rounded to f32 like the reference's stored arrays) goes to snap_mean / snap_var for
 // normalising the step observations; the second update's result to mean / var / count.
-constexpr int M2COLS = 16, M2LANES = 64;
+#ifndef M2C
+#define M2C 8  // columns per workgroup (measured 7.0 / 6.0 / 6.4 us at 16 / 8 / 4)
+#endif
+constexpr int M2COLS = M2C, M2LANES = 64;
 
 __global__ __launch_bounds__(M2COLS * M2LANES) void rms_merge2_kernel(
     const double* p1, const double* p2, const double* blk_done, int64_t nblk, int64_t dim,
     int64_t k, float* mean, float* var, double* count, float* snap_mean, float* snap_var,
     unsigned int* ticket) {
-    __shared__ double sh[4][M2LANES][M2COLS];
-    __shared__ double sh_nd[M2COLS * M2LANES / kWave];
+    constexpr int NW = M2COLS * M2LANES / kWave;  // waves; each holds 64 / M2COLS lanes per column
+    __shared__ double sh[5][NW][M2COLS];
     const int tid = threadIdx.x;
     const int col = tid % M2COLS;
     const int lane = tid / M2COLS;
-    double c = 0.0;
-    for (int64_t b = tid; b < nblk; b += M2COLS * M2LANES) c += blk_done[b];
-    c = wave_sum(c);
-    if ((tid & (kWave - 1)) == 0) sh_nd[tid / kWave] = c;
-    const double old_count = *count;
-    __syncthreads();
-    double nd = 0.0;
-    for (int w = 0; w < M2COLS * M2LANES / kWave; ++w) nd += sh_nd[w];
-    const double bc1 = (double)k;
-    const double tot1 = old_count + bc1, tot2 = tot1 + nd;
     const int64_t d = (int64_t)blockIdx.x * M2COLS + col;
-    double s1 = 0.0, q1 = 0.0, s2 = 0.0, q2 = 0.0;
-    if (d < dim) {
-        for (int64_t b = lane; b < nblk; b += M2LANES) {
-            const double2 a = *reinterpret_cast<const double2*>(p1 + (b * dim + d) * 2);
-            s1 += a.x;
-            q1 += a.y;
-            if (blk_done[b] > 0.0) {
-                const double2 r = *reinterpret_cast<const double2*>(p2 + (b * dim + d) * 2);
-                s2 += r.x;
-                q2 += r.y;
-            }
-        }
+    const int64_t dc = d < dim ? d : dim - 1;  // in-bounds address for idle columns
+    const double old_count = *count;
+    // every load of the loop is independent: the P2 slots of blocks without a reset row
+    // (not written this step) are read and dropped by a select instead of a branch; the
+    // reset-row count rides along (each column's lanes see every block once)
+    double nd = 0.0, s1 = 0.0, q1 = 0.0, s2 = 0.0, q2 = 0.0;
+    for (int64_t b = lane; b < nblk; b += M2LANES) {
+        const double bd = blk_done[b];
+        const double2 a = *reinterpret_cast<const double2*>(p1 + (b * dim + dc) * 2);
+        const double2 r = *reinterpret_cast<const double2*>(p2 + (b * dim + dc) * 2);
+        nd += bd;
+        s1 += a.x;
+        q1 += a.y;
+        s2 += bd > 0.0 ? r.x : 0.0;
+        q2 += bd > 0.0 ? r.y : 0.0;
     }
-    sh[0][lane][col] = s1;
-    sh[1][lane][col] = q1;
-    sh[2][lane][col] = s2;
-    sh[3][lane][col] = q2;
-    __syncthreads();
-    // fixed-order tree over the lanes
-    for (int st = M2LANES / 2; st > 0; st >>= 1) {
-        if (lane < st) {
+    // the 4 lanes of a column inside a wave (tid bits 4-5), then the waves through LDS in
+    // fixed order (one barrier instead of a 6-level LDS tree)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) sh[q][lane][col] += sh[q][lane + st][col];
-        }
-        __syncthreads();
+    for (int off = M2COLS; off < kWave; off <<= 1) {
+        nd += __shfl_xor(nd, off, kWave);
+        s1 += __shfl_xor(s1, off, kWave);
+        q1 += __shfl_xor(q1, off, kWave);
+        s2 += __shfl_xor(s2, off, kWave);
+        q2 += __shfl_xor(q2, off, kWave);
     }
-    if (lane == 0 && d < dim) {
-        const double S1 = sh[0][0][col], Q1 = sh[1][0][col], S2 = sh[2][0][col],
-                     Q2 = sh[3][0][col];
-        double m0 = (double)mean[d], v0 = (double)var[d];
-        if (bc1 > 0.0) {
-            const double bm = S1 / bc1;
-            double bv = Q1 / bc1 - bm * bm;
-            bv = bv < 0.0 ? 0.0 : bv;
-            const double delta = bm - m0;
-            const double nm = m0 + delta * bc1 / tot1;
-            const double m2 = v0 * old_count + bv * bc1 + delta * delta * old_count * bc1 / tot1;
-            m0 = (double)(float)nm;
-            v0 = (double)(float)(m2 / tot1);
+    const int w = tid / kWave;
+    if ((tid & (kWave - 1)) < M2COLS) {
+        sh[0][w][col] = nd;
+        sh[1][w][col] = s1;
+        sh[2][w][col] = q1;
+        sh[3][w][col] = s2;
+        sh[4][w][col] = q2;
+    }
+    __syncthreads();
+    double tot2 = 0.0;
+    if (tid < M2COLS) {
+        double ND = 0.0, S1 = 0.0, Q1 = 0.0, S2 = 0.0, Q2 = 0.0;
+        for (int v = 0; v < NW; ++v) {
+            ND += sh[0][v][col];
+            S1 += sh[1][v][col];
+            Q1 += sh[2][v][col];
+            S2 += sh[3][v][col];
+            Q2 += sh[4][v][col];
         }
-        snap_mean[d] = (float)m0;
-        snap_var[d] = (float)v0;
-        if (nd > 0.0) {
-            const double bm = S2 / nd;
-            double bv = Q2 / nd - bm * bm;
-            bv = bv < 0.0 ? 0.0 : bv;
-            const double delta = bm - m0;
-            const double nm = m0 + delta * nd / tot2;
-            const double m2 = v0 * tot1 + bv * nd + delta * delta * tot1 * nd / tot2;
-            m0 = (double)(float)nm;
-            v0 = (double)(float)(m2 / tot2);
+        const double bc1 = (double)k;
+        const double tot1 = old_count + bc1;
+        tot2 = tot1 + ND;
+        if (d < dim) {
+            double m0 = (double)mean[d], v0 = (double)var[d];
+            if (bc1 > 0.0) {
+                const double bm = S1 / bc1;
+                double bv = Q1 / bc1 - bm * bm;
+                bv = bv < 0.0 ? 0.0 : bv;
+                const double delta = bm - m0;
+                const double nm = m0 + delta * bc1 / tot1;
+                const double m2 =
+                    v0 * old_count + bv * bc1 + delta * delta * old_count * bc1 / tot1;
+                m0 = (double)(float)nm;
+                v0 = (double)(float)(m2 / tot1);
+            }
+            snap_mean[d] = (float)m0;
+            snap_var[d] = (float)v0;
+            if (ND > 0.0) {
+                const double bm = S2 / ND;
+                double bv = Q2 / ND - bm * bm;
+                bv = bv < 0.0 ? 0.0 : bv;
+                const double delta = bm - m0;
+                const double nm = m0 + delta * ND / tot2;
+                const double m2 = v0 * tot1 + bv * ND + delta * delta * tot1 * ND / tot2;
+                m0 = (double)(float)nm;
+                v0 = (double)(float)(m2 / tot2);
+            }
+            mean[d] = (float)m0;
+            var[d] = (float)v0;
         }
-        mean[d] = (float)m0;
-        var[d] = (float)v0;
     }
     if (tid == 0) {
         const unsigned int t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL,

@@ -92,6 +92,9 @@ _SIGS = {
                           ctypes.c_int),
     "tsrl_nstep_return": ([_p, _p, _p, _p, _p, _i64, _i64, _p, _i64, _i64, _d, _p, _i64,
                            ctypes.c_int, _p, _p], ctypes.c_int),
+    "tsrl_clip_adam_partials": ([_i64], _i64),
+    "tsrl_clip_adam": ([_p, _p, _p, _p, _i64, _p, _i64, _f, _f, _f, _f, _f, _p, _p, _p, _p],
+                       ctypes.c_int),
     "tsrl_segtree_set": ([_p, _i64, _p, _p, _i64, _i64, _p, _p], ctypes.c_int),
     "tsrl_segtree_reduce": ([_p, _i64, _i64, _i64, _p, _p], ctypes.c_int),
     "tsrl_segtree_prefix_idx": ([_p, _i64, _p, ctypes.c_int, _i64, _p, _p], ctypes.c_int),

@@ -87,6 +87,7 @@ class FusedActorCritic:
         self.params = [p for p in params]
         self._flat = None
         self._bufs: Dict[str, torch.Tensor] = {}
+        self._adam = None  # flat parameter / moment storage of bind_adam
 
     # -- gradient storage -----------------------------------------------------------------------
     def bind_grads(self) -> None:
@@ -115,6 +116,80 @@ class FusedActorCritic:
             _C.ptr(L["w2a"].weight), _C.ptr(L["w2a"].bias), _C.ptr(L["w2c"].weight),
             _C.ptr(L["w2c"].bias), _C.ptr(L["w3a"].weight), _C.ptr(L["w3a"].bias),
             _C.ptr(L["w3c"].weight), _C.ptr(L["w3c"].bias), _C.ptr(L["sigma"]))
+
+    # -- clip_grad_norm_ + Adam as one HIP pass (csrc/optim.hip) --------------------------------
+    @staticmethod
+    def _plain_adam(optim, params) -> bool:
+        if not isinstance(optim, torch.optim.Adam) or len(optim.param_groups) != 1:
+            return False
+        g = optim.param_groups[0]
+        if g.get("amsgrad") or g.get("weight_decay", 0) != 0 or g.get("maximize") or \
+                g.get("differentiable") or isinstance(g["lr"], torch.Tensor):
+            return False
+        return len(g["params"]) == len(params) and \
+            all(a is b for a, b in zip(g["params"], params))
+
+    def adam_bound(self, optim) -> bool:
+        st = self._adam
+        return st is not None and st["optim"] is optim and all(
+            p.data_ptr() == v.data_ptr() for p, v in zip(self.params, st["pviews"]))
+
+    def bind_adam(self, optim) -> bool:
+        """Move every parameter and its Adam moments into flat buffers (parameter .data and
+        ``optim.state[p]`` become views, so state_dict()/load and torch's own step keep
+        working) when ``optim`` is a plain Adam over exactly these parameters; then
+        ``clip_adam`` replaces clip_grad_norm_ + optim.step()."""
+        if self.adam_bound(optim):
+            return True
+        if not self._plain_adam(optim, self.params):
+            self._adam = None
+            return False
+        dev = self.params[0].device
+        n = sum(p.numel() for p in self.params)
+        flat_p = torch.empty(n, dtype=torch.float32, device=dev)
+        flat_m = torch.zeros(n, dtype=torch.float32, device=dev)
+        flat_v = torch.zeros(n, dtype=torch.float32, device=dev)
+        steps = torch.zeros(len(self.params), dtype=torch.float32, device=dev)
+        pviews = []
+        o = 0
+        for i, p in enumerate(self.params):
+            k = p.numel()
+            flat_p[o:o + k].copy_(p.detach().reshape(-1))
+            st = optim.state.get(p, {})
+            if "exp_avg" in st:
+                flat_m[o:o + k].copy_(st["exp_avg"].reshape(-1))
+                flat_v[o:o + k].copy_(st["exp_avg_sq"].reshape(-1))
+                steps[i] = float(st["step"])
+            with torch.no_grad():
+                p.data = flat_p[o:o + k].view_as(p)
+            optim.state[p] = {"step": steps[i],
+                              "exp_avg": flat_m[o:o + k].view_as(p),
+                              "exp_avg_sq": flat_v[o:o + k].view_as(p)}
+            pviews.append(p.data)
+            o += k
+        steps.fill_(float(steps.max()) if len(steps) else 0.0)
+        self._adam = dict(optim=optim, p=flat_p, m=flat_m, v=flat_v, steps=steps, pviews=pviews,
+                          ticket=torch.zeros(1, dtype=torch.int32, device=dev),
+                          partials=torch.zeros(
+                              max(int(_C.lib().tsrl_clip_adam_partials(n)), 1),
+                              dtype=torch.float64, device=dev),
+                          norm=torch.zeros(2, dtype=torch.float32, device=dev))
+        self._flat = None  # parameter addresses moved: bind_grads re-derives every pointer
+        self.bind_grads()
+        return True
+
+    def clip_adam(self, max_norm: Optional[float]) -> None:
+        """clip_grad_norm_(max_norm) (when given) + Adam.step() over the flat buffers."""
+        st = self._adam
+        g = st["optim"].param_groups[0]
+        b1, b2 = g["betas"]
+        _C.check(_C.lib().tsrl_clip_adam(
+            _C.ptr(st["p"]), _C.ptr(self._flat), _C.ptr(st["m"]), _C.ptr(st["v"]),
+            st["p"].numel(), _C.ptr(st["steps"]), st["steps"].numel(), float(g["lr"]),
+            float(b1), float(b2), float(g["eps"]), float(max_norm) if max_norm else 0.0,
+            _C.ptr(st["partials"]), _C.ptr(st["norm"]), _C.ptr(st["ticket"]),
+            _C.stream_ptr(st["p"].device)),
+            "tsrl_clip_adam")
 
     def _weights(self) -> "_C.TailWeights":
         L = self.L

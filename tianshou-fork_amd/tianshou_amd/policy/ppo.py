@@ -163,6 +163,8 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
         # replay whole epochs of the fused minibatch step from a captured HIP graph
         self.graph_learn = True
         self._learn_graph = None
+        # clip_grad_norm_ + Adam as one HIP pass over flat parameter storage (csrc/optim.hip)
+        self.fused_adam = True
 
     def _params(self, b_global: float) -> _C.PPOParams:
         p = _C.PPOParams()
@@ -215,6 +217,8 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
             perm = self._permutation(n, dev)
             mlp_ok = self._mlp is not None and batch.obs.is_cuda and \
                 batch.obs.dtype == torch.float32 and batch.obs.dim() == 2
+            if mlp_ok and self.fused_adam:
+                self._mlp.bind_adam(self.optim)
             obs_all = self._mlp.rows(batch.obs) if mlp_ok else None
             if mlp_ok and self._graph_ready():
                 terms.append(self._epoch_graph(obs_all, (act, logp_old, adv, ret, v_s), perm, n,
@@ -226,10 +230,7 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
                     params = self._params((e - s) * self.dp.world)
                     t = self._mlp.minibatch(obs_all, idx, e - s, act, logp_old, adv, ret, v_s,
                                             params, self.dp)
-                    if self._grad_norm:
-                        nn.utils.clip_grad_norm_(self._actor_critic.parameters(),
-                                                 max_norm=self._grad_norm)
-                    self.optim.step()
+                    self._opt_step()
                     terms.append(t)
                     continue
                 obs_mb = gather_rows(batch.obs, idx)
@@ -252,6 +253,17 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
         return {"loss": vals[:, 0].tolist(), "loss/clip": vals[:, 1].tolist(),
                 "loss/vf": vals[:, 2].tolist(), "loss/ent": vals[:, 3].tolist()}
 
+    def _opt_step(self) -> None:
+        """clip_grad_norm_ + optim.step() of ppo.py:143-151: one fused HIP pass
+        (tsrl_clip_adam) when the optimiser is a plain Adam over the fused MLP's parameters,
+        torch's otherwise."""
+        if self._mlp is not None and self._mlp.adam_bound(self.optim):
+            self._mlp.clip_adam(self._grad_norm)
+            return
+        if self._grad_norm:
+            nn.utils.clip_grad_norm_(self._actor_critic.parameters(), max_norm=self._grad_norm)
+        self.optim.step()
+
     # -- HIP-graph replay of whole epochs ------------------------------------------------------
     def _graph_ready(self) -> bool:
         """An epoch of fused minibatches can be captured once and replayed: single process
@@ -260,6 +272,8 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
         if not self.graph_learn or self.dp.active or self._recompute_adv:
             return False
         opt = self.optim
+        if self._mlp is not None and self._mlp.adam_bound(opt):
+            return True
         if not opt.defaults.get("capturable", False) or len(opt.state) == 0:
             return False
         return all(p in opt.state for g in opt.param_groups for p in g["params"])
@@ -272,7 +286,8 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
         bounds = split_bounds(n, batch_size, merge_last=True)
         key = (n, batch_size, obs_all.data_ptr(), tuple(obs_all.shape),
                tuple(a.shape for a in arrays), self._mlp.flat_grad is not None and
-               self._mlp.flat_grad.data_ptr())
+               self._mlp.flat_grad.data_ptr(), self._mlp.adam_bound(self.optim),
+               tuple(float(g["lr"]) for g in self.optim.param_groups))
         st = self._learn_graph
         if st is None or st["key"] != key:
             st = None
@@ -290,10 +305,7 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
                 for i, (s, e) in enumerate(bounds):
                     t = self._mlp.minibatch(obs_all, sperm[s:e], e - s, *static,
                                             self._params(e - s), self.dp)
-                    if self._grad_norm:
-                        nn.utils.clip_grad_norm_(self._actor_critic.parameters(),
-                                                 max_norm=self._grad_norm)
-                    self.optim.step()
+                    self._opt_step()
                     sterms[i].copy_(t)
             st = dict(key=key, graph=graph, static=static, perm=sperm, terms=sterms)
             self._learn_graph = st
