@@ -23,12 +23,17 @@
 // (B[k=l>>5][j=l&31]) when the A operand is read with the matching permuted k; so layer 2,
 // the heads and the whole backward chain run without moving activations between lanes.
 // Only the weight gradients (which sum over the minibatch rows) transpose through LDS.
-#include "tsrl_common.h"
+#include "x6.h"
 
 namespace tsrl {
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+using x6::bf16x8;
+using x6::mfma6;
+using x6::NPL;
+using x6::split1;
+using x6::sw_off;
 
 constexpr int H = 64;           // hidden width of each net (fast path)
 constexpr int HC = 2 * H;       // actor + critic first-layer features
@@ -220,9 +225,66 @@ __device__ __forceinline__ int rs_reg(int l) {
 // the loss gradient w.r.t. mu depends only on actor outputs and w.r.t. the value only on
 // critic outputs, so the halves are independent and each keeps half the live state.
 constexpr int SH = 18;   // half-tile transpose scratch: [64 features][16 rows], stride 18
-constexpr int T_W2 = 0, T_W3 = T_W2 + H * WS2, T_B2 = T_W3 + AMAX * WS2, T_B3 = T_B2 + H,
-              T_W3C = T_B3 + AMAX, T_VAR = T_W3C + H, T_LS = T_VAR + AMAX, T_SCR = T_LS + AMAX,
-              T_END = T_SCR + 4 * 2 * H * SH;
+constexpr int T_B2 = 0, T_B3 = T_B2 + H, T_W3C = T_B3 + AMAX, T_VAR = T_W3C + H,
+              T_LS = T_VAR + AMAX, T_SCR = T_LS + AMAX, T_END = T_SCR + 4 * 2 * H * SH;
+
+// The chain products (layer 2, mu head, dZ2 = W3^T dMu, dZ1 = W2^T dZ2) run as bf16x6 (x6.h):
+// their activation operand is the C-layout tile itself -- registers 8s..8s+7 of a 32x32 tile
+// are the 8 k of k-step s on each lane half, element j of half h being feature
+// 16s + 8(j>>2) + 4h + (j&3) of the tile -- split in registers, and the weight operand is an
+// LDS image of the matrix, split once per workgroup into 3 bf16 planes whose rows hold the
+// k in exactly that order.  Image of an [rows][32*nkc] matrix: plane p, 32-k chunk kc, row r
+// at byte ((p*nkc + kc)*rows)*64 + sw_off(r, q), q = 2s + h the 16-byte chunk of (s, h).
+constexpr int IMG_W2 = 0;                              // W2   [64 out][64 in]
+constexpr int IMG_W2T = IMG_W2 + NPL * 2 * H * 64;     // W2^T [64 in][64 out]
+constexpr int IMG_W3 = IMG_W2T + NPL * 2 * H * 64;     // W3   [32 act][64]      (actor)
+constexpr int IMG_W3T = IMG_W3 + NPL * 2 * AMAX * 64;  // W3^T [64][32 act]      (actor)
+constexpr int IMG_ACTOR = IMG_W3T + NPL * 1 * H * 64, IMG_CRITIC = IMG_W3;
+
+__device__ __forceinline__ int img_off(int p, int kc, int row, int q, int nkc, int rows) {
+    return (p * nkc + kc) * rows * 64 + sw_off(row, q);
+}
+
+// Split M(row, k) (k < 32*nkc) into the image; every thread writes whole 16-byte chunks.
+template <typename F>
+__device__ __forceinline__ void build_img(char* img, int rows, int nkc, F val) {
+    for (int i = threadIdx.x; i < rows * nkc * 4; i += TAIL_TPB) {
+        const int q = i & 3, kc = (i >> 2) % nkc, row = (i >> 2) / nkc;
+        bf16x8 p0, p1, p2;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = 32 * kc + 16 * (q >> 1) + 8 * (j >> 2) + 4 * (q & 1) + (j & 3);
+            __bf16 a, b, c;
+            split1(val(row, k), a, b, c);
+            p0[j] = a;
+            p1[j] = b;
+            p2[j] = c;
+        }
+        *reinterpret_cast<bf16x8*>(img + img_off(0, kc, row, q, nkc, rows)) = p0;
+        *reinterpret_cast<bf16x8*>(img + img_off(1, kc, row, q, nkc, rows)) = p1;
+        *reinterpret_cast<bf16x8*>(img + img_off(2, kc, row, q, nkc, rows)) = p2;
+    }
+}
+
+// The 3 planes of one operand fragment: row `row`, 32-k chunk kc, k-step s, lane half h.
+__device__ __forceinline__ void ld_img(const char* img, int nkc, int rows, int kc, int row,
+                                       int s, int h, bf16x8 (&a)[NPL]) {
+#pragma unroll
+    for (int p = 0; p < NPL; ++p)
+        a[p] = *reinterpret_cast<const bf16x8*>(img + img_off(p, kc, row, 2 * s + h, nkc, rows));
+}
+
+// B fragment of k-step s from registers 8s..8s+7 of a C-layout tile, split in registers.
+__device__ __forceinline__ void split_frag(const float (&v)[16], int s, bf16x8 (&b)[NPL]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        __bf16 x0, x1, x2;
+        split1(v[8 * s + j], x0, x1, x2);
+        b[0][j] = x0;
+        b[1][j] = x1;
+        b[2][j] = x2;
+    }
+}
 
 // Accumulate D += A^T-in-LDS . B^T-in-LDS over 16 minibatch rows: the two operands were
 // written feature-major ([feature][row], stride SH) from the C layout; tiles ot x ft.
@@ -267,15 +329,16 @@ __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// the actor half needs ~330 registers (1 wave per SIMD); the critic half fits 2 per SIMD
+// one workgroup per CU: the bf16x6 weight images (72 KB actor / 48 KB critic) + scratch
 template <int NET>
-__global__ __launch_bounds__(TAIL_TPB, 2) void ppo_tail_kernel(
+__global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
     const float* __restrict__ h1f, int64_t n, const int64_t* __restrict__ idx, TailWeights wt,
     const float* __restrict__ act, const float* __restrict__ logp_old,
     const float* __restrict__ adv, const float* __restrict__ ret, const float* __restrict__ v_s,
     const double* __restrict__ adv_sums, TailParams p, float* __restrict__ dz1,
     float* __restrict__ slab_f, double* __restrict__ slab_d) {
     __shared__ __attribute__((aligned(16))) float sm[T_END];
+    __shared__ __attribute__((aligned(16))) char img[NET == 0 ? IMG_ACTOR : IMG_CRITIC];
     __shared__ double sred[4][SL_D];
     const int t = threadIdx.x;
     const int w = t >> 6, l = t & 63, h = l >> 5, c = l & 31;
@@ -285,13 +348,15 @@ __global__ __launch_bounds__(TAIL_TPB, 2) void ppo_tail_kernel(
     {
         const float* w2 = actor ? wt.w2a : wt.w2c;
         const float* b2 = actor ? wt.b2a : wt.b2c;
-        for (int i = t; i < H * H; i += TAIL_TPB) sm[T_W2 + (i >> 6) * WS2 + (i & 63)] = w2[i];
+        build_img(img + IMG_W2, H, 2, [=](int r, int k) { return w2[r * H + k]; });
+        build_img(img + IMG_W2T, H, 2, [=](int r, int k) { return w2[k * H + r]; });
         if (t < H) sm[T_B2 + t] = b2[t];
         if (actor) {
-            for (int i = t; i < AMAX * H; i += TAIL_TPB) {
-                const int a = i >> 6;
-                sm[T_W3 + a * WS2 + (i & 63)] = a < A ? wt.w3a[i] : 0.0f;
-            }
+            const float* w3 = wt.w3a;
+            build_img(img + IMG_W3, AMAX, 2,
+                      [=](int r, int k) { return r < A ? w3[r * H + k] : 0.0f; });
+            build_img(img + IMG_W3T, H, 1,
+                      [=](int r, int k) { return k < A ? w3[k * H + r] : 0.0f; });
             if (t < AMAX) {
                 sm[T_B3 + t] = t < A ? wt.b3a[t] : 0.0f;
                 const float sig = t < A ? expf(wt.log_std[t]) : 1.0f;
@@ -303,8 +368,6 @@ __global__ __launch_bounds__(TAIL_TPB, 2) void ppo_tail_kernel(
         }
     }
     __syncthreads();
-    const float* sW2 = sm + T_W2;
-    const float* sW3 = sm + T_W3;
     float* S1 = sm + T_SCR + w * 2 * H * SH;
     float* S2 = S1 + H * SH;
     const float b3c = wt.b3c[0];
@@ -353,31 +416,39 @@ __global__ __launch_bounds__(TAIL_TPB, 2) void ppo_tail_kernel(
         // ---- layer 2 -----------------------------------------------------------------------
         __builtin_amdgcn_sched_barrier(0);
         float h2[2][16];
+        {
+            f32x16 z0 = zero16(), z1 = zero16();
 #pragma unroll
-        for (int ot = 0; ot < 2; ++ot) {
-            __builtin_amdgcn_sched_barrier(0);
-            f32x16 z = zero16();
-            const float* wa = sW2 + (32 * ot + c) * WS2 + 4 * h;
+            for (int kc = 0; kc < 2; ++kc)
 #pragma unroll
-            for (int it = 0; it < 2; ++it)
+                for (int s = 0; s < 2; ++s) {
+                    bf16x8 b[NPL], a[NPL];
+                    split_frag(h1[kc], s, b);
+                    ld_img(img + IMG_W2, 2, H, kc, c, s, h, a);
+                    z0 = mfma6(a, b, z0);
+                    ld_img(img + IMG_W2, 2, H, kc, 32 + c, s, h, a);
+                    z1 = mfma6(a, b, z1);
+                }
 #pragma unroll
-                for (int r = 0; r < 16; ++r) z = mfma(wa[32 * it + rho(r)], h1[it][r], z);
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-                h2[ot][r] = tanh_nb(z[r] + sm[T_B2 + 32 * ot + rho(r) + 4 * h]);
+            for (int r = 0; r < 16; ++r) {
+                h2[0][r] = tanh_nb(z0[r] + sm[T_B2 + rho(r) + 4 * h]);
+                h2[1][r] = tanh_nb(z1[r] + sm[T_B2 + 32 + rho(r) + 4 * h]);
+            }
         }
         float dz2[2][16];
         if constexpr (actor) {
             // ---- mu head + clipped surrogate ----------------------------------------------
             __builtin_amdgcn_sched_barrier(0);
             f32x16 mu = zero16();
-            {
-                const float* wa = sW3 + c * WS2 + 4 * h;
 #pragma unroll
-                for (int it = 0; it < 2; ++it)
+            for (int kc = 0; kc < 2; ++kc)
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) mu = mfma(wa[32 * it + rho(r)], h2[it][r], mu);
-            }
+                for (int s = 0; s < 2; ++s) {
+                    bf16x8 b[NPL], a[NPL];
+                    split_frag(h2[kc], s, b);
+                    ld_img(img + IMG_W3, 2, AMAX, kc, c, s, h, a);
+                    mu = mfma6(a, b, mu);
+                }
             float diff[16];
             float lp = 0.0f;
 #pragma unroll
@@ -455,15 +526,22 @@ __global__ __launch_bounds__(TAIL_TPB, 2) void ppo_tail_kernel(
             }
             // dZ2 = (W3a^T dMu) * (1 - H2^2)
             __builtin_amdgcn_sched_barrier(0);
+            {
+                bf16x8 bd0[NPL], bd1[NPL];
+                split_frag(dmu[0], 0, bd0);
+                split_frag(dmu[0], 1, bd1);
 #pragma unroll
-            for (int ft = 0; ft < 2; ++ft) {
-                __builtin_amdgcn_sched_barrier(0);
-                f32x16 d = zero16();
+                for (int ft = 0; ft < 2; ++ft) {
+                    f32x16 d = zero16();
+                    bf16x8 a[NPL];
+                    ld_img(img + IMG_W3T, 1, H, 0, 32 * ft + c, 0, h, a);
+                    d = mfma6(a, bd0, d);
+                    ld_img(img + IMG_W3T, 1, H, 0, 32 * ft + c, 1, h, a);
+                    d = mfma6(a, bd1, d);
 #pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    d = mfma(sW3[(rho(r) + 4 * h) * WS2 + 32 * ft + c], dmu[0][r], d);
-#pragma unroll
-                for (int r = 0; r < 16; ++r) dz2[ft][r] = d[r] * (1.0f - h2[ft][r] * h2[ft][r]);
+                    for (int r = 0; r < 16; ++r)
+                        dz2[ft][r] = d[r] * (1.0f - h2[ft][r] * h2[ft][r]);
+                }
             }
         } else {
             // ---- value head + value loss ----------------------------------------------------
@@ -546,15 +624,22 @@ __global__ __launch_bounds__(TAIL_TPB, 2) void ppo_tail_kernel(
                 }
             }
         }
+        f32x16 dd0 = zero16(), dd1 = zero16();
+#pragma unroll
+        for (int kc = 0; kc < 2; ++kc)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                bf16x8 b[NPL], a[NPL];
+                split_frag(dz2[kc], s, b);
+                ld_img(img + IMG_W2T, 2, H, kc, c, s, h, a);
+                dd0 = mfma6(a, b, dd0);
+                ld_img(img + IMG_W2T, 2, H, kc, 32 + c, s, h, a);
+                dd1 = mfma6(a, b, dd1);
+            }
 #pragma unroll
         for (int ft = 0; ft < 2; ++ft) {
             __builtin_amdgcn_sched_barrier(0);
-            f32x16 d = zero16();
-#pragma unroll
-            for (int ot = 0; ot < 2; ++ot)
-#pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    d = mfma(sW2[(32 * ot + rho(r) + 4 * h) * WS2 + 32 * ft + c], dz2[ot][r], d);
+            const f32x16 d = ft == 0 ? dd0 : dd1;
             if (live) {
                 float v[16];
 #pragma unroll

@@ -23,29 +23,26 @@
 // matrix cores are 28 % busy (SQ_VALU_MFMA_BUSY_CYCLES).  The gathered X rows and the
 // single-buffered chunk loop (two barriers per 32 k) bound it, not the MFMA rate; reading all
 // of a step's LDS operands ahead of its MFMAs (sched_barrier) measured 6 % slower.
-#include "tsrl_common.h"
+#include "x6.h"
 
 namespace tsrl {
 namespace {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
+using x6::bf16x8;
+using x6::f32x16;
+using x6::mfma6;
+using x6::NPL;
+using x6::split1;
+using x6::sw_off;
 
 constexpr int H = 64;
 constexpr int HC = 2 * H;   // actor + critic first-layer features
 constexpr int NT = HC / 32;
 constexpr int XR = 128;     // minibatch rows per workgroup
 constexpr int KC = 32;      // k per staged chunk (two 16-k MFMA steps)
-constexpr int NPL = 3;      // split planes
 constexpr int ROWB = KC * 2;  // bytes per LDS row of one plane (32 bf16)
 
 __device__ __forceinline__ int rho(int r) { return (r & 3) + 8 * (r >> 2); }
-
-// Byte offset of 16-byte chunk q (0..3) of LDS row `row`: chunks XOR-swizzled by row bits 2-3
-// so that the 16 lanes of a ds_read_b128 phase (rows c..c+15, one chunk) hit all 64 banks.
-__device__ __forceinline__ int sw_off(int row, int q) {
-    return row * ROWB + 16 * (q ^ ((row >> 2) & 3));
-}
 
 // f32 rows of KC floats (128 B, chunks q = 0..7): chunk index XOR row bits 1-3, so the
 // 16-lane phases of a ds_read_b128 (rows r..r+15, one chunk) cover all banks.
@@ -59,14 +56,6 @@ __device__ __forceinline__ float4 keep4(bool keep, float4 v) {
     return make_float4(keep ? v.x : 0.f, keep ? v.y : 0.f, keep ? v.z : 0.f, keep ? v.w : 0.f);
 }
 
-// One f32 split exactly into three bf16 pieces.
-__device__ __forceinline__ void split1(float x, __bf16& a0, __bf16& a1, __bf16& a2) {
-    a0 = (__bf16)x;
-    const float r1 = x - (float)a0;
-    a1 = (__bf16)r1;
-    a2 = (__bf16)(r1 - (float)a1);
-}
-
 // Elements o..o+3 of the three split planes from one float4.
 __device__ __forceinline__ void split4(float4 v, bf16x8& p0, bf16x8& p1, bf16x8& p2, int o) {
     __bf16 a, b, c;
@@ -78,17 +67,6 @@ __device__ __forceinline__ void split4(float4 v, bf16x8& p0, bf16x8& p1, bf16x8&
     p0[o + 2] = a, p1[o + 2] = b, p2[o + 2] = c;
     split1(v.w, a, b, c);
     p0[o + 3] = a, p1[o + 3] = b, p2[o + 3] = c;
-}
-
-__device__ __forceinline__ f32x16 mfma6(const bf16x8 (&a)[NPL], const bf16x8 (&b)[NPL],
-                                        f32x16 acc) {
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], acc, 0, 0, 0);
-    return acc;
 }
 
 // Split planes of the stacked first-layer weight: out[p][f][k] (f < 64 actor, >= 64 critic;
