@@ -1002,6 +1002,116 @@ __global__ __launch_bounds__(256, 2) void dw_kernel(
             o[(int64_t)(32 * i + rho(r) + 4 * h) * ncolpad + col0 + 32 * w + c] = acc[i][r];
 }
 
+// bf16x6 form of dw_kernel (x6.h): the same workgroup tiling and partial layout, rows staged
+// 32 at a time, but every staged element is split once, by the thread that loads it, into
+// three bf16 planes stored transposed ([feature or column][32 rows], x6::sw_off rows), so a
+// lane's MFMA fragment (8 consecutive minibatch rows of one feature / column) is one
+// ds_read_b128 per plane and the inner loop is 15 LDS reads + 24 bf16 MFMAs per 16 rows.
+// Staging: thread t owns feature / column (t & 127) and the 8-row groups {rg, rg + 2} of the
+// chunk (rg = t >> 7, wave-uniform, so the row indices come in through scalar loads); the
+// next chunk's 32 values are loaded into registers during the current chunk's MFMAs.
+#ifndef DWX6_OCC
+#define DWX6_OCC 2
+#endif
+__global__ __launch_bounds__(256, DWX6_OCC) void dw_x6_kernel(
+    const float* __restrict__ dz, const float* __restrict__ X, int64_t ldx,
+    const int64_t* __restrict__ idx, int64_t n, int D, int64_t rows_per_split, int ncolpad,
+    float* __restrict__ part) {
+    constexpr int PL = 128 * 64;  // bytes per plane: 128 rows of 32 bf16
+    __shared__ __attribute__((aligned(16))) char Zi[NPL * PL];
+    __shared__ __attribute__((aligned(16))) char Xi[NPL * PL];
+    const int t = threadIdx.x;
+    const int w = t >> 6, l = t & 63, h = l >> 5, c = l & 31;
+    const int col0 = blockIdx.x * DW_COLS;
+    const int64_t r0 = (int64_t)blockIdx.y * rows_per_split;
+    const int64_t r1 = min(n, r0 + rows_per_split);
+    const int fc = t & 127;                                  // staged feature / column
+    const int rg = __builtin_amdgcn_readfirstlane(t >> 7);   // 8-row groups rg, rg + 2
+    const int k = col0 + fc;
+    const float ones = k == D ? 1.0f : 0.0f;  // db1 through a ones column at k == D
+    const bool kin = k < D;
+    const float* xcol = X + (kin ? k : 0);
+    float zr[16], xr[16];
+#define DWX6_LOAD(rb)                                                                       \
+    {                                                                                       \
+        _Pragma("unroll") for (int q = 0; q < 16; ++q) {                                    \
+            const int64_t r = (rb) + 8 * (rg + 2 * (q >> 3)) + (q & 7);                     \
+            const int64_t rr = r < r1 ? r : r1 - 1;                                          \
+            const int64_t ri = idx ? idx[rr] : rr;                                          \
+            zr[q] = dz[rr * HC + fc];                                                       \
+            xr[q] = xcol[ri * ldx];                                                         \
+        }                                                                                   \
+    }
+    /* masks applied at the LDS store, not next to the loads (a select on a loaded value */ \
+    /* there would make the wave wait for the data before the chunk's MFMAs)           */ \
+#define DWX6_STORE(rb)                                                                      \
+    {                                                                                       \
+        _Pragma("unroll") for (int g = 0; g < 2; ++g) {                                     \
+            bf16x8 zp[NPL], xp[NPL];                                                        \
+            _Pragma("unroll") for (int j = 0; j < 8; ++j) {                                 \
+                const bool lv = (rb) + 8 * (rg + 2 * g) + j < r1;                           \
+                const float zv = lv ? zr[8 * g + j] : 0.0f;                                 \
+                const float xv = lv ? (kin ? xr[8 * g + j] : ones) : 0.0f;                  \
+                __bf16 a0, a1, a2;                                                          \
+                split1(zv, a0, a1, a2);                                                     \
+                zp[0][j] = a0;                                                              \
+                zp[1][j] = a1;                                                              \
+                zp[2][j] = a2;                                                              \
+                split1(xv, a0, a1, a2);                                                     \
+                xp[0][j] = a0;                                                              \
+                xp[1][j] = a1;                                                              \
+                xp[2][j] = a2;                                                              \
+            }                                                                               \
+            const int off = sw_off(fc, rg + 2 * g);                                         \
+            _Pragma("unroll") for (int p = 0; p < NPL; ++p) {                               \
+                *reinterpret_cast<bf16x8*>(Zi + p * PL + off) = zp[p];                      \
+                *reinterpret_cast<bf16x8*>(Xi + p * PL + off) = xp[p];                      \
+            }                                                                               \
+        }                                                                                   \
+    }
+    f32x16 acc[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) acc[i] = zero16();
+    const int64_t nchunk = r1 > r0 ? (r1 - r0 + DW_KB - 1) / DW_KB : 0;
+    if (nchunk > 0) {
+        DWX6_LOAD(r0)
+        DWX6_STORE(r0)
+    }
+    __syncthreads();
+    for (int64_t ch = 0; ch < nchunk; ++ch) {
+        if (ch + 1 < nchunk) DWX6_LOAD(r0 + (ch + 1) * DW_KB)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            bf16x8 b[NPL];
+            const int xo = sw_off(32 * w + c, 2 * s + h);
+#pragma unroll
+            for (int p = 0; p < NPL; ++p) b[p] = *reinterpret_cast<const bf16x8*>(Xi + p * PL + xo);
+#pragma unroll
+            for (int i = 0; i < NT; ++i) {
+                bf16x8 a[NPL];
+                const int zo = sw_off(32 * i + c, 2 * s + h);
+#pragma unroll
+                for (int p = 0; p < NPL; ++p)
+                    a[p] = *reinterpret_cast<const bf16x8*>(Zi + p * PL + zo);
+                acc[i] = mfma6(a, b, acc[i]);
+            }
+        }
+        if (ch + 1 < nchunk) {
+            __syncthreads();
+            DWX6_STORE(r0 + (ch + 1) * DW_KB)
+            __syncthreads();
+        }
+    }
+#undef DWX6_LOAD
+#undef DWX6_STORE
+    float* o = part + (int64_t)blockIdx.y * HC * ncolpad;
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            o[(int64_t)(32 * i + rho(r) + 4 * h) * ncolpad + col0 + 32 * w + c] = acc[i][r];
+}
+
 __global__ __launch_bounds__(256) void dw_reduce_kernel(const float* __restrict__ part,
                                                         int nsplit, int ncolpad, int D,
                                                         float* __restrict__ gWa,
@@ -1140,8 +1250,15 @@ extern "C" int tsrl_mlp_dw(const float* dz1, const float* X, int64_t ldx, const 
     const int nsplit = dw_nsplit(n);
     const int64_t rps = ((n + nsplit - 1) / nsplit + DW_KB - 1) / DW_KB * DW_KB;
     float* part = reinterpret_cast<float*>(workspace);
-    hipLaunchKernelGGL(dw_kernel, dim3(ncolt, nsplit), dim3(256), 0, as_stream(stream), dz1, X, ldx,
-                       idx, n, (int)D, rps, ncolpad, part);
+#ifndef DW_X6
+#define DW_X6 1
+#endif
+    if (DW_X6)
+        hipLaunchKernelGGL(dw_x6_kernel, dim3(ncolt, nsplit), dim3(256), 0, as_stream(stream), dz1,
+                           X, ldx, idx, n, (int)D, rps, ncolpad, part);
+    else
+        hipLaunchKernelGGL(dw_kernel, dim3(ncolt, nsplit), dim3(256), 0, as_stream(stream), dz1,
+                           X, ldx, idx, n, (int)D, rps, ncolpad, part);
     TSRL_LAUNCH_CHECK("tsrl_mlp_dw");
     const int64_t outs = (int64_t)HC * ncolpad;
     hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((outs + 63) / 64)), dim3(256), 0,
