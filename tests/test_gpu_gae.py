@@ -183,3 +183,47 @@ def test_ret_rms_update(dev):
         np.testing.assert_allclose(rms.mean, host.mean, rtol=1e-10)
         np.testing.assert_allclose(rms.var, host.var, rtol=1e-10)
         assert rms.count == host.count
+
+
+@pytest.mark.parametrize("envs,steps", [(4096, 2048), (64, 4096), (256, 128), (96, 512)])
+@pytest.mark.parametrize("scaled", [False, True])
+def test_gae_staged_rows_kernel(dev, envs, steps, scaled, monkeypatch):
+    """The LDS-staged row kernel (f32 outputs only, rows a multiple of the 2048-transition
+    tile -- the layout process_fn hands over) gives the same bits as the per-thread-load row
+    kernel (adv, ret, ret_rms partials) and matches the C oracle."""
+    from tianshou_amd.policy.base import gae_device
+    from tianshou_amd import _C
+    g = torch.Generator(device=dev).manual_seed(envs + 11 * steps)
+    n = envs * steps
+    v_s = torch.randn(n, device=dev, generator=g)
+    v_n = torch.randn(n, device=dev, generator=g)
+    rew = torch.rand(n, device=dev, generator=g, dtype=torch.float64)
+    u = torch.rand(n, device=dev, generator=g)
+    term = u < 0.002
+    trunc = (u > 0.998) & ~term
+    scale = torch.tensor([1.37], dtype=torch.float64, device=dev) if scaled else None
+    nparts = int(_C.lib().tsrl_gae_num_partials(n, steps))
+    outs = []
+    for unstaged in (False, True):
+        if unstaged:
+            monkeypatch.setenv("TSRL_GAE_UNSTAGED", "1")
+        parts = torch.full((nparts * 3,), -1.0, dtype=torch.float64, device=dev) if scaled \
+            else None
+        adv32, ret32, _, _ = gae_device(v_s, v_n, rew, term, trunc, 0.99, 0.95, steps, None,
+                                        scale, ret_partials=parts)
+        outs.append((adv32.cpu().numpy(), ret32.cpu().numpy(),
+                     None if parts is None else parts.cpu().numpy()))
+    monkeypatch.delenv("TSRL_GAE_UNSTAGED")
+    (a0, r0, p0), (a1, r1, p1) = outs
+    np.testing.assert_array_equal(a0, a1)
+    np.testing.assert_array_equal(r0, r1)
+    if scaled:
+        np.testing.assert_array_equal(p0, p1)
+    s = 1.37 if scaled else 1.0
+    ret_o, adv_o = ref.compute_episodic_return(
+        rew.cpu().numpy(), term.cpu().numpy(), trunc.cpu().numpy(), np.arange(n),
+        np.arange(steps - 1, n, steps), v_n.cpu().numpy().astype(np.float64) * s
+        if scaled else v_n.cpu().numpy(), v_s.cpu().numpy().astype(np.float64) * s
+        if scaled else v_s.cpu().numpy(), 0.99, 0.95)
+    _tol(a0, adv_o)
+    _tol(r0, ret_o / s)

@@ -261,6 +261,47 @@ __device__ __forceinline__ Welford block_welford_fast(Welford v, Welford* sh) {
     return r;
 }
 
+// Chan merge of two partials with equal power-of-two counts (every lane of a full tile holds
+// 8 returns, so every butterfly level merges equal counts): delta*n/(2n) = delta*0.5 and
+// delta^2*n*n/(2n) = delta^2*(n/2) are exact scalings, so this is chan() bit for bit without
+// its two f64 divisions.
+__device__ __forceinline__ Welford chan_eq(Welford x, Welford y) {
+    Welford r;
+    r.n = x.n + y.n;
+    const double delta = y.mean - x.mean;
+    r.mean = x.mean + delta * 0.5;
+    r.m2 = x.m2 + y.m2 + delta * delta * (x.n * 0.5);
+    return r;
+}
+
+// block_welford_fast for a full tile (all 256 lanes hold EPT returns): butterfly inside each
+// wave, then the 4 wave results as a pairwise tree ((w0,w1),(w2,w3)).  Result in thread 0.
+__device__ __forceinline__ Welford block_welford_full(Welford v, Welford* sh) {
+#pragma unroll
+    for (int off = kWave / 2; off > 0; off >>= 1) {
+        Welford o;
+        o.n = __shfl_xor(v.n, off, kWave);
+        o.mean = __shfl_xor(v.mean, off, kWave);
+        o.m2 = __shfl_xor(v.m2, off, kWave);
+        v = chan_eq(v, o);
+    }
+    const int w = threadIdx.x / kWave;
+    if ((threadIdx.x & (kWave - 1)) == 0) sh[w] = v;
+    __syncthreads();
+    static_assert(NWAVE == 4, "pairwise wave fold assumes 4 waves");
+    return chan_eq(chan_eq(sh[0], sh[1]), chan_eq(sh[2], sh[3]));
+}
+
+// a / b, correctly rounded, from y = RN(1/b): q0 = RN(a*y) is faithful, and one correction
+// with the exact fma residual a - q0*b rounds to RN(a/b) (Markstein) -- 3 operations instead
+// of the ~10 of a full f64 division, for the rew_norm `returns / sqrt(var + eps)`
+// (a2c.py:110-111).  Non-finite quotients pass through.
+__device__ __forceinline__ double div_by(double a, double b, double y) {
+    const double q0 = a * y;
+    const double r = __builtin_fma(-q0, b, a);
+    return __builtin_isfinite(r) ? __builtin_fma(r, y, q0) : q0;
+}
+
 // One tile [tb, te) with carry-in `carry` (= adv at te, 0 beyond a segment end).
 // Returns the carry for the tile to its left (adv at tb).
 template <bool F64V, bool VEC>
@@ -275,6 +316,7 @@ __device__ double gae_tile(const GaeArgs& p, int64_t tb, int64_t te, double carr
     const double carry_out = so.total.a + so.total.b * carry;
 
     double g = x;
+    const double rscale = 1.0 / scale;
     double adv[EPT], ret[EPT];
 #pragma unroll
     for (int k = EPT - 1; k >= 0; --k) {
@@ -294,7 +336,8 @@ __device__ double gae_tile(const GaeArgs& p, int64_t tb, int64_t te, double carr
         if (p.ret) {
             float r[EPT];
 #pragma unroll
-            for (int k = 0; k < EPT; ++k) r[k] = F64V ? (float)(ret[k] / scale) : (float)ret[k];
+            for (int k = 0; k < EPT; ++k)
+                r[k] = F64V ? (float)div_by(ret[k], scale, rscale) : (float)ret[k];
             float4* o = reinterpret_cast<float4*>(p.ret + base);
             o[0] = make_float4(r[0], r[1], r[2], r[3]);
             o[1] = make_float4(r[4], r[5], r[6], r[7]);
@@ -315,7 +358,7 @@ __device__ double gae_tile(const GaeArgs& p, int64_t tb, int64_t te, double carr
             if (e.validb & (1u << k)) {
                 const int64_t i = base + k;
                 if (p.adv) p.adv[i] = (float)adv[k];
-                if (p.ret) p.ret[i] = F64V ? (float)(ret[k] / scale) : (float)ret[k];
+                if (p.ret) p.ret[i] = F64V ? (float)div_by(ret[k], scale, rscale) : (float)ret[k];
                 if (p.adv64) p.adv64[i] = adv[k];
                 if (p.ret64) p.ret64[i] = ret[k];
             }
@@ -335,7 +378,8 @@ __device__ double gae_tile(const GaeArgs& p, int64_t tb, int64_t te, double carr
             for (int k = 0; k < EPT; ++k)
                 if (e.validb & (1u << k)) { const double dv = ret[k] - w.mean; w.m2 += dv * dv; }
         }
-        Welford t = block_welford_fast(w, reinterpret_cast<Welford*>(wsh));
+        Welford t = VEC ? block_welford_full(w, reinterpret_cast<Welford*>(wsh))
+                        : block_welford_fast(w, reinterpret_cast<Welford*>(wsh));
         if (threadIdx.x == 0) *acc = chan(t, *acc);
     }
     __syncthreads();  // lds reuse by the next tile
@@ -346,12 +390,134 @@ __device__ __forceinline__ double load_scale(const GaeArgs& p) {
     return p.scale ? *p.scale : 1.0;
 }
 
+// LDS staging for one full, aligned tile (the sample(0) row layout at every row_len that is
+// a multiple of 8).  rew (f64) and v_s_ arrive with fully coalesced 16-byte loads (lane l of
+// a wave reads vector l: one 1 KB span per instruction, instead of the 4 KB / 2 KB spans a
+// thread-owns-8-elements load touches) and are redistributed through LDS; after the scan the
+// same regions carry adv and ret (f32) back out as coalesced stores.  v_s and the u8 flags
+// keep per-thread loads (32 B and 8 B per lane).
+struct Stage {
+    double rew[TILE];  // rew; after the scan, ret as f32 in the first half
+    float vn[TILE];    // v_s_; after the scan, adv as f32
+};
+
+template <bool F64V>
+__device__ double gae_tile_staged(const GaeArgs& p, int64_t tb, double carry, double scale,
+                                  Stage& st, Aff* lds, double* wsh, Welford* acc) {
+    const int t = threadIdx.x;
+    {
+        const double2* r2 = reinterpret_cast<const double2*>(p.rew + tb);
+        const float4* n4 = reinterpret_cast<const float4*>(p.vn + tb);
+        double2 r[4];
+        float4 nv[2];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r[j] = r2[t + TPB * j];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) nv[j] = n4[t + TPB * j];
+        double2* sr = reinterpret_cast<double2*>(st.rew);
+        float4* sn = reinterpret_cast<float4*>(st.vn);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sr[t + TPB * j] = r[j];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) sn[t + TPB * j] = nv[j];
+    }
+    const int64_t base = tb + (int64_t)t * EPT;
+    const float4* s4 = reinterpret_cast<const float4*>(p.vs + base);
+    const float4 s0 = s4[0], s1 = s4[1];
+    const uint2 tm = *reinterpret_cast<const uint2*>(p.term + base);
+    const uint2 tr = *reinterpret_cast<const uint2*>(p.trunc + base);
+    uint2 ex = make_uint2(0u, 0u);
+    if (p.extra) ex = *reinterpret_cast<const uint2*>(p.extra + base);
+    __syncthreads();
+
+    const float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    Elems e;
+    e.endb = 0;
+    e.validb = 0;
+    {
+        const double2* sr = reinterpret_cast<const double2*>(st.rew + t * EPT);
+        const float4* sn = reinterpret_cast<const float4*>(st.vn + t * EPT);
+        const double2 r0 = sr[0], r1 = sr[1], r2 = sr[2], r3 = sr[3];
+        const float4 n0 = sn[0], n1 = sn[1];
+        const double rv[8] = {r0.x, r0.y, r1.x, r1.y, r2.x, r2.y, r3.x, r3.y};
+        const float nvv[8] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w};
+        int64_t rem = p.row_len > 0 ? (base + 1) % p.row_len : 0;
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) {
+            const uint32_t wt = k < 4 ? tm.x : tm.y;
+            const uint32_t wr = k < 4 ? tr.x : tr.y;
+            const uint32_t wx = k < 4 ? ex.x : ex.y;
+            const int sh = (k & 3) * 8;
+            bool forced = false;
+            if (p.row_len > 0) {
+                forced = rem == 0;
+                rem = (rem + 1 == p.row_len) ? 0 : rem + 1;
+            }
+            make_elem<F64V, float>(p, k, base + k, rv[k], sv[k], nvv[k], (uint8_t)(wt >> sh),
+                                   (uint8_t)(wr >> sh), (uint8_t)(wx >> sh), forced, scale, e);
+        }
+    }
+    const Aff m = local_map(e, p.gl);
+    // The scan's barrier orders every thread's LDS reads above before the writes below.
+    const ScanOut so = block_suffix_scan(m, lds);
+    const double x = so.excl.a + so.excl.b * carry;
+    const double carry_out = so.total.a + so.total.b * carry;
+
+    double g = x;
+    const double rscale = 1.0 / scale;
+    double ret[EPT];
+    float* sadv = st.vn + t * EPT;
+    float* sret = reinterpret_cast<float*>(st.rew) + t * EPT;
+#pragma unroll
+    for (int k = EPT - 1; k >= 0; --k) {
+        const double c = (e.endb & (1u << k)) ? 0.0 : p.gl;
+        g = e.d[k] + c * g;
+        sadv[k] = (float)g;
+        // v_s for the return is re-derived from the f32 input (as make_elem does) rather
+        // than kept in e.vsd: 16 fewer live VGPRs across the scan.
+        ret[k] = g + (F64V ? (double)sv[k] * scale : (double)sv[k]);
+        sret[k] = F64V ? (float)div_by(ret[k], scale, rscale) : (float)ret[k];
+    }
+    if (F64V && p.partials) {
+        Welford w;
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) s += ret[k];
+        w.n = (double)EPT;
+        w.mean = s / w.n;
+        w.m2 = 0.0;
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) { const double dv = ret[k] - w.mean; w.m2 += dv * dv; }
+        // block_welford_fast's barrier also publishes the f32 adv/ret written above.
+        Welford tw = block_welford_full(w, reinterpret_cast<Welford*>(wsh));
+        if (threadIdx.x == 0) *acc = chan(tw, *acc);
+    } else {
+        __syncthreads();
+    }
+    {
+        const float4* sn = reinterpret_cast<const float4*>(st.vn);
+        const float4* sr = reinterpret_cast<const float4*>(st.rew);
+        if (p.adv) {
+            float4* o = reinterpret_cast<float4*>(p.adv + tb);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) o[t + TPB * j] = sn[t + TPB * j];
+        }
+        if (p.ret) {
+            float4* o = reinterpret_cast<float4*>(p.ret + tb);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) o[t + TPB * j] = sr[t + TPB * j];
+        }
+    }
+    __syncthreads();  // LDS reuse by the next tile
+    return carry_out;
+}
+
 // Fast path: block b owns [b*range_len, min((b+1)*range_len, n)), independent of others.
 template <bool F64V>
 __global__ __launch_bounds__(TPB) void gae_rows_kernel(GaeArgs p, int64_t range_len,
                                                        int vec_ok) {
     __shared__ Aff lds[NWAVE];
-    __shared__ double wsh[F64V ? 3 * TPB : 1];
+    __shared__ double wsh[F64V ? 3 * NWAVE : 1];
     const int64_t s = (int64_t)blockIdx.x * range_len;
     const int64_t e = min(s + range_len, p.n);
     const double scale = load_scale(p);
@@ -367,6 +533,26 @@ __global__ __launch_bounds__(TPB) void gae_rows_kernel(GaeArgs p, int64_t range_
         else
             carry = gae_tile<F64V, false>(p, tb, te, carry, scale, lds, wsh, &acc);
     }
+    if (F64V && p.partials && threadIdx.x == 0) {
+        p.partials[3 * blockIdx.x + 0] = acc.n;
+        p.partials[3 * blockIdx.x + 1] = acc.mean;
+        p.partials[3 * blockIdx.x + 2] = acc.m2;
+    }
+}
+
+// Staged variant of gae_rows_kernel for the layout bench / process_fn produce: rows of
+// row_len % TILE == 0 transitions, n % row_len == 0, 16-byte aligned f32 outputs only.
+template <bool F64V>
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(4, 8))) void gae_rows_staged_kernel(GaeArgs p, int64_t range_len) {
+    __shared__ Aff lds[NWAVE];
+    __shared__ double wsh[F64V ? 3 * NWAVE : 1];
+    __shared__ Stage st;
+    const int64_t s = (int64_t)blockIdx.x * range_len;
+    const double scale = load_scale(p);
+    double carry = 0.0;
+    Welford acc = {0.0, 0.0, 0.0};
+    for (int64_t tb = s + range_len - TILE; tb >= s; tb -= TILE)
+        carry = gae_tile_staged<F64V>(p, tb, carry, scale, st, lds, wsh, &acc);
     if (F64V && p.partials && threadIdx.x == 0) {
         p.partials[3 * blockIdx.x + 0] = acc.n;
         p.partials[3 * blockIdx.x + 1] = acc.mean;
@@ -525,6 +711,18 @@ extern "C" int tsrl_gae(const float* v_s, const float* v_s_next, const double* r
         const int64_t r = range_len_for(row_len);
         const int64_t grid = (n + r - 1) / r;
         TSRL_CHECK_ARG(grid < (1ll << 31), "tsrl_gae: too many ranges");
+        const bool staged = vec_ok && !adv64_out && !ret64_out && r % TILE == 0 &&
+                            n % r == 0 && !getenv("TSRL_GAE_UNSTAGED");
+        if (staged) {
+            if (f64v)
+                hipLaunchKernelGGL(gae_rows_staged_kernel<true>, dim3((unsigned)grid), dim3(TPB),
+                                   0, s, p, r);
+            else
+                hipLaunchKernelGGL(gae_rows_staged_kernel<false>, dim3((unsigned)grid), dim3(TPB),
+                                   0, s, p, r);
+            TSRL_LAUNCH_CHECK("tsrl_gae(rows, staged)");
+            return 0;
+        }
         if (f64v)
             hipLaunchKernelGGL(gae_rows_kernel<true>, dim3((unsigned)grid), dim3(TPB), 0, s, p, r,
                                vec_ok);
