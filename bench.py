@@ -49,7 +49,10 @@ def parse():
     ap.add_argument("--repeat", type=int, default=4)
     ap.add_argument("--minibatches", type=int, default=32)
     ap.add_argument("--ep-len", type=int, default=None)
-    ap.add_argument("--perm", choices=["numpy", "device"], default="device")
+    ap.add_argument("--perm", choices=["numpy", "device", "sorted"], default="sorted",
+                    help="minibatch permutation: numpy (reference stream), device "
+                         "(torch.randperm), sorted (torch.randperm, rows of each minibatch "
+                         "in ascending buffer order: same minibatch sets)")
     ap.add_argument("--cpu-steps", type=int, default=None,
                     help="T' of the bounded CPU-baseline sample (envs x T')")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -127,7 +130,7 @@ def build_atari(args, dev, rank):
                        eps_clip=0.1, value_clip=True, dual_clip=None,
                        advantage_normalization=False, recompute_advantage=False,
                        reward_normalization=False,
-                       perm_device=(args.perm == "device")).to(dev)
+                       perm_device=(args.perm != "numpy")).to(dev)
     buf = VectorReplayBuffer(E * T, E, stack_num=4, ignore_obs_next=True,
                              save_only_last_obs=True, device=dev)
     return Collector(policy, env, buf, exploration_noise=True), policy, buf
@@ -174,10 +177,11 @@ def main():
                            reward_normalization=True, advantage_normalization=True,
                            recompute_advantage=False, eps_clip=0.2, value_clip=False,
                            dual_clip=None, action_bound_method="clip",
-                           perm_device=(args.perm == "device")).to(dev)
+                           perm_device=(args.perm != "numpy")).to(dev)
         buf = VectorReplayBuffer(n, E, device=dev)
         coll = Collector(policy, env, buf)
     policy.graph_learn = not args.eager_learn
+    policy.sort_minibatch = args.perm == "sorted"
     timer = GaeTimer()
     pbase.GAE_HOOK = timer
     phase = {"collect": 0.0, "update": 0.0}

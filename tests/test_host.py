@@ -130,3 +130,34 @@ def test_device_stats_construct_without_gpu_use():
     assert r.dp == "dp"
     s = DeviceScalarRMS("cpu")
     assert (s.mean, s.var, s.count) == (0.0, 1.0, 0)
+
+
+@pytest.mark.parametrize("n,bs", [(1024, 128), (1000, 128), (1000, 300), (7, 10)])
+def test_sorted_minibatch_permutation_same_sets(n, bs):
+    """PPOPolicy.sort_minibatch: each minibatch holds the same rows as Batch.split over the
+    reference's np.random.permutation stream, visited in ascending order."""
+    import types
+    import torch
+    from tianshou_amd.policy.ppo import PPOPolicy, split_bounds
+    fake = types.SimpleNamespace(perm_device=False, sort_minibatch=True)
+    np.random.seed(5)
+    got = PPOPolicy._permutation(fake, n, torch.device("cpu"), bs).numpy()
+    np.random.seed(5)
+    want = np.random.permutation(n)
+    for s, e in split_bounds(n, bs, merge_last=True):
+        np.testing.assert_array_equal(got[s:e], np.sort(want[s:e]))
+
+
+@pytest.mark.parametrize("n,bs", [(1024, 128), (1000, 128), (1000, 300), (7, 10)])
+def test_sorted_minibatch_device_labels(n, bs):
+    """Device path of sort_minibatch: the returned order is a permutation whose Batch.split
+    chunks are ascending and have the split sizes."""
+    import types
+    import torch
+    from tianshou_amd.policy.ppo import PPOPolicy, split_bounds
+    fake = types.SimpleNamespace(perm_device=True, sort_minibatch=True)
+    torch.manual_seed(0)
+    got = PPOPolicy._permutation(fake, n, torch.device("cpu"), bs).numpy()
+    np.testing.assert_array_equal(np.sort(got), np.arange(n))
+    for s, e in split_bounds(n, bs, merge_last=True):
+        assert np.all(np.diff(got[s:e]) > 0)

@@ -24,6 +24,8 @@ def main():
                     help="time one kernel only (l1_fwd, l1_fwd_x6, tail, dw, minibatch): PMC passes")
     ap.add_argument("--contig", action="store_true",
                     help="minibatch rows contiguous (no permutation gather)")
+    ap.add_argument("--sorted", action="store_true",
+                    help="random minibatch rows, gathered in ascending row order")
     a = ap.parse_args()
     from tianshou_amd import _C
     from tianshou_amd.dist import DataParallel
@@ -44,6 +46,8 @@ def main():
     ret = torch.randn(N, device=dev)
     v_s = torch.randn(N, device=dev)
     idx = None if a.contig else torch.randperm(N, device=dev)[:B]
+    if a.sorted:
+        idx = idx.sort().values
     p = _C.PPOParams()
     p.eps_clip, p.dual_clip, p.vf_coef, p.ent_coef, p.adv_eps = 0.2, 0.0, 0.25, 0.0, 1e-8
     p.b_global, p.value_clip, p.norm_adv = float(B), 0, 1
