@@ -60,9 +60,10 @@ def parse():
                     help="diagnostic: under torch.distributed.run with ONE rank, run the "
                          "data-parallel code path (RCCL collectives over a one-rank "
                          "communicator) -- rehearses the N>1 path on a one-GPU box")
-    ap.add_argument("--eager-learn", action="store_true",
-                    help="diagnostic: run learn() eagerly (no HIP-graph epoch replay), as the "
-                         "data-parallel (N>1) path does")
+    ap.add_argument("--graph-learn", choices=["auto", "on", "off"], default="auto",
+                    help="learn() epochs from captured HIP graphs: auto = only for minibatches "
+                         "< 65536 rows (PPOPolicy default); on at the headline shape measured "
+                         "~5 %% slower per update than eager launches")
     a = ap.parse_args()
     defaults = dict(humanoid=(4096, 2048, 376, 17, 256, 1000),
                     small=(512, 128, 17, 6, 128, 1000),
@@ -180,7 +181,7 @@ def main():
                            perm_device=(args.perm != "numpy")).to(dev)
         buf = VectorReplayBuffer(n, E, device=dev)
         coll = Collector(policy, env, buf)
-    policy.graph_learn = not args.eager_learn
+    policy.graph_learn = {"auto": None, "on": True, "off": False}[args.graph_learn]
     policy.sort_minibatch = args.perm == "sorted"
     timer = GaeTimer()
     pbase.GAE_HOOK = timer
@@ -263,6 +264,7 @@ def main():
                        "minibatch": n // args.minibatches * world,
                        "parallelism": f"env-sharded dp{world}",
                        "permutation": args.perm,
+                       "learn_graph": args.graph_learn,
                        "collect_s": phase["collect"] / args.steps,
                        "update_s": phase["update"] / args.steps},
             "roofline": {"kernel": "tsrl_gae (gae_rows_kernel)", "bound": "hbm",

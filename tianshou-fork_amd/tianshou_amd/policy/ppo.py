@@ -166,8 +166,13 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
         # the get_actor_critic shape (policy/fused_mlp.py); fused_mlp=False keeps the torch
         # layers + fused loss kernel.
         self._init_fused_eval(actor, critic, dist_fn, fused_mlp)
-        # replay whole epochs of the fused minibatch step from a captured HIP graph
-        self.graph_learn = True
+        # graph_learn=True replays whole epochs of the fused minibatch step from a captured
+        # HIP graph; None (default) = only for minibatches below GRAPH_LEARN_MAX_ROWS.  Large
+        # minibatches launch eagerly: with ~15 launches per 0.75 ms minibatch the host stays
+        # far ahead of the GPU, and eager launches measured 100 ms per update vs 105 ms for
+        # graph replay (bench.py, MI355X, 4096x2048: graph nodes cost more per kernel); small
+        # ones (config 2: 2048 rows, ~50 us of GPU work) are host-bound without the graph.
+        self.graph_learn = None
         self._learn_graph = None
         # clip_grad_norm_ + Adam as one HIP pass over flat parameter storage (csrc/optim.hip)
         self.fused_adam = True
@@ -245,7 +250,7 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
             if mlp_ok and self.fused_adam:
                 self._mlp.bind_adam(self.optim)
             obs_all = self._mlp.rows(batch.obs) if mlp_ok else None
-            if mlp_ok and self._graph_ready():
+            if mlp_ok and self._use_graph(batch_size) and self._graph_ready():
                 terms.append(self._epoch_graph(obs_all, (act, logp_old, adv, ret, v_s), perm, n,
                                                batch_size, first=(step == 0)))
                 continue
@@ -290,11 +295,18 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
         self.optim.step()
 
     # -- HIP-graph replay of whole epochs ------------------------------------------------------
+    GRAPH_LEARN_MAX_ROWS = 65536
+
+    def _use_graph(self, batch_size: int) -> bool:
+        if self.graph_learn is None:
+            return batch_size < self.GRAPH_LEARN_MAX_ROWS
+        return bool(self.graph_learn)
+
     def _graph_ready(self) -> bool:
         """An epoch of fused minibatches can be captured once and replayed: single process
         (no collective in the step), no advantage recomputation, and a capturable optimiser
         whose state already exists (the first update runs eagerly)."""
-        if not self.graph_learn or self.dp.active or self._recompute_adv:
+        if self.graph_learn is False or self.dp.active or self._recompute_adv:
             return False
         opt = self.optim
         if self._mlp is not None and self._mlp.adam_bound(opt):
