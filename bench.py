@@ -267,7 +267,7 @@ def main():
                        "learn_graph": args.graph_learn,
                        "collect_s": phase["collect"] / args.steps,
                        "update_s": phase["update"] / args.steps},
-            "roofline": {"kernel": "tsrl_gae (gae_rows_kernel)", "bound": "hbm",
+            "roofline": {"kernel": "tsrl_gae (gae_rows_staged_kernel)", "bound": "hbm",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "launch_us": gae_ms * 1e3,
