@@ -113,3 +113,38 @@ def test_atari_fused_cat_learn_matches_torch_formulation(dev):
         np.testing.assert_allclose(results[0][0][k], results[1][0][k], rtol=1e-4, atol=1e-5)
     for k, v in results[0][1].items():
         np.testing.assert_allclose(v.numpy(), results[1][1][k].numpy(), rtol=1e-3, atol=1e-5)
+
+
+def test_atari_shared_trunk_process_fn_matches_separate_passes(dev):
+    """process_fn with the shared DQN trunk (one trunk pass per row for V(s) and logp_old,
+    V(s') read from V(s) through next(), base.py:380-381) against the reference's three
+    separate passes (a2c.py:86-93 critic(obs), critic(obs_next); ppo.py:95-96 actor(obs))."""
+    from tianshou_amd.policy.base import gae_device
+    E, T, L = 8, 24, 9
+    _, policy, buf, coll = _setup(dev, E, T, L, seed=2)
+    policy._rew_norm = False
+    assert policy._shared_trunk
+    coll.collect(n_step=E * T)
+    batch, idx = buf.sample(0)
+    with torch.no_grad():
+        v_ref = policy.critic(batch.obs).flatten()
+        vn_ref = policy.critic(batch.obs_next).flatten()
+        x, _ = policy.actor(batch.obs)
+        lp_ref = torch.distributions.Categorical(logits=x).log_prob(batch.act.reshape(-1))
+    p = policy._next_positions(buf, idx, dev)
+    assert p is not None
+    want_p = buf.next(idx)  # host next() over the same ring
+    assert np.array_equal(p.cpu().numpy(), want_p)
+    out = policy.process_fn(batch, buf, idx)
+    np.testing.assert_allclose(out.v_s.cpu().numpy(), v_ref.cpu().numpy(), rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(out.logp_old.cpu().numpy(), lp_ref.cpu().numpy(), rtol=1e-5,
+                               atol=1e-6)
+    adv, ret, _, _ = gae_device(v_ref.contiguous(), vn_ref.contiguous(),
+                                batch.rew.contiguous(), batch.terminated.contiguous(),
+                                batch.truncated.contiguous(), 0.99, 0.95, T)
+    np.testing.assert_allclose(out.adv.cpu().numpy(), adv.cpu().numpy(), rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(out.returns.cpu().numpy(), ret.cpu().numpy(), rtol=1e-5,
+                               atol=1e-5)
+    # a partial sample whose next rows are missing falls back to evaluating obs_next
+    sub = idx[::3]
+    assert policy._next_positions(buf, sub, dev) is None

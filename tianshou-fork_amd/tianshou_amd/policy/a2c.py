@@ -55,8 +55,35 @@ class A2CPolicy(PGPolicy):
         return out
 
     def _eval_values(self, batch, obs, obs_next, buffer, indices):
-        """V(s) and V(s') of a2c.py:86-93."""
-        return self._values(obs), self._values(obs_next)
+        """V(s) and V(s') of a2c.py:86-93 (V(s') read from V(s) when obs_next rows are
+        rows of obs, see _next_positions)."""
+        v_s = self._values(obs)
+        p = self._next_positions(buffer, indices, obs.device)
+        return v_s, (v_s[p] if p is not None else self._values(obs_next))
+
+    @staticmethod
+    def _next_positions(buffer, indices, dev) -> Optional[torch.Tensor]:
+        """Buffers that do not store obs_next (ignore_obs_next) return
+        ``obs_next[i] = get(next(indices[i]), "obs")`` (base.py:380-381): byte for byte the
+        ``obs`` row of the batch position j with ``indices[j] == next(indices[i])`` (stacked
+        the same way, manager.py:279-297).  Returns those positions when every next-row is in
+        the batch (always for sample(0)), else None.  Per-row critic outputs do not depend on
+        the other rows, so ``V(obs_next) = V(obs)[p]``."""
+        if getattr(buffer, "_save_obs_next", True) or not hasattr(buffer, "_step_dev") or \
+                indices is None:
+            return None
+        idx = np.asarray(indices, np.int64).reshape(-1)
+        n = len(idx)
+        if n == 0:
+            return None
+        it = torch.as_tensor(idx % buffer.maxsize, device=dev)
+        nxt = buffer._step_dev(it, -1)
+        pos = torch.full((buffer.maxsize,), -1, dtype=torch.int64, device=dev)
+        pos[it] = torch.arange(n, device=dev)
+        p = pos[nxt]
+        if bool((p < 0).any()):
+            return None
+        return p
 
     @staticmethod
     def _gae_layout(buffer, indices):

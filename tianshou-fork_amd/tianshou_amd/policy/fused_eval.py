@@ -13,7 +13,7 @@ from torch.distributions import Independent, Normal
 
 from tianshou_amd import _C
 from tianshou_amd.policy import fused_mlp as _fmlp
-from tianshou_amd.utils.net import ActorProb
+from tianshou_amd.utils.net import ActorProb, DiscreteActor, DiscreteCritic
 
 
 def _is_fixed_std_normal(dist_fn) -> bool:
@@ -64,6 +64,10 @@ class FusedEvalMixin:
         # the get_actor_critic MLPs as fused HIP kernels (policy/fused_mlp.py)
         self._mlp = None
         self._pending_logp = None
+        # one preprocess net under both heads (examples/atari/atari_ppo.py:104-125 shares the
+        # features_only DQN trunk): the trunk runs once per row for V(s) and the actor output
+        self._shared_trunk = isinstance(actor, DiscreteActor) and \
+            isinstance(critic, DiscreteCritic) and actor.preprocess is critic.preprocess
         if self._fused and fused_mlp:
             layers = _fmlp.match(actor, critic)
             if layers is not None:
@@ -95,6 +99,8 @@ class FusedEvalMixin:
         the stored obs_next of step t unless the episode ended at t), so only the episode-end
         and segment-end rows are evaluated on obs_next; the values are bit-identical to a full
         evaluation because every row's arithmetic is independent of the other rows."""
+        if self._cat is not None and self._shared_trunk and obs.is_cuda:
+            return self._eval_values_shared(batch, obs, obs_next, buffer, indices)
         if self._mlp is None or not obs.is_cuda or obs.dtype != torch.float32 or obs.dim() != 2:
             return super()._eval_values(batch, obs, obs_next, buffer, indices)
         obs = obs.contiguous()
@@ -129,6 +135,35 @@ class FusedEvalMixin:
             _C.check(L.tsrl_gauss_logp(_C.ptr(mu), _C.ptr(log_std), _C.ptr(act[s:e]), e - s, A,
                                        _C.ptr(out[s:e]), _C.stream_ptr(dev)), "tsrl_gauss_logp")
         return out
+
+    def _trunk_heads(self, obs: torch.Tensor):
+        """(actor output, V) of a shared-trunk DiscreteActor / DiscreteCritic pair with ONE
+        trunk pass: actor.forward (utils/net.py DiscreteActor, discrete.py:52-71) and
+        critic.forward (discrete.py:111-121) both start with preprocess(obs, None) on the same
+        module, so the features are computed once and fed to both heads.  Forward values are
+        those of the two separate passes; in backward the two heads' feature gradients are
+        summed before the trunk instead of after it (float summation order only)."""
+        h, _ = self.actor.preprocess(obs, None)
+        x = self.actor.last(h)
+        if self.actor.softmax_output:
+            x = torch.softmax(x, dim=-1)
+        return x, self.critic.last(h).flatten()
+
+    def _eval_values_shared(self, batch, obs, obs_next, buffer, indices):
+        """Shared-trunk process_fn evaluation: V(s) and logp_old (kept for _logp_old) from one
+        trunk pass per row; V(s') from V(s) when the buffer's obs_next rows are batch rows."""
+        n = obs.shape[0]
+        dev = obs.device
+        v_s = torch.empty(n, dtype=torch.float32, device=dev)
+        logp = torch.empty(n, dtype=torch.float32, device=dev)
+        act = torch.as_tensor(batch.act, device=dev).reshape(n)
+        for s, e in self._chunks(n, obs[0].numel() if n else 1):
+            x, v = self._trunk_heads(obs[s:e])
+            v_s[s:e] = v
+            logp[s:e] = cat_logp(x, act[s:e], self._cat)
+        self._pending_logp = logp
+        p = self._next_positions(buffer, indices, dev)
+        return v_s, (v_s[p] if p is not None else self._values(obs_next))
 
     def _logp_cat(self, obs: torch.Tensor, act: torch.Tensor) -> torch.Tensor:
         n = obs.shape[0]

@@ -375,8 +375,11 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
             for s, e in split_bounds(n, batch_size, merge_last=True):
                 idx = perm[s:e]
                 obs_mb = gather_rows(batch.obs, idx)
-                x, _ = self.actor(obs_mb)
-                value = self.critic(obs_mb).flatten()
+                if self._shared_trunk:
+                    x, value = self._trunk_heads(obs_mb)
+                else:
+                    x, _ = self.actor(obs_mb)
+                    value = self.critic(obs_mb).flatten()
                 params = self._params((e - s) * self.dp.world)
                 loss, t = _CatPPOLoss.apply(x, value, (act, logp_old, adv, ret, v_s, idx, params,
                                                        self.dp, self._cat))

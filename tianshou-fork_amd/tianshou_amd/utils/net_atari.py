@@ -5,7 +5,11 @@ the Nature-DQN conv trunk over a uint8 4x84x84 frame stack scaled by 1/255
 
 The convolutions and the two linear layers run on MIOpen / hipBLASLt through PyTorch-ROCm
 (the conv trunk is MFMA-bound library work); the PPO loss around it is the
-fused tsrl_ppo_cat kernel (policy/ppo.py)."""
+fused tsrl_ppo_cat kernel (policy/ppo.py).  The conv weights and the scaled input are kept
+channels_last (NHWC): MIOpen's NHWC f32 kernels measured 7.1 vs 8.8 ms per 8192-row
+minibatch forward+backward on MI355X (tools/atari_trunk_bench.py); values are the same
+function of the same weights (summation order only), and state_dict() holds the same
+tensors."""
 from typing import Any, Dict, Optional, Sequence
 
 import numpy as np
@@ -26,7 +30,8 @@ class DQN(nn.Module):
 
     def __init__(self, c: int, h: int, w: int, action_shape: Sequence[int], device="cpu",
                  features_only: bool = False, output_dim: Optional[int] = None,
-                 layer_init=lambda x: x, scale: float = 255.0) -> None:
+                 layer_init=lambda x: x, scale: float = 255.0,
+                 channels_last: bool = True) -> None:
         super().__init__()
         self.device = device
         self.scale = scale
@@ -46,10 +51,15 @@ class DQN(nn.Module):
             self.net = nn.Sequential(self.net, layer_init(nn.Linear(self.output_dim, output_dim)),
                                      nn.ReLU(inplace=True))
             self.output_dim = output_dim
+        self.channels_last = channels_last
+        if channels_last:
+            self.net.to(memory_format=torch.channels_last)
 
     def forward(self, obs, state: Any = None, info: Dict[str, Any] = {}):
         obs = torch.as_tensor(obs, device=self.device)
         x = obs.to(torch.float32)
         if self.scale:
             x = x / self.scale  # scale_obs (atari_network.py:18-30)
+        if self.channels_last:
+            x = x.contiguous(memory_format=torch.channels_last)
         return self.net(x), state
