@@ -136,7 +136,10 @@ def test_atari_shared_trunk_process_fn_matches_separate_passes(dev):
     want_p = buf.next(idx)  # host next() over the same ring
     assert np.array_equal(p.cpu().numpy(), want_p)
     out = policy.process_fn(batch, buf, idx)
-    np.testing.assert_allclose(out.v_s.cpu().numpy(), v_ref.cpu().numpy(), rtol=1e-6, atol=1e-7)
+    # same weights, same rows; MIOpen may pick other kernels for the other call sequence
+    vmax = float(v_ref.abs().max())
+    np.testing.assert_allclose(out.v_s.cpu().numpy(), v_ref.cpu().numpy(), rtol=1e-5,
+                               atol=1e-5 * vmax)
     np.testing.assert_allclose(out.logp_old.cpu().numpy(), lp_ref.cpu().numpy(), rtol=1e-5,
                                atol=1e-6)
     adv, ret, _, _ = gae_device(v_ref.contiguous(), vn_ref.contiguous(),

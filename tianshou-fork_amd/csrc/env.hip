@@ -161,10 +161,14 @@ __global__ __launch_bounds__(1024) void box_step_reset_kernel(
 // time max(t - (S-1-q), t0) (t0 = the episode's first time step, whose frame a reset repeats
 // S times).  fk[r][q] holds the key of that frame; S == 1 is the plain u8 observation.
 constexpr int MAX_STACK = 8;
+// u8 frame rows per workgroup: one row (28 KB of hashed bytes for 4x84x84) keeps 1024 env
+// rows on 1024 workgroups; 16 rows per workgroup left 64 workgroups for 256 CUs
+// (rocprofv3: 131 us per 1024-row step).
+constexpr int U8_ROWS = 1;
 
 __device__ void u8_rows(const RowState* rs, const uint64_t (*fk)[MAX_STACK], int64_t r0,
                         int64_t k, int64_t nbytes, int S, uint8_t* obs) {
-    const int nrows = (int)min((int64_t)ROWS, k - r0);
+    const int nrows = (int)min((int64_t)U8_ROWS, k - r0);
     const int64_t fbytes = nbytes / S;
     for (int r = 0; r < nrows; ++r) {
         if (!rs[r].active) continue;
@@ -207,10 +211,10 @@ __global__ __launch_bounds__(TPB) void u8_step_kernel(const int64_t* ids, int64_
                                                       int64_t ep_len, int64_t* ep_j,
                                                       int64_t* ep_t, uint8_t* obs, double* rew,
                                                       uint8_t* term, uint8_t* trunc) {
-    __shared__ RowState rs[ROWS];
-    __shared__ uint64_t fk[ROWS][MAX_STACK];
-    const int64_t r0 = (int64_t)blockIdx.x * ROWS;
-    if (threadIdx.x < ROWS) {
+    __shared__ RowState rs[U8_ROWS];
+    __shared__ uint64_t fk[U8_ROWS][MAX_STACK];
+    const int64_t r0 = (int64_t)blockIdx.x * U8_ROWS;
+    if (threadIdx.x < U8_ROWS) {
         const int64_t r = r0 + threadIdx.x;
         RowState st = {0ull, 0};
         if (r < k) {
@@ -238,10 +242,10 @@ __global__ __launch_bounds__(TPB) void u8_reset_kernel(const int64_t* ids, const
                                                        uint64_t s_seed, int64_t ep_len,
                                                        int64_t* ep_j, int64_t* ep_t,
                                                        uint8_t* obs) {
-    __shared__ RowState rs[ROWS];
-    __shared__ uint64_t fk[ROWS][MAX_STACK];
-    const int64_t r0 = (int64_t)blockIdx.x * ROWS;
-    if (threadIdx.x < ROWS) {
+    __shared__ RowState rs[U8_ROWS];
+    __shared__ uint64_t fk[U8_ROWS][MAX_STACK];
+    const int64_t r0 = (int64_t)blockIdx.x * U8_ROWS;
+    if (threadIdx.x < U8_ROWS) {
         const int64_t r = r0 + threadIdx.x;
         RowState st = {0ull, 0};
         if (r < k && (!mask || mask[r])) {
@@ -261,6 +265,7 @@ __global__ __launch_bounds__(TPB) void u8_reset_kernel(const int64_t* ids, const
 }
 
 inline unsigned blocks_for(int64_t k) { return (unsigned)((k + ROWS - 1) / ROWS); }
+inline unsigned u8_blocks_for(int64_t k) { return (unsigned)((k + U8_ROWS - 1) / U8_ROWS); }
 
 }  // namespace
 }  // namespace tsrl
@@ -335,8 +340,8 @@ extern "C" int tsrl_synth_u8_step(const int64_t* ids, int64_t k, int64_t obs_byt
     if (k == 0) return 0;
     TSRL_CHECK_ARG(ep_j && ep_t && obs_out && rew_out && term_out && trunc_out,
                    "tsrl_synth_u8_step: null pointer");
-    hipLaunchKernelGGL(u8_step_kernel, dim3(blocks_for(k)), dim3(TPB), 0, as_stream(stream), ids,
-                       k, obs_bytes, (int)frame_stack, sm64(seed), ep_len, ep_j, ep_t, obs_out,
+    hipLaunchKernelGGL(u8_step_kernel, dim3(u8_blocks_for(k)), dim3(TPB), 0, as_stream(stream),
+                       ids, k, obs_bytes, (int)frame_stack, sm64(seed), ep_len, ep_j, ep_t, obs_out,
                        rew_out, term_out, trunc_out);
     TSRL_LAUNCH_CHECK("tsrl_synth_u8_step");
     return 0;
@@ -353,7 +358,7 @@ extern "C" int tsrl_synth_u8_reset(const int64_t* ids, const uint8_t* mask, int6
                    MAX_STACK);
     if (k == 0) return 0;
     TSRL_CHECK_ARG(ep_j && ep_t && obs_out, "tsrl_synth_u8_reset: null pointer");
-    hipLaunchKernelGGL(u8_reset_kernel, dim3(blocks_for(k)), dim3(TPB), 0, as_stream(stream),
+    hipLaunchKernelGGL(u8_reset_kernel, dim3(u8_blocks_for(k)), dim3(TPB), 0, as_stream(stream),
                        ids, mask, k, obs_bytes, (int)frame_stack, sm64(seed), ep_len, ep_j, ep_t,
                        obs_out);
     TSRL_LAUNCH_CHECK("tsrl_synth_u8_reset");

@@ -221,6 +221,16 @@ class Collector:
         policy = result.get("policy", Batch())
         return act, policy
 
+    def _noise_active(self) -> bool:
+        """exploration_noise=True with a policy that keeps BasePolicy.exploration_noise (the
+        identity, base.py:121-133; every on-policy algorithm, e.g. examples/atari/atari_ppo.py's
+        Collector(..., exploration_noise=True)) changes nothing, so such steps stay eligible
+        for the fused act kernel and HIP-graph replay."""
+        if not self.exploration_noise:
+            return False
+        from tianshou_amd.policy.base import BasePolicy
+        return type(self.policy).exploration_noise is not BasePolicy.exploration_noise
+
     # -- fused device path ------------------------------------------------------------------
     def _act_spec(self):
         act_space = self._action_space
@@ -343,7 +353,7 @@ class Collector:
     def _collect_fused(self, n_step, n_episode, random, no_grad):
         self._alloc_scratch()
         prep = getattr(self.policy, "prepare_fused_act", None)
-        self._fused_act_on = bool(not random and not self.exploration_noise and
+        self._fused_act_on = bool(not random and not self._noise_active() and
                                   self.use_fused_act and prep is not None and prep())
         s, b, buf = self._scratch, self._base, self.buffer
         N = self.env_num
@@ -362,7 +372,7 @@ class Collector:
         while True:
             if (n_step is not None and self.graph_steps and not random and kk == N
                     and kk == buf.buffer_num and buf._ring.uniform_rel() is not None
-                    and eager_steps > 0 and not self.exploration_noise):
+                    and eager_steps > 0 and not self._noise_active()):
                 n_left = -(-(n_step - step_count) // N)
                 done_steps = self._replay_steps(no_grad, n_left, written)
                 step_count += done_steps * N

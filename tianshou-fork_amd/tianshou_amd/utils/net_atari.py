@@ -57,9 +57,10 @@ class DQN(nn.Module):
 
     def forward(self, obs, state: Any = None, info: Dict[str, Any] = {}):
         obs = torch.as_tensor(obs, device=self.device)
-        x = obs.to(torch.float32)
-        if self.scale:
-            x = x / self.scale  # scale_obs (atari_network.py:18-30)
-        if self.channels_last:
-            x = x.contiguous(memory_format=torch.channels_last)
+        if self.channels_last and obs.dim() == 4:
+            obs = obs.contiguous(memory_format=torch.channels_last)  # 1-byte frames
+        # scale_obs (atari_network.py:18-30) divides the frames in f64 and the trunk casts to
+        # f32 (:84); f32(u8) / 255 in f32 is bit-identical for all 256 byte values, and the
+        # division reads the u8 frames directly (one pass, NHWC kept)
+        x = (obs / self.scale).to(torch.float32) if self.scale else obs.to(torch.float32)
         return self.net(x), state
