@@ -214,6 +214,13 @@ int tsrl_stack_gather(const void* src, int64_t frame_bytes, const int64_t* idx, 
                       const int64_t* lengths, int64_t size, int64_t num, void* dst,
                       int64_t* chain_out, void* stream);
 
+/* Frame-stack input of the Atari trunk: dst[r][p][ch] = lut[src[r][ch][p]] for n rows of c
+ * planes of hw bytes -- the uint8 [n, c, h, w] observations as the channels_last (NHWC) f32
+ * tensor the conv trunk reads, scaled through a 256-entry table the caller computes exactly as
+ * scale_obs does (obs / 255, examples/atari/atari_network.py:18-30 + :84), in one HBM pass. */
+int tsrl_frames_to_f32_nhwc(const uint8_t* src, int64_t n, int64_t c, int64_t hw,
+                            const float* lut, float* dst, void* stream);
+
 /* Row gather: dst[i] = src[idx[i]] for rows of row_bytes bytes (Batch.__getitem__ /
  * ReplayBuffer.__getitem__ fancy indexing, tianshou/data/batch.py:446-460,
  * buffer/base.py:360-389). */

@@ -151,3 +151,39 @@ def test_atari_shared_trunk_process_fn_matches_separate_passes(dev):
     # a partial sample whose next rows are missing falls back to evaluating obs_next
     sub = idx[::3]
     assert policy._next_positions(buf, sub, dev) is None
+
+
+def test_frames_to_f32_nhwc_bit_exact(dev):
+    """tsrl_frames_to_f32_nhwc = scale_obs (atari_network.py:18-30: obs / 255 in f64, then the
+    trunk's f32 cast, :84) + the NHWC layout, bit for bit: the 4-channel vector path and the
+    general path (odd plane sizes, other channel counts)."""
+    from tianshou_amd.utils.net_atari import DQN, frames_to_f32_nhwc
+    g = torch.Generator(device="cpu").manual_seed(0)
+    lut = DQN(4, 84, 84, (6,), device=dev, features_only=True)._scale_lut(dev)
+    for shape in ((37, 4, 84, 84), (5, 4, 7, 9), (3, 3, 84, 84), (2, 1, 5, 5), (0, 4, 84, 84)):
+        obs = torch.randint(0, 256, shape, generator=g, dtype=torch.uint8)
+        want = torch.as_tensor((obs.numpy() / 255.0).astype(np.float32))
+        got = frames_to_f32_nhwc(obs.to(dev), lut)
+        assert got.shape == shape and got.is_contiguous(memory_format=torch.channels_last)
+        assert torch.equal(got.cpu(), want), shape
+
+
+def test_dqn_nhwc_trunk_matches_nchw(dev):
+    """The NHWC trunk fed by tsrl_frames_to_f32_nhwc against the plain NCHW module with the
+    same weights (summation order only)."""
+    from tianshou_amd.utils.net_atari import DQN, layer_init
+    torch.manual_seed(0)
+    a = DQN(4, 84, 84, (6,), device=dev, features_only=True, output_dim=512,
+            layer_init=layer_init).to(dev)
+    torch.manual_seed(0)
+    b = DQN(4, 84, 84, (6,), device=dev, features_only=True, output_dim=512,
+            layer_init=layer_init, channels_last=False).to(dev)
+    x = torch.randint(0, 256, (64, 4, 84, 84), dtype=torch.uint8, device=dev)
+    ya, yb = a(x)[0], b(x)[0]
+    torch.testing.assert_close(ya, yb, rtol=1e-4, atol=1e-5 * float(yb.abs().max()))
+    g = torch.randn_like(ya)
+    ya.backward(g)
+    yb.backward(g)
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        torch.testing.assert_close(pa.grad, pb.grad, rtol=1e-3,
+                                   atol=1e-4 * float(pb.grad.abs().max()))

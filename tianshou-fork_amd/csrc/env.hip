@@ -174,16 +174,19 @@ __device__ void u8_rows(const RowState* rs, const uint64_t (*fk)[MAX_STACK], int
         if (!rs[r].active) continue;
         uint8_t* row = obs + (r0 + r) * nbytes;
         if ((fbytes & 3) == 0 && (((uintptr_t)row) & 3) == 0) {
-            uint32_t* w = reinterpret_cast<uint32_t*>(row);
-            for (int64_t q = threadIdx.x; q < nbytes / 4; q += TPB) {
-                const int f = (int)((4 * q) / fbytes);
+            // frame by frame: no 64-bit division per word
+            const int fw = (int)(fbytes / 4);
+            for (int f = 0; f < S; ++f) {
+                uint32_t* w = reinterpret_cast<uint32_t*>(row + f * fbytes);
                 const uint64_t key = fk[r][f];
-                const uint64_t i0 = (uint64_t)(4 * q - f * fbytes);
-                uint32_t v = 0;
+                for (int q = threadIdx.x; q < fw; q += TPB) {
+                    const uint64_t i0 = 4ull * (uint64_t)q;
+                    uint32_t v = 0;
 #pragma unroll
-                for (int b = 0; b < 4; ++b)
-                    v |= (uint32_t)(sm64(key + (i0 + b) * GOLD) & 0xFF) << (8 * b);
-                w[q] = v;
+                    for (int b = 0; b < 4; ++b)
+                        v |= (uint32_t)(sm64(key + (i0 + b) * GOLD) & 0xFF) << (8 * b);
+                    w[q] = v;
+                }
             }
         } else {
             for (int64_t i = threadIdx.x; i < nbytes; i += TPB) {

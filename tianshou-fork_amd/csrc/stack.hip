@@ -59,10 +59,70 @@ __global__ __launch_bounds__(TPB) void stack_gather_kernel(Ring g, const char* s
     if (chain && lane == 0) chain[wv] = i;
 }
 
+// frames_to_f32_nhwc: [n][c][hw] u8 -> [n][hw][c] f32 through a 256-entry table (the scaled
+// byte values, computed by the caller).  Vector path (c == 4, hw % 4 == 0): a thread owns
+// four consecutive pixels of one row, reads one 4-byte word per channel plane (coalesced
+// across lanes) and writes the 4x4 floats as four 16-byte stores (64 contiguous bytes).
+__global__ __launch_bounds__(TPB) void frames_nhwc4_kernel(const uint32_t* src, uint32_t hw4,
+                                                           uint32_t total, const float* lut,
+                                                           float4* dst) {
+    __shared__ float t[256];
+    t[threadIdx.x] = lut[threadIdx.x];
+    __syncthreads();
+    const uint32_t i = blockIdx.x * TPB + threadIdx.x;
+    if (i >= total) return;
+    const uint32_t r = i / hw4, p4 = i - r * hw4;
+    const uint32_t* s = src + (size_t)r * 4 * hw4 + p4;
+    uint32_t w[4];
+#pragma unroll
+    for (int ch = 0; ch < 4; ++ch) w[ch] = s[(size_t)ch * hw4];
+    float4* d = dst + (size_t)i * 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int sh = 8 * j;
+        d[j] = make_float4(t[(w[0] >> sh) & 0xFF], t[(w[1] >> sh) & 0xFF],
+                           t[(w[2] >> sh) & 0xFF], t[(w[3] >> sh) & 0xFF]);
+    }
+}
+
+__global__ __launch_bounds__(TPB) void frames_nhwc_kernel(const uint8_t* src, int64_t c,
+                                                          int64_t hw, int64_t total,
+                                                          const float* lut, float* dst) {
+    __shared__ float t[256];
+    t[threadIdx.x] = lut[threadIdx.x];
+    __syncthreads();
+    const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;  // output element
+    if (i >= total) return;
+    const int64_t ch = i % c, rp = i / c, p = rp % hw, r = rp / hw;
+    dst[i] = t[src[(r * c + ch) * hw + p]];
+}
+
 }  // namespace
 }  // namespace tsrl
 
 using namespace tsrl;
+
+extern "C" int tsrl_frames_to_f32_nhwc(const uint8_t* src, int64_t n, int64_t c, int64_t hw,
+                                       const float* lut, float* dst, void* stream) {
+    TSRL_CHECK_ARG(n >= 0 && c > 0 && hw > 0, "tsrl_frames_to_f32_nhwc: bad sizes");
+    if (n == 0) return 0;
+    TSRL_CHECK_ARG(src && lut && dst, "tsrl_frames_to_f32_nhwc: null pointer");
+    const int64_t total = n * c * hw;
+    if (c == 4 && hw % 4 == 0 && (((uintptr_t)src) & 3) == 0 && aligned16(dst) &&
+        total / 4 < (1ll << 32) - TPB) {
+        const uint32_t t4 = (uint32_t)(total / 16);  // threads: 4 pixels x 4 channels each
+        hipLaunchKernelGGL(frames_nhwc4_kernel, dim3((t4 + TPB - 1) / TPB), dim3(TPB), 0,
+                           as_stream(stream), reinterpret_cast<const uint32_t*>(src),
+                           (uint32_t)(hw / 4), t4, lut, reinterpret_cast<float4*>(dst));
+    } else {
+        const int64_t grid = (total + TPB - 1) / TPB;
+        TSRL_CHECK_ARG(grid < (1ll << 31), "tsrl_frames_to_f32_nhwc: too many elements");
+        hipLaunchKernelGGL(frames_nhwc_kernel, dim3((unsigned)grid), dim3(TPB), 0,
+                           as_stream(stream), src, c, hw, total, lut, dst);
+    }
+    TSRL_LAUNCH_CHECK("tsrl_frames_to_f32_nhwc");
+    return 0;
+}
 
 static int check_ring(const uint8_t* done, const int64_t* last_index, const int64_t* lengths,
                       int64_t size, int64_t num, const char* who) {

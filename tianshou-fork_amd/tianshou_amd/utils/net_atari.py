@@ -16,6 +16,22 @@ import numpy as np
 import torch
 from torch import nn
 
+from tianshou_amd import _C
+
+
+def frames_to_f32_nhwc(obs: torch.Tensor, lut: torch.Tensor) -> torch.Tensor:
+    """uint8 [n, c, h, w] frame stacks -> f32 [n, c, h, w] in channels_last memory, each byte
+    mapped through ``lut`` (tsrl_frames_to_f32_nhwc: one HBM pass instead of torch's layout
+    copy + dtype conversion + division)."""
+    assert obs.dtype == torch.uint8 and obs.dim() == 4 and obs.is_cuda
+    obs = obs.contiguous()
+    n, c, h, w = obs.shape
+    out = torch.empty((n, h, w, c), dtype=torch.float32, device=obs.device)
+    _C.check(_C.lib().tsrl_frames_to_f32_nhwc(_C.ptr(obs), n, c, h * w, _C.ptr(lut),
+                                              _C.ptr(out), _C.stream_ptr(obs.device)),
+             "tsrl_frames_to_f32_nhwc")
+    return out.permute(0, 3, 1, 2)
+
 
 def layer_init(layer: nn.Module, std: float = np.sqrt(2), bias_const: float = 0.0):
     torch.nn.init.orthogonal_(layer.weight, std)
@@ -55,12 +71,25 @@ class DQN(nn.Module):
         if channels_last:
             self.net.to(memory_format=torch.channels_last)
 
+    def _scale_lut(self, dev) -> torch.Tensor:
+        """The 256 scaled byte values, divided on the host: f32 division there is
+        bit-identical to scale_obs's f64 division + f32 cast for every byte (torch's GPU
+        division by a scalar multiplies by the reciprocal instead, which is not)."""
+        key = (str(dev), float(self.scale))
+        lut = getattr(self, "_lut", None)
+        if lut is None or lut[0] != key:
+            t = (torch.arange(256, dtype=torch.uint8) / self.scale).to(torch.float32)
+            self._lut = lut = (key, t.to(dev).contiguous())
+        return lut[1]
+
     def forward(self, obs, state: Any = None, info: Dict[str, Any] = {}):
         obs = torch.as_tensor(obs, device=self.device)
+        if self.channels_last and obs.dim() == 4 and obs.dtype == torch.uint8 and \
+                obs.is_cuda and self.scale:
+            return self.net(frames_to_f32_nhwc(obs, self._scale_lut(obs.device))), state
         if self.channels_last and obs.dim() == 4:
             obs = obs.contiguous(memory_format=torch.channels_last)  # 1-byte frames
         # scale_obs (atari_network.py:18-30) divides the frames in f64 and the trunk casts to
-        # f32 (:84); f32(u8) / 255 in f32 is bit-identical for all 256 byte values, and the
-        # division reads the u8 frames directly (one pass, NHWC kept)
+        # f32 (:84); other inputs (host tensors, non-u8 frames) take torch's division
         x = (obs / self.scale).to(torch.float32) if self.scale else obs.to(torch.float32)
         return self.net(x), state
