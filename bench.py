@@ -102,8 +102,11 @@ class GaeTimer:
         else:
             self.events[-1][1] = ev
 
+    def each_ms(self):
+        return [a.elapsed_time(b) for a, b in self.events if b is not None]
+
     def mean_ms(self):
-        ts = [a.elapsed_time(b) for a, b in self.events if b is not None]
+        ts = self.each_ms()
         return float(np.mean(ts)) if ts else float("nan")
 
 
@@ -158,8 +161,8 @@ def main():
     from tianshou_amd.policy import PPOPolicy, base as pbase
     from tianshou_amd.utils.models import fixed_std_normal, get_actor_critic, init_and_get_optim
 
-    torch.manual_seed(rank)
-    np.random.seed(rank)
+    torch.manual_seed(0)  # identical network init on every rank (the policy also
+    np.random.seed(rank)  # broadcasts rank 0's parameters before its first update)
     E, T, D, A = args.envs, args.T, args.obs, args.act
     n = E * T
     if args.workload == "atari":
@@ -181,6 +184,7 @@ def main():
                            perm_device=(args.perm != "numpy")).to(dev)
         buf = VectorReplayBuffer(n, E, device=dev)
         coll = Collector(policy, env, buf)
+    torch.manual_seed(rank)  # per-rank action sampling streams
     policy.graph_learn = {"auto": None, "on": True, "off": False}[args.graph_learn]
     policy.sort_minibatch = args.perm == "sorted"
     timer = GaeTimer()
@@ -271,6 +275,7 @@ def main():
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "launch_us": gae_ms * 1e3,
+                         "launch_us_each": [round(t * 1e3, 2) for t in timer.each_ms()],
                          "bytes_per_launch": gae_bytes},
             "cpu_baseline": cpu,
         }

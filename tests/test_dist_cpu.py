@@ -55,7 +55,12 @@ def _worker(rank, world, port, out):
     a = torch.randn(64, dtype=torch.float64, generator=torch.Generator().manual_seed(3))
     mine = a[rank::world]
     sums = dp.all_reduce_(torch.stack([mine.sum(), (mine * mine).sum()]))
-    out[rank] = (grads_sum, grads_avg, sums)
+    # replicas built from different seeds become rank 0's (A2CPolicy._sync_replicas)
+    torch.manual_seed(100 + rank)
+    rep = torch.nn.Sequential(torch.nn.Linear(7, 16), torch.nn.Tanh(), torch.nn.Linear(16, 3))
+    dp.broadcast_params_(rep.parameters())
+    flat = torch.cat([q.detach().reshape(-1) for q in rep.parameters()])
+    out[rank] = (grads_sum, grads_avg, sums, flat)
     dist.destroy_process_group()
 
 
@@ -70,8 +75,12 @@ def test_data_parallel_gloo_two_ranks():
     y = torch.randn(64, 3, generator=torch.Generator().manual_seed(2))
     ((net(x) - y) ** 2).mean().backward()
     full = [p.grad for p in net.parameters()]
+    torch.manual_seed(100)
+    rep0 = torch.nn.Sequential(torch.nn.Linear(7, 16), torch.nn.Tanh(), torch.nn.Linear(16, 3))
+    want = torch.cat([q.detach().reshape(-1) for q in rep0.parameters()])
     for r in range(2):
-        gs, ga, sums = out[r]
+        gs, ga, sums, flat = out[r]
+        assert torch.equal(flat, want)
         for a, b in zip(gs, full):
             np.testing.assert_allclose(a.numpy(), b.numpy(), rtol=1e-5, atol=1e-7)
         for a, b in zip(ga, full):  # equal shards: mean of means == global mean

@@ -111,8 +111,17 @@ def test_atari_fused_cat_learn_matches_torch_formulation(dev):
                             policy.state_dict().items()}))
     for k in ("loss", "loss/clip", "loss/vf", "loss/ent"):
         np.testing.assert_allclose(results[0][0][k], results[1][0][k], rtol=1e-4, atol=1e-5)
-    for k, v in results[0][1].items():
-        np.testing.assert_allclose(v.numpy(), results[1][1][k].numpy(), rtol=1e-3, atol=1e-5)
+    # parameters after 4 Adam steps: Adam normalises each element's step to ~lr, so an
+    # element whose gradient sits at the f32 noise level (summation order differs between the
+    # two formulations and MIOpen's kernel choice) can move by up to lr per step either way;
+    # allow that for at most 0.1 % of the elements, everything else within rtol 1e-3
+    lr, steps = 2.5e-4, 4
+    keys = list(results[0][1])
+    a = np.concatenate([results[0][1][k].numpy().ravel() for k in keys])
+    b = np.concatenate([results[1][1][k].numpy().ravel() for k in keys])
+    bad = ~np.isclose(a, b, rtol=1e-3, atol=1e-5)
+    assert bad.mean() <= 1e-3, bad.sum()
+    assert np.abs(a - b).max() <= lr * steps
 
 
 def test_atari_shared_trunk_process_fn_matches_separate_passes(dev):

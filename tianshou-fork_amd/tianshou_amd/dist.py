@@ -43,6 +43,23 @@ class DataParallel:
         dist.all_gather(out, t.contiguous(), group=self.group)
         return torch.cat(out)
 
+    def broadcast_params_(self, params: Iterable[torch.nn.Parameter], src: int = 0) -> None:
+        """Make every rank's replica rank ``src``'s (one bucketed broadcast): data-parallel
+        learning keeps identical replicas by applying the same all-reduced step, which needs
+        identical starting parameters whatever seed each rank built its networks with."""
+        if not self.active:
+            return
+        ps = [p for p in params]
+        if not ps:
+            return
+        flat = torch.cat([p.detach().reshape(-1) for p in ps])
+        dist.broadcast(flat, src=src, group=self.group)
+        o = 0
+        with torch.no_grad():
+            for p in ps:
+                p.copy_(flat[o:o + p.numel()].view_as(p))
+                o += p.numel()
+
     def all_reduce_grads_(self, params: Iterable[torch.nn.Parameter],
                           average: bool = False) -> None:
         """One bucketed all-reduce of every gradient.  SUM by default (the fused PPO loss

@@ -99,7 +99,15 @@ class A2CPolicy(PGPolicy):
         mask = np.isin(np.asarray(indices), buffer.unfinished_index()).astype(np.uint8)
         return 0, torch.as_tensor(mask, device=buffer.device)
 
+    def _sync_replicas(self) -> None:
+        """Data parallel: rank 0's parameters on every rank before the first update (the
+        process_fn evaluation and every later step then run on identical replicas)."""
+        if self.dp.active and not getattr(self, "_replicas_synced", False):
+            self.dp.broadcast_params_(self._actor_critic.parameters())
+            self._replicas_synced = True
+
     def _compute_returns(self, batch: Batch, buffer, indices: np.ndarray) -> Batch:
+        self._sync_replicas()
         obs = torch.as_tensor(batch.obs)
         dev = next(self.critic.parameters()).device
         obs = obs.to(dev)
