@@ -41,7 +41,9 @@ def parse():
                          "(Box 17/6, 512 envs x 128 steps); atari: config 5 (u8 4x84x84 frame "
                          "stacks, Discrete(6), Nature-DQN trunk, 1024 envs x 256 steps)")
     ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--warmup", type=int, default=2,
+                    help="untimed iterations; the second one completes the collect-graph "
+                         "captures (remainder graphs of a new ring phase)")
     ap.add_argument("--envs", type=int, default=None)
     ap.add_argument("--T", type=int, default=None)
     ap.add_argument("--obs", type=int, default=None)
