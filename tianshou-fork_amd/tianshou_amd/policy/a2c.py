@@ -43,8 +43,12 @@ class A2CPolicy(PGPolicy):
 
     def _chunks(self, n: int, row_numel: int = 1):
         """Evaluation chunks: at most EVAL_CHUNK rows and 2**30 input elements per chunk (a
-        conv trunk's activations are ~2x its uint8 frame stack per row in f32)."""
-        c = max(self._batch, min(EVAL_CHUNK, (1 << 30) // max(int(row_numel), 1)))
+        conv trunk's activations are ~2x its uint8 frame stack per row in f32), rounded down
+        to a power of two: the Nature-DQN trunk ran 0.385 us/row at the 38043-row chunk that
+        the element bound gives for 4x84x84 frames and 0.306 at 32768 (MIOpen kernel choice,
+        tools/atari_eval_chunk_probe.py)."""
+        c = min(EVAL_CHUNK, (1 << 30) // max(int(row_numel), 1))
+        c = max(self._batch, 1 << (max(c, 1).bit_length() - 1))
         return [(s, min(s + c, n)) for s in range(0, n, c)]
 
     def _values(self, obs: torch.Tensor) -> torch.Tensor:
