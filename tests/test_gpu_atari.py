@@ -196,3 +196,24 @@ def test_dqn_nhwc_trunk_matches_nchw(dev):
     for pa, pb in zip(a.parameters(), b.parameters()):
         torch.testing.assert_close(pa.grad, pb.grad, rtol=1e-3,
                                    atol=1e-4 * float(pb.grad.abs().max()))
+
+
+def test_atari_shared_trunk_process_fn_wrapped_ring(dev):
+    """As above on a ring that has wrapped (collect more steps than the buffer holds) and on
+    a random-index sample: next() positions equal the host next(), and process_fn's V(s')
+    equals the critic on the batch's obs_next rows."""
+    E, T, L = 6, 16, 7
+    _, policy, buf, coll = _setup(dev, E, T, L, seed=5)
+    policy._rew_norm = False
+    coll.collect(n_step=E * (T + 5))  # 5 steps past the end of every sub-buffer
+    batch, idx = buf.sample(0)
+    assert not np.array_equal(idx, np.arange(E * T))  # ring order, not storage order
+    p = policy._next_positions(buf, idx, dev)
+    assert p is not None
+    assert np.array_equal(idx[p.cpu().numpy()], buf.next(idx))
+    with torch.no_grad():  # as _compute_returns calls it
+        vn_ref = policy.critic(batch.obs_next).flatten()
+        v_s, v_s_ = policy._eval_values(batch, batch.obs.to(dev), batch.obs_next.to(dev), buf,
+                                        idx)
+    np.testing.assert_allclose(v_s_.cpu().numpy(), vn_ref.cpu().numpy(), rtol=1e-5,
+                               atol=1e-5 * float(vn_ref.abs().max()))
