@@ -51,8 +51,9 @@ def parse():
     ap.add_argument("--repeat", type=int, default=4)
     ap.add_argument("--minibatches", type=int, default=32)
     ap.add_argument("--ep-len", type=int, default=None)
-    ap.add_argument("--perm", choices=["numpy", "device", "sorted"], default="sorted",
-                    help="minibatch permutation: numpy (reference stream), device "
+    ap.add_argument("--perm", choices=["numpy", "device", "sorted"], default="numpy",
+                    help="minibatch permutation: numpy (the reference np.random.permutation "
+                         "stream, bit-exact: host MT19937 draws + device shuffle), device "
                          "(torch.randperm), sorted (torch.randperm, rows of each minibatch "
                          "in ascending buffer order: same minibatch sets)")
     ap.add_argument("--cpu-steps", type=int, default=None,

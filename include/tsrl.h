@@ -221,6 +221,26 @@ int tsrl_stack_gather(const void* src, int64_t frame_bytes, const int64_t* idx, 
 int tsrl_frames_to_f32_nhwc(const uint8_t* src, int64_t n, int64_t c, int64_t hw,
                             const float* lut, float* dst, void* stream);
 
+/* ---------------------------------------------------------------------------------
+ * np.random.permutation(n) of the global legacy RandomState, bit-exact: the shuffle order
+ * of Batch.split (tianshou/data/batch.py:896-912, one permutation per PPO repeat,
+ * ppo.py:106-107).  NumPy's legacy permutation = arange(n) shuffled by
+ * `for i in n-1..1: j = random_interval(i); swap(x[i], x[j])`.
+ *
+ * tsrl_np_shuffle_draws (HOST function, host pointers): the MT19937 stream and the masked
+ *   rejection loop.  key[624]/pos are the ('MT19937', key, pos, ...) of
+ *   np.random.get_state(); both are advanced in place exactly as NumPy advances them, so the
+ *   caller writes them back with set_state.  draws[i] = j_i for 1 <= i < n, draws[0] = 0.
+ *   n < 2^32.  No HIP call; safe from any host thread.
+ * tsrl_shuffle_apply (device): out[0..n) = the permutation those draws produce (int64),
+ *   resolved in parallel (one stable radix sort of (j, step) + a pointer chase); workspace
+ *   from tsrl_shuffle_apply_workspace_bytes(n).
+ * ------------------------------------------------------------------------------- */
+int tsrl_np_shuffle_draws(uint32_t* key, int32_t* pos, int64_t n, uint32_t* draws);
+int64_t tsrl_shuffle_apply_workspace_bytes(int64_t n);
+int tsrl_shuffle_apply(const uint32_t* draws, int64_t n, int64_t* out, void* workspace,
+                       int64_t workspace_bytes, void* stream);
+
 /* Row gather: dst[i] = src[idx[i]] for rows of row_bytes bytes (Batch.__getitem__ /
  * ReplayBuffer.__getitem__ fancy indexing, tianshou/data/batch.py:446-460,
  * buffer/base.py:360-389). */

@@ -45,3 +45,19 @@ void oracle_gae_f64vals(const double *v_s, const double *v_next_masked, const do
         adv_out[i] = gae;
     }
 }
+
+/*
+ * Sequential Fisher-Yates application of shuffle draws (NumPy legacy RandomState.shuffle,
+ * mtrand.pyx _shuffle_raw: for i = n-1 .. 1, swap x[i] and x[draws[i]]) onto arange(n).
+ * Checker for tsrl_np_shuffle_draws / tsrl_shuffle_apply.
+ */
+void oracle_shuffle_apply(const uint32_t *draws, int64_t n, int64_t *out)
+{
+    for (int64_t i = 0; i < n; ++i) out[i] = i;
+    for (int64_t i = n - 1; i >= 1; --i) {
+        int64_t j = (int64_t)draws[i];
+        int64_t t = out[i];
+        out[i] = out[j];
+        out[j] = t;
+    }
+}

@@ -34,12 +34,24 @@ def lib():
             fn.restype = None
             fn.argtypes = [vt, vt, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                            ctypes.c_double, ctypes.c_double, ctypes.c_void_p]
+        L.oracle_shuffle_apply.restype = None
+        L.oracle_shuffle_apply.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
         _LIB = L
     return _LIB
 
 
 def _ptr(a):
     return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def shuffle_apply(draws):
+    """arange(n) shuffled by the draws of NumPy's legacy shuffle (mtrand.pyx _shuffle_raw:
+    for i = n-1 .. 1 swap x[i], x[draws[i]]), sequentially in C."""
+    d = np.ascontiguousarray(draws, np.uint32)
+    out = np.empty(len(d), np.int64)
+    if len(d):
+        lib().oracle_shuffle_apply(_ptr(d), len(d), _ptr(out))
+    return out
 
 
 # ---------------------------------------------------------------------------------------

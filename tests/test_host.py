@@ -139,7 +139,9 @@ def test_sorted_minibatch_permutation_same_sets(n, bs):
     import types
     import torch
     from tianshou_amd.policy.ppo import PPOPolicy, split_bounds
-    fake = types.SimpleNamespace(perm_device=False, sort_minibatch=True)
+    # host logic only: the device permutation itself is tests/test_gpu_perm.py
+    fake = types.SimpleNamespace(perm_device=False, sort_minibatch=True,
+                                 _np_perm=lambda k, d: torch.as_tensor(np.random.permutation(k)))
     np.random.seed(5)
     got = PPOPolicy._permutation(fake, n, torch.device("cpu"), bs).numpy()
     np.random.seed(5)

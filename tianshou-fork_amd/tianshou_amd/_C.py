@@ -86,6 +86,9 @@ _SIGS = {
     "tsrl_buffer_add": ([ctypes.POINTER(AddArgs), _p], ctypes.c_int),
     "tsrl_ring_advance": ([_p, _i64, _p], ctypes.c_int),
     "tsrl_gather_rows": ([_p, _i64, _p, _i64, _p, _p], ctypes.c_int),
+    "tsrl_np_shuffle_draws": ([_p, _p, _i64, _p], ctypes.c_int),
+    "tsrl_shuffle_apply_workspace_bytes": ([_i64], _i64),
+    "tsrl_shuffle_apply": ([_p, _i64, _p, _p, _i64, _p], ctypes.c_int),
     "tsrl_ring_step_index": ([_p, _i64, _p, _p, _p, _i64, _i64, ctypes.c_int, _p, _p],
                              ctypes.c_int),
     "tsrl_stack_gather": ([_p, _i64, _p, _i64, _i64, _p, _p, _p, _i64, _i64, _p, _p, _p],

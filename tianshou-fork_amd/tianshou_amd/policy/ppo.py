@@ -19,6 +19,7 @@ from tianshou_amd import _C
 from tianshou_amd.data.batch import Batch, gather_rows, split_indices
 from tianshou_amd.policy.a2c import A2CPolicy
 from tianshou_amd.policy.fused_eval import FusedEvalMixin, cat_logp, cat_mode  # noqa: F401
+from tianshou_amd.utils.np_perm import LegacyPermutation
 
 
 def split_bounds(length: int, size: int, merge_last: bool):
@@ -153,8 +154,11 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
         self._norm_adv = advantage_normalization
         self._recompute_adv = recompute_advantage
         # perm_device=False: minibatch order from np.random.permutation (the reference's
-        # global RandomState stream, bit-exact); True: torch.randperm on the GPU.
+        # global RandomState stream, bit-exact: MT19937 draws on the host, the shuffle
+        # resolved on the device, the next update's draws prefetched in a host thread --
+        # utils/np_perm.py); True: torch.randperm on the GPU.
         self.perm_device = perm_device
+        self._np_perm = LegacyPermutation()
         # sort_minibatch=True: the rows of every minibatch are visited in ascending buffer
         # order (same minibatch SETS as Batch.split over the permutation; only the order of
         # rows inside a minibatch -- i.e. the float summation order -- changes).  The fused
@@ -215,7 +219,8 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
                     return torch.sort(lab.to(torch.uint8), stable=True).indices
             perm = torch.randperm(n, device=dev)
         else:
-            perm = torch.as_tensor(np.random.permutation(n), device=dev)
+            perm = self._np_perm(n, dev)
+            self._np_perm_used = True
         if self.sort_minibatch and batch_size:
             bounds = split_bounds(n, batch_size, merge_last=True)
             sizes = {e - s for s, e in bounds}
@@ -227,6 +232,14 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
 
     def learn(self, batch: Batch, batch_size: int, repeat: int, **kwargs: Any
               ) -> Dict[str, List[float]]:
+        self._np_perm_used = False
+        out = self._learn(batch, batch_size, repeat)
+        if self._np_perm_used:
+            # the next update's np.random.permutation draws, computed while it collects
+            self._np_perm.prefetch(len(batch.v_s), repeat)
+        return out
+
+    def _learn(self, batch: Batch, batch_size: int, repeat: int) -> Dict[str, List[float]]:
         if not self._fused:
             if self._cat is not None and isinstance(batch.obs, torch.Tensor) and \
                     batch.obs.is_cuda:
