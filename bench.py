@@ -143,8 +143,30 @@ def build_atari(args, dev, rank):
     return Collector(policy, env, buf, exploration_noise=True), policy, buf
 
 
+def spawn_ranks(n: int) -> int:
+    """``--gpus N`` without a launcher: start N rank processes of this script (one per GPU,
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment) before this process
+    touches the GPU; rank 0 prints the JSON line.  Returns the worst exit code."""
+    import socket
+    import subprocess
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rcs = [p.wait() for p in procs]
+    return max(abs(rc) for rc in rcs)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -155,6 +177,10 @@ def main():
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=dev)
+        if dist.get_world_size() != args.gpus:
+            print(f"bench.py: RCCL world size {dist.get_world_size()} != --gpus {args.gpus}",
+                  file=sys.stderr)
+            sys.exit(2)
         if args.force_dp:
             from tianshou_amd.dist import DataParallel
             DataParallel.force = True
@@ -190,6 +216,9 @@ def main():
     torch.manual_seed(rank)  # per-rank action sampling streams
     policy.graph_learn = {"auto": None, "on": True, "off": False}[args.graph_learn]
     policy.sort_minibatch = args.perm == "sorted"
+    # weak scaling: every rank splits its own rows with its own np.random stream (a global
+    # permutation of world x n rows is O(world x n) sequential host draws per rank)
+    policy.dp_permutation = "local"
     timer = GaeTimer()
     pbase.GAE_HOOK = timer
     phase = {"collect": 0.0, "update": 0.0}
@@ -270,8 +299,11 @@ def main():
                        "envs_per_gpu": E, "steps_per_env": T, "global_batch": n * world,
                        "minibatch": n // args.minibatches * world,
                        "parallelism": f"env-sharded dp{world}",
-                       "permutation": args.perm,
+                       "permutation": args.perm + (" (per-rank stream)" if world > 1 else ""),
+                       "rccl_world_size": world if distributed else None,
                        "learn_graph": args.graph_learn,
+                       "learn_graph_capture_failed": bool(getattr(policy, "_graph_failed",
+                                                                  False)),
                        "collect_s": phase["collect"] / args.steps,
                        "update_s": phase["update"] / args.steps},
             "roofline": {"kernel": "tsrl_gae (gae_rows_staged_kernel)", "bound": "hbm",

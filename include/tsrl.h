@@ -127,7 +127,15 @@ int tsrl_rms_merge(const double* col_partials, int64_t nblk, int64_t dim,
 int tsrl_rms_merge2(const double* partials_step, const double* partials_reset,
                     const double* blk_done, int64_t nblk, int64_t dim, int64_t k, float* mean,
                     float* var, double* count, float* snap_mean, float* snap_var,
-                    unsigned int* ticket, void* stream);
+                    unsigned int* ticket, const double* k_dev, void* stream);
+/* Data parallel: fold this rank's merge2 inputs into out[4*dim+2] f64 = [step (sum, sumsq)
+ * x dim | reset (sum, sumsq) x dim | reset-row count | step-row count k]; after an
+ * all-reduce over the ranks, tsrl_rms_merge2(out, out + 2*dim, out + 4*dim, nblk = 1, dim,
+ * k_dev = out + 4*dim + 1) applies the reference's single global VectorEnvNormObs update
+ * (venv_wrappers.py:93-99).  k_dev (nullable) in merge2 overrides k. */
+int tsrl_rms_sum_partials2(const double* partials_step, const double* partials_reset,
+                           const double* blk_done, int64_t nblk, int64_t dim, int64_t k,
+                           double* out, void* stream);
 int tsrl_rms_norm_rows(const float* x, const uint8_t* mask, int64_t k, int64_t dim,
                        const float* mean, const float* var, float eps, float clip,
                        float* out, void* stream);
@@ -279,6 +287,14 @@ typedef struct tsrl_ppo_params {
 int64_t tsrl_ppo_num_partials(int64_t b);
 int tsrl_adv_moments(const float* adv, const int64_t* idx, int64_t b, double* partials,
                      void* stream);
+/* Advantage moments (sum adv, sum adv^2) of every minibatch of an epoch in one pass:
+ * segment g = rows [bounds[g], bounds[g+1]) of idx (device int64 [nseg+1]); out [nseg, 2]
+ * f64; partials [nseg, tsrl_adv_moments_seg_parts(max_seg), 2] f64 scratch, max_seg = the
+ * longest segment.  Under data parallelism one all-reduce of out serves the whole epoch. */
+int64_t tsrl_adv_moments_seg_parts(int64_t max_seg);
+int tsrl_adv_moments_seg(const float* adv, const int64_t* idx, const int64_t* bounds,
+                         int64_t nseg, int64_t max_seg, double* partials, double* out,
+                         void* stream);
 int tsrl_reduce_partials(const double* partials, int64_t nblk, int64_t width, double* out,
                          void* stream);
 int tsrl_ppo_gauss_fwd_bwd(const float* mu, const float* log_std, const float* value,
@@ -437,12 +453,14 @@ int tsrl_segtree_prefix_idx(const double* tree, int64_t bound, const void* value
  * tsrl_clip_adam_partials(n) entries) receive slice norms, norm_out[0] = gradient norm,
  * norm_out[1] = clip coefficient (max_norm <= 0: no clipping, partials / norm_out may be
  * NULL); the gradient is left scaled in place; step[0..nstep) (device f32 step counters, all
- * equal) is advanced by one.  ticket: one device uint32, zero-initialised, kept zero. */
+ * equal) is advanced by one.  ticket: one device uint32, zero-initialised, kept zero.
+ * lr_dev (nullable device f32): the learning rate read at run time instead of `lr`, so a
+ * captured learn graph follows an lr_scheduler (BasePolicy.update, base.py:312-313). */
 int64_t tsrl_clip_adam_partials(int64_t n);
 int tsrl_clip_adam(float* param, float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                    float* step, int64_t nstep, float lr, float beta1, float beta2, float eps,
                    float max_norm, double* partials, float* norm_out, unsigned int* ticket,
-                   void* stream);
+                   const float* lr_dev, void* stream);
 
 #ifdef __cplusplus
 }

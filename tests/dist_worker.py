@@ -52,10 +52,16 @@ def main():
     data = make_data(n, D, A, dev)
     sl = slice(rank * n // world, (rank + 1) * n // world)
     policy = build_policy(D, A, dev)
-    np.random.seed(rank)
+    np.random.seed(0)  # one global np.random stream (dp_permutation="global")
     batch = Batch(**{k: v[sl].contiguous() for k, v in data.items()})
     res = policy.learn(batch, batch_size=n // world, repeat=1)
     sd = {k: v.cpu() for k, v in policy.state_dict().items()}
+    # several global minibatches over 2 repeats: the reference's Batch.split of the GLOBAL
+    # batch (dp_permutation="global": the same np.random stream on every rank)
+    policy2 = build_policy(D, A, dev)
+    np.random.seed(0)
+    res2 = policy2.learn(batch, batch_size=256, repeat=2)
+    sd2 = {k: v.cpu() for k, v in policy2.state_dict().items()}
     # obs_rms kept global across ranks (sync_obs_rms): different env shards per rank
     E, T = 32, 24
     env = VectorEnvNormObs(SyntheticVectorEnv(E, (D,), A, ep_len=9, seed=rank, device=dev))
@@ -63,7 +69,10 @@ def main():
     coll = Collector(policy, env, buf, sync_obs_rms=True)
     coll.collect(n_step=E * T)
     rms = env.get_obs_rms()
-    torch.save(dict(sd=sd, loss=torch.tensor(res["loss"]), rms_mean=torch.as_tensor(rms.mean),
+    torch.save(dict(sd=sd, loss=torch.tensor(res["loss"]), sd2=sd2,
+                    loss2=torch.tensor([res2[k] for k in ("loss", "loss/clip", "loss/vf",
+                                                          "loss/ent")]),
+                    rms_mean=torch.as_tensor(rms.mean),
                     rms_var=torch.as_tensor(rms.var), rms_count=torch.tensor(rms.count)),
                os.path.join(outdir, f"rank{rank}.pt"))
     dist.barrier()

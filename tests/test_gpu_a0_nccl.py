@@ -41,3 +41,7 @@ def test_bench_force_dp_one_rank_rccl():
     out = json.loads(lines[-1])
     assert out["value"] > 0 and out["n_gpus"] == 1
     assert out["config"]["global_batch"] == 512 * 128
+    # the RCCL all-reduces were captured into the learn graphs (2048-row minibatches replay
+    # whole epochs) and into the collect graphs (global obs_rms), not run eagerly
+    assert out["config"]["learn_graph_capture_failed"] is False
+    assert "capture failed" not in p.stderr

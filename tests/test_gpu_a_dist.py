@@ -1,6 +1,9 @@
 """Data-parallel (env-sharded) PPO update with 2 ranks on one MI355X over gloo: one global
 minibatch split across ranks must give the single-process full-batch update (up to
-summation order), and sync_obs_rms must leave both ranks with identical global statistics.
+summation order) -- one minibatch, and several global minibatches of the reference's
+Batch.split over the global batch (every rank draws the same permutation) -- and the default
+global obs_rms must leave both ranks with the statistics of ONE VectorEnvNormObs over both
+env shards (checked against the NumPy env and a host RunningMeanStd).
 
 Runs first among the GPU tests (file name) so that this pytest process has not initialised
 HIP when it starts the rank processes."""
@@ -59,3 +62,48 @@ def test_two_rank_update_matches_single_process(tmp_path):
     # near-zero gradient summed in another order can move it differently: atol = lr / 3
     for k, v in r0["sd"].items():
         np.testing.assert_allclose(v.numpy(), sd[k].cpu().numpy(), rtol=1e-4, atol=1e-4)
+    # global minibatches: 8 per epoch x 2 repeats, rank shares of varying size
+    for k in r0["sd2"]:
+        assert torch.equal(r0["sd2"][k], r1["sd2"][k]), k
+    torch.testing.assert_close(r0["loss2"], r1["loss2"], rtol=1e-6, atol=0)
+    policy2 = w.build_policy(23, 5, dev)
+    np.random.seed(0)
+    res2 = policy2.learn(Batch(**data), batch_size=512, repeat=2)
+    want = np.array([res2[k] for k in ("loss", "loss/clip", "loss/vf", "loss/ent")])
+    assert want.shape == tuple(r0["loss2"].shape) == (4, 16)
+    np.testing.assert_allclose(r0["loss2"].numpy(), want, rtol=1e-4, atol=1e-5)
+    sd2 = policy2.state_dict()
+    for k, v in r0["sd2"].items():
+        np.testing.assert_allclose(v.numpy(), sd2[k].cpu().numpy(), rtol=1e-4, atol=1e-4)
+    # obs_rms of one VectorEnvNormObs over both shards: NumPy env (rank r = seed r, E envs)
+    # and a RunningMeanStd with f64 batch moments stored as f32 (the device recipe)
+    from oracle.synth_env import SynthVecEnvNP
+    E, T, D = 32, 24, 23
+    envs = [SynthVecEnvNP(E, (D,), 5, 9, seed=r) for r in range(2)]
+    mean, var, count = np.zeros(D, np.float32), np.ones(D, np.float32), 0.0
+
+    def upd(x):
+        nonlocal mean, var, count
+        if len(x) == 0:
+            return
+        x = x.astype(np.float64)
+        bm, bv, bc = x.mean(0), x.var(0), float(len(x))
+        delta = bm - mean
+        tot = count + bc
+        nm = mean + delta * bc / tot
+        m2 = var * count + bv * bc + delta ** 2 * count * bc / tot
+        mean, var, count = nm.astype(np.float32), (m2 / tot).astype(np.float32), tot
+
+    upd(np.concatenate([e.reset() for e in envs]))
+    for _ in range(T):
+        outs = [e.step() for e in envs]
+        upd(np.concatenate([o[0] for o in outs]))
+        resets = []
+        for e, o in zip(envs, outs):
+            ids = np.flatnonzero(o[2] | o[3])
+            if len(ids):
+                resets.append(e.reset(ids))
+        upd(np.concatenate(resets) if resets else np.zeros((0, D), np.float32))
+    assert int(r0["rms_count"]) == int(count)
+    np.testing.assert_allclose(r0["rms_mean"].numpy(), mean, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(r0["rms_var"].numpy(), var, rtol=1e-5, atol=1e-6)

@@ -58,7 +58,7 @@ __global__ __launch_bounds__(OTPB) void clip_adam_kernel(float* __restrict__ p,
                                                          float* __restrict__ step, int64_t nstep,
                                                          AdamArgs a, const double* __restrict__ partials,
                                                          float* __restrict__ norm_out,
-                                                         unsigned int* ticket) {
+                                                         unsigned int* ticket, const float* __restrict__ lr_dev) {
     __shared__ float s_scale;
     const int t = threadIdx.x;
     const bool clip = a.max_norm > 0.0f;
@@ -84,7 +84,7 @@ __global__ __launch_bounds__(OTPB) void clip_adam_kernel(float* __restrict__ p,
     const float scale = clip ? s_scale : 1.0f;
     const float bc1 = 1.0f - powf(a.beta1, st);
     const float bc2_sqrt = sqrtf(1.0f - powf(a.beta2, st));
-    const float step_size = a.lr / bc1;
+    const float step_size = (lr_dev ? *lr_dev : a.lr) / bc1;
     const int64_t i0 = (int64_t)blockIdx.x * OCHUNK;
     const int64_t i1 = min(n, i0 + OCHUNK);
     // g is only read here (other workgroups are still summing it); the clipped gradient is
@@ -126,7 +126,8 @@ extern "C" int64_t tsrl_clip_adam_partials(int64_t n) { return (n + OCHUNK - 1) 
 extern "C" int tsrl_clip_adam(float* param, float* grad, float* exp_avg, float* exp_avg_sq,
                               int64_t n, float* step, int64_t nstep, float lr, float beta1,
                               float beta2, float eps, float max_norm, double* partials,
-                              float* norm_out, unsigned int* ticket, void* stream) {
+                              float* norm_out, unsigned int* ticket, const float* lr_dev,
+                              void* stream) {
     TSRL_CHECK_ARG(n >= 0 && nstep >= 1, "tsrl_clip_adam: bad sizes");
     if (n == 0) return 0;
     TSRL_CHECK_ARG(param && grad && exp_avg && exp_avg_sq && step && ticket,
@@ -142,7 +143,7 @@ extern "C" int tsrl_clip_adam(float* param, float* grad, float* exp_avg, float* 
     const AdamArgs a{lr, beta1, beta2, eps, max_norm};
     hipLaunchKernelGGL(clip_adam_kernel, dim3((unsigned)grid), dim3(OTPB), 0,
                        as_stream(stream), param, grad, exp_avg, exp_avg_sq, n, step, nstep, a,
-                       partials, norm_out, ticket);
+                       partials, norm_out, ticket, lr_dev);
     TSRL_LAUNCH_CHECK("tsrl_clip_adam");
     if (max_norm > 0.0f) {
         const unsigned g2 = (unsigned)std::min<int64_t>((n + OTPB - 1) / OTPB, 1024);

@@ -85,6 +85,54 @@ __global__ __launch_bounds__(TPB) void reduce_partials_kernel(const double* part
     }
 }
 
+// Advantage moments of every minibatch of an epoch at once (one all-reduce per epoch under
+// data parallelism instead of one per minibatch).  Segment g = rows [bounds[g], bounds[g+1])
+// of idx; workgroup (p, g) folds a strided 1/nparts share of segment g into partials[g][p],
+// then one workgroup per segment sums its partials in fixed order.
+__global__ __launch_bounds__(TPB) void adv_moments_seg_kernel(const float* adv, const int64_t* idx,
+                                                              const int64_t* bounds, int nparts,
+                                                              double* partials) {
+    __shared__ double sh[NW][2];
+    const int g = blockIdx.y;
+    const int64_t s0 = bounds[g], s1 = bounds[g + 1];
+    double s = 0.0, ss = 0.0;
+    for (int64_t r = s0 + (int64_t)blockIdx.x * TPB + threadIdx.x; r < s1;
+         r += (int64_t)nparts * TPB) {
+        const double a = (double)adv[idx ? idx[r] : r];
+        s += a;
+        ss += a * a;
+    }
+    s = wave_sum(s);
+    ss = wave_sum(ss);
+    const int w = threadIdx.x / kWave;
+    if ((threadIdx.x & (kWave - 1)) == 0) {
+        sh[w][0] = s;
+        sh[w][1] = ss;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        double t = 0.0;
+        for (int i = 0; i < NW; ++i) t += sh[i][threadIdx.x];
+        partials[((int64_t)g * nparts + blockIdx.x) * 2 + threadIdx.x] = t;
+    }
+}
+
+__global__ __launch_bounds__(kWave) void adv_moments_seg_reduce_kernel(const double* partials,
+                                                                       int nparts, double* out) {
+    const int g = blockIdx.x;
+    double s = 0.0, ss = 0.0;
+    for (int i = threadIdx.x; i < nparts; i += kWave) {
+        s += partials[((int64_t)g * nparts + i) * 2];
+        ss += partials[((int64_t)g * nparts + i) * 2 + 1];
+    }
+    s = wave_sum(s);
+    ss = wave_sum(ss);
+    if (threadIdx.x == 0) {
+        out[2 * g] = s;
+        out[2 * g + 1] = ss;
+    }
+}
+
 // One workgroup = 256 minibatch rows.  The [256, A] mu tile (contiguous) and the gathered
 // act rows are staged through LDS with coalesced / row-contiguous loads, the per-row math
 // reads LDS (row stride A: conflict-free for odd A), and grad_mu goes back out through the
@@ -289,6 +337,29 @@ extern "C" int tsrl_adv_moments(const float* adv, const int64_t* idx, int64_t b,
     hipLaunchKernelGGL(adv_moments_kernel, dim3((unsigned)tsrl_ppo_num_partials(b)), dim3(TPB), 0,
                        as_stream(stream), adv, idx, b, partials);
     TSRL_LAUNCH_CHECK("tsrl_adv_moments");
+    return 0;
+}
+
+extern "C" int64_t tsrl_adv_moments_seg_parts(int64_t max_seg) {
+    const int64_t p = (max_seg + 4 * TPB - 1) / (4 * TPB);  // ~4 rows per thread
+    return p < 1 ? 1 : (p > 256 ? 256 : p);
+}
+
+extern "C" int tsrl_adv_moments_seg(const float* adv, const int64_t* idx, const int64_t* bounds,
+                                    int64_t nseg, int64_t max_seg, double* partials,
+                                    double* out, void* stream) {
+    TSRL_CHECK_ARG(nseg >= 0 && nseg <= 65535 && max_seg >= 0,
+                   "tsrl_adv_moments_seg: nseg=%lld max_seg=%lld", (long long)nseg,
+                   (long long)max_seg);
+    if (nseg == 0) return 0;
+    TSRL_CHECK_ARG(adv && bounds && partials && out, "tsrl_adv_moments_seg: null pointer");
+    const int nparts = (int)tsrl_adv_moments_seg_parts(max_seg);
+    hipLaunchKernelGGL(adv_moments_seg_kernel, dim3((unsigned)nparts, (unsigned)nseg), dim3(TPB),
+                       0, as_stream(stream), adv, idx, bounds, nparts, partials);
+    TSRL_LAUNCH_CHECK("adv_moments_seg_kernel");
+    hipLaunchKernelGGL(adv_moments_seg_reduce_kernel, dim3((unsigned)nseg), dim3(kWave), 0,
+                       as_stream(stream), partials, nparts, out);
+    TSRL_LAUNCH_CHECK("adv_moments_seg_reduce_kernel");
     return 0;
 }
 

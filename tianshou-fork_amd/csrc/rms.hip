@@ -104,7 +104,7 @@ constexpr int M2COLS = M2C, M2LANES = 64;
 __global__ __launch_bounds__(M2COLS * M2LANES) void rms_merge2_kernel(
     const double* p1, const double* p2, const double* blk_done, int64_t nblk, int64_t dim,
     int64_t k, float* mean, float* var, double* count, float* snap_mean, float* snap_var,
-    unsigned int* ticket) {
+    unsigned int* ticket, const double* k_dev) {
     constexpr int NW = M2COLS * M2LANES / kWave;  // waves; each holds 64 / M2COLS lanes per column
     __shared__ double sh[5][NW][M2COLS];
     const int tid = threadIdx.x;
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(M2COLS * M2LANES) void rms_merge2_kernel(
             S2 += sh[3][v][col];
             Q2 += sh[4][v][col];
         }
-        const double bc1 = (double)k;
+        const double bc1 = k_dev ? *k_dev : (double)k;
         const double tot1 = old_count + bc1;
         tot2 = tot1 + ND;
         if (d < dim) {
@@ -243,7 +243,8 @@ extern "C" int tsrl_rms_merge(const double* col_partials, int64_t nblk, int64_t 
 extern "C" int tsrl_rms_merge2(const double* partials_step, const double* partials_reset,
                                const double* blk_done, int64_t nblk, int64_t dim, int64_t k,
                                float* mean, float* var, double* count, float* snap_mean,
-                               float* snap_var, unsigned int* ticket, void* stream) {
+                               float* snap_var, unsigned int* ticket, const double* k_dev,
+                               void* stream) {
     TSRL_CHECK_ARG(partials_step && partials_reset && blk_done && mean && var && count &&
                        snap_mean && snap_var && ticket && dim > 0 && nblk >= 0 && k >= 0,
                    "tsrl_rms_merge2: bad arguments");
@@ -252,8 +253,55 @@ extern "C" int tsrl_rms_merge2(const double* partials_step, const double* partia
     const int64_t grid = (dim + M2COLS - 1) / M2COLS;
     hipLaunchKernelGGL(rms_merge2_kernel, dim3((unsigned)grid), dim3(M2COLS * M2LANES), 0,
                        as_stream(stream), partials_step, partials_reset, blk_done, nblk, dim, k,
-                       mean, var, count, snap_mean, snap_var, ticket);
+                       mean, var, count, snap_mean, snap_var, ticket, k_dev);
     TSRL_LAUNCH_CHECK("tsrl_rms_merge2");
+    return 0;
+}
+
+// Data-parallel form of merge2's inputs: this rank's step/reset moments folded over its
+// partial blocks into one [4*dim + 2] f64 vector (sum/sumsq of the step rows, of the reset
+// rows, the reset-row count and the step-row count k) -- the payload of ONE all-reduce per env step, after which
+// tsrl_rms_merge2(nblk = 1) applies both global updates.
+__global__ __launch_bounds__(kWave) void rms_sum_partials2_kernel(const double* p1, const double* p2,
+                                                                   const double* blk_done,
+                                                                   int64_t nblk, int64_t dim,
+                                                                   int64_t k, double* out) {
+    const int64_t d = (int64_t)blockIdx.x * kWave + threadIdx.x;
+    if (d > dim) return;
+    if (d == dim) {
+        double nd = 0.0;
+        for (int64_t b = 0; b < nblk; ++b) nd += blk_done[b];
+        out[4 * dim] = nd;
+        out[4 * dim + 1] = (double)k;
+        return;
+    }
+    double s1 = 0.0, q1 = 0.0, s2 = 0.0, q2 = 0.0;
+    for (int64_t b = 0; b < nblk; ++b) {
+        const double2 a = *reinterpret_cast<const double2*>(p1 + (b * dim + d) * 2);
+        s1 += a.x;
+        q1 += a.y;
+        if (blk_done[b] > 0.0) {
+            const double2 r = *reinterpret_cast<const double2*>(p2 + (b * dim + d) * 2);
+            s2 += r.x;
+            q2 += r.y;
+        }
+    }
+    out[2 * d] = s1;
+    out[2 * d + 1] = q1;
+    out[2 * dim + 2 * d] = s2;
+    out[2 * dim + 2 * d + 1] = q2;
+}
+
+extern "C" int tsrl_rms_sum_partials2(const double* partials_step, const double* partials_reset,
+                                      const double* blk_done, int64_t nblk, int64_t dim,
+                                      int64_t k, double* out, void* stream) {
+    TSRL_CHECK_ARG(partials_step && partials_reset && blk_done && out && dim > 0 && nblk >= 0,
+                   "tsrl_rms_sum_partials2: bad arguments");
+    const int64_t grid = (dim + 1 + kWave - 1) / kWave;
+    hipLaunchKernelGGL(rms_sum_partials2_kernel, dim3((unsigned)grid), dim3(kWave), 0,
+                       as_stream(stream), partials_step, partials_reset, blk_done, nblk, dim, k,
+                       out);
+    TSRL_LAUNCH_CHECK("tsrl_rms_sum_partials2");
     return 0;
 }
 

@@ -74,7 +74,7 @@ _SIGS = {
                             ctypes.c_int),
     "tsrl_synth_box_step_reset": ([_i64, _i64, _u64, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p,
                                    _p, _p, _p], ctypes.c_int),
-    "tsrl_rms_merge2": ([_p, _p, _p, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p, _p],
+    "tsrl_rms_merge2": ([_p, _p, _p, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p],
                         ctypes.c_int),
     "tsrl_synth_box_reset": ([_p, _p, _i64, _i64, _u64, _i64, _p, _p, _p, _p, _p], ctypes.c_int),
     "tsrl_synth_u8_step": ([_p, _i64, _i64, _i64, _u64, _i64, _p, _p, _p, _p, _p, _p, _p],
@@ -82,6 +82,7 @@ _SIGS = {
     "tsrl_synth_u8_reset": ([_p, _p, _i64, _i64, _i64, _u64, _i64, _p, _p, _p, _p],
                             ctypes.c_int),
     "tsrl_rms_merge": ([_p, _i64, _i64, _p, _i64, _p, _p, _p, _p, _p, _p], ctypes.c_int),
+    "tsrl_rms_sum_partials2": ([_p, _p, _p, _i64, _i64, _i64, _p, _p], ctypes.c_int),
     "tsrl_rms_norm_rows": ([_p, _p, _i64, _i64, _p, _p, _f, _f, _p, _p], ctypes.c_int),
     "tsrl_buffer_add": ([ctypes.POINTER(AddArgs), _p], ctypes.c_int),
     "tsrl_ring_advance": ([_p, _i64, _p], ctypes.c_int),
@@ -97,7 +98,8 @@ _SIGS = {
     "tsrl_nstep_return": ([_p, _p, _p, _p, _p, _i64, _i64, _p, _i64, _i64, _d, _p, _i64,
                            ctypes.c_int, _p, _p], ctypes.c_int),
     "tsrl_clip_adam_partials": ([_i64], _i64),
-    "tsrl_clip_adam": ([_p, _p, _p, _p, _i64, _p, _i64, _f, _f, _f, _f, _f, _p, _p, _p, _p],
+    "tsrl_clip_adam": ([_p, _p, _p, _p, _i64, _p, _i64, _f, _f, _f, _f, _f, _p, _p, _p, _p,
+                        _p],
                        ctypes.c_int),
     "tsrl_segtree_set": ([_p, _i64, _p, _p, _i64, _i64, _p, _p], ctypes.c_int),
     "tsrl_segtree_reduce": ([_p, _i64, _i64, _i64, _p, _p], ctypes.c_int),
@@ -107,6 +109,8 @@ _SIGS = {
     "tsrl_ppo_num_partials": ([_i64], _i64),
     "tsrl_adv_moments": ([_p, _p, _i64, _p, _p], ctypes.c_int),
     "tsrl_reduce_partials": ([_p, _i64, _i64, _p, _p], ctypes.c_int),
+    "tsrl_adv_moments_seg_parts": ([_i64], _i64),
+    "tsrl_adv_moments_seg": ([_p, _p, _p, _i64, _i64, _p, _p, _p], ctypes.c_int),
     "tsrl_ppo_gauss_fwd_bwd": ([_p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _p, PPOParams,
                                 _p, _p, _p, _p], ctypes.c_int),
     "tsrl_ppo_gauss_finalize": ([_p, _i64, _p, PPOParams, _p, _p, _p], ctypes.c_int),

@@ -33,11 +33,12 @@ def _empty_data() -> Batch:
 class Collector:
     def __init__(self, policy, env, buffer: Optional[ReplayBuffer] = None,
                  preprocess_fn: Optional[Callable[..., Batch]] = None,
-                 exploration_noise: bool = False, sync_obs_rms: bool = False) -> None:
-        """``sync_obs_rms`` (data-parallel runs only): keep ONE global VectorEnvNormObs
-        statistic across ranks (an all-reduce of the batch moments per env step; the fused
-        step then runs eagerly, without HIP-graph replay).  Default: each rank's env shard
-        normalises with its own running statistics."""
+                 exploration_noise: bool = False, sync_obs_rms: bool = True) -> None:
+        """``sync_obs_rms`` (data-parallel runs only; default True): keep ONE global
+        VectorEnvNormObs statistic across ranks -- the reference's single wrapper over all
+        envs -- with one all-reduce of the step+reset batch moments per env step (captured
+        into the collect HIP graphs when the backend is RCCL; eager steps over gloo).  False:
+        each rank's env shard normalises with its own running statistics."""
         self.env = env
         self.env_num = len(env)
         self.exploration_noise = exploration_noise
@@ -64,7 +65,8 @@ class Collector:
         self.dp = default_dp()
         if sync_obs_rms and self.dp.active and self._norm is not None:
             self._norm.obs_rms.sync_with(self.dp)
-            self.graph_steps = 0
+            if not self.dp.capturable:
+                self.graph_steps = 0
         self.reset(False)
 
     def _assign_buffer(self, buffer) -> None:
@@ -259,11 +261,10 @@ class Collector:
         raw, rew = s["raw"][:kk], s["rew"][:kk]
         term, trunc, done = s["term"][:kk], s["trunc"][:kk], s["done"][:kk]
         norm_obj = self._norm
-        if (ids_t is None and not b.u8 and getattr(b, "supports_step_reset", False)
-                and (norm_obj is None or norm_obj.obs_rms.dp is None
-                     or not norm_obj.obs_rms.dp.active)):
-            # step + auto-reset (one env launch), both obs_rms updates (one launch), buffer
-            # add with the step/reset normalisation and the ring advance (one launch)
+        if ids_t is None and not b.u8 and getattr(b, "supports_step_reset", False):
+            # step + auto-reset (one env launch), both obs_rms updates (one launch; data
+            # parallel: + one all-reduce), buffer add with the step/reset normalisation and
+            # the ring advance (one launch)
             upd = norm_obj is not None and norm_obj.update_obs_rms
             blk = s["blk_done"]
             b._step_reset_raw(kk, raw, s["reset_raw"][:kk], rew, term, trunc, done,

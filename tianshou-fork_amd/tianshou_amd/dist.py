@@ -30,6 +30,11 @@ class DataParallel:
     def active(self) -> bool:
         return self.enabled and (self.world > 1 or DataParallel.force)
 
+    @property
+    def capturable(self) -> bool:
+        """Collectives of this group can be captured into a HIP graph (RCCL); gloo cannot."""
+        return self.enabled and dist.get_backend(self.group) == "nccl"
+
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         if self.active:
             dist.all_reduce(t, group=self.group)

@@ -99,7 +99,10 @@ class FusedActorCritic:
                 for p, v in zip(self.params, self._views)):
             return
         n = sum(p.numel() for p in self.params)
-        self._flat = torch.zeros(n, dtype=torch.float32, device=dev)
+        # one bucket: the flat gradients, then (data-parallel) the minibatch's loss partial
+        # sums, so a single all-reduce per minibatch carries both
+        self._bucket = torch.zeros(n + 4 + MAX_ACT, dtype=torch.float32, device=dev)
+        self._flat = self._bucket[:n]
         self._views = []
         o = 0
         for p in self.params:
@@ -173,21 +176,35 @@ class FusedActorCritic:
                           partials=torch.zeros(
                               max(int(_C.lib().tsrl_clip_adam_partials(n)), 1),
                               dtype=torch.float64, device=dev),
-                          norm=torch.zeros(2, dtype=torch.float32, device=dev))
+                          norm=torch.zeros(2, dtype=torch.float32, device=dev),
+                          lr=torch.zeros(1, dtype=torch.float32, device=dev))
         self._flat = None  # parameter addresses moved: bind_grads re-derives every pointer
         self.bind_grads()
         return True
 
+    def set_lr(self) -> None:
+        """Publish the optimiser's current lr to the device word the Adam kernel reads (one
+        tiny fill per epoch; captured learn graphs then follow an lr_scheduler without being
+        re-captured)."""
+        st = self._adam
+        lr = float(st["optim"].param_groups[0]["lr"])
+        if st.get("lr_host") != lr:
+            st["lr"].fill_(lr)
+            st["lr_host"] = lr
+
     def clip_adam(self, max_norm: Optional[float]) -> None:
-        """clip_grad_norm_(max_norm) (when given) + Adam.step() over the flat buffers."""
+        """clip_grad_norm_(max_norm) (when given) + Adam.step() over the flat buffers; the
+        learning rate comes from the device word of set_lr()."""
         st = self._adam
         g = st["optim"].param_groups[0]
         b1, b2 = g["betas"]
+        if st.get("lr_host") is None:
+            self.set_lr()
         _C.check(_C.lib().tsrl_clip_adam(
             _C.ptr(st["p"]), _C.ptr(self._flat), _C.ptr(st["m"]), _C.ptr(st["v"]),
             st["p"].numel(), _C.ptr(st["steps"]), st["steps"].numel(), float(g["lr"]),
             float(b1), float(b2), float(g["eps"]), float(max_norm) if max_norm else 0.0,
-            _C.ptr(st["partials"]), _C.ptr(st["norm"]), _C.ptr(st["ticket"]),
+            _C.ptr(st["partials"]), _C.ptr(st["norm"]), _C.ptr(st["ticket"]), _C.ptr(st["lr"]),
             _C.stream_ptr(st["p"].device)),
             "tsrl_clip_adam")
 
@@ -278,13 +295,33 @@ class FusedActorCritic:
             self._bufs[key] = b
         return b
 
+    # -- advantage moments of a whole epoch ------------------------------------------------------
+    def epoch_adv_moments(self, adv: torch.Tensor, idx: torch.Tensor, bounds: torch.Tensor,
+                          max_seg: int, dp) -> torch.Tensor:
+        """[n_minibatch, 2] f64 (sum adv, sum adv^2) of every minibatch of the epoch
+        (bounds = device int64 [n_minibatch + 1] into idx), summed over the data-parallel
+        ranks with ONE all-reduce per epoch (ppo.py:109-113 normalises per minibatch)."""
+        lib = _C.lib()
+        nseg = bounds.numel() - 1
+        parts = int(lib.tsrl_adv_moments_seg_parts(max_seg))
+        pa = self._buf("adv_seg_part", nseg * parts * 2, torch.float64)
+        out = self._buf("adv_seg", nseg * 2, torch.float64)[:nseg * 2].view(nseg, 2)
+        _C.check(lib.tsrl_adv_moments_seg(_C.ptr(adv), _C.ptr(idx), _C.ptr(bounds), nseg,
+                                          max_seg, _C.ptr(pa), _C.ptr(out),
+                                          _C.stream_ptr(adv.device)), "tsrl_adv_moments_seg")
+        dp.all_reduce_(out)
+        return out
+
     # -- one minibatch --------------------------------------------------------------------------
     def minibatch(self, obs: torch.Tensor, idx: Optional[torch.Tensor], b: int,
                   act: torch.Tensor, logp_old: torch.Tensor, adv: torch.Tensor,
-                  ret: torch.Tensor, v_s: torch.Tensor, params: "_C.PPOParams", dp
-                  ) -> torch.Tensor:
+                  ret: torch.Tensor, v_s: torch.Tensor, params: "_C.PPOParams", dp,
+                  adv_sums: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Gradients of the minibatch loss into the parameters' .grad; returns the device
-        tensor [loss, clip, vf, ent] (ppo.py:140-142).  ``obs`` are the rows of ``rows()``."""
+        tensor [loss, clip, vf, ent] (ppo.py:140-142).  ``obs`` are the rows of ``rows()``;
+        ``adv_sums`` = this minibatch's row of epoch_adv_moments (computed here when None).
+        Under data parallelism ONE all-reduce carries the gradients and the loss sums; a rank
+        whose share of the global minibatch is empty (b == 0) contributes zeros."""
         self.bind_grads()
         L, lib = self.L, _C.lib()
         dev = obs.device
@@ -294,9 +331,10 @@ class FusedActorCritic:
         ldx = self.Dp
         assert act.shape[-1] == A and act.is_contiguous()
         ip = _C.ptr(idx) if idx is not None else None
+        if b == 0:
+            return self._empty_minibatch(params, dp, adv_sums)
         # advantage moments of the (global) minibatch
-        adv_sums = None
-        if params.norm_adv:
+        if params.norm_adv and adv_sums is None:
             nblk = int(lib.tsrl_ppo_num_partials(b))
             pa = self._buf("adv_part", 2 * nblk, torch.float64)
             _C.check(lib.tsrl_adv_moments(_C.ptr(adv), ip, b, _C.ptr(pa), s), "tsrl_adv_moments")
@@ -321,10 +359,27 @@ class FusedActorCritic:
             _C.ptr(dz1), _C.ptr(obs), ldx, ip, b, D, _C.ptr(L["w1a"].weight.grad),
             _C.ptr(L["w1a"].bias.grad), _C.ptr(L["w1c"].weight.grad),
             _C.ptr(L["w1c"].bias.grad), _C.ptr(ws2), wsb2, s), "tsrl_mlp_dw")
-        dp.all_reduce_(self._flat)
-        dp.all_reduce_(sums)
+        return self._reduce_finalize(sums, params, dp)
+
+    def _empty_minibatch(self, params, dp, adv_sums) -> torch.Tensor:
+        sums = self._buf("sums", 4 + self.A, torch.float64)[:4 + self.A]
+        sums.zero_()
+        self._flat.zero_()
+        return self._reduce_finalize(sums, params, dp)
+
+    def _reduce_finalize(self, sums: torch.Tensor, params, dp) -> torch.Tensor:
+        """One all-reduce of [flat grads | loss sums] (sums travel as f32 in the bucket
+        tail), then the loss terms and the log-std gradient from the global sums."""
+        L, lib = self.L, _C.lib()
+        dev = sums.device
+        if dp.active:
+            P, k = self._flat.numel(), sums.numel()
+            bucket = self._bucket[:P + k]
+            bucket[P:].copy_(sums)
+            dp.all_reduce_(bucket)
+            sums.copy_(bucket[P:])
         terms = torch.empty(4, dtype=torch.float32, device=dev)
         _C.check(lib.tsrl_ppo_gauss_finalize(
-            _C.ptr(sums), A, _C.ptr(L["sigma"]), params, _C.ptr(terms),
-            _C.ptr(L["sigma"].grad), s), "tsrl_ppo_gauss_finalize")
+            _C.ptr(sums), self.A, _C.ptr(L["sigma"]), params, _C.ptr(terms),
+            _C.ptr(L["sigma"].grad), _C.stream_ptr(dev)), "tsrl_ppo_gauss_finalize")
         return terms

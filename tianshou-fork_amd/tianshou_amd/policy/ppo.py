@@ -9,6 +9,7 @@ values are accumulated on device (no per-minibatch .item() syncs; the returned l
 read back once at the end).  Other actor/dist combinations run the reference's torch
 formulation on the GPU.
 """
+import zlib
 from typing import Any, Callable, Dict, List, Optional
 
 import numpy as np
@@ -159,6 +160,12 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
         # utils/np_perm.py); True: torch.randperm on the GPU.
         self.perm_device = perm_device
         self._np_perm = LegacyPermutation()
+        self._np_perm_used, self._np_perm_n = False, 0
+        # data-parallel minibatch composition (see _minibatch_plan): "global" = the
+        # reference's split of the global batch, "local" = every rank splits its own rows
+        self.dp_permutation = "global"
+        self._bounds_cache = None
+        self._graph_failed = False
         # sort_minibatch=True: the rows of every minibatch are visited in ascending buffer
         # order (same minibatch SETS as Batch.split over the permutation; only the order of
         # rows inside a minibatch -- i.e. the float summation order -- changes).  The fused
@@ -221,6 +228,7 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
         else:
             perm = self._np_perm(n, dev)
             self._np_perm_used = True
+            self._np_perm_n = n
         if self.sort_minibatch and batch_size:
             bounds = split_bounds(n, batch_size, merge_last=True)
             sizes = {e - s for s, e in bounds}
@@ -236,7 +244,7 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
         out = self._learn(batch, batch_size, repeat)
         if self._np_perm_used:
             # the next update's np.random.permutation draws, computed while it collects
-            self._np_perm.prefetch(len(batch.v_s), repeat)
+            self._np_perm.prefetch(self._np_perm_n, repeat)
         return out
 
     def _learn(self, batch: Batch, batch_size: int, repeat: int) -> Dict[str, List[float]]:
@@ -257,29 +265,35 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
             adv = batch.adv.reshape(-1).to(**f32).contiguous()
             ret = batch.returns.reshape(-1).to(**f32).contiguous()
             v_s = batch.v_s.reshape(-1).to(**f32).contiguous()
-            perm = self._permutation(n, dev, batch_size)
             mlp_ok = self._mlp is not None and batch.obs.is_cuda and \
                 batch.obs.dtype == torch.float32 and batch.obs.dim() == 2
-            if mlp_ok and self.fused_adam:
-                self._mlp.bind_adam(self.optim)
+            perm, chunks = self._minibatch_plan(n, dev, batch_size, allow_global=mlp_ok)
+            if mlp_ok and self.fused_adam and self._mlp.bind_adam(self.optim):
+                self._mlp.set_lr()
             obs_all = self._mlp.rows(batch.obs) if mlp_ok else None
-            if mlp_ok and self._use_graph(batch_size) and self._graph_ready():
-                terms.append(self._epoch_graph(obs_all, (act, logp_old, adv, ret, v_s), perm, n,
-                                               batch_size, first=(step == 0)))
-                continue
-            for s, e in split_bounds(n, batch_size, merge_last=True):
+            if mlp_ok and self._use_graph(batch_size) and self._graph_ready(chunks):
+                t = self._epoch_graph(obs_all, (act, logp_old, adv, ret, v_s), perm, chunks,
+                                      first=(step == 0))
+                if t is not None:
+                    terms.append(t)
+                    continue
+            adv_mom = None
+            if mlp_ok and self._norm_adv:
+                bounds, max_seg = self._dev_bounds(chunks, dev)
+                adv_mom = self._mlp.epoch_adv_moments(adv, perm, bounds, max_seg, self.dp)
+            for k, (s, e, b_glob) in enumerate(chunks):
                 idx = perm[s:e]
+                params = self._params(b_glob)
                 if mlp_ok:
-                    params = self._params((e - s) * self.dp.world)
                     t = self._mlp.minibatch(obs_all, idx, e - s, act, logp_old, adv, ret, v_s,
-                                            params, self.dp)
+                                            params, self.dp,
+                                            adv_sums=None if adv_mom is None else adv_mom[k])
                     self._opt_step()
                     terms.append(t)
                     continue
                 obs_mb = gather_rows(batch.obs, idx)
                 mu = self.actor.forward_mu(obs_mb)
                 value = self.critic(obs_mb).flatten()
-                params = self._params((e - s) * self.dp.world)
                 loss, t = _GaussPPOLoss.apply(mu, self.actor.sigma_param, value,
                                               (act, logp_old, adv, ret, v_s, idx, params,
                                                self.dp))
@@ -295,6 +309,62 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
             np.zeros((0, 4), np.float32)
         return {"loss": vals[:, 0].tolist(), "loss/clip": vals[:, 1].tolist(),
                 "loss/vf": vals[:, 2].tolist(), "loss/ent": vals[:, 3].tolist()}
+
+    # -- minibatch plan (Batch.split over a permutation; data-parallel shares) ----------------
+    def _minibatch_plan(self, n: int, dev, batch_size: int, allow_global: bool = False):
+        """(idx, [(start, end, b_global)]): minibatch k = rows idx[start:end] of this rank,
+        b_global = the size of the global minibatch (the loss divides by it).
+
+        Single process: Batch.split(batch_size, shuffle=True, merge_last=True) over one
+        permutation (batch.py:896-912).  Data parallel, ``dp_permutation == "global"``: the
+        reference's split of the GLOBAL batch -- every rank draws the same
+        np.random.permutation(world * n) (identical global RandomState on every rank; rank r
+        owns global rows [r*n, (r+1)*n), the env-major order of one VectorReplayBuffer over
+        all ranks' envs) with global minibatches of world * batch_size rows, and keeps its
+        own rows of each, in permutation order.  ``"local"``: each rank splits its own n rows
+        (weak scaling: the sequential host draws stay O(n) per rank)."""
+        W = self.dp.world if self.dp.active else 1
+        if W > 1 and allow_global and self.dp_permutation == "global" and not self.perm_device:
+            N, B = n * W, batch_size * W
+            gb = split_bounds(N, B, merge_last=True)
+            if not self._np_perm_used:  # once per learn(): every rank holds the same stream
+                st = np.random.get_state()
+                h = zlib.crc32(np.ascontiguousarray(st[1]).tobytes() +
+                               int(st[2]).to_bytes(4, "little"))
+                hs = self.dp.all_gather_cat(torch.tensor([h, n], dtype=torch.int64,
+                                                         device=dev)).view(W, 2)
+                if not bool((hs == hs[0]).all()):
+                    raise RuntimeError(
+                        "dp_permutation='global' needs the same global np.random state and "
+                        "the same number of rows on every rank (seed np.random identically, "
+                        "or set dp_permutation='local')")
+            perm_g = self._np_perm(N, dev)
+            self._np_perm_used = True
+            self._np_perm_n = N
+            lo = self.dp.rank * n
+            pos = torch.nonzero((perm_g >= lo) & (perm_g < lo + n)).squeeze(1)
+            idx = (perm_g[pos] - lo).contiguous()
+            lab = torch.div(pos, B, rounding_mode="floor").clamp_(max=len(gb) - 1)
+            counts = torch.bincount(lab, minlength=len(gb)).cpu().tolist()
+            chunks, o = [], 0
+            for (gs, ge), c in zip(gb, counts):
+                chunks.append((o, o + c, ge - gs))
+                o += c
+            return idx, chunks
+        perm = self._permutation(n, dev, batch_size)
+        return perm, [(s, e, (e - s) * W) for s, e in split_bounds(n, batch_size, True)]
+
+    def _dev_bounds(self, chunks, dev):
+        """Device int64 [n_minibatch + 1] start offsets of the chunks (cached per plan)."""
+        key = tuple((s, e) for s, e, _ in chunks)
+        c = self._bounds_cache
+        if c is None or c[0] != key or c[1].device != dev:
+            host = torch.tensor([s for s, _, _ in chunks] + [chunks[-1][1]],
+                                dtype=torch.int64).pin_memory()
+            t = torch.empty(len(host), dtype=torch.int64, device=dev)
+            t.copy_(host, non_blocking=True)
+            c = self._bounds_cache = (key, t, max(e - s for s, e, _ in chunks), host)
+        return c[1], c[2]
 
     def _opt_step(self) -> None:
         """clip_grad_norm_ + optim.step() of ppo.py:143-151: one fused HIP pass
@@ -315,12 +385,17 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
             return batch_size < self.GRAPH_LEARN_MAX_ROWS
         return bool(self.graph_learn)
 
-    def _graph_ready(self) -> bool:
-        """An epoch of fused minibatches can be captured once and replayed: single process
-        (no collective in the step), no advantage recomputation, and a capturable optimiser
-        whose state already exists (the first update runs eagerly)."""
-        if self.graph_learn is False or self.dp.active or self._recompute_adv:
+    def _graph_ready(self, chunks) -> bool:
+        """An epoch of fused minibatches can be captured once and replayed: a static plan
+        (single process, or data parallel with per-rank splits and a capturable backend --
+        the RCCL all-reduces are then graph nodes), no advantage recomputation, and a
+        capturable optimiser whose state already exists (the first update runs eagerly)."""
+        if self.graph_learn is False or self._recompute_adv or self._graph_failed:
             return False
+        if self.dp.active:
+            static = self.dp_permutation == "local" or self.dp.world == 1 or self.perm_device
+            if not (static and self.dp.capturable):
+                return False
         opt = self.optim
         if self._mlp is not None and self._mlp.adam_bound(opt):
             return True
@@ -328,36 +403,53 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
             return False
         return all(p in opt.state for g in opt.param_groups for p in g["params"])
 
-    def _epoch_graph(self, obs_all, arrays, perm, n: int, batch_size: int, first: bool):
-        """One epoch (every minibatch of Batch.split over ``perm``: forward, loss, backward,
-        clip_grad_norm_, optimiser step) as a replay of a captured HIP graph.  The per-update
-        arrays and the permutation are copied into static buffers the graph reads; returns
-        the [n_minibatch, 4] loss terms."""
-        bounds = split_bounds(n, batch_size, merge_last=True)
-        key = (n, batch_size, obs_all.data_ptr(), tuple(obs_all.shape),
+    def _epoch_graph(self, obs_all, arrays, perm, chunks, first: bool):
+        """One epoch (the epoch's advantage moments, then every minibatch of the plan:
+        forward, loss, backward, clip_grad_norm_, optimiser step) as a replay of a captured
+        HIP graph.  The per-update arrays and the permutation are copied into static buffers
+        the graph reads, the learning rate is a device word (FusedActorCritic.set_lr);
+        returns the [n_minibatch, 4] loss terms, or None if the capture failed (the caller
+        then runs the epoch eagerly, and later epochs do too)."""
+        n = perm.numel()
+        key = (n, tuple(chunks), obs_all.data_ptr(), tuple(obs_all.shape),
                tuple(a.shape for a in arrays), self._mlp.flat_grad is not None and
-               self._mlp.flat_grad.data_ptr(), self._mlp.adam_bound(self.optim),
-               tuple(float(g["lr"]) for g in self.optim.param_groups))
+               self._mlp.flat_grad.data_ptr(), self._mlp.adam_bound(self.optim))
         st = self._learn_graph
         if st is None or st["key"] != key:
             st = None
             self._learn_graph = None
+            dev = perm.device
             static = [torch.empty_like(a) for a in arrays]
-            sperm = torch.empty(n, dtype=torch.int64, device=perm.device)
-            sterms = torch.empty(len(bounds), 4, dtype=torch.float32, device=perm.device)
+            sperm = torch.empty(n, dtype=torch.int64, device=dev)
+            sterms = torch.empty(len(chunks), 4, dtype=torch.float32, device=dev)
             for d, a in zip(static, arrays):
                 d.copy_(a)
             sperm.copy_(perm)
+            bounds, max_seg = self._dev_bounds(chunks, dev)
+            sbounds = bounds.clone()
             self._mlp.bind_grads()
             torch.cuda.synchronize()
             graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
-                for i, (s, e) in enumerate(bounds):
-                    t = self._mlp.minibatch(obs_all, sperm[s:e], e - s, *static,
-                                            self._params(e - s), self.dp)
-                    self._opt_step()
-                    sterms[i].copy_(t)
-            st = dict(key=key, graph=graph, static=static, perm=sperm, terms=sterms)
+            try:
+                with torch.cuda.graph(graph):
+                    mom = None
+                    if self._norm_adv:
+                        mom = self._mlp.epoch_adv_moments(static[2], sperm, sbounds, max_seg,
+                                                          self.dp)
+                    for i, (s, e, b_glob) in enumerate(chunks):
+                        t = self._mlp.minibatch(obs_all, sperm[s:e], e - s, *static,
+                                                self._params(b_glob), self.dp,
+                                                adv_sums=None if mom is None else mom[i])
+                        self._opt_step()
+                        sterms[i].copy_(t)
+            except RuntimeError as err:  # e.g. a collective backend that cannot be captured
+                import warnings
+                warnings.warn(f"learn-graph capture failed, running epochs eagerly: {err}")
+                self._graph_failed = True
+                torch.cuda.synchronize()
+                return None
+            st = dict(key=key, graph=graph, static=static, perm=sperm, terms=sterms,
+                      bounds=sbounds)
             self._learn_graph = st
             first = False  # static arrays already hold this update's data
         if first:
@@ -421,7 +513,19 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
                 dist = self(minibatch).dist
                 adv = minibatch.adv
                 if self._norm_adv:
-                    mean, std = adv.mean(), adv.std()
+                    if self.dp.active:
+                        # moments of the GLOBAL minibatch (every rank's share): torch's
+                        # unbiased std from the all-reduced (count, sum, sum of squares)
+                        a64 = adv.detach().double()
+                        m = torch.stack([a64.new_tensor(float(a64.numel())), a64.sum(),
+                                         (a64 * a64).sum()])
+                        self.dp.all_reduce_(m)
+                        cnt, s1, s2 = m[0], m[1], m[2]
+                        mean = (s1 / cnt).to(adv.dtype)
+                        std = ((s2 - s1 * s1 / cnt) / (cnt - 1)).clamp_(min=0).sqrt_() \
+                            .to(adv.dtype)
+                    else:
+                        mean, std = adv.mean(), adv.std()
                     adv = (adv - mean) / (std + self._eps)
                 ratio = (dist.log_prob(minibatch.act) - minibatch.logp_old).exp().float()
                 ratio = ratio.reshape(ratio.size(0), -1).transpose(0, 1)
@@ -450,10 +554,15 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
                     nn.utils.clip_grad_norm_(self._actor_critic.parameters(),
                                              max_norm=self._grad_norm)
                 self.optim.step()
-                clip_losses.append(clip_loss.detach())
-                vf_losses.append(vf_loss.detach())
-                ent_losses.append(ent_loss.detach())
-                losses.append(loss.detach())
+                terms4 = torch.stack([loss.detach(), clip_loss.detach(), vf_loss.detach(),
+                                      ent_loss.detach()]).float()
+                if self.dp.active:  # equal per-rank shares: global mean = mean over ranks
+                    self.dp.all_reduce_(terms4)
+                    terms4 /= self.dp.world
+                losses.append(terms4[0])
+                clip_losses.append(terms4[1])
+                vf_losses.append(terms4[2])
+                ent_losses.append(terms4[3])
         out = {}
         for k, v in (("loss", losses), ("loss/clip", clip_losses), ("loss/vf", vf_losses),
                      ("loss/ent", ent_losses)):

@@ -59,6 +59,7 @@ class DeviceRunningMeanStd:
         self.dp = None  # tianshou_amd.dist.DataParallel: sync the moments over ranks
         self.snap_mean_t = None  # state after the step-batch update of merge2
         self.snap_var_t = None
+        self._payload = None  # data-parallel merge2 all-reduce vector
 
     def sync_with(self, dp) -> None:
         self.dp = dp
@@ -111,15 +112,32 @@ class DeviceRunningMeanStd:
     def merge2(self, partials_step: torch.Tensor, partials_reset: torch.Tensor,
                blk_done: torch.Tensor, nblk: int, k: int) -> None:
         """The step-batch update followed by the reset-rows update in one launch; the state
-        after the first lands in ``snap_mean_t`` / ``snap_var_t`` (single-process only)."""
+        after the first lands in ``snap_mean_t`` / ``snap_var_t``.  With ``self.dp`` active
+        both updates use the GLOBAL batches (every rank's env shard, the reference's single
+        VectorEnvNormObs over all envs, venv_wrappers.py:93-99): this rank's moments are
+        folded into one [4*dim + 2] vector and summed over the ranks with ONE all-reduce per
+        env step (a graph node when the backend is RCCL)."""
         if self.snap_mean_t is None:
             self.snap_mean_t = torch.empty_like(self.mean_t)
             self.snap_var_t = torch.empty_like(self.var_t)
-        _C.check(_C.lib().tsrl_rms_merge2(
+        L, st = _C.lib(), _C.stream_ptr()
+        k_dev = None
+        if self.dp is not None and self.dp.active:
+            D = self.dim
+            if self._payload is None:
+                self._payload = torch.empty(4 * D + 2, dtype=torch.float64, device=self.device)
+            pl = self._payload
+            _C.check(L.tsrl_rms_sum_partials2(_C.ptr(partials_step), _C.ptr(partials_reset),
+                                              _C.ptr(blk_done), nblk, D, k, _C.ptr(pl), st),
+                     "tsrl_rms_sum_partials2")
+            self.dp.all_reduce_(pl)
+            partials_step, partials_reset, blk_done = pl[:2 * D], pl[2 * D:4 * D], pl[4 * D:]
+            k_dev, nblk = pl[4 * D + 1:], 1
+        _C.check(L.tsrl_rms_merge2(
             _C.ptr(partials_step), _C.ptr(partials_reset), _C.ptr(blk_done), nblk, self.dim, k,
             _C.ptr(self.mean_t), _C.ptr(self.var_t), _C.ptr(self.count_t),
             _C.ptr(self.snap_mean_t), _C.ptr(self.snap_var_t), _C.ptr(self.ticket_t),
-            _C.stream_ptr()), "tsrl_rms_merge2")
+            _C.ptr(k_dev), st), "tsrl_rms_merge2")
 
     def update(self, x: torch.Tensor, mask: Optional[torch.Tensor] = None) -> None:
         x = x.reshape(len(x), -1)
