@@ -36,10 +36,20 @@ SPIN_CYCLES = 100_000          # device spin ahead of the GAE start event (see G
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--workload", choices=["humanoid", "small", "atari"], default="humanoid",
+    ap.add_argument("--workload", choices=["humanoid", "small", "atari", "cartpole"],
+                    default="humanoid",
                     help="humanoid: BASELINE config 3 (the headline line); small: config 2 "
                          "(Box 17/6, 512 envs x 128 steps); atari: config 5 (u8 4x84x84 frame "
-                         "stacks, Discrete(6), Nature-DQN trunk, 1024 envs x 256 steps)")
+                         "stacks, Discrete(6), Nature-DQN trunk, 1024 envs x 256 steps); "
+                         "cartpole: config 1 (CartPole-v1, 4 envs x 500 steps = "
+                         "step_per_collect 2000, Net 64-64 shared by Categorical(probs) actor "
+                         "and critic, batch 64, repeat 10: test/discrete/test_ppo.py)")
+    ap.add_argument("--cartpole-env", choices=["host", "device"], default="host",
+                    help="config 1 envs: host = DummyVectorEnv of CartPoleEnv (the reference's "
+                         "setup, the Collector's generic host-env loop); device = "
+                         "CartPoleVectorEnv (HIP kernel, fused device collect)")
+    ap.add_argument("--batch-size", type=int, default=None,
+                    help="minibatch rows (default: envs x T / minibatches)")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=2,
                     help="untimed iterations; the second one completes the collect-graph "
@@ -70,12 +80,18 @@ def parse():
     a = ap.parse_args()
     defaults = dict(humanoid=(4096, 2048, 376, 17, 256, 1000),
                     small=(512, 128, 17, 6, 128, 1000),
-                    atari=(1024, 256, 0, 6, 16, 256))[a.workload]
+                    atari=(1024, 256, 0, 6, 16, 256),
+                    cartpole=(4, 500, 4, 2, 0, 500))[a.workload]
     for k, v in zip(("envs", "T", "obs", "act", "cpu_steps", "ep_len"), defaults):
         if getattr(a, k) is None:
             setattr(a, k, v)
-    if a.workload == "atari":
+    if a.workload in ("atari", "cartpole"):
         a.no_cpu_baseline = True  # the CPU port covers the Box workloads only
+    if a.workload == "cartpole":
+        if a.batch_size is None:
+            a.batch_size = 64
+        if "--repeat" not in " ".join(sys.argv):
+            a.repeat = 10
     return a
 
 
@@ -163,6 +179,40 @@ def spawn_ranks(n: int) -> int:
     return max(abs(rc) for rc in rcs)
 
 
+def build_cartpole(args, dev, rank):
+    """BASELINE config 1: test/discrete/test_ppo.py's PPO (Net 64-64 shared by the
+    Categorical(probs) actor and the critic, orthogonal init, Adam 3e-4, vf .5, ent 0,
+    max_grad_norm .5, gae .95, no rew/adv normalisation) over 4 CartPole-v1 envs."""
+    from tianshou_amd.data import Collector, VectorReplayBuffer
+    from tianshou_amd.env import CartPoleEnv, CartPoleVectorEnv, Discrete, DummyVectorEnv
+    from tianshou_amd.policy import PPOPolicy
+    from tianshou_amd.utils.net import ActorCritic, DiscreteActor, DiscreteCritic, Net
+    E = args.envs
+    if args.cartpole_env == "host":
+        env = DummyVectorEnv([CartPoleEnv for _ in range(E)])
+        env.seed(1626 + 1000 * rank)
+    else:
+        env = CartPoleVectorEnv(E, seed=1626 + rank, device=dev)
+    net = Net(4, hidden_sizes=(64, 64), device=dev)
+    actor = DiscreteActor(net, 2, device=dev).to(dev)
+    critic = DiscreteCritic(net, device=dev).to(dev)
+    ac = ActorCritic(actor, critic)
+    for m in ac.modules():
+        if isinstance(m, torch.nn.Linear):
+            torch.nn.init.orthogonal_(m.weight)
+            torch.nn.init.zeros_(m.bias)
+    optim = torch.optim.Adam(ac.parameters(), lr=3e-4)
+    policy = PPOPolicy(actor, critic, optim, torch.distributions.Categorical,
+                       discount_factor=0.99, max_grad_norm=0.5, eps_clip=0.2, vf_coef=0.5,
+                       ent_coef=0.0, gae_lambda=0.95, reward_normalization=False,
+                       dual_clip=None, value_clip=False, action_space=Discrete(2),
+                       deterministic_eval=True, advantage_normalization=False,
+                       recompute_advantage=False, action_scaling=False,
+                       perm_device=(args.perm != "numpy")).to(dev)
+    buf = VectorReplayBuffer(20000, E, device=dev)
+    return Collector(policy, env, buf), policy, buf
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -197,6 +247,8 @@ def main():
     if args.workload == "atari":
         coll, policy, buf = build_atari(args, dev, rank)
         D = "4x84x84 u8"
+    elif args.workload == "cartpole":
+        coll, policy, buf = build_cartpole(args, dev, rank)
     else:
         env = VectorEnvNormObs(SyntheticVectorEnv(E, (D,), A, ep_len=args.ep_len, seed=rank,
                                                   device=dev))
@@ -228,7 +280,8 @@ def main():
         coll.collect(n_step=n)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        policy.update(0, buf, batch_size=n // args.minibatches, repeat=args.repeat)
+        policy.update(0, buf, batch_size=args.batch_size or n // args.minibatches,
+                      repeat=args.repeat)
         coll.reset_buffer(keep_statistics=True)
         torch.cuda.synchronize()
         phase["collect"] += t1 - t0
@@ -291,13 +344,17 @@ def main():
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f32 (GAE scan f64)", "data": "synthetic",
-            "config": {"workload": f"Synthetic {'Discrete' if args.workload == 'atari' else 'Box'}"
-                                   f"(obs={D}, act={A}), {E} envs x {T} steps "
+            "config": {"workload": (f"CartPole-v1 ({args.cartpole_env} envs)"
+                                    if args.workload == "cartpole" else
+                                    f"Synthetic {'Discrete' if args.workload == 'atari' else 'Box'}"
+                                    f"(obs={D}, act={A})") +
+                                   f", {E} envs x {T} steps "
                                    f"per GPU, GAE+PPO (repeat {args.repeat}, "
-                                   f"{args.minibatches} minibatches)",
-                       "baseline_config": dict(humanoid=3, small=2, atari=5)[args.workload],
+                                   f"minibatch {args.batch_size or n // args.minibatches})",
+                       "baseline_config": dict(humanoid=3, small=2, atari=5,
+                                               cartpole=1)[args.workload],
                        "envs_per_gpu": E, "steps_per_env": T, "global_batch": n * world,
-                       "minibatch": n // args.minibatches * world,
+                       "minibatch": (args.batch_size or n // args.minibatches) * world,
                        "parallelism": f"env-sharded dp{world}",
                        "permutation": args.perm + (" (per-rank stream)" if world > 1 else ""),
                        "rccl_world_size": world if distributed else None,

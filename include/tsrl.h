@@ -107,6 +107,21 @@ int tsrl_synth_u8_reset(const int64_t* ids, const uint8_t* mask, int64_t k,
                         int64_t obs_bytes, int64_t frame_stack, uint64_t seed, int64_t ep_len,
                         int64_t* ep_j, int64_t* ep_t, uint8_t* obs_out, void* stream);
 
+/* CartPole-v1 (BASELINE config 1; gymnasium classic_control cartpole.py + TimeLimit(500),
+ * restated -- gymnasium parity unpinned): state f64 [N, 4] (x, x_dot, theta, theta_dot),
+ * ep_t / ep_j per env.  step: rows r < k act on env ids[r] (NULL -> r) with Discrete(2)
+ * actions act[r] (int64); writes obs f32 [k, 4], rew f64 (1, or 0 after termination),
+ * terminated (x / theta thresholds) and truncated (ep_t >= max_steps).  reset: rows with
+ * mask[r] (NULL -> all) start episode ep_j+1 from U(-0.05, 0.05)^4 of a counter hash
+ * (oracle/cartpole.py).  Stands behind the Collector's env.step/reset for CartPoleVectorEnv
+ * (tianshou/env/venvs.py:300-381 over gym envs in the reference). */
+int tsrl_cartpole_step(const int64_t* ids, int64_t k, const int64_t* act, int64_t max_steps,
+                       double* state, int64_t* ep_t, float* obs_out, double* rew_out,
+                       uint8_t* term_out, uint8_t* trunc_out, void* stream);
+int tsrl_cartpole_reset(const int64_t* ids, const uint8_t* mask, int64_t k, uint64_t seed,
+                        double* state, int64_t* ep_j, int64_t* ep_t, float* obs_out,
+                        void* stream);
+
 /* ---------------------------------------------------------------------------------
  * Observation RunningMeanStd (VectorEnvNormObs, tianshou/env/venv_wrappers.py:65-112;
  * RunningMeanStd, tianshou/utils/statistics.py:69-114).

@@ -1,0 +1,161 @@
+"""BASELINE config 1 -- CartPole-v1 PPO over DummyVectorEnv x 4 (test/discrete/test_ppo.py
+configuration) through the Collector's generic host-env loop (collector.py:258-361), with the
+VectorReplayBuffer, process_fn and the Categorical(probs) PPO update on the GPU, against the
+reference run recorded by tools/gen_goldens.py gen_cartpole (tests/golden/cartpole.npz).
+
+The env is this build's CartPole-v1 restatement (tianshou_amd/env/cartpole.py) in both runs:
+gymnasium is not installed, so gymnasium parity of the dynamics is unpinned; everything the
+reference computes on top of the env is pinned.  Tolerances: collected obs / act / rew /
+flags / env ids / episode statistics bit-exact (host env + host action sampling on both
+sides; the evaluation collect takes the argmax of the GPU policy's probabilities);
+process_fn values / returns / advantages rtol 1e-5 (atol 1e-6 * max|ref|, north_star's GAE
+tolerance), logp_old rtol 1e-5; learn() losses rtol 1e-4 and parameters rtol 1e-3 after 70
+Adam steps (GPU GEMMs vs the reference's CPU torch, as in test_gpu_ppo_discrete.py).
+
+The device CartPoleVectorEnv (csrc/cartpole.hip) is checked against oracle/cartpole.py."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    return torch.device("cuda", 0)
+
+
+def _build(z, dev):
+    from tianshou_amd.data import Collector, VectorReplayBuffer
+    from tianshou_amd.env import CartPoleEnv, Discrete, DummyVectorEnv
+    from tianshou_amd.policy import PPOPolicy
+    from tianshou_amd.utils.net import ActorCritic, DiscreteActor, DiscreteCritic, Net
+    seed, E = int(z["seed"]), int(z["E"])
+    envs = DummyVectorEnv([CartPoleEnv for _ in range(E)])
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    envs.seed(seed)
+    net = Net(4, hidden_sizes=(64, 64), device=dev)
+    actor = DiscreteActor(net, 2, device=dev).to(dev)
+    critic = DiscreteCritic(net, device=dev).to(dev)
+    optim = torch.optim.Adam(ActorCritic(actor, critic).parameters(), lr=3e-4)
+    policy = PPOPolicy(actor, critic, optim, torch.distributions.Categorical,
+                       discount_factor=0.99, max_grad_norm=0.5, eps_clip=0.2, vf_coef=0.5,
+                       ent_coef=0.0, gae_lambda=0.95, reward_normalization=False,
+                       dual_clip=None, value_clip=False, action_space=Discrete(2),
+                       deterministic_eval=True, advantage_normalization=False,
+                       recompute_advantage=False, action_scaling=False).to(dev)
+    policy.load_state_dict({k[len("init_"):]: torch.as_tensor(z[k]) for k in z.files
+                            if k.startswith("init_")})
+    buf = VectorReplayBuffer(20000, E, device=dev)
+    return envs, policy, buf, Collector(policy, envs, buf)
+
+
+def _check_stats(z, prefix, res):
+    assert res["n/ep"] == int(z[prefix + "n_ep"])
+    assert res["n/st"] == int(z[prefix + "n_st"])
+    for k in ("lens", "idxs", "rews"):
+        assert np.asarray(res[k]).tolist() == z[prefix + k].tolist(), k
+    assert res["rew"] == pytest.approx(float(z[prefix + "rew"]), rel=1e-12)
+    assert res["len_std"] == pytest.approx(float(z[prefix + "len_std"]), rel=1e-12)
+
+
+def _check_buf(z, prefix, buf):
+    m = buf._meta
+    for k in ("obs", "obs_next", "act", "rew", "terminated", "truncated", "done"):
+        got = getattr(m, k).cpu().numpy()
+        want = z[prefix + k]
+        assert got.shape == want.shape, k
+        assert np.array_equal(got.astype(want.dtype), want), k
+    written = np.abs(z[prefix + "obs"]).sum(-1) > 0
+    assert np.array_equal(m.info.env_id.cpu().numpy()[written], z[prefix + "env_id"][written])
+
+
+def test_cartpole_config1_matches_reference(golden_dir, dev):
+    z = np.load(os.path.join(golden_dir, "cartpole.npz"))
+    envs, policy, buf, c = _build(z, dev)
+    assert policy._cat == 1 and policy._shared_trunk
+    np.testing.assert_array_equal(np.asarray(c.data.obs), z["c0_data_obs"])
+    n_step = int(z["n_step"])
+    # 1. random-action collect (each env's seeded Discrete space)
+    res1 = c.collect(n_step=n_step, random=True)
+    _check_stats(z, "c1_", res1)
+    _check_buf(z, "c1_buf_", buf)
+    assert buf._lengths.tolist() == z["c1_lengths"].tolist()
+    assert buf.last_index.tolist() == z["c1_last_index"].tolist()
+    # 2. update: sample(0) -> process_fn -> learn (batch 64, repeat 10)
+    np.random.seed(77)
+    batch, idx = buf.sample(0)
+    assert np.asarray(idx).tolist() == z["c1_indices"].tolist()
+    batch = policy.process_fn(batch, buf, idx)
+    for k in ("v_s", "logp_old", "returns", "adv"):
+        want = z["pf_" + k]
+        np.testing.assert_allclose(batch[k].cpu().numpy(), want, rtol=1e-5,
+                                   atol=1e-6 * float(np.abs(want).max()), err_msg=k)
+    res = policy.learn(batch, batch_size=64, repeat=10)
+    for k in ("loss", "loss/clip", "loss/vf", "loss/ent"):
+        np.testing.assert_allclose(res[k], z["learn_" + k.replace("/", "_")], rtol=1e-4,
+                                   atol=1e-5, err_msg=k)
+    sd = policy.state_dict()
+    for k in z.files:
+        if k.startswith("final_actor.") or k.startswith("final_critic."):
+            np.testing.assert_allclose(sd[k[len("final_"):]].cpu().numpy(), z[k], rtol=1e-3,
+                                       atol=1e-5, err_msg=k)
+    # 3. deterministic evaluation collect with the updated policy (argmax of the probs)
+    c.reset_buffer(keep_statistics=True)
+    policy.eval()
+    res2 = c.collect(n_step=n_step)
+    policy.train()
+    _check_stats(z, "c2_", res2)
+    _check_buf(z, "c2_buf_", buf)
+
+
+def test_cartpole_n_episode_collect(golden_dir, dev):
+    """n_episode collection with surplus-env removal (collector.py:350-361) on host envs."""
+    from tianshou_amd.data import Collector, VectorReplayBuffer
+    from tianshou_amd.env import CartPoleEnv, DummyVectorEnv
+    z = np.load(os.path.join(golden_dir, "cartpole.npz"))
+    _, policy, _, _ = _build(z, dev)
+    E = int(z["E"])
+    envs3 = DummyVectorEnv([CartPoleEnv for _ in range(E)])
+    envs3.seed(int(z["seed"]) + 100)
+    buf3 = VectorReplayBuffer(20000, E, device=dev)
+    c3 = Collector(policy, envs3, buf3)
+    res3 = c3.collect(n_episode=6, random=True)
+    _check_stats(z, "c3_", res3)
+    _check_buf(z, "c3_buf_", buf3)
+    assert buf3._lengths.tolist() == z["c3_lengths"].tolist()
+    assert buf3.last_index.tolist() == z["c3_last_index"].tolist()
+
+
+def test_device_cartpole_matches_oracle(dev):
+    """CartPoleVectorEnv (HIP, f64 dynamics, hash resets) vs oracle/cartpole.py over 600
+    steps of random actions with resets of finished envs: terminated / truncated / rew
+    bit-exact, obs within 1 f32 ulp-scale (device sin/cos may differ from glibc's by an ulp
+    in f64, re-synchronised at every reset)."""
+    from oracle.cartpole import CartPoleHashVecNP
+    from tianshou_amd.env import CartPoleVectorEnv
+    N = 64
+    env = CartPoleVectorEnv(N, seed=5, device=dev, max_episode_steps=40)
+    ora = CartPoleHashVecNP(N, seed=5, max_steps=40)
+    obs, _ = env.reset()
+    np.testing.assert_array_equal(obs.cpu().numpy(), ora.reset())
+    rng = np.random.default_rng(0)
+    n_term = n_trunc = 0
+    for _ in range(600):
+        a = rng.integers(0, 2, N)
+        o, r, te, tr, info = env.step(torch.as_tensor(a, device=dev))
+        wo, wr, wte, wtr = ora.step(a)
+        np.testing.assert_allclose(o.cpu().numpy(), wo, rtol=1e-6, atol=1e-7)
+        assert np.array_equal(r.cpu().numpy(), wr)
+        assert np.array_equal(te.cpu().numpy(), wte)
+        assert np.array_equal(tr.cpu().numpy(), wtr)
+        done = np.flatnonzero(wte | wtr)
+        n_term += int(wte.sum())
+        n_trunc += int(wtr.sum())
+        if len(done):
+            ro, _ = env.reset(done)
+            np.testing.assert_array_equal(ro.cpu().numpy(), ora.reset(done))
+    assert n_term > 100 and n_trunc > 10

@@ -81,6 +81,8 @@ _SIGS = {
                            ctypes.c_int),
     "tsrl_synth_u8_reset": ([_p, _p, _i64, _i64, _i64, _u64, _i64, _p, _p, _p, _p],
                             ctypes.c_int),
+    "tsrl_cartpole_step": ([_p, _i64, _p, _i64, _p, _p, _p, _p, _p, _p, _p], ctypes.c_int),
+    "tsrl_cartpole_reset": ([_p, _p, _i64, _u64, _p, _p, _p, _p, _p], ctypes.c_int),
     "tsrl_rms_merge": ([_p, _i64, _i64, _p, _i64, _p, _p, _p, _p, _p, _p], ctypes.c_int),
     "tsrl_rms_sum_partials2": ([_p, _p, _p, _i64, _i64, _i64, _p, _p], ctypes.c_int),
     "tsrl_rms_norm_rows": ([_p, _p, _i64, _i64, _p, _p, _f, _f, _p, _p], ctypes.c_int),

@@ -55,9 +55,31 @@ def _index_value(v, index):
     return v
 
 
+def _stack_dicts(seq) -> "Batch":
+    """Batch.stack of a sequence of dicts (batch.py:_parse_value for a list / object array
+    of dicts, e.g. the per-env info dicts a host vector env returns): keys present in every
+    dict are stacked."""
+    keys = set(seq[0].keys())
+    for d in seq[1:]:
+        keys &= set(d.keys())
+    out = {}
+    for k in sorted(keys):
+        vals = [d[k] for d in seq]
+        if all(isinstance(x, dict) for x in vals):
+            out[k] = _stack_dicts(vals)
+        else:
+            out[k] = np.stack([np.asarray(x) for x in vals])
+    return Batch(out)
+
+
 def _parse(v):
     if isinstance(v, dict):
         return Batch(v)
+    if isinstance(v, np.ndarray) and v.dtype == object and v.ndim == 1 and len(v) and \
+            all(isinstance(x, dict) for x in v):
+        return _stack_dicts(list(v))
+    if isinstance(v, (list, tuple)) and len(v) and all(isinstance(x, dict) for x in v):
+        return _stack_dicts(list(v))
     if isinstance(v, (list, tuple)) and not isinstance(v, Batch):
         if any(isinstance(x, torch.Tensor) for x in v):
             return v  # e.g. logits=(mu, sigma) of a Gaussian actor

@@ -236,6 +236,8 @@ class Collector:
     # -- fused device path ------------------------------------------------------------------
     def _act_spec(self):
         act_space = self._action_space
+        if isinstance(act_space, (list, tuple)):  # host vector envs: one space per env
+            act_space = act_space[0]
         if hasattr(act_space, "n"):
             return (), torch.int64
         return tuple(act_space.shape), torch.float32

@@ -30,6 +30,19 @@ class DeviceVectorEnv:
     def seed(self, seed=None):
         return [seed] * self.env_num
 
+    def _ids(self, id):
+        if id is None:
+            return None, self.env_num
+        ids = np.atleast_1d(np.asarray(id, dtype=np.int64))
+        return torch.as_tensor(ids, device=self.device), len(ids)
+
+    def reset(self, id=None, **kwargs):
+        ids, k = self._ids(id)
+        obs = self.alloc_obs(k)
+        self._reset_raw(ids, None, k, obs, None)
+        env_id = ids if ids is not None else torch.arange(k, device=self.device)
+        return obs, {"env_id": env_id}
+
 
 class SyntheticVectorEnv(DeviceVectorEnv):
     """Box(obs_dim) f32 or u8 (e.g. 4x84x84) observations, Box(act_dim) or Discrete actions;
@@ -120,19 +133,6 @@ class SyntheticVectorEnv(DeviceVectorEnv):
                                             _C.ptr(partials), s), "tsrl_synth_box_reset")
 
     # -- BaseVectorEnv surface ----------------------------------------------------------------
-    def _ids(self, id):
-        if id is None:
-            return None, self.env_num
-        ids = np.atleast_1d(np.asarray(id, dtype=np.int64))
-        return torch.as_tensor(ids, device=self.device), len(ids)
-
-    def reset(self, id=None, **kwargs):
-        ids, k = self._ids(id)
-        obs = self.alloc_obs(k)
-        self._reset_raw(ids, None, k, obs, None)
-        env_id = ids if ids is not None else torch.arange(k, device=self.device)
-        return obs, {"env_id": env_id}
-
     def step(self, action, id=None):
         ids, k = self._ids(id)
         obs = self.alloc_obs(k)

@@ -776,12 +776,96 @@ def gen_replay():
     _save("replay.npz", **out)
 
 
+# --------------------------------------------------------------------------------------
+# 11. BASELINE config 1: CartPole-v1 PPO over DummyVectorEnv x 4 in the configuration of
+#     test/discrete/test_ppo.py:19-146 (Net 64-64 shared by Actor(softmax probs) and
+#     Critic, orthogonal init, Categorical on probs, Adam 3e-4, vf .5, ent 0, max_grad_norm
+#     .5, deterministic_eval, seed 1626, batch 64, repeat 10) -- the Collector's generic
+#     host-env loop (collector.py:258-361) and DummyVectorEnv (venvs.py:260-403), driven by
+#     the restated CartPole env (tianshou_amd/env/cartpole.py; gymnasium is absent here).
+# --------------------------------------------------------------------------------------
+def gen_cartpole():
+    sys.path.insert(0, os.path.join(ROOT, "tianshou-fork_amd"))
+    from tianshou_amd.env.cartpole import CartPoleEnv as _CP
+    from tianshou.utils.net.common import ActorCritic, Net
+
+    class CartPoleEnv(_CP, gym.Env):  # the reference's venvs accept gymnasium.Env only
+        pass
+
+    from tianshou.utils.net.discrete import Actor, Critic
+    seed, E, n_step = 1626, 4, 400
+    out = dict(seed=np.array(seed), E=np.array(E), n_step=np.array(n_step))
+    envs = DummyVectorEnv([lambda: CartPoleEnv() for _ in range(E)])
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    envs.seed(seed)
+    net = Net(4, hidden_sizes=[64, 64])
+    actor = Actor(net, 2)
+    critic = Critic(net)
+    ac = ActorCritic(actor, critic)
+    for m in ac.modules():
+        if isinstance(m, torch.nn.Linear):
+            torch.nn.init.orthogonal_(m.weight)
+            torch.nn.init.zeros_(m.bias)
+    optim = torch.optim.Adam(ac.parameters(), lr=3e-4)
+    policy = PPOPolicy(actor, critic, optim, torch.distributions.Categorical,
+                       discount_factor=0.99, max_grad_norm=0.5, eps_clip=0.2, vf_coef=0.5,
+                       ent_coef=0.0, gae_lambda=0.95, reward_normalization=0, dual_clip=None,
+                       value_clip=0, action_space=gym.spaces.Discrete(2),
+                       deterministic_eval=True, advantage_normalization=0,
+                       recompute_advantage=0,
+                       # the fork's BasePolicy rejects action_scaling (default True) for a
+                       # Discrete space (base.py:94-98), so test_ppo.py as written raises;
+                       # action_scaling=False is the only accepted configuration
+                       action_scaling=False)
+    out.update(_sd_arrays("init_", policy))
+    buf = VectorReplayBuffer(20000, E)
+    c = Collector(policy, envs, buf)
+    out["c0_data_obs"] = np.asarray(c.data.obs)
+    # 1. random actions (the trainer's optional warm-up collect): each env's action space
+    res1 = c.collect(n_step=n_step, random=True)
+    out.update(_stats_arrays("c1_", res1))
+    out.update(_buf_arrays("c1_buf_", buf))
+    out["c1_lengths"], out["c1_last_index"] = np.asarray(buf._lengths), \
+        np.asarray(buf.last_index)
+    # 2. one on-policy update on it: sample(0) -> process_fn -> learn (10 x 7 minibatches)
+    np.random.seed(77)
+    batch, idx = buf.sample(0)
+    out["c1_indices"] = idx
+    batch = policy.process_fn(batch, buf, idx)
+    for k in ("v_s", "returns", "adv", "logp_old"):
+        out["pf_" + k] = batch[k].detach().numpy()
+    res = policy.learn(batch, batch_size=64, repeat=10)
+    for k in ("loss", "loss/clip", "loss/vf", "loss/ent"):
+        out["learn_" + k.replace("/", "_")] = np.array(res[k])
+    out.update(_sd_arrays("final_", policy))
+    c.reset_buffer(keep_statistics=True)
+    # 3. deterministic evaluation collect (argmax of the probs) with the updated policy
+    policy.eval()
+    res2 = c.collect(n_step=n_step)
+    policy.train()
+    out.update(_stats_arrays("c2_", res2))
+    out.update(_buf_arrays("c2_buf_", buf))
+    # 4. episode-count collection (surplus-env removal) on a fresh collector, sampled actions
+    envs3 = DummyVectorEnv([lambda: CartPoleEnv() for _ in range(E)])
+    envs3.seed(seed + 100)
+    buf3 = VectorReplayBuffer(20000, E)
+    c3 = Collector(policy, envs3, buf3)
+    res3 = c3.collect(n_episode=6, random=True)
+    out.update(_stats_arrays("c3_", res3))
+    out.update(_buf_arrays("c3_buf_", buf3))
+    out["c3_lengths"], out["c3_last_index"] = np.asarray(buf3._lengths), \
+        np.asarray(buf3.last_index)
+    _save("cartpole.npz", **out)
+
+
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     which = sys.argv[1:] or ["returns", "gae", "buffer", "split", "rms", "ppo", "collector",
-                             "stack", "ppo_discrete", "npg", "replay"]
+                             "stack", "ppo_discrete", "npg", "replay", "cartpole"]
     table = dict(returns=gen_returns_known, gae=gen_gae_random, buffer=gen_buffer_traces,
                  split=gen_split, rms=gen_rms, ppo=gen_ppo, collector=gen_collector,
-                 stack=gen_stack, ppo_discrete=gen_ppo_discrete, npg=gen_npg, replay=gen_replay)
+                 stack=gen_stack, ppo_discrete=gen_ppo_discrete, npg=gen_npg, replay=gen_replay,
+                 cartpole=gen_cartpole)
     for w in which:
         table[w]()
