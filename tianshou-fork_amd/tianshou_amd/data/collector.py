@@ -201,10 +201,12 @@ class Collector:
                 "idxs": idxs, "rew": rew_mean, "len": len_mean, "rew_std": rew_std,
                 "len_std": len_std}
 
-    def _policy_act(self, obs, info, random: bool, no_grad: bool, k: int):
+    def _policy_act(self, obs, info, random: bool, no_grad: bool, k: int, ids=None):
         if random:
+            # collector.py:262-266: one sample per READY env from that env's own space
+            ids = range(k) if ids is None else ids
             try:
-                acts = [self._action_space[i].sample() for i in range(k)]
+                acts = [self._action_space[i].sample() for i in ids]
             except TypeError:
                 acts = [self._action_space.sample() for _ in range(k)]
             act = torch.as_tensor(np.asarray(acts), device=self.device)
@@ -450,7 +452,7 @@ class Collector:
         while True:
             obs = torch.as_tensor(np.asarray(self.data.obs), device=self.buffer._ensure_device())
             act, policy = self._policy_act(obs, self.data.info, random, no_grad,
-                                           len(ready_env_ids))
+                                           len(ready_env_ids), ready_env_ids)
             act_np = act.detach().cpu().numpy() if isinstance(act, torch.Tensor) else act
             self.data.update(policy=policy, act=act_np)
             action_remap = self.policy.map_action(act_np)

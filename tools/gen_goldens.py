@@ -777,6 +777,54 @@ def gen_replay():
 
 
 # --------------------------------------------------------------------------------------
+# 10b. BasePolicy.update with an lr_scheduler (base.py:288-315; get_linear_lr_schedular,
+#      utils/lr_scheduler.py:47-56 -- the fork's lr_decay default) and, in one variant,
+#      recompute_advantage (ppo.py:104-105: A6/A5 rerun for every repeat after the first),
+#      over 3 updates of the same filled VectorReplayBuffer, rew_norm on.
+# --------------------------------------------------------------------------------------
+def _sched_buffer(E, T, D, A, rng):
+    buf = VectorReplayBuffer(E * T, E)
+    for t in range(T):
+        done_t = (rng.random(E) < 0.06) | (t == T - 1) & (rng.random(E) < 0.5)
+        term = done_t & (rng.random(E) < 0.5)
+        buf.add(Batch(obs=rng.standard_normal((E, D)).astype(np.float32),
+                      act=rng.standard_normal((E, A)).astype(np.float32),
+                      rew=rng.standard_normal(E), terminated=term, truncated=done_t & ~term,
+                      obs_next=rng.standard_normal((E, D)).astype(np.float32),
+                      info={}))
+    return buf
+
+
+def gen_sched():
+    from tianshou.utils.lr_scheduler import get_linear_lr_schedular
+    out = {}
+    E, T, D, A = 8, 40, 11, 3
+    for tag, recompute, bs in (("recompute", True, 64), ("graph", False, 32)):
+        rng = np.random.default_rng(31)
+        buf = _sched_buffer(E, T, D, A, rng)
+        policy = _make_policy(D, A, seed=4, reward_normalization=True,
+                              recompute_advantage=recompute, ent_coef=0.01)
+        policy.lr_scheduler = get_linear_lr_schedular(policy.optim, step_per_epoch=3000,
+                                                      step_per_collect=1000, epochs=2)
+        p = tag + "_"
+        out.update(_sd_arrays(p + "init_", policy))
+        for k in ("obs", "obs_next", "act", "rew", "terminated", "truncated", "done"):
+            out[p + "buf_" + k] = np.array(buf._meta[k], copy=True)
+        np.random.seed(8)
+        for u in range(3):
+            res = policy.update(0, buf, batch_size=bs, repeat=3)
+            for k in ("loss", "loss/clip", "loss/vf", "loss/ent"):
+                out[p + f"u{u}_" + k.replace("/", "_")] = np.array(res[k])
+            out[p + f"u{u}_lr"] = np.array(policy.optim.param_groups[0]["lr"])
+            out[p + f"u{u}_ret_rms"] = np.array([policy.ret_rms.mean, policy.ret_rms.var,
+                                                 policy.ret_rms.count], dtype=np.float64)
+        out.update(_sd_arrays(p + "final_", policy))
+        out[p + "cfg"] = np.array(json.dumps(dict(E=E, T=T, D=D, A=A, bs=bs,
+                                                   recompute=recompute)))
+    _save("ppo_sched.npz", **out)
+
+
+# --------------------------------------------------------------------------------------
 # 11. BASELINE config 1: CartPole-v1 PPO over DummyVectorEnv x 4 in the configuration of
 #     test/discrete/test_ppo.py:19-146 (Net 64-64 shared by Actor(softmax probs) and
 #     Critic, orthogonal init, Categorical on probs, Adam 3e-4, vf .5, ent 0, max_grad_norm
@@ -862,10 +910,10 @@ def gen_cartpole():
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     which = sys.argv[1:] or ["returns", "gae", "buffer", "split", "rms", "ppo", "collector",
-                             "stack", "ppo_discrete", "npg", "replay", "cartpole"]
+                             "stack", "ppo_discrete", "npg", "replay", "cartpole", "sched"]
     table = dict(returns=gen_returns_known, gae=gen_gae_random, buffer=gen_buffer_traces,
                  split=gen_split, rms=gen_rms, ppo=gen_ppo, collector=gen_collector,
                  stack=gen_stack, ppo_discrete=gen_ppo_discrete, npg=gen_npg, replay=gen_replay,
-                 cartpole=gen_cartpole)
+                 cartpole=gen_cartpole, sched=gen_sched)
     for w in which:
         table[w]()
