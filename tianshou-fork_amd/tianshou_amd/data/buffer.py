@@ -215,7 +215,81 @@ class VectorReplayBuffer:
             self._dev["ep_idx"].zero_()
 
     def set_batch(self, batch: Batch) -> None:
-        raise NotImplementedError("set_batch/update/hdf5 are out of scope (SURVEY.md §8f)")
+        """Manually choose the batch the buffer manages (base.py:141-146; manager.py:64-66
+        re-points the sub-buffers at slices of it).  Every key is moved into HBM; the ring
+        bookkeeping is left as it is, like the reference's.  Rows written this way carry no
+        Collector obs / obs_next chain."""
+        batch = batch if isinstance(batch, Batch) else Batch(batch)
+        assert len(batch) == self.maxsize and set(batch.keys()).issubset(
+            self._reserved_keys), "Input batch doesn't meet ReplayBuffer's data form requirement."
+        self._alloc_state()
+        meta = Batch()
+        for k, v in batch.items():
+            if isinstance(v, Batch):
+                meta.__dict__[k] = Batch({kk: self._to_dev(vv) for kk, vv in v.items()
+                                          if not isinstance(vv, Batch)})
+                continue
+            t = self._to_dev(v)
+            if k == "rew":
+                t = t.to(torch.float64)
+            elif k in ("terminated", "truncated", "done"):
+                t = t.bool()
+            elif t.dtype == torch.float64 and k in ("obs", "obs_next", "act"):
+                t = t.float()
+            meta.__dict__[k] = t
+        if "done" not in meta.keys() and "terminated" in meta.keys():
+            meta.done = meta.terminated | meta.truncated
+        if "info" not in meta.keys():
+            meta.info = Batch()
+        if "env_id" not in meta.info.keys():  # the add kernel records each row's env id
+            meta.info.env_id = torch.zeros(self.maxsize, dtype=torch.int64, device=self.device)
+        self._meta = meta
+        self.obs_chain = False
+        self._last_sample0 = None
+
+    @classmethod
+    def from_data(cls, obs, act, rew, terminated, truncated, done, obs_next
+                  ) -> "VectorReplayBuffer":
+        """base.py:109-132 (the hdf5-free part): a one-env buffer of len(obs) rows managing
+        the given arrays, _size = len(obs), cursor at 0."""
+        size = len(obs)
+        assert all(len(d) == size for d in [obs, act, rew, terminated, truncated, done,
+                                            obs_next]), \
+            "Lengths of all hdf5 datasets need to be equal."
+        buf = cls(size) if cls is not VectorReplayBuffer else cls(size, 1)
+        if size == 0:
+            return buf
+        buf.set_batch(Batch(obs=np.asarray(obs), act=np.asarray(act), rew=np.asarray(rew),
+                            terminated=np.asarray(terminated), truncated=np.asarray(truncated),
+                            done=np.asarray(done), obs_next=np.asarray(obs_next)))
+        buf._ring.lengths[0] = size
+        return buf
+
+    # -- pickling (base.py:81-87): storage travels as host arrays, back into HBM on load ----
+    def __getstate__(self):
+        def host(v):
+            if isinstance(v, Batch):
+                return {"__batch__": {k: host(x) for k, x in v.items()}}
+            return v.detach().cpu().numpy() if isinstance(v, torch.Tensor) else v
+        st = {k: v for k, v in self.__dict__.items()
+              if k not in ("_meta", "_dev", "_last_sample0", "device")}
+        st["_meta"] = host(self._meta)
+        st["_dev"] = None if self._dev is None else {k: host(v) for k, v in self._dev.items()}
+        return st
+
+    def __setstate__(self, state) -> None:
+        dev = _default_device()
+
+        def back(v):
+            if isinstance(v, dict) and "__batch__" in v:
+                return Batch({k: back(x) for k, x in v["__batch__"].items()})
+            return torch.as_tensor(v, device=dev) if isinstance(v, np.ndarray) else v
+        meta, d = state.pop("_meta"), state.pop("_dev")
+        self.__dict__.update(state)
+        self.device = dev
+        self._last_sample0 = None
+        self._meta = back(meta) if isinstance(meta, dict) else Batch()
+        self._dev = None if d is None else {k: back(v) for k, v in d.items()}
 
     def update(self, buffer) -> np.ndarray:
         raise NotImplementedError  # ReplayBufferManager cannot be updated (manager.py:99-101)

@@ -777,6 +777,88 @@ def gen_replay():
 
 
 # --------------------------------------------------------------------------------------
+# 10a. Buffer persistence (without h5py): ReplayBuffer.from_data
+#      (base.py:109-132) + set_batch (base.py:141-146) followed by adds, and
+#      ReplayBufferManager.set_batch (manager.py:64-66) in the middle of a ragged trace.
+# --------------------------------------------------------------------------------------
+def _persist_snap(p, buf, out):
+    for k in ("obs", "act", "rew", "terminated", "truncated", "done", "obs_next"):
+        out[p + k] = np.array(buf._meta[k], copy=True)
+    n = buf.maxsize
+    out[p + "sample0"] = buf.sample_indices(0)
+    out[p + "unfinished"] = buf.unfinished_index()
+    out[p + "prev"] = buf.prev(np.arange(n))
+    out[p + "next"] = buf.next(np.arange(n))
+    out[p + "last_index"] = np.array(buf.last_index, copy=True)
+    out[p + "len"] = np.array(len(buf))
+
+
+def _persist_row(rng, k, D):
+    term = rng.random(k) < 0.25
+    trunc = ~term & (rng.random(k) < 0.15)
+    return Batch(obs=rng.standard_normal((k, D)).astype(np.float32),
+                 act=rng.integers(0, 4, k), rew=rng.standard_normal(k), terminated=term,
+                 truncated=trunc, obs_next=rng.standard_normal((k, D)).astype(np.float32))
+
+
+def gen_persist():
+    rng = np.random.default_rng(5)
+    out = {}
+    D, n = 3, 13
+    arr = _persist_row(rng, n, D)
+    done = arr.terminated | arr.truncated
+    buf = ReplayBuffer.from_data(arr.obs, arr.act, arr.rew, arr.terminated, arr.truncated,
+                                 done, arr.obs_next)
+    # copies: the reference's set_batch keeps the given arrays and later adds write into them
+    for k in ("obs", "act", "rew", "terminated", "truncated", "obs_next"):
+        out["fd_in_" + k] = np.array(arr[k], copy=True)
+    out["fd_in_done"] = done.copy()
+    _persist_snap("fd0_", buf, out)
+    ptrs, eps = [], []
+    for _ in range(6):
+        one = _persist_row(rng, 1, D)
+        out.setdefault("fd_add_rows", [])
+        ptr, ep_rew, ep_len, ep_idx = buf.add(one[0])
+        ptrs.append(ptr[0])
+        eps.append([float(ep_rew[0]), ep_len[0], ep_idx[0]])
+        for k in ("obs", "act", "rew", "terminated", "truncated", "obs_next"):
+            out.setdefault("fd_add_" + k, []).append(np.asarray(one[k][0]))
+    out.pop("fd_add_rows")
+    for k in ("obs", "act", "rew", "terminated", "truncated", "obs_next"):
+        out["fd_add_" + k] = np.stack(out["fd_add_" + k])
+    out["fd_add_ptr"], out["fd_add_ep"] = np.array(ptrs), np.array(eps)
+    _persist_snap("fd1_", buf, out)
+    # manager: ragged adds, set_batch, more adds
+    vbuf = VectorReplayBuffer(24, 3)
+    ids_seq = [[0, 1, 2], [0, 2], [1], [0, 1, 2], [2], [0, 1, 2], [0, 1], [2, 0]]
+    for i, ids in enumerate(ids_seq):
+        one = _persist_row(rng, len(ids), D)
+        for k in ("obs", "act", "rew", "terminated", "truncated", "obs_next"):
+            out[f"mg_add{i}_" + k] = np.asarray(one[k])
+        vbuf.add(one, buffer_ids=ids)
+    _persist_snap("mg0_", vbuf, out)
+    new = _persist_row(rng, 24, D)
+    new.done = new.terminated | new.truncated
+    for k in ("obs", "act", "rew", "terminated", "truncated", "done", "obs_next"):
+        out["mg_set_" + k] = np.array(new[k], copy=True)
+    vbuf.set_batch(new)
+    _persist_snap("mg1_", vbuf, out)
+    ids_seq2 = [[0, 1, 2], [1, 2], [0, 2]]
+    eps = []
+    for i, ids in enumerate(ids_seq2):
+        one = _persist_row(rng, len(ids), D)
+        for k in ("obs", "act", "rew", "terminated", "truncated", "obs_next"):
+            out[f"mg_more{i}_" + k] = np.asarray(one[k])
+        ptr, ep_rew, ep_len, ep_idx = vbuf.add(one, buffer_ids=ids)
+        eps.append(np.stack([ptr, ep_rew, ep_len, ep_idx]))
+        out[f"mg_more{i}_ret"] = eps[-1]
+    _persist_snap("mg2_", vbuf, out)
+    out["mg_ids"] = np.array(json.dumps(ids_seq))
+    out["mg_ids2"] = np.array(json.dumps(ids_seq2))
+    _save("persist.npz", **out)
+
+
+# --------------------------------------------------------------------------------------
 # 10b. BasePolicy.update with an lr_scheduler (base.py:288-315; get_linear_lr_schedular,
 #      utils/lr_scheduler.py:47-56 -- the fork's lr_decay default) and, in one variant,
 #      recompute_advantage (ppo.py:104-105: A6/A5 rerun for every repeat after the first),
@@ -910,10 +992,12 @@ def gen_cartpole():
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     which = sys.argv[1:] or ["returns", "gae", "buffer", "split", "rms", "ppo", "collector",
-                             "stack", "ppo_discrete", "npg", "replay", "cartpole", "sched"]
+                             "stack", "ppo_discrete", "npg", "replay", "cartpole", "sched",
+                             "persist"]
     table = dict(returns=gen_returns_known, gae=gen_gae_random, buffer=gen_buffer_traces,
                  split=gen_split, rms=gen_rms, ppo=gen_ppo, collector=gen_collector,
                  stack=gen_stack, ppo_discrete=gen_ppo_discrete, npg=gen_npg, replay=gen_replay,
-                 cartpole=gen_cartpole, sched=gen_sched)
+                 cartpole=gen_cartpole, sched=gen_sched,
+                 persist=gen_persist)
     for w in which:
         table[w]()
