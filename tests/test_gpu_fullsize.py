@@ -1,0 +1,183 @@
+"""Headline-size (BASELINE config 3: 4096 envs x 2048 steps, Box(376)/Box(17)) end-to-end
+property checks of one collect + process_fn through the production path (fused collect
+steps replayed from HIP graphs, global-layout GAE kernel, fused critic evaluation):
+
+* rew / terminated / truncated / done of all 8 388 608 transitions bit-exact against the
+  closed form of the synthetic env (oracle/synth_env.py: splitmix64 keys of (env, episode,
+  t), episodes of L steps starting at phase env % L, auto-reset);
+* obs_rms after the collect against an independent recomputation: the env replayed through
+  its public step / masked-reset calls, batch moments by torch f64 reductions, the
+  reference's RunningMeanStd merge (statistics.py:93-114) in NumPy f64 with f32 storage
+  after every update, step batch then reset rows (venv_wrappers.py:77-99): rtol 2e-5 (f32
+  storage roundings over ~4100 merges, see the test);
+* process_fn's returns / advantages (rew_norm path, a2c.py:95-116) against the C oracle GAE
+  (oracle/gae_oracle.c) run on the same device values V(s) and V(s') (all rows re-evaluated
+  without the V(s)-reuse shortcut, which must give the same bits): rtol 1e-5, atol
+  1e-6 * max|ref|; ret_rms against an f64 Welford of the unnormalised returns: rel 1e-9."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+E, T, D, A, L = 4096, 2048, 376, 17, 1000
+
+
+def _closed_form_env(seed=0):
+    """(rew f64, terminated, truncated) of every (env, step) of the first collect, env-major."""
+    from oracle import synth_env
+    e = np.repeat(np.arange(E, dtype=np.int64), T)
+    s = np.tile(np.arange(T, dtype=np.int64), E)
+    q = e % L + s + 1
+    later = q > L
+    r = q - L
+    j = np.where(later, 1 + (r - 1) // L, 0)
+    t = np.where(later, (r - 1) % L + 1, q)
+    rew = synth_env.reward(synth_env.key(seed, e, j, t))
+    done = t == L
+    return rew, done & (e % 2 == 0), done & (e % 2 == 1)
+
+
+def _rms_replay(dev):
+    """obs_rms of the collect recomputed through the env's public calls + host merge."""
+    from tianshou_amd.env import SyntheticVectorEnv
+    env = SyntheticVectorEnv(E, (D,), A, ep_len=L, device=dev)
+    obs, _ = env.reset()
+    mom = torch.empty((T + 1, 2, 3, D), dtype=torch.float64, device=dev)
+
+    def moments(x, mask=None):
+        x = x.double()
+        if mask is not None:
+            x = torch.where(mask[:, None], x, torch.zeros_like(x))
+        cnt = (mask.sum() if mask is not None else torch.tensor(float(len(x)), device=dev))
+        return torch.stack([x.sum(0), (x * x).sum(0), cnt.double().expand(D)])
+
+    mom[0, 0] = moments(obs)
+    mom[0, 1].zero_()
+    raw = env.alloc_obs(E)
+    rew = torch.empty(E, dtype=torch.float64, device=dev)
+    term = torch.empty(E, dtype=torch.bool, device=dev)
+    trunc = torch.empty(E, dtype=torch.bool, device=dev)
+    reset = env.alloc_obs(E)
+    part = env.alloc_partials(E)
+    for i in range(T):
+        env._step_raw(None, E, raw, rew, term, trunc, part, None)
+        done = term | trunc
+        mom[i + 1, 0] = moments(raw)
+        env._reset_raw(None, done, E, reset, part)
+        mom[i + 1, 1] = moments(reset, done)
+    mom = mom.cpu().numpy()
+    mean, var, count = np.zeros(D, np.float32), np.ones(D, np.float32), 0.0
+    for i in range(T + 1):
+        for b in range(2):
+            s1, s2, c = mom[i, b, 0], mom[i, b, 1], float(mom[i, b, 2, 0])
+            if c == 0:
+                continue
+            bm = s1 / c
+            bv = np.maximum(s2 / c - bm * bm, 0.0)
+            delta = bm - mean
+            tot = count + c
+            nm = mean + delta * c / tot
+            m2 = var * count + bv * c + delta * delta * count * c / tot
+            mean, var, count = nm.astype(np.float32), (m2 / tot).astype(np.float32), tot
+    return mean, var, count
+
+
+def test_headline_collect_and_process_fn_full_size():
+    from oracle import ref
+    from tianshou_amd.data import Collector, VectorReplayBuffer
+    from tianshou_amd.env import SyntheticVectorEnv, VectorEnvNormObs
+    from tianshou_amd.policy import PPOPolicy
+    from tianshou_amd.utils.models import fixed_std_normal, get_actor_critic, init_and_get_optim
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    np.random.seed(0)
+    env = VectorEnvNormObs(SyntheticVectorEnv(E, (D,), A, ep_len=L, device=dev))
+    actor, critic = get_actor_critic((D,), (64, 64), (A,), dev)
+    actor, critic = actor.to(dev), critic.to(dev)
+    optim = init_and_get_optim(actor, critic, 3e-4)
+    policy = PPOPolicy(actor, critic, optim, fixed_std_normal, action_space=env.action_space,
+                       discount_factor=0.99, gae_lambda=0.95, max_grad_norm=0.5, vf_coef=0.25,
+                       ent_coef=0.0, reward_normalization=True, advantage_normalization=True,
+                       eps_clip=0.2).to(dev)
+    buf = VectorReplayBuffer(E * T, E, device=dev)
+    coll = Collector(policy, env, buf)
+    res = coll.collect(n_step=E * T)
+    assert res["n/st"] == E * T
+    m = buf._meta
+    rew, term, trunc = _closed_form_env()
+    assert np.array_equal(m.rew.cpu().numpy(), rew)
+    assert np.array_equal(m.terminated.cpu().numpy(), term)
+    assert np.array_equal(m.truncated.cpu().numpy(), trunc)
+    assert np.array_equal(m.done.cpu().numpy(), term | trunc)
+    assert res["n/ep"] == int((term | trunc).sum())
+    # obs_rms vs the independent replay
+    mean, var, count = _rms_replay(dev)
+    rms = env.get_obs_rms()
+    assert rms.count == int(count) == E * (T + 1) + int((term | trunc).sum())
+    # both sides store mean / var as f32 after each of the ~4100 merges; a one-ulp
+    # difference in one merge's f64 sums (another summation order) propagates as a random
+    # walk of f32 roundings: ~sqrt(4100) * 6e-8 = 4e-6 relative, hence 2e-5
+    np.testing.assert_allclose(rms.mean, mean, rtol=2e-5, atol=1e-6)
+    np.testing.assert_allclose(rms.var, var, rtol=2e-5, atol=1e-6)
+    # process_fn vs the C oracle on the same device values
+    batch, idx = buf.sample(0)
+    var0 = policy.ret_rms.var
+    batch = policy.process_fn(batch, buf, idx)
+    v_s = batch.v_s.cpu().numpy()
+    v_all, _ = policy._mlp.evaluate(m.obs)
+    assert np.array_equal(v_all.cpu().numpy(), v_s)
+    v_next, _ = policy._mlp.evaluate(m.obs_next)
+    v_next = v_next.cpu().numpy()
+    scale = np.sqrt(var0 + policy._eps)
+    ret_o, adv_o = ref.compute_episodic_return(
+        rew, term, trunc, np.asarray(idx), buf.unfinished_index(),
+        v_next.astype(np.float64) * scale, v_s.astype(np.float64) * scale, 0.99, 0.95)
+    want_ret = (ret_o / scale).astype(np.float32)
+    want_adv = adv_o.astype(np.float32)
+    for got, want, name in ((batch.returns, want_ret, "returns"), (batch.adv, want_adv, "adv")):
+        g = got.cpu().numpy()
+        np.testing.assert_allclose(g, want, rtol=1e-5, atol=1e-6 * np.abs(want).max(),
+                                   err_msg=name)
+        print(f"{name}: bit-exact fraction {np.mean(g == want):.5f}")
+    # first update of a fresh RunningMeanStd (count 0): mean / var of the batch itself
+    assert policy.ret_rms.count == E * T
+    assert policy.ret_rms.mean == pytest.approx(ret_o.mean(), rel=1e-9)
+    assert policy.ret_rms.var == pytest.approx(ret_o.var(), rel=1e-9)
+
+
+def test_atari_stack_gather_full_size_buffer():
+    """Config 5's frame-stack buffer at full size (1024 envs x 256 steps of 84x84 frames,
+    save_only_last_obs, ignore_obs_next, stack_num 4) after a ragged fill: stacked obs and
+    obs_next of 20000 random rows (plus every env's first / last rows) byte-exact vs the
+    oracle's stack_get (base.py:317-358 with manager.py:259-297 prev/next)."""
+    from oracle import ref
+    from tianshou_amd.data import Batch, VectorReplayBuffer
+    dev = torch.device("cuda", 0)
+    NE, NT, S = 1024, 256, 4
+    buf = VectorReplayBuffer(NE * NT, NE, stack_num=S, ignore_obs_next=True,
+                             save_only_last_obs=True, device=dev)
+    rng = np.random.default_rng(3)
+    g = torch.Generator(device=dev).manual_seed(3)
+    frames = torch.empty((NE * NT, 84, 84), dtype=torch.uint8, device=dev)
+    ix = ref.VecBufferIndex(NE * NT, NE)
+    for t in range(NT):
+        obs = torch.randint(0, 256, (NE, S, 84, 84), dtype=torch.uint8, device=dev,
+                            generator=g)
+        term = rng.random(NE) < 0.02
+        trunc = ~term & (rng.random(NE) < 0.01)
+        buf.add(Batch(obs=obs, act=np.zeros(NE, np.int64), rew=np.zeros(NE),
+                      terminated=term, truncated=trunc), buffer_ids=np.arange(NE))
+        ix.add(np.zeros(NE), term, trunc, np.arange(NE))
+        rows = np.arange(NE) * NT + t
+        frames[torch.as_tensor(rows, device=dev)] = obs[:, -1]
+    assert torch.equal(buf._meta.obs, frames)
+    assert np.array_equal(buf.last_index, ix.last_index)
+    idx = np.unique(np.concatenate([rng.integers(0, NE * NT, 20000), np.arange(NE) * NT,
+                                    np.arange(NE) * NT + NT - 1]))
+    got = buf[idx]
+    fr = frames.cpu().numpy()
+    assert np.array_equal(buf.next(idx), ix.next(idx))
+    assert np.array_equal(got.obs.cpu().numpy(), ref.stack_get(fr, idx, S, ix.prev))
+    assert np.array_equal(got.obs_next.cpu().numpy(),
+                          ref.stack_get(fr, ix.next(idx), S, ix.prev))

@@ -476,6 +476,15 @@ def gen_collector():
     batch = policy.process_fn(batch, buf, idx)
     for k in ("v_s", "returns", "adv", "logp_old"):
         out["pf_" + k] = batch[k].detach().numpy()
+    # V(s') as a2c.py:86-93 evaluated it (same 256-row chunks), so the GAE can be checked
+    # on the reference's own values
+    with torch.no_grad():
+        vs, vn = [], []
+        for mb in batch.split(policy._batch, shuffle=False, merge_last=True):
+            vs.append(policy.critic(mb.obs).flatten())
+            vn.append(policy.critic(mb.obs_next).flatten())
+    assert np.array_equal(torch.cat(vs).numpy(), out["pf_v_s"])
+    out["pf_v_s_next"] = torch.cat(vn).numpy()
     out["pf_ret_rms_mean"] = np.asarray(policy.ret_rms.mean)
     out["pf_ret_rms_var"] = np.asarray(policy.ret_rms.var)
     out["pf_ret_rms_count"] = np.asarray(policy.ret_rms.count)
