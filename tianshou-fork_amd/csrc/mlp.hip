@@ -394,24 +394,61 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
 
     const int64_t ntiles = (n + 31) / 32;
     const int64_t gw = (int64_t)blockIdx.x * 4 + w, nw = (int64_t)gridDim.x * 4;
+    // Software pipeline over this wave's tiles (one wave per SIMD: nothing else hides
+    // latency): while tile bt computes, the NEXT tile's H1 fragments and gathered per-row
+    // inputs are in flight, and the index of the tile after that.  Loads are branch-free:
+    // rows past n read row 0 / tile 0 and are discarded by `live`.
+    float nh1[2][16], nav[16];
+    float nx0 = 0.f, nx1 = 0.f;  // actor: logp_old, adv; critic: ret, v_s
+    auto row_index = [&](int64_t bt_) -> int64_t {
+        const int64_t br_ = bt_ * 32 + c;
+        return (bt_ < ntiles && br_ < n) ? (idx ? idx[br_] : br_) : 0;
+    };
+#define TAIL_PREFETCH(BT, J)                                                                \
+    {                                                                                       \
+        const int64_t bts_ = (BT) < ntiles ? (BT) : 0;                                      \
+        _Pragma("unroll") for (int i_ = 0; i_ < 2; ++i_) {                                  \
+            const float4* src_ = reinterpret_cast<const float4*>(                           \
+                h1f + ((bts_ * NT + 2 * net + i_) * 64 + l) * 16);                          \
+            _Pragma("unroll") for (int q_ = 0; q_ < 4; ++q_) {                              \
+                const float4 v_ = src_[q_];                                                 \
+                nh1[i_][4 * q_] = v_.x;                                                     \
+                nh1[i_][4 * q_ + 1] = v_.y;                                                 \
+                nh1[i_][4 * q_ + 2] = v_.z;                                                 \
+                nh1[i_][4 * q_ + 3] = v_.w;                                                 \
+            }                                                                               \
+        }                                                                                   \
+        if constexpr (actor) {                                                              \
+            _Pragma("unroll") for (int r_ = 0; r_ < 16; ++r_) {                             \
+                const int a_ = rho(r_) + 4 * h;                                             \
+                nav[r_] = act[(J) * A + (a_ < A ? a_ : 0)];                                 \
+            }                                                                               \
+            nx0 = logp_old[J];                                                              \
+            nx1 = adv[J];                                                                   \
+        } else {                                                                            \
+            nx0 = ret[J];                                                                   \
+            nx1 = p.value_clip ? v_s[J] : 0.0f;                                             \
+        }                                                                                   \
+    }
+    int64_t j_next = row_index(gw);
+    TAIL_PREFETCH(gw, j_next)
+    j_next = row_index(gw + nw);
     for (int64_t bt = gw; bt < ntiles; bt += nw) {
         const int64_t brow = bt * 32 + c;
         const bool live = brow < n;
-        const int64_t j = live ? (idx ? idx[brow] : brow) : 0;
-        // ---- this net's H1 tiles -----------------------------------------------------------
-        float h1[2][16];
+        // ---- this tile's inputs (prefetched), then the next tile's loads --------------------
+        float h1[2][16], av[16];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const float4* src =
-                reinterpret_cast<const float4*>(h1f + ((bt * NT + 2 * net + i) * 64 + l) * 16);
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float4 v = src[q];
-                h1[i][4 * q] = v.x;
-                h1[i][4 * q + 1] = v.y;
-                h1[i][4 * q + 2] = v.z;
-                h1[i][4 * q + 3] = v.w;
-            }
+            for (int r = 0; r < 16; ++r) h1[i][r] = nh1[i][r];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) av[r] = nav[r];
+        const float x0 = nx0, x1 = nx1;
+        {
+            const int64_t jn = j_next;
+            TAIL_PREFETCH(bt + nw, jn)
+            j_next = row_index(bt + 2 * nw);
         }
         // ---- layer 2 -----------------------------------------------------------------------
         __builtin_amdgcn_sched_barrier(0);
@@ -456,7 +493,7 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
                 const int a = rho(r) + 4 * h;
                 diff[r] = 0.0f;
                 if (a < A && live) {
-                    diff[r] = act[j * A + a] - (mu[r] + sm[T_B3 + a]);
+                    diff[r] = av[r] - (mu[r] + sm[T_B3 + a]);
                     lp += -(diff[r] * diff[r]) / (2.0f * sm[T_VAR + a]) - sm[T_LS + a] -
                           LOG_SQRT_2PI;
                 }
@@ -464,9 +501,9 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
             const float logp = lp + __shfl_xor(lp, 32, 64);
             float g_logp = 0.0f;
             if (live) {
-                float an = adv[j];
+                float an = x1;
                 if (p.norm_adv) an = (an - mean_f) / (std_f + p.adv_eps);
-                const float ratio = expf(logp - logp_old[j]);
+                const float ratio = expf(logp - x0);
                 const float surr1 = ratio * an;
                 const float rc = fminf(fmaxf(ratio, p.lo), p.hi);
                 const float surr2 = rc * an;
@@ -554,10 +591,10 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
             const float value = vpart + __shfl_xor(vpart, 32, 64) + b3c;
             float gv = 0.0f;
             if (live) {
-                const float rt = ret[j];
+                const float rt = x0;
                 float dv, vf;
                 if (p.value_clip) {
-                    const float vs = v_s[j];
+                    const float vs = x1;
                     const float dlt = value - vs;
                     const float dcl = fminf(fmaxf(dlt, -p.eps_clip), p.eps_clip);
                     const float vcl = vs + dcl;
@@ -665,6 +702,7 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
             acc_wgrad<2, 2>(gW2, S1, S2, c, h);
         }
     }
+#undef TAIL_PREFETCH
     // ---- fold the 4 waves (fixed order) into this workgroup's slab --------------------------
     __syncthreads();
     float* red = sm;  // T_END >= 4 * 32 * 64 floats
