@@ -467,15 +467,25 @@ int tsrl_segtree_prefix_idx(const double* tree, int64_t bound, const void* value
  * flat f32 parameter / gradient / moment buffers of n elements: partials (f64,
  * tsrl_clip_adam_partials(n) entries) receive slice norms, norm_out[0] = gradient norm,
  * norm_out[1] = clip coefficient (max_norm <= 0: no clipping, partials / norm_out may be
- * NULL); the gradient is left scaled in place; step[0..nstep) (device f32 step counters, all
- * equal) is advanced by one.  ticket: one device uint32, zero-initialised, kept zero.
+ * NULL); step[0..nstep) (device f32 step counters, all equal) is advanced by one.  ticket:
+ * one device uint32, zero-initialised, kept zero.
  * lr_dev (nullable device f32): the learning rate read at run time instead of `lr`, so a
- * captured learn graph follows an lr_scheduler (BasePolicy.update, base.py:312-313). */
+ * captured learn graph follows an lr_scheduler (BasePolicy.update, base.py:312-313).
+ * scale_grads: leave the gradient scaled by the clip coefficient in place (what p.grad holds
+ * after clip_grad_norm_); 0 skips that pass when the gradient is overwritten next anyway.
+ * split (nullable): also write the updated first-layer weights of both nets (flat element
+ * ranges [off_a, off_a + 64 d) and [off_c, off_c + 64 d), row-major [64][d]) as the bf16x6
+ * planes of tsrl_mlp_split_w (row pitch kp), fusing the next minibatch's re-split. */
+typedef struct {
+    void* out;
+    int64_t off_a, off_c, d, kp;
+} tsrl_w1_split;
 int64_t tsrl_clip_adam_partials(int64_t n);
 int tsrl_clip_adam(float* param, float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                    float* step, int64_t nstep, float lr, float beta1, float beta2, float eps,
                    float max_norm, double* partials, float* norm_out, unsigned int* ticket,
-                   const float* lr_dev, void* stream);
+                   const float* lr_dev, const tsrl_w1_split* split, int scale_grads,
+                   void* stream);
 
 #ifdef __cplusplus
 }

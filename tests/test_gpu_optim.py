@@ -55,3 +55,41 @@ def test_clip_adam_matches_torch(max_norm):
     # the state dict round-trips through torch
     sd = opt.state_dict()
     assert len(sd["state"]) == len(list(ac1.parameters()))
+
+
+@pytest.mark.parametrize("D", [376, 17, 24])
+def test_clip_adam_split_epilogue_equals_split_w(D):
+    """clip_adam(split_w1=True) leaves the bf16x6 planes of the UPDATED first-layer weights
+    byte-identical to a fresh tsrl_mlp_split_w, and scale_grads=False leaves .grad
+    unclipped while the parameter update is the same as with scaling."""
+    from tianshou_amd import _C
+    from tianshou_amd.policy import fused_mlp
+    from tianshou_amd.utils.models import get_actor_critic, init_actor_critic
+    from tianshou_amd.utils.net import ActorCritic
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(3)
+    a, c = get_actor_critic((D,), (64, 64), (6,), dev)
+    a, c = a.to(dev), c.to(dev)
+    init_actor_critic(a, c)
+    ac = ActorCritic(a, c)
+    opt = torch.optim.Adam(ac.parameters(), lr=1e-3)
+    fm = fused_mlp.FusedActorCritic(fused_mlp.match(a, c), ac.parameters())
+    assert fm.bind_adam(opt)
+    g = torch.Generator(device=dev).manual_seed(5)
+    L = _C.lib()
+    nb = (int(L.tsrl_mlp_split_bytes(D)) + 3) // 4
+    for step in range(3):
+        fm.bind_grads()
+        for p in ac.parameters():
+            p.grad.copy_(torch.randn(p.shape, device=dev, generator=g) * 3.0)
+        raw = [p.grad.clone() for p in ac.parameters()]
+        fm.split_w1()
+        fm.clip_adam(0.5, scale_grads=False, split_w1=True)
+        torch.cuda.synchronize()
+        got = fm._bufs["w1split"][:nb].clone()
+        want = torch.empty(nb, dtype=torch.float32, device=dev)
+        _C.check(L.tsrl_mlp_split_w(_C.ptr(fm.L["w1a"].weight), _C.ptr(fm.L["w1c"].weight), D,
+                                    _C.ptr(want), _C.stream_ptr(dev)), "split")
+        assert torch.equal(got.view(torch.int32), want.view(torch.int32)), f"step {step}"
+        for p, r in zip(ac.parameters(), raw):
+            assert torch.equal(p.grad, r)

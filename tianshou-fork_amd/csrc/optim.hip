@@ -25,6 +25,33 @@ struct AdamArgs {
     float lr, beta1, beta2, eps, max_norm;
 };
 
+// Optional epilogue: the updated first-layer weights of both nets re-split into the bf16x6
+// planes the next minibatch's tsrl_mlp_l1_fwd_x6 reads (the split_w kernel's layout:
+// out[plane][f][k], f < 64 actor rows, >= 64 critic rows, k < kp; columns >= d stay zero).
+struct SplitOut {
+    __bf16* out;
+    int64_t off_a, off_c, d, kp, plane;
+};
+
+__device__ __forceinline__ void split_store(const SplitOut& so, int64_t i, float x) {
+    int64_t r = -1, f0 = 0;
+    if (i >= so.off_a && i < so.off_a + 64 * so.d) {
+        r = i - so.off_a;
+    } else if (i >= so.off_c && i < so.off_c + 64 * so.d) {
+        r = i - so.off_c;
+        f0 = 64;
+    }
+    if (r < 0) return;
+    const int64_t f = f0 + r / so.d, k = r - (r / so.d) * so.d;
+    const __bf16 a0 = (__bf16)x;
+    const float r1 = x - (float)a0;
+    const __bf16 a1 = (__bf16)r1;
+    __bf16* o = so.out + f * so.kp + k;
+    o[0] = a0;
+    o[so.plane] = a1;
+    o[2 * so.plane] = (__bf16)(r1 - (float)a1);
+}
+
 // Sum of squares of each 2048-element gradient slice (f64), one workgroup per slice.
 __global__ __launch_bounds__(OTPB) void norm_partials_kernel(const float* __restrict__ g,
                                                              int64_t n, double* partials) {
@@ -58,7 +85,8 @@ __global__ __launch_bounds__(OTPB) void clip_adam_kernel(float* __restrict__ p,
                                                          float* __restrict__ step, int64_t nstep,
                                                          AdamArgs a, const double* __restrict__ partials,
                                                          float* __restrict__ norm_out,
-                                                         unsigned int* ticket, const float* __restrict__ lr_dev) {
+                                                         unsigned int* ticket, const float* __restrict__ lr_dev,
+                                                         SplitOut so) {
     __shared__ float s_scale;
     const int t = threadIdx.x;
     const bool clip = a.max_norm > 0.0f;
@@ -95,7 +123,9 @@ __global__ __launch_bounds__(OTPB) void clip_adam_kernel(float* __restrict__ p,
         const float vi = a.beta2 * v[i] + (1.0f - a.beta2) * gi * gi;
         m[i] = mi;
         v[i] = vi;
-        p[i] -= step_size * mi / (sqrtf(vi) / bc2_sqrt + a.eps);
+        const float pi = p[i] - step_size * mi / (sqrtf(vi) / bc2_sqrt + a.eps);
+        p[i] = pi;
+        if (so.out) split_store(so, i, pi);
     }
     if (t == 0) {
         const unsigned int done = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL,
@@ -127,7 +157,7 @@ extern "C" int tsrl_clip_adam(float* param, float* grad, float* exp_avg, float* 
                               int64_t n, float* step, int64_t nstep, float lr, float beta1,
                               float beta2, float eps, float max_norm, double* partials,
                               float* norm_out, unsigned int* ticket, const float* lr_dev,
-                              void* stream) {
+                              const tsrl_w1_split* split, int scale_grads, void* stream) {
     TSRL_CHECK_ARG(n >= 0 && nstep >= 1, "tsrl_clip_adam: bad sizes");
     if (n == 0) return 0;
     TSRL_CHECK_ARG(param && grad && exp_avg && exp_avg_sq && step && ticket,
@@ -141,11 +171,20 @@ extern "C" int tsrl_clip_adam(float* param, float* grad, float* exp_avg, float* 
         TSRL_LAUNCH_CHECK("tsrl_clip_adam (norm)");
     }
     const AdamArgs a{lr, beta1, beta2, eps, max_norm};
+    SplitOut so{nullptr, 0, 0, 1, 1, 0};
+    if (split) {
+        TSRL_CHECK_ARG(split->out && split->d > 0 && split->kp >= split->d &&
+                           split->off_a >= 0 && split->off_c >= 0 &&
+                           split->off_a + 64 * split->d <= n && split->off_c + 64 * split->d <= n,
+                       "tsrl_clip_adam: bad first-layer split ranges");
+        so = SplitOut{reinterpret_cast<__bf16*>(split->out), split->off_a, split->off_c,
+                      split->d, split->kp, 128 * split->kp};
+    }
     hipLaunchKernelGGL(clip_adam_kernel, dim3((unsigned)grid), dim3(OTPB), 0,
                        as_stream(stream), param, grad, exp_avg, exp_avg_sq, n, step, nstep, a,
-                       partials, norm_out, ticket, lr_dev);
+                       partials, norm_out, ticket, lr_dev, so);
     TSRL_LAUNCH_CHECK("tsrl_clip_adam");
-    if (max_norm > 0.0f) {
+    if (max_norm > 0.0f && scale_grads) {
         const unsigned g2 = (unsigned)std::min<int64_t>((n + OTPB - 1) / OTPB, 1024);
         hipLaunchKernelGGL(clip_scale_kernel, dim3(g2), dim3(OTPB), 0, as_stream(stream), grad,
                            n, norm_out);

@@ -54,6 +54,11 @@ class TailWeights(ctypes.Structure):
                                   "log_std")]
 
 
+class W1Split(ctypes.Structure):
+    """Mirror of ``tsrl_w1_split``."""
+    _fields_ = [("out", _p), ("off_a", _i64), ("off_c", _i64), ("d", _i64), ("kp", _i64)]
+
+
 class TailGrads(ctypes.Structure):
     """Mirror of ``tsrl_tail_grads``."""
     _fields_ = [(k, _p) for k in ("w2a", "b2a", "w2c", "b2c", "w3a", "b3a", "w3c", "b3c")]
@@ -101,7 +106,7 @@ _SIGS = {
                            ctypes.c_int, _p, _p], ctypes.c_int),
     "tsrl_clip_adam_partials": ([_i64], _i64),
     "tsrl_clip_adam": ([_p, _p, _p, _p, _i64, _p, _i64, _f, _f, _f, _f, _f, _p, _p, _p, _p,
-                        _p],
+                        ctypes.POINTER(W1Split), ctypes.c_int, _p],
                        ctypes.c_int),
     "tsrl_segtree_set": ([_p, _i64, _p, _p, _i64, _i64, _p, _p], ctypes.c_int),
     "tsrl_segtree_reduce": ([_p, _i64, _i64, _i64, _p, _p], ctypes.c_int),

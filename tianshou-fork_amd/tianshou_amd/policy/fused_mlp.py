@@ -171,7 +171,10 @@ class FusedActorCritic:
             pviews.append(p.data)
             o += k
         steps.fill_(float(steps.max()) if len(steps) else 0.0)
+        base = flat_p.data_ptr()
+        off = lambda t: (t.data_ptr() - base) // 4  # noqa: E731
         self._adam = dict(optim=optim, p=flat_p, m=flat_m, v=flat_v, steps=steps, pviews=pviews,
+                          w1_off=(off(self.L["w1a"].weight), off(self.L["w1c"].weight)),
                           ticket=torch.zeros(1, dtype=torch.int32, device=dev),
                           partials=torch.zeros(
                               max(int(_C.lib().tsrl_clip_adam_partials(n)), 1),
@@ -192,20 +195,29 @@ class FusedActorCritic:
             st["lr"].fill_(lr)
             st["lr_host"] = lr
 
-    def clip_adam(self, max_norm: Optional[float]) -> None:
+    def clip_adam(self, max_norm: Optional[float], scale_grads: bool = True,
+                  split_w1: bool = False) -> None:
         """clip_grad_norm_(max_norm) (when given) + Adam.step() over the flat buffers; the
-        learning rate comes from the device word of set_lr()."""
+        learning rate comes from the device word of set_lr().  ``scale_grads=False`` skips
+        the in-place clipping of .grad (only the last step of a learn() needs it: every
+        minibatch overwrites the gradients); ``split_w1`` re-splits the updated first-layer
+        weights for the next minibatch in the same pass (no split_w launch)."""
         st = self._adam
         g = st["optim"].param_groups[0]
         b1, b2 = g["betas"]
         if st.get("lr_host") is None:
             self.set_lr()
+        sp = None
+        if split_w1 and L1_X6:
+            ws = self._buf("w1split", (int(_C.lib().tsrl_mlp_split_bytes(self.D)) + 3) // 4)
+            sp = _C.W1Split(_C.ptr(ws), st["w1_off"][0], st["w1_off"][1], self.D,
+                            (self.D + 31) // 32 * 32)
         _C.check(_C.lib().tsrl_clip_adam(
             _C.ptr(st["p"]), _C.ptr(self._flat), _C.ptr(st["m"]), _C.ptr(st["v"]),
             st["p"].numel(), _C.ptr(st["steps"]), st["steps"].numel(), float(g["lr"]),
             float(b1), float(b2), float(g["eps"]), float(max_norm) if max_norm else 0.0,
             _C.ptr(st["partials"]), _C.ptr(st["norm"]), _C.ptr(st["ticket"]), _C.ptr(st["lr"]),
-            _C.stream_ptr(st["p"].device)),
+            sp, int(bool(scale_grads)), _C.stream_ptr(st["p"].device)),
             "tsrl_clip_adam")
 
     def _weights(self) -> "_C.TailWeights":
@@ -235,6 +247,16 @@ class FusedActorCritic:
                                      _C.ptr(L["w1a"].bias), _C.ptr(L["w1c"].weight),
                                      _C.ptr(L["w1c"].bias), 1, out, frag_out, s),
                  "tsrl_mlp_l1_fwd")
+
+    def split_w1(self) -> None:
+        """Split the current first-layer weights into the bf16x6 planes (tsrl_mlp_split_w)."""
+        if not L1_X6:
+            return
+        L, lib = self.L, _C.lib()
+        ws = self._buf("w1split", (int(lib.tsrl_mlp_split_bytes(self.D)) + 3) // 4)
+        _C.check(lib.tsrl_mlp_split_w(_C.ptr(L["w1a"].weight), _C.ptr(L["w1c"].weight), self.D,
+                                      _C.ptr(ws), _C.stream_ptr(self.params[0].device)),
+                 "tsrl_mlp_split_w")
 
     def rows(self, obs: torch.Tensor, key: str = "xpad") -> torch.Tensor:
         """The observation rows as the kernels read them: obs itself when D % 4 == 0, else a
@@ -316,12 +338,15 @@ class FusedActorCritic:
     def minibatch(self, obs: torch.Tensor, idx: Optional[torch.Tensor], b: int,
                   act: torch.Tensor, logp_old: torch.Tensor, adv: torch.Tensor,
                   ret: torch.Tensor, v_s: torch.Tensor, params: "_C.PPOParams", dp,
-                  adv_sums: Optional[torch.Tensor] = None) -> torch.Tensor:
+                  adv_sums: Optional[torch.Tensor] = None, split_w: bool = True
+                  ) -> torch.Tensor:
         """Gradients of the minibatch loss into the parameters' .grad; returns the device
         tensor [loss, clip, vf, ent] (ppo.py:140-142).  ``obs`` are the rows of ``rows()``;
         ``adv_sums`` = this minibatch's row of epoch_adv_moments (computed here when None).
         Under data parallelism ONE all-reduce carries the gradients and the loss sums; a rank
-        whose share of the global minibatch is empty (b == 0) contributes zeros."""
+        whose share of the global minibatch is empty (b == 0) contributes zeros.
+        ``split_w=False``: the bf16x6 planes of W1 are already current (split_w1(), or the
+        previous clip_adam(split_w1=True))."""
         self.bind_grads()
         L, lib = self.L, _C.lib()
         dev = obs.device
@@ -343,7 +368,7 @@ class FusedActorCritic:
                      "tsrl_reduce_partials")
             dp.all_reduce_(adv_sums)
         h1 = self._buf("h1", int(lib.tsrl_mlp_frag_floats(b)))
-        self._l1_fwd(_C.ptr(obs), ldx, ip, b, _C.ptr(h1), 1)
+        self._l1_fwd(_C.ptr(obs), ldx, ip, b, _C.ptr(h1), 1, split=split_w)
         dz1 = self._buf("dz1", b * 2 * 64)
         sums = self._buf("sums", 4 + A, torch.float64)[:4 + A]
         wsb = int(lib.tsrl_ppo_tail_workspace_bytes(b))

@@ -281,14 +281,18 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
             if mlp_ok and self._norm_adv:
                 bounds, max_seg = self._dev_bounds(chunks, dev)
                 adv_mom = self._mlp.epoch_adv_moments(adv, perm, bounds, max_seg, self.dp)
+            fused_opt = mlp_ok and self._mlp.adam_bound(self.optim)
+            if fused_opt:
+                self._mlp.split_w1()  # later minibatches get the planes from the Adam pass
             for k, (s, e, b_glob) in enumerate(chunks):
                 idx = perm[s:e]
                 params = self._params(b_glob)
                 if mlp_ok:
                     t = self._mlp.minibatch(obs_all, idx, e - s, act, logp_old, adv, ret, v_s,
                                             params, self.dp,
-                                            adv_sums=None if adv_mom is None else adv_mom[k])
-                    self._opt_step()
+                                            adv_sums=None if adv_mom is None else adv_mom[k],
+                                            split_w=not fused_opt)
+                    self._opt_step(last=(k == len(chunks) - 1))
                     terms.append(t)
                     continue
                 obs_mb = gather_rows(batch.obs, idx)
@@ -366,12 +370,14 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
             c = self._bounds_cache = (key, t, max(e - s for s, e, _ in chunks), host)
         return c[1], c[2]
 
-    def _opt_step(self) -> None:
+    def _opt_step(self, last: bool = True) -> None:
         """clip_grad_norm_ + optim.step() of ppo.py:143-151: one fused HIP pass
-        (tsrl_clip_adam) when the optimiser is a plain Adam over the fused MLP's parameters,
-        torch's otherwise."""
+        (tsrl_clip_adam) when the optimiser is a plain Adam over the fused MLP's parameters
+        -- it also re-splits the first-layer weights for the next minibatch, and leaves the
+        clipped gradients in .grad only after an epoch's last minibatch (the next minibatch
+        overwrites them otherwise) -- torch's otherwise."""
         if self._mlp is not None and self._mlp.adam_bound(self.optim):
-            self._mlp.clip_adam(self._grad_norm)
+            self._mlp.clip_adam(self._grad_norm, scale_grads=last, split_w1=True)
             return
         if self._grad_norm:
             nn.utils.clip_grad_norm_(self._actor_critic.parameters(), max_norm=self._grad_norm)
@@ -436,11 +442,15 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
                     if self._norm_adv:
                         mom = self._mlp.epoch_adv_moments(static[2], sperm, sbounds, max_seg,
                                                           self.dp)
+                    fused_opt = self._mlp.adam_bound(self.optim)
+                    if fused_opt:
+                        self._mlp.split_w1()
                     for i, (s, e, b_glob) in enumerate(chunks):
                         t = self._mlp.minibatch(obs_all, sperm[s:e], e - s, *static,
                                                 self._params(b_glob), self.dp,
-                                                adv_sums=None if mom is None else mom[i])
-                        self._opt_step()
+                                                adv_sums=None if mom is None else mom[i],
+                                                split_w=not fused_opt)
+                        self._opt_step(last=(i == len(chunks) - 1))
                         sterms[i].copy_(t)
             except RuntimeError as err:  # e.g. a collective backend that cannot be captured
                 import warnings
