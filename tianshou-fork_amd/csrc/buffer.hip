@@ -6,7 +6,7 @@
 //          arithmetic (which it can do without reading device data).  The Collector's
 //          obs_next normalisation (VectorEnvNormObs) is fused into the obs_next row copy.
 // gather : fancy-index row gather (Batch.__getitem__, batch.py:446-460).
-#include "tsrl_common.h"
+#include "add_row.h"
 
 namespace tsrl {
 namespace {
@@ -14,135 +14,11 @@ namespace {
 constexpr int TPB = 256;
 constexpr int ROWS_PER_BLOCK = TPB / kWave;  // one wave per row
 
-__device__ __forceinline__ void copy_row(const void* src, void* dst, int64_t bytes, int lane) {
-    const char* s = reinterpret_cast<const char*>(src);
-    char* d = reinterpret_cast<char*>(dst);
-    if ((bytes & 15) == 0 && aligned16(s) && aligned16(d)) {
-        const int4* s4 = reinterpret_cast<const int4*>(s);
-        int4* d4 = reinterpret_cast<int4*>(d);
-        for (int64_t i = lane; i < bytes / 16; i += kWave) d4[i] = s4[i];
-    } else if ((bytes & 3) == 0 && (((uintptr_t)s | (uintptr_t)d) & 3) == 0) {
-        const int* s4 = reinterpret_cast<const int*>(s);
-        int* d4 = reinterpret_cast<int*>(d);
-        for (int64_t i = lane; i < bytes / 4; i += kWave) d4[i] = s4[i];
-    } else {
-        for (int64_t i = lane; i < bytes; i += kWave) d[i] = s[i];
-    }
-}
-
-__device__ __forceinline__ float norm1(float x, float m, float v, float eps, float clip) {
-    float y = (x - m) / __builtin_sqrtf(v + eps);
-    if (clip > 0.0f) y = fminf(fmaxf(y, -clip), clip);
-    return y;
-}
-
 __global__ __launch_bounds__(TPB) void buffer_add_kernel(tsrl_add_args a) {
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t r = (int64_t)blockIdx.x * ROWS_PER_BLOCK + threadIdx.x / kWave;
     const int64_t urel = a.rel_dev ? *a.rel_dev : a.uniform_rel;
-    if (r < a.k) {
-        const int64_t b = a.ids ? a.ids[r] : r;
-        const int64_t ptr = a.ptr ? a.ptr[r] : a.offset[b] + urel;
-
-        const int64_t obs_pitch = a.obs_src_pitch ? a.obs_src_pitch : a.obs_row_bytes;
-        const int64_t next_pitch = a.obs_next_src_pitch ? a.obs_next_src_pitch : a.obs_row_bytes;
-        if (a.obs_src && a.obs_dst)
-            copy_row((const char*)a.obs_src + r * obs_pitch,
-                     (char*)a.obs_dst + ptr * a.obs_row_bytes, a.obs_row_bytes, lane);
-        if (a.act_src && a.act_dst)
-            copy_row((const char*)a.act_src + r * a.act_row_bytes,
-                     (char*)a.act_dst + ptr * a.act_row_bytes, a.act_row_bytes, lane);
-        if (a.obs_next_src_raw && a.obs_next_dst_raw)
-            copy_row((const char*)a.obs_next_src_raw + r * next_pitch,
-                     (char*)a.obs_next_dst_raw + ptr * a.obs_row_bytes, a.obs_row_bytes, lane);
-        if (a.obs_next_src && (a.obs_next_dst || a.cur_obs)) {
-            const float* src = a.obs_next_src + r * a.obs_dim;
-            float* dst = a.obs_next_dst ? a.obs_next_dst + ptr * a.obs_dim : nullptr;
-            float* cur = a.cur_obs ? a.cur_obs + r * a.obs_dim : nullptr;
-            const bool nrm = a.norm_mean != nullptr;
-            const bool rst = a.reset_mask && a.reset_mask[r];
-            // 16-byte path: a lane handles 4 consecutive columns (376 columns = 94 float4,
-            // two passes of the wave instead of six); same per-element arithmetic
-            const bool v4 = (a.obs_dim & 3) == 0 && aligned16(src) && (!dst || aligned16(dst)) &&
-                            (!cur || aligned16(cur)) && (!nrm || (aligned16(a.norm_mean) &&
-                                                                 aligned16(a.norm_var))) &&
-                            (!rst || (aligned16(a.reset_src + r * a.obs_dim) &&
-                                      (!a.reset_mean || (aligned16(a.reset_mean) &&
-                                                         aligned16(a.reset_var)))));
-            if (v4) {
-                const int64_t nq = a.obs_dim >> 2;
-                for (int64_t q = lane; q < nq; q += kWave) {
-                    float4 x = reinterpret_cast<const float4*>(src)[q];
-                    if (nrm) {
-                        const float4 m = reinterpret_cast<const float4*>(a.norm_mean)[q];
-                        const float4 v = reinterpret_cast<const float4*>(a.norm_var)[q];
-                        x.x = norm1(x.x, m.x, v.x, a.norm_eps, a.norm_clip);
-                        x.y = norm1(x.y, m.y, v.y, a.norm_eps, a.norm_clip);
-                        x.z = norm1(x.z, m.z, v.z, a.norm_eps, a.norm_clip);
-                        x.w = norm1(x.w, m.w, v.w, a.norm_eps, a.norm_clip);
-                    }
-                    if (dst) reinterpret_cast<float4*>(dst)[q] = x;
-                    if (cur) {
-                        if (rst) {
-                            x = reinterpret_cast<const float4*>(a.reset_src + r * a.obs_dim)[q];
-                            if (a.reset_mean) {
-                                const float4 m = reinterpret_cast<const float4*>(a.reset_mean)[q];
-                                const float4 v = reinterpret_cast<const float4*>(a.reset_var)[q];
-                                x.x = norm1(x.x, m.x, v.x, a.norm_eps, a.norm_clip);
-                                x.y = norm1(x.y, m.y, v.y, a.norm_eps, a.norm_clip);
-                                x.z = norm1(x.z, m.z, v.z, a.norm_eps, a.norm_clip);
-                                x.w = norm1(x.w, m.w, v.w, a.norm_eps, a.norm_clip);
-                            }
-                        }
-                        reinterpret_cast<float4*>(cur)[q] = x;
-                    }
-                }
-            } else
-            for (int64_t d = lane; d < a.obs_dim; d += kWave) {
-                float x = src[d];
-                if (nrm) x = norm1(x, a.norm_mean[d], a.norm_var[d], a.norm_eps, a.norm_clip);
-                if (dst) dst[d] = x;
-                if (cur) {
-                    if (rst) {
-                        x = a.reset_src[r * a.obs_dim + d];
-                        if (a.reset_mean)
-                            x = norm1(x, a.reset_mean[d], a.reset_var[d], a.norm_eps, a.norm_clip);
-                    }
-                    cur[d] = x;
-                }
-            }
-        }
-        if (lane == 0) {
-            const double rew = a.rew ? a.rew[r] : 0.0;
-            const uint8_t tm = a.term ? a.term[r] : 0;
-            const uint8_t tr = a.trunc ? a.trunc[r] : 0;
-            const uint8_t done = (uint8_t)((tm != 0) | (tr != 0));
-            if (a.rew_dst) a.rew_dst[ptr] = rew;
-            if (a.term_dst) a.term_dst[ptr] = (uint8_t)(tm != 0);
-            if (a.trunc_dst) a.trunc_dst[ptr] = (uint8_t)(tr != 0);
-            if (a.done_dst) a.done_dst[ptr] = done;
-            if (a.env_id_dst) a.env_id_dst[ptr] = b;
-            // ReplayBuffer._add_index episode bookkeeping (base.py:205-214)
-            const double er = a.ep_rew[b] + rew;
-            const int64_t el = a.ep_len[b] + 1;
-            const int64_t ei = a.ep_idx[b] + a.offset[b];
-            if (a.out_ep_rew) a.out_ep_rew[r] = done ? er : er * 0.0;
-            if (a.out_ep_len) a.out_ep_len[r] = done ? el : 0;
-            if (a.out_ep_idx) a.out_ep_idx[r] = ei;
-            if (done) {
-                if (a.stat_rew) a.stat_rew[ptr] = er;
-                if (a.stat_len) a.stat_len[ptr] = el;
-                if (a.stat_idx) a.stat_idx[ptr] = ei;
-                a.ep_rew[b] = 0.0;
-                a.ep_len[b] = 0;
-                a.ep_idx[b] = a.next_rel ? a.next_rel[r]
-                                          : (a.rel_dev ? (urel + 1) % a.ring_size : a.uniform_next);
-            } else {
-                a.ep_rew[b] = er;
-                a.ep_len[b] = el;
-            }
-        }
-    }
+    if (r < a.k) add_row(a, r, lane, urel);
     // ring cursor for the next step: written to the other slot of a ping-pong pair, so no
     // workgroup can observe it before every workgroup of this launch has read *rel_dev
     if (a.rel_next && blockIdx.x == 0 && threadIdx.x == 0) *a.rel_next = (urel + 1) % a.ring_size;

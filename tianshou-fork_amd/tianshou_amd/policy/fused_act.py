@@ -50,7 +50,7 @@ class FusedGaussAct:
         # generator at each pack() (reproducible under torch.manual_seed); "torch": noise
         # from torch.randn on the GPU stream (the torch path's exact noise, one extra launch)
         self.rng = "device"
-        self._seed = 0
+        self._seed = None
         self._ctr = None      # own [2] counter pair when the caller passes none
         self._parity = 0
 
@@ -65,7 +65,12 @@ class FusedGaussAct:
         _C.check(lib.tsrl_policy_pack_l1(_C.ptr(w.detach()), self.D, _C.ptr(self.packed),
                                          _C.stream_ptr(w.device)), "tsrl_policy_pack_l1")
         if self.rng == "device":
-            self._seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+            # one seed per policy, drawn at the first pack from torch's CPU generator: steps
+            # replayed from HIP graphs carry the seed captured with them, so a per-collect
+            # reseed would give eager and replayed steps different streams; fresh noise comes
+            # from the collector's step counters, which never repeat
+            if self._seed is None:
+                self._seed = int(torch.randint(0, 2 ** 62, (1,)).item())
             if self._ctr is None or self._ctr.device != w.device:
                 self._ctr = torch.zeros(2, dtype=torch.int64, device=w.device)
             self._ctr.zero_()
