@@ -159,3 +159,37 @@ def test_device_cartpole_matches_oracle(dev):
             ro, _ = env.reset(done)
             np.testing.assert_array_equal(ro.cpu().numpy(), ora.reset(done))
     assert n_term > 100 and n_trunc > 10
+
+
+def test_cartpole_learn_graph_equals_eager(golden_dir, dev):
+    """The Categorical learn path with the flat Adam pass (policy/flat_adam.py): epochs
+    replayed from the captured HIP graph give the same losses and parameters as the eager
+    minibatch loop (same kernels, same order), across two updates (the second replays the
+    graph captured in the first), and the Adam state stays torch-loadable."""
+    z = np.load(os.path.join(golden_dir, "cartpole.npz"))
+    runs = []
+    for graph in (False, None):
+        envs, policy, buf, c = _build(z, dev)
+        policy.graph_learn = graph
+        c.collect(n_step=int(z["n_step"]), random=True)
+        np.random.seed(77)
+        out = []
+        for _ in range(2):
+            batch, idx = buf.sample(0)
+            batch = policy.process_fn(batch, buf, idx)
+            out.append(policy.learn(batch, batch_size=64, repeat=4))
+        assert policy._cat_adam is not None and policy._cat_adam.adam_bound(policy.optim)
+        assert (policy._learn_graph is not None) == (graph is None)
+        assert not policy._graph_failed
+        sd = {k: v.detach().cpu().numpy() for k, v in policy.state_dict().items()}
+        runs.append((out, sd, policy.optim.state_dict()))
+    (o0, sd0, os0), (o1, sd1, os1) = runs
+    for a, b in zip(o0, o1):
+        for k in a:
+            np.testing.assert_allclose(b[k], a[k], rtol=1e-6, atol=1e-7, err_msg=k)
+    for k in sd0:
+        np.testing.assert_allclose(sd1[k], sd0[k], rtol=1e-6, atol=1e-7, err_msg=k)
+    from tianshou_amd.policy.ppo import split_bounds
+    n_mb = len(split_bounds(int(z["n_step"]), 64, True))
+    for i, st in os0["state"].items():
+        assert float(st["step"]) == float(os1["state"][i]["step"]) == 8 * n_mb

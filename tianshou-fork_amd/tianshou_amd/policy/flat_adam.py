@@ -1,0 +1,161 @@
+"""Flat gradient / Adam storage for one parameter list: every ``.grad`` is a view into one
+bucket, and -- when the optimiser is a plain ``torch.optim.Adam`` over exactly these
+parameters -- the parameters and their Adam moments become views into flat buffers, so
+``clip_grad_norm_`` + ``optim.step()`` (ppo.py:143-151) run as ONE HIP pass
+(``tsrl_clip_adam``, csrc/optim.hip) whose learning rate is a device word.  Both properties
+make a whole epoch of minibatches capturable as one HIP graph: no host-side optimiser logic,
+no allocation, no synchronisation.
+
+``optim.state[p]`` entries are views too, so ``optim.state_dict()`` / ``load_state_dict``
+and torch's own ``optim.step()`` keep working on the same storage.
+
+Used by the fused Gaussian MLP (policy/fused_mlp.py, which adds its kernels' pointers) and by
+the Categorical learn path of PPOPolicy (any torch actor / critic networks).
+"""
+from typing import Optional
+
+import torch
+
+from tianshou_amd import _C
+
+
+class FlatAdam:
+    # extra f32 words after the flat gradients in the bucket (data-parallel loss sums ride
+    # in the same all-reduce as the gradients)
+    BUCKET_TAIL = 0
+
+    def __init__(self, params) -> None:
+        self.params = [p for p in params]
+        self._flat = None
+        self._bucket = None
+        self._views = []
+        self._adam = None  # flat parameter / moment storage of bind_adam
+
+    # -- gradient storage -----------------------------------------------------------------------
+    def bind_grads(self) -> None:
+        """Point every parameter's .grad at a slice of one flat buffer (kept across
+        minibatches; re-bound if the optimiser or user replaced a .grad)."""
+        dev = self.params[0].device
+        if self._flat is not None and all(
+                p.grad is not None and p.grad.data_ptr() == v.data_ptr()
+                for p, v in zip(self.params, self._views)):
+            return
+        n = sum(p.numel() for p in self.params)
+        self._bucket = torch.zeros(n + self.BUCKET_TAIL, dtype=torch.float32, device=dev)
+        self._flat = self._bucket[:n]
+        self._views = []
+        o = 0
+        for p in self.params:
+            v = self._flat[o:o + p.numel()].view_as(p)
+            p.grad = v
+            self._views.append(v)
+            o += p.numel()
+        self._grads_bound()
+
+    def _grads_bound(self) -> None:
+        """Hook: the gradient addresses changed."""
+
+    @property
+    def flat_grad(self) -> Optional[torch.Tensor]:
+        return self._flat
+
+    def zero_grad(self) -> None:
+        """optim.zero_grad() for views that must keep their addresses: autograd then
+        accumulates into the flat bucket in place."""
+        self.bind_grads()
+        self._flat.zero_()
+
+    # -- clip_grad_norm_ + Adam as one HIP pass ---------------------------------------------------
+    @staticmethod
+    def _plain_adam(optim, params) -> bool:
+        if not isinstance(optim, torch.optim.Adam) or len(optim.param_groups) != 1:
+            return False
+        g = optim.param_groups[0]
+        if g.get("amsgrad") or g.get("weight_decay", 0) != 0 or g.get("maximize") or \
+                g.get("differentiable") or isinstance(g["lr"], torch.Tensor):
+            return False
+        return len(g["params"]) == len(params) and \
+            all(a is b for a, b in zip(g["params"], params))
+
+    def adam_bound(self, optim) -> bool:
+        st = self._adam
+        return st is not None and st["optim"] is optim and all(
+            p.data_ptr() == v.data_ptr() for p, v in zip(self.params, st["pviews"]))
+
+    def bind_adam(self, optim) -> bool:
+        """Move every parameter and its Adam moments into flat buffers (parameter .data and
+        ``optim.state[p]`` become views) when ``optim`` is a plain Adam over exactly these
+        parameters; then ``clip_adam`` replaces clip_grad_norm_ + optim.step()."""
+        if self.adam_bound(optim):
+            return True
+        if not self._plain_adam(optim, self.params):
+            self._adam = None
+            return False
+        dev = self.params[0].device
+        n = sum(p.numel() for p in self.params)
+        flat_p = torch.empty(n, dtype=torch.float32, device=dev)
+        flat_m = torch.zeros(n, dtype=torch.float32, device=dev)
+        flat_v = torch.zeros(n, dtype=torch.float32, device=dev)
+        steps = torch.zeros(len(self.params), dtype=torch.float32, device=dev)
+        pviews = []
+        o = 0
+        for i, p in enumerate(self.params):
+            k = p.numel()
+            flat_p[o:o + k].copy_(p.detach().reshape(-1))
+            st = optim.state.get(p, {})
+            if "exp_avg" in st:
+                flat_m[o:o + k].copy_(st["exp_avg"].reshape(-1))
+                flat_v[o:o + k].copy_(st["exp_avg_sq"].reshape(-1))
+                steps[i] = float(st["step"])
+            with torch.no_grad():
+                p.data = flat_p[o:o + k].view_as(p)
+            optim.state[p] = {"step": steps[i],
+                              "exp_avg": flat_m[o:o + k].view_as(p),
+                              "exp_avg_sq": flat_v[o:o + k].view_as(p)}
+            pviews.append(p.data)
+            o += k
+        steps.fill_(float(steps.max()) if len(steps) else 0.0)
+        self._adam = dict(optim=optim, p=flat_p, m=flat_m, v=flat_v, steps=steps, pviews=pviews,
+                          ticket=torch.zeros(1, dtype=torch.int32, device=dev),
+                          partials=torch.zeros(
+                              max(int(_C.lib().tsrl_clip_adam_partials(n)), 1),
+                              dtype=torch.float64, device=dev),
+                          norm=torch.zeros(2, dtype=torch.float32, device=dev),
+                          lr=torch.zeros(1, dtype=torch.float32, device=dev))
+        self._flat = None  # parameter addresses moved: bind_grads re-derives every pointer
+        self.bind_grads()
+        return True
+
+    def flat_offset(self, t: torch.Tensor) -> int:
+        """Element offset of parameter storage ``t`` inside the flat parameter buffer."""
+        return (t.data_ptr() - self._adam["p"].data_ptr()) // 4
+
+    def set_lr(self) -> None:
+        """Publish the optimiser's current lr to the device word the Adam kernel reads (one
+        tiny fill per epoch; captured learn graphs then follow an lr_scheduler without being
+        re-captured)."""
+        st = self._adam
+        lr = float(st["optim"].param_groups[0]["lr"])
+        if st.get("lr_host") != lr:
+            st["lr"].fill_(lr)
+            st["lr_host"] = lr
+
+    def clip_adam(self, max_norm: Optional[float], scale_grads: bool = True,
+                  split=None) -> None:
+        """clip_grad_norm_(max_norm) (when given) + Adam.step() over the flat buffers; the
+        learning rate comes from the device word of set_lr().  ``scale_grads=False`` skips
+        the in-place clipping of .grad (only the last step of a learn() needs it: every
+        minibatch overwrites the gradients); ``split`` (a _C.W1Split) re-splits first-layer
+        weights into bf16x6 planes in the same pass."""
+        st = self._adam
+        g = st["optim"].param_groups[0]
+        b1, b2 = g["betas"]
+        if st.get("lr_host") is None:
+            self.set_lr()
+        _C.check(_C.lib().tsrl_clip_adam(
+            _C.ptr(st["p"]), _C.ptr(self._flat), _C.ptr(st["m"]), _C.ptr(st["v"]),
+            st["p"].numel(), _C.ptr(st["steps"]), st["steps"].numel(), float(g["lr"]),
+            float(b1), float(b2), float(g["eps"]), float(max_norm) if max_norm else 0.0,
+            _C.ptr(st["partials"]), _C.ptr(st["norm"]), _C.ptr(st["ticket"]), _C.ptr(st["lr"]),
+            split, int(bool(scale_grads)), _C.stream_ptr(st["p"].device)),
+            "tsrl_clip_adam")

@@ -20,6 +20,7 @@ import torch
 from torch import nn
 
 from tianshou_amd import _C
+from tianshou_amd.policy.flat_adam import FlatAdam
 
 HIDDEN = 64
 MAX_ACT = 32
@@ -78,38 +79,20 @@ def match(actor, critic) -> Optional[Dict[str, nn.Linear]]:
             "D": D, "A": h_a.out_features, "sigma": actor.sigma_param}
 
 
-class FusedActorCritic:
+class FusedActorCritic(FlatAdam):
+    # data-parallel: the minibatch's loss partial sums ride after the flat gradients, so a
+    # single all-reduce per minibatch carries both
+    BUCKET_TAIL = 4 + MAX_ACT
+
     def __init__(self, layers: Dict, params) -> None:
+        super().__init__(params)
         self.L = layers
         self.D = layers["D"]
         self.Dp = (self.D + 3) // 4 * 4  # row stride the kernels read (16-byte rows)
         self.A = layers["A"]
-        self.params = [p for p in params]
-        self._flat = None
         self._bufs: Dict[str, torch.Tensor] = {}
-        self._adam = None  # flat parameter / moment storage of bind_adam
 
-    # -- gradient storage -----------------------------------------------------------------------
-    def bind_grads(self) -> None:
-        """Point every parameter's .grad at a slice of one flat buffer (kept across
-        minibatches; re-bound if the optimiser or user replaced a .grad)."""
-        dev = self.params[0].device
-        if self._flat is not None and all(
-                p.grad is not None and p.grad.data_ptr() == v.data_ptr()
-                for p, v in zip(self.params, self._views)):
-            return
-        n = sum(p.numel() for p in self.params)
-        # one bucket: the flat gradients, then (data-parallel) the minibatch's loss partial
-        # sums, so a single all-reduce per minibatch carries both
-        self._bucket = torch.zeros(n + 4 + MAX_ACT, dtype=torch.float32, device=dev)
-        self._flat = self._bucket[:n]
-        self._views = []
-        o = 0
-        for p in self.params:
-            v = self._flat[o:o + p.numel()].view_as(p)
-            p.grad = v
-            self._views.append(v)
-            o += p.numel()
+    def _grads_bound(self) -> None:
         L = self.L
         g = lambda m: _C.ptr(m.grad)  # noqa: E731
         self._tail_grads = _C.TailGrads(
@@ -120,105 +103,17 @@ class FusedActorCritic:
             _C.ptr(L["w2c"].bias), _C.ptr(L["w3a"].weight), _C.ptr(L["w3a"].bias),
             _C.ptr(L["w3c"].weight), _C.ptr(L["w3c"].bias), _C.ptr(L["sigma"]))
 
-    # -- clip_grad_norm_ + Adam as one HIP pass (csrc/optim.hip) --------------------------------
-    @staticmethod
-    def _plain_adam(optim, params) -> bool:
-        if not isinstance(optim, torch.optim.Adam) or len(optim.param_groups) != 1:
-            return False
-        g = optim.param_groups[0]
-        if g.get("amsgrad") or g.get("weight_decay", 0) != 0 or g.get("maximize") or \
-                g.get("differentiable") or isinstance(g["lr"], torch.Tensor):
-            return False
-        return len(g["params"]) == len(params) and \
-            all(a is b for a, b in zip(g["params"], params))
-
-    def adam_bound(self, optim) -> bool:
-        st = self._adam
-        return st is not None and st["optim"] is optim and all(
-            p.data_ptr() == v.data_ptr() for p, v in zip(self.params, st["pviews"]))
-
-    def bind_adam(self, optim) -> bool:
-        """Move every parameter and its Adam moments into flat buffers (parameter .data and
-        ``optim.state[p]`` become views, so state_dict()/load and torch's own step keep
-        working) when ``optim`` is a plain Adam over exactly these parameters; then
-        ``clip_adam`` replaces clip_grad_norm_ + optim.step()."""
-        if self.adam_bound(optim):
-            return True
-        if not self._plain_adam(optim, self.params):
-            self._adam = None
-            return False
-        dev = self.params[0].device
-        n = sum(p.numel() for p in self.params)
-        flat_p = torch.empty(n, dtype=torch.float32, device=dev)
-        flat_m = torch.zeros(n, dtype=torch.float32, device=dev)
-        flat_v = torch.zeros(n, dtype=torch.float32, device=dev)
-        steps = torch.zeros(len(self.params), dtype=torch.float32, device=dev)
-        pviews = []
-        o = 0
-        for i, p in enumerate(self.params):
-            k = p.numel()
-            flat_p[o:o + k].copy_(p.detach().reshape(-1))
-            st = optim.state.get(p, {})
-            if "exp_avg" in st:
-                flat_m[o:o + k].copy_(st["exp_avg"].reshape(-1))
-                flat_v[o:o + k].copy_(st["exp_avg_sq"].reshape(-1))
-                steps[i] = float(st["step"])
-            with torch.no_grad():
-                p.data = flat_p[o:o + k].view_as(p)
-            optim.state[p] = {"step": steps[i],
-                              "exp_avg": flat_m[o:o + k].view_as(p),
-                              "exp_avg_sq": flat_v[o:o + k].view_as(p)}
-            pviews.append(p.data)
-            o += k
-        steps.fill_(float(steps.max()) if len(steps) else 0.0)
-        base = flat_p.data_ptr()
-        off = lambda t: (t.data_ptr() - base) // 4  # noqa: E731
-        self._adam = dict(optim=optim, p=flat_p, m=flat_m, v=flat_v, steps=steps, pviews=pviews,
-                          w1_off=(off(self.L["w1a"].weight), off(self.L["w1c"].weight)),
-                          ticket=torch.zeros(1, dtype=torch.int32, device=dev),
-                          partials=torch.zeros(
-                              max(int(_C.lib().tsrl_clip_adam_partials(n)), 1),
-                              dtype=torch.float64, device=dev),
-                          norm=torch.zeros(2, dtype=torch.float32, device=dev),
-                          lr=torch.zeros(1, dtype=torch.float32, device=dev))
-        self._flat = None  # parameter addresses moved: bind_grads re-derives every pointer
-        self.bind_grads()
-        return True
-
-    def set_lr(self) -> None:
-        """Publish the optimiser's current lr to the device word the Adam kernel reads (one
-        tiny fill per epoch; captured learn graphs then follow an lr_scheduler without being
-        re-captured)."""
-        st = self._adam
-        lr = float(st["optim"].param_groups[0]["lr"])
-        if st.get("lr_host") != lr:
-            st["lr"].fill_(lr)
-            st["lr_host"] = lr
-
     def clip_adam(self, max_norm: Optional[float], scale_grads: bool = True,
                   split_w1: bool = False) -> None:
-        """clip_grad_norm_(max_norm) (when given) + Adam.step() over the flat buffers; the
-        learning rate comes from the device word of set_lr().  ``scale_grads=False`` skips
-        the in-place clipping of .grad (only the last step of a learn() needs it: every
-        minibatch overwrites the gradients); ``split_w1`` re-splits the updated first-layer
-        weights for the next minibatch in the same pass (no split_w launch)."""
-        st = self._adam
-        g = st["optim"].param_groups[0]
-        b1, b2 = g["betas"]
-        if st.get("lr_host") is None:
-            self.set_lr()
+        """FlatAdam.clip_adam; ``split_w1`` re-splits the updated first-layer weights into
+        the bf16x6 planes the next minibatch's layer-1 kernels read (no split_w launch)."""
         sp = None
         if split_w1 and L1_X6:
             ws = self._buf("w1split", (int(_C.lib().tsrl_mlp_split_bytes(self.D)) + 3) // 4)
-            sp = _C.W1Split(_C.ptr(ws), st["w1_off"][0], st["w1_off"][1], self.D,
+            sp = _C.W1Split(_C.ptr(ws), self.flat_offset(self.L["w1a"].weight),
+                            self.flat_offset(self.L["w1c"].weight), self.D,
                             (self.D + 31) // 32 * 32)
-        _C.check(_C.lib().tsrl_clip_adam(
-            _C.ptr(st["p"]), _C.ptr(self._flat), _C.ptr(st["m"]), _C.ptr(st["v"]),
-            st["p"].numel(), _C.ptr(st["steps"]), st["steps"].numel(), float(g["lr"]),
-            float(b1), float(b2), float(g["eps"]), float(max_norm) if max_norm else 0.0,
-            _C.ptr(st["partials"]), _C.ptr(st["norm"]), _C.ptr(st["ticket"]), _C.ptr(st["lr"]),
-            sp, int(bool(scale_grads)), _C.stream_ptr(st["p"].device)),
-            "tsrl_clip_adam")
+        super().clip_adam(max_norm, scale_grads, sp)
 
     def _weights(self) -> "_C.TailWeights":
         L = self.L
@@ -305,10 +200,6 @@ class FusedActorCritic:
                                        logp.data_ptr() + s0 * 4 if logp is not None else None,
                                        s), "tsrl_ppo_eval")
         return values, logp
-
-    @property
-    def flat_grad(self) -> torch.Tensor:
-        return self._flat
 
     def _buf(self, key: str, numel: int, dtype=torch.float32) -> torch.Tensor:
         b = self._bufs.get(key)

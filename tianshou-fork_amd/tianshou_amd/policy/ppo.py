@@ -19,6 +19,7 @@ from torch import nn
 from tianshou_amd import _C
 from tianshou_amd.data.batch import Batch, gather_rows, split_indices
 from tianshou_amd.policy.a2c import A2CPolicy
+from tianshou_amd.policy.flat_adam import FlatAdam
 from tianshou_amd.policy.fused_eval import FusedEvalMixin, cat_logp, cat_mode  # noqa: F401
 from tianshou_amd.utils.np_perm import LegacyPermutation
 
@@ -187,6 +188,8 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
         self._learn_graph = None
         # clip_grad_norm_ + Adam as one HIP pass over flat parameter storage (csrc/optim.hip)
         self.fused_adam = True
+        self._cat_adam: Optional[FlatAdam] = None
+        self._cat_warm = False
 
     def _params(self, b_global: float) -> _C.PPOParams:
         p = _C.PPOParams()
@@ -403,8 +406,9 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
             if not (static and self.dp.capturable):
                 return False
         opt = self.optim
-        if self._mlp is not None and self._mlp.adam_bound(opt):
-            return True
+        for flat in (self._mlp, self._cat_adam):
+            if flat is not None and flat.adam_bound(opt):
+                return True
         if not opt.defaults.get("capturable", False) or len(opt.state) == 0:
             return False
         return all(p in opt.state for g in opt.param_groups for p in g["params"])
@@ -473,43 +477,122 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
                    ) -> Dict[str, List[float]]:
         """ppo.py:99-162 for Categorical policies: torch actor/critic (MLP or conv trunk on
         MIOpen/hipBLASLt), minibatch rows gathered once through the permutation, the loss and
-        its gradient w.r.t. the dist_fn input from the fused tsrl_ppo_cat kernel."""
+        its gradient w.r.t. the dist_fn input from the fused tsrl_ppo_cat kernel.  With a
+        plain Adam the gradients live in one flat bucket and clip_grad_norm_ + Adam.step() are
+        one HIP pass (policy/flat_adam.py); epochs after the first eager one then replay from
+        a captured HIP graph (small minibatches -- test_ppo.py's 64 rows -- are otherwise
+        bound by ~40 host launches each)."""
         dev = batch.v_s.device
         n = len(batch.v_s)
         terms = []
         f32 = dict(device=dev, dtype=torch.float32)
+        fa = self._cat_flat_adam()
         for step in range(repeat):
             if self._recompute_adv and step > 0:
                 batch = self._compute_returns(batch, self._buffer, self._indices)
             act = torch.as_tensor(batch.act, device=dev).reshape(n).to(torch.int64).contiguous()
-            logp_old = batch.logp_old.reshape(-1).to(**f32).contiguous()
-            adv = batch.adv.reshape(-1).to(**f32).contiguous()
-            ret = batch.returns.reshape(-1).to(**f32).contiguous()
-            v_s = batch.v_s.reshape(-1).to(**f32).contiguous()
+            arrays = (act, batch.logp_old.reshape(-1).to(**f32).contiguous(),
+                      batch.adv.reshape(-1).to(**f32).contiguous(),
+                      batch.returns.reshape(-1).to(**f32).contiguous(),
+                      batch.v_s.reshape(-1).to(**f32).contiguous())
             perm = self._permutation(n, dev)
-            for s, e in split_bounds(n, batch_size, merge_last=True):
-                idx = perm[s:e]
-                obs_mb = gather_rows(batch.obs, idx)
-                if self._shared_trunk:
-                    x, value = self._trunk_heads(obs_mb)
-                else:
-                    x, _ = self.actor(obs_mb)
-                    value = self.critic(obs_mb).flatten()
-                params = self._params((e - s) * self.dp.world)
-                loss, t = _CatPPOLoss.apply(x, value, (act, logp_old, adv, ret, v_s, idx, params,
-                                                       self.dp, self._cat))
-                self.optim.zero_grad()
-                loss.backward()
-                self.dp.all_reduce_grads_(self._actor_critic.parameters())
-                if self._grad_norm:
-                    nn.utils.clip_grad_norm_(self._actor_critic.parameters(),
-                                             max_norm=self._grad_norm)
-                self.optim.step()
-                terms.append(t)
+            chunks = [(s, e, (e - s) * self.dp.world)
+                      for s, e in split_bounds(n, batch_size, merge_last=True)]
+            if fa is not None:
+                fa.set_lr()
+                # conv trunks (MIOpen) stay eager unless graph_learn=True
+                graph = self._use_graph(batch_size) and (batch.obs.dim() == 2 or
+                                                         self.graph_learn is True)
+                if self._cat_warm and graph and self._graph_ready(chunks):
+                    t = self._cat_epoch_graph(fa, batch.obs, arrays, perm, chunks,
+                                              first=(step == 0))
+                    if t is not None:
+                        terms.append(t)
+                        continue
+            for k, (s, e, b_glob) in enumerate(chunks):
+                terms.append(self._cat_minibatch(fa, batch.obs, perm[s:e], b_glob, arrays,
+                                                 last=(k == len(chunks) - 1)))
+            self._cat_warm = True
         vals = torch.cat([t.reshape(-1, 4) for t in terms]).cpu().numpy() if terms else \
             np.zeros((0, 4), np.float32)
         return {"loss": vals[:, 0].tolist(), "loss/clip": vals[:, 1].tolist(),
                 "loss/vf": vals[:, 2].tolist(), "loss/ent": vals[:, 3].tolist()}
+
+    def _cat_flat_adam(self) -> Optional[FlatAdam]:
+        """The flat gradient / Adam storage of the actor-critic parameters when the optimiser
+        is a plain Adam over exactly them (None otherwise: torch's optimiser runs)."""
+        if not self.fused_adam:
+            return None
+        fa = self._cat_adam
+        if fa is None:
+            fa = self._cat_adam = FlatAdam(self._actor_critic.parameters())
+        return fa if fa.bind_adam(self.optim) else None
+
+    def _cat_minibatch(self, fa: Optional[FlatAdam], obs: torch.Tensor, idx: torch.Tensor,
+                       b_glob: int, arrays, last: bool) -> torch.Tensor:
+        """One Categorical minibatch (ppo.py:107-151): forward, fused loss, backward,
+        gradient all-reduce, clip_grad_norm_ + Adam.step(); returns the [4] loss terms."""
+        obs_mb = gather_rows(obs, idx)
+        if self._shared_trunk:
+            x, value = self._trunk_heads(obs_mb)
+        else:
+            x, _ = self.actor(obs_mb)
+            value = self.critic(obs_mb).flatten()
+        loss, t = _CatPPOLoss.apply(x, value, (*arrays, idx, self._params(b_glob), self.dp,
+                                               self._cat))
+        if fa is not None:
+            fa.zero_grad()  # autograd accumulates into the flat bucket in place
+            loss.backward()
+            self.dp.all_reduce_(fa.flat_grad)
+            fa.clip_adam(self._grad_norm, scale_grads=last)
+            return t
+        self.optim.zero_grad()
+        loss.backward()
+        self.dp.all_reduce_grads_(self._actor_critic.parameters())
+        if self._grad_norm:
+            nn.utils.clip_grad_norm_(self._actor_critic.parameters(), max_norm=self._grad_norm)
+        self.optim.step()
+        return t
+
+    def _cat_epoch_graph(self, fa: FlatAdam, obs, arrays, perm, chunks, first: bool):
+        """One Categorical epoch replayed from a captured HIP graph (the torch forward /
+        autograd backward, the fused loss kernels and the flat Adam pass of every minibatch).
+        Static copies of the per-update arrays and the permutation feed it; the obs rows are
+        read in place (their address is part of the key).  None if the capture failed."""
+        n = perm.numel()
+        key = (n, tuple(chunks), obs.data_ptr(), tuple(obs.shape), obs.dtype,
+               tuple(a.shape for a in arrays), fa.flat_grad.data_ptr(),
+               tuple(p.data_ptr() for p in fa.params))
+        st = self._learn_graph
+        if st is None or st["key"] != key:
+            self._learn_graph = None
+            dev = perm.device
+            static = [a.clone() for a in arrays]
+            sperm = perm.clone()
+            sterms = torch.empty(len(chunks), 4, dtype=torch.float32, device=dev)
+            torch.cuda.synchronize()
+            graph = torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.graph(graph):
+                    for i, (s, e, b_glob) in enumerate(chunks):
+                        t = self._cat_minibatch(fa, obs, sperm[s:e], b_glob, static,
+                                                last=(i == len(chunks) - 1))
+                        sterms[i].copy_(t)
+            except RuntimeError as err:
+                import warnings
+                warnings.warn(f"learn-graph capture failed, running epochs eagerly: {err}")
+                self._graph_failed = True
+                torch.cuda.synchronize()
+                return None
+            st = self._learn_graph = dict(key=key, graph=graph, static=static, perm=sperm,
+                                          terms=sterms)
+            first = False
+        if first:
+            for d, a in zip(st["static"], arrays):
+                d.copy_(a)
+        st["perm"].copy_(perm)
+        st["graph"].replay()
+        return st["terms"].clone()
 
     def _learn_generic(self, batch: Batch, batch_size: int, repeat: int
                        ) -> Dict[str, List[float]]:
