@@ -61,11 +61,13 @@ def parse():
     ap.add_argument("--repeat", type=int, default=4)
     ap.add_argument("--minibatches", type=int, default=32)
     ap.add_argument("--ep-len", type=int, default=None)
-    ap.add_argument("--perm", choices=["numpy", "device", "sorted"], default="numpy",
+    ap.add_argument("--perm", choices=["numpy", "numpy-sorted", "device", "sorted"],
+                    default="numpy",
                     help="minibatch permutation: numpy (the reference np.random.permutation "
-                         "stream, bit-exact: host MT19937 draws + device shuffle), device "
-                         "(torch.randperm), sorted (torch.randperm, rows of each minibatch "
-                         "in ascending buffer order: same minibatch sets)")
+                         "stream, bit-exact: host MT19937 draws + device shuffle), "
+                         "numpy-sorted (the same minibatch sets, rows of each visited in "
+                         "ascending buffer order), device (torch.randperm), sorted "
+                         "(torch.randperm, rows of each minibatch in ascending order)")
     ap.add_argument("--cpu-steps", type=int, default=None,
                     help="T' of the bounded CPU-baseline sample (envs x T')")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -153,7 +155,7 @@ def build_atari(args, dev, rank):
                        eps_clip=0.1, value_clip=True, dual_clip=None,
                        advantage_normalization=False, recompute_advantage=False,
                        reward_normalization=False,
-                       perm_device=(args.perm != "numpy")).to(dev)
+                       perm_device=args.perm in ("device", "sorted")).to(dev)
     buf = VectorReplayBuffer(E * T, E, stack_num=4, ignore_obs_next=True,
                              save_only_last_obs=True, device=dev)
     return Collector(policy, env, buf, exploration_noise=True), policy, buf
@@ -208,7 +210,7 @@ def build_cartpole(args, dev, rank):
                        dual_clip=None, value_clip=False, action_space=Discrete(2),
                        deterministic_eval=True, advantage_normalization=False,
                        recompute_advantage=False, action_scaling=False,
-                       perm_device=(args.perm != "numpy")).to(dev)
+                       perm_device=args.perm in ("device", "sorted")).to(dev)
     buf = VectorReplayBuffer(20000, E, device=dev)
     return Collector(policy, env, buf), policy, buf
 
@@ -262,12 +264,12 @@ def main():
                            reward_normalization=True, advantage_normalization=True,
                            recompute_advantage=False, eps_clip=0.2, value_clip=False,
                            dual_clip=None, action_bound_method="clip",
-                           perm_device=(args.perm != "numpy")).to(dev)
+                           perm_device=args.perm in ("device", "sorted")).to(dev)
         buf = VectorReplayBuffer(n, E, device=dev)
         coll = Collector(policy, env, buf)
     torch.manual_seed(rank)  # per-rank action sampling streams
     policy.graph_learn = {"auto": None, "on": True, "off": False}[args.graph_learn]
-    policy.sort_minibatch = args.perm == "sorted"
+    policy.sort_minibatch = args.perm in ("sorted", "numpy-sorted")
     # weak scaling: every rank splits its own rows with its own np.random stream (a global
     # permutation of world x n rows is O(world x n) sequential host draws per rank)
     policy.dp_permutation = "local"
