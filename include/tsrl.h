@@ -244,6 +244,17 @@ int tsrl_stack_gather(const void* src, int64_t frame_bytes, const int64_t* idx, 
 int tsrl_frames_to_f32_nhwc(const uint8_t* src, int64_t n, int64_t c, int64_t hw,
                             const float* lut, float* dst, void* stream);
 
+/* First convolution + ReLU of the Nature-DQN trunk straight from uint8 frame stacks:
+ * out = relu(conv(frames, w) / scale + bias), frames [n][4][84][84] u8 (contiguous, 4-byte
+ * aligned), w [32][4][8][8] f32 addressed through its element strides (sw0..sw3, so a
+ * channels_last weight needs no copy), bias [32] (nullable), out [n][20][20][32] f32 (NHWC,
+ * 16-byte aligned).  Replaces scale_obs + Conv2d(4, 32, 8, 4) + ReLU of
+ * examples/atari/atari_network.py:18-30,53-90 in DQN.forward (:84): bytes are exact bf16
+ * operands, weights split exactly into 3 bf16 planes (f32 GEMM error). */
+int tsrl_dqn_conv1_fwd(const uint8_t* frames, int64_t n, const float* w, int64_t sw0,
+                       int64_t sw1, int64_t sw2, int64_t sw3, const float* bias, float scale,
+                       int relu, float* out, void* stream);
+
 /* ---------------------------------------------------------------------------------
  * np.random.permutation(n) of the global legacy RandomState, bit-exact: the shuffle order
  * of Batch.split (tianshou/data/batch.py:896-912, one permutation per PPO repeat,

@@ -187,6 +187,7 @@ def test_dqn_nhwc_trunk_matches_nchw(dev):
     torch.manual_seed(0)
     b = DQN(4, 84, 84, (6,), device=dev, features_only=True, output_dim=512,
             layer_init=layer_init, channels_last=False).to(dev)
+    a.fused_conv1 = b.fused_conv1 = False
     x = torch.randint(0, 256, (64, 4, 84, 84), dtype=torch.uint8, device=dev)
     ya, yb = a(x)[0], b(x)[0]
     torch.testing.assert_close(ya, yb, rtol=1e-4, atol=1e-5 * float(yb.abs().max()))
@@ -196,6 +197,58 @@ def test_dqn_nhwc_trunk_matches_nchw(dev):
     for pa, pb in zip(a.parameters(), b.parameters()):
         torch.testing.assert_close(pa.grad, pb.grad, rtol=1e-3,
                                    atol=1e-4 * float(pb.grad.abs().max()))
+
+
+@pytest.mark.parametrize("n", [1, 37, 1024])
+def test_conv1_u8_kernel_vs_f64(dev, n):
+    """tsrl_dqn_conv1_fwd (uint8 frames, bf16 byte operands x 3-plane split weights) against
+    an fp64 relu(conv(frames / 255) + b): elementwise within 1e-6 of sum|w x| + |b| (f32 GEMM
+    error), and in RMS no worse than 2x torch's own f32 convolution of the f32 frames; the
+    weight is channels_last (strided access) and the batch ragged (tiles straddle
+    samples)."""
+    from tianshou_amd.utils.net_atari import DQN, conv1_u8, layer_init
+    torch.manual_seed(n)
+    net = DQN(4, 84, 84, (6,), device=dev, features_only=True, output_dim=512,
+              layer_init=layer_init).to(dev)
+    conv = net._conv1_parts()[0]
+    with torch.no_grad():
+        conv.bias.uniform_(-0.5, 0.5)
+    x = torch.randint(0, 256, (n, 4, 84, 84), dtype=torch.uint8, device=dev)
+    got = conv1_u8(x, conv, 255.0)
+    assert got.shape == (n, 32, 20, 20) and got.is_contiguous(memory_format=torch.channels_last)
+    w64, b64 = conv.weight.double(), conv.bias.double()
+    x64 = x.double() / 255.0
+    ref = torch.relu(torch.nn.functional.conv2d(x64, w64, b64, 4))
+    mag = torch.nn.functional.conv2d(x64, w64.abs(), b64.abs(), 4)
+    err = (got.double() - ref).abs()
+    assert bool((err <= 1e-6 * mag + 1e-12).all()), float((err / (mag + 1e-30)).max())
+    xf = net._scale_lut(dev)[x.long()]
+    tref = torch.relu(torch.nn.functional.conv2d(xf, conv.weight, conv.bias, 4)).double()
+    rms = lambda e: float(e.pow(2).mean().sqrt())  # noqa: E731
+    assert rms(err) <= 2 * rms(tref - ref) + 1e-9, (rms(err), rms(tref - ref))
+
+
+def test_dqn_fused_conv1_matches_miopen(dev):
+    """The whole trunk with the uint8 first layer (forward: tsrl_dqn_conv1_fwd; backward:
+    ReLU mask + MIOpen weight/bias gradient over the scaled frames) against the same module
+    on MIOpen throughout: outputs and every parameter gradient."""
+    from tianshou_amd.utils.net_atari import DQN, layer_init
+    torch.manual_seed(1)
+    a = DQN(4, 84, 84, (6,), device=dev, features_only=True, output_dim=512,
+            layer_init=layer_init).to(dev)
+    x = torch.randint(0, 256, (96, 4, 84, 84), dtype=torch.uint8, device=dev)
+    outs = []
+    for fused in (True, False):
+        a.fused_conv1 = fused
+        a.zero_grad(set_to_none=True)
+        y = a(x)[0]
+        g = torch.randn(y.shape, device=dev, generator=torch.Generator(device=dev).manual_seed(2))
+        y.backward(g)
+        outs.append((y.detach(), [p.grad.clone() for p in a.parameters()]))
+    (ya, ga), (yb, gb) = outs
+    torch.testing.assert_close(ya, yb, rtol=1e-4, atol=1e-5 * float(yb.abs().max()))
+    for pa, pb in zip(ga, gb):
+        torch.testing.assert_close(pa, pb, rtol=1e-3, atol=1e-4 * float(pb.abs().max()))
 
 
 def test_atari_shared_trunk_process_fn_wrapped_ring(dev):

@@ -1,0 +1,170 @@
+// First convolution of the Nature-DQN trunk of BASELINE config 5
+// (examples/atari/atari_network.py:53-90: Conv2d(4, 32, 8, stride 4) + ReLU over
+// scale_obs(frames) = frames / 255, :18-30) straight from the uint8 frame stacks, as an
+// implicit GEMM on the bf16 matrix cores.
+//
+// Exactness: a frame byte u (0..255) is exact in bf16, so the "input" operand needs ONE
+// plane; every f32 weight is split exactly into three bf16 pieces (x6.h), so each of the
+// three products w_p . u is exact in the f32 MFMA accumulator and the sum over k carries f32
+// GEMM error of sum_k w_k u_k.  The output is relu(acc / scale + b): the same function as
+// the reference's conv(f32(u / 255)) + b, whose own input rounding (2^-24 relative per
+// element) is of the order of that accumulation error.  Three bf16 MFMAs per 16 k instead of
+// the six of the f32-f32 split, and the u8 -> f32 frame conversion (and its 4x larger
+// activation tensor) disappears from the forward path.
+//
+// GEMM view: D[32 channels][32 pixels] += W[32][16 k] . P[16 k][32 pixels] per MFMA
+// (v_mfma_f32_32x32x16_bf16), k = c*64 + kh*8 + kw, so the 8 k of one lane half are the 8
+// consecutive bytes x[c][4 oh + kh][4 ow .. 4 ow + 7] of one input row: one 8-byte load.
+// Workgroup = 4 waves, persistent over pixel tiles; the three split planes of W (48 KB) are
+// staged once per workgroup in LDS (rows of 512 B, 16-byte chunks XOR-swizzled by row so a
+// ds_read_b128 phase hits distinct banks).  A wave owns two 32-pixel tiles at a time (flat
+// pixel index over the batch, so tiles may straddle samples): the 32 eight-byte loads of
+// both tiles are issued up front, then 16 k-steps of 3 + 3 MFMAs share each A fragment.
+// Epilogue: bias + ReLU, NHWC f32 output ([n][20][20][32], channels_last of [n,32,20,20]).
+#include <algorithm>
+
+#include "x6.h"
+
+namespace tsrl {
+namespace {
+
+using x6::bf16x8;
+using x6::f32x16;
+using x6::NPL;
+
+constexpr int C1_CIN = 4, C1_HW = 84, C1_K = 8, C1_S = 4, C1_OUT = 20, C1_OC = 32;
+constexpr int C1_KK = C1_CIN * C1_K * C1_K;       // 256
+constexpr int C1_PIX = C1_OUT * C1_OUT;           // 400 output pixels per sample
+constexpr int C1_FRAME = C1_CIN * C1_HW * C1_HW;  // 28224 bytes per frame stack
+constexpr int C1_ROWB = C1_KK * 2;                // LDS bytes per weight row of one plane
+
+// LDS byte offset of 16-byte chunk q (0..31) of weight row m (0..31) of one plane.
+__device__ __forceinline__ int c1_off(int m, int q) { return m * C1_ROWB + 16 * (q ^ (m & 15)); }
+
+// 8 bytes (two little-endian words) -> 8 bf16 (exact: integers 0..255).
+__device__ __forceinline__ bf16x8 bytes_to_bf16(uint32_t lo, uint32_t hi) {
+    bf16x8 b;
+    b[0] = (__bf16)(float)(lo & 0xFF);
+    b[1] = (__bf16)(float)((lo >> 8) & 0xFF);
+    b[2] = (__bf16)(float)((lo >> 16) & 0xFF);
+    b[3] = (__bf16)(float)(lo >> 24);
+    b[4] = (__bf16)(float)(hi & 0xFF);
+    b[5] = (__bf16)(float)((hi >> 8) & 0xFF);
+    b[6] = (__bf16)(float)((hi >> 16) & 0xFF);
+    b[7] = (__bf16)(float)(hi >> 24);
+    return b;
+}
+
+__global__ __launch_bounds__(256, 2) void dqn_conv1_fwd_kernel(
+    const uint8_t* __restrict__ X, int64_t npix, const float* __restrict__ W, int64_t sw0,
+    int64_t sw1, int64_t sw2, int64_t sw3, const float* __restrict__ bias, float scale,
+    int relu, float* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) char Ws[NPL][C1_OC * C1_ROWB];
+    __shared__ float sb[C1_OC];
+    const int t = threadIdx.x;
+    const int w = t >> 6, l = t & 63, h = l >> 5, c = l & 31;
+    // stage the split weight planes: element (m, k), k = ci*64 + kh*8 + kw
+    for (int i = t; i < C1_OC * C1_KK; i += 256) {
+        const int m = i / C1_KK, k = i - m * C1_KK;
+        const int ci = k >> 6, kh = (k >> 3) & 7, kw = k & 7;
+        const float v = W[m * sw0 + ci * sw1 + kh * sw2 + kw * sw3];
+        __bf16 a0, a1, a2;
+        x6::split1(v, a0, a1, a2);
+        const int o = c1_off(m, k >> 3) + 2 * (k & 7);
+        *reinterpret_cast<__bf16*>(&Ws[0][o]) = a0;
+        *reinterpret_cast<__bf16*>(&Ws[1][o]) = a1;
+        *reinterpret_cast<__bf16*>(&Ws[2][o]) = a2;
+    }
+    if (t < C1_OC) sb[t] = bias ? bias[t] : 0.0f;
+    __syncthreads();
+    const int64_t ntile2 = (npix + 63) / 64;  // pairs of 32-pixel tiles
+    for (int64_t tp = (int64_t)blockIdx.x * 4 + w; tp < ntile2; tp += (int64_t)gridDim.x * 4) {
+        // this lane's pixel in each of the two tiles
+        const int64_t p0 = tp * 64 + c, p1 = p0 + 32;
+        const bool v0 = p0 < npix, v1 = p1 < npix;
+        const uint8_t* base0;
+        const uint8_t* base1;
+        {
+            const int64_t q0 = v0 ? p0 : 0, q1 = v1 ? p1 : 0;
+            const int64_t s0 = q0 / C1_PIX, s1 = q1 / C1_PIX;
+            const int r0 = (int)(q0 - s0 * C1_PIX), r1 = (int)(q1 - s1 * C1_PIX);
+            const int oh0 = r0 / C1_OUT, ow0 = r0 - oh0 * C1_OUT;
+            const int oh1 = r1 / C1_OUT, ow1 = r1 - oh1 * C1_OUT;
+            base0 = X + s0 * C1_FRAME + (C1_S * oh0 + h) * C1_HW + C1_S * ow0;
+            base1 = X + s1 * C1_FRAME + (C1_S * oh1 + h) * C1_HW + C1_S * ow1;
+        }
+        // k-step j: channel j / 4, kernel row 2 (j % 4) + h
+        uint32_t x0[32], x1[32];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int off = (j >> 2) * (C1_HW * C1_HW) + 2 * (j & 3) * C1_HW;
+            const uint32_t* a = reinterpret_cast<const uint32_t*>(base0 + off);
+            const uint32_t* b = reinterpret_cast<const uint32_t*>(base1 + off);
+            x0[2 * j] = a[0];
+            x0[2 * j + 1] = a[1];
+            x1[2 * j] = b[0];
+            x1[2 * j + 1] = b[1];
+        }
+        f32x16 acc0, acc1;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int ao = c1_off(c, 2 * j + h);
+            const bf16x8 w0 = *reinterpret_cast<const bf16x8*>(&Ws[0][ao]);
+            const bf16x8 w1 = *reinterpret_cast<const bf16x8*>(&Ws[1][ao]);
+            const bf16x8 w2 = *reinterpret_cast<const bf16x8*>(&Ws[2][ao]);
+            const bf16x8 b0 = bytes_to_bf16(x0[2 * j], x0[2 * j + 1]);
+            const bf16x8 b1 = bytes_to_bf16(x1[2 * j], x1[2 * j + 1]);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0, b0, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0, b1, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1, b0, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1, b1, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2, b0, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2, b1, acc1, 0, 0, 0);
+        }
+        // epilogue: lane (pixel c, half h) holds channels rho(r) + 4h
+#define C1_EPI(ACC, P, V)                                                                   \
+        if (V) {                                                                            \
+            float4* o_ = reinterpret_cast<float4*>(out + (P) * C1_OC);                      \
+            _Pragma("unroll") for (int q = 0; q < 4; ++q) {                                 \
+                float v_[4];                                                                \
+                _Pragma("unroll") for (int e = 0; e < 4; ++e) {                             \
+                    const float z_ = ACC[4 * q + e] / scale + sb[8 * q + 4 * h + e];        \
+                    v_[e] = relu ? fmaxf(z_, 0.0f) : z_;                                    \
+                }                                                                           \
+                o_[2 * q + h] = make_float4(v_[0], v_[1], v_[2], v_[3]);                    \
+            }                                                                               \
+        }
+        C1_EPI(acc0, p0, v0)
+        C1_EPI(acc1, p1, v1)
+#undef C1_EPI
+    }
+}
+
+}  // namespace
+}  // namespace tsrl
+
+using namespace tsrl;
+
+extern "C" int tsrl_dqn_conv1_fwd(const uint8_t* frames, int64_t n, const float* w, int64_t sw0,
+                                  int64_t sw1, int64_t sw2, int64_t sw3, const float* bias,
+                                  float scale, int relu, float* out, void* stream) {
+    TSRL_CHECK_ARG(n >= 0, "tsrl_dqn_conv1_fwd: n < 0");
+    if (n == 0) return 0;
+    TSRL_CHECK_ARG(frames && w && out, "tsrl_dqn_conv1_fwd: null pointer");
+    TSRL_CHECK_ARG((((uintptr_t)frames) & 3) == 0 && aligned16(out),
+                   "tsrl_dqn_conv1_fwd: frames must be 4-byte and out 16-byte aligned");
+    TSRL_CHECK_ARG(scale > 0.0f, "tsrl_dqn_conv1_fwd: scale must be > 0");
+    const int64_t npix = n * C1_PIX;
+    const int64_t pairs = (npix + 63) / 64;
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) == hipSuccess)
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const int64_t grid = std::min<int64_t>((pairs + 3) / 4, (int64_t)ncu * 3);
+    hipLaunchKernelGGL(dqn_conv1_fwd_kernel, dim3((unsigned)grid), dim3(256), 0,
+                       as_stream(stream), frames, npix, w, sw0, sw1, sw2, sw3, bias, scale, relu,
+                       out);
+    TSRL_LAUNCH_CHECK("tsrl_dqn_conv1_fwd");
+    return 0;
+}

@@ -33,6 +33,51 @@ def frames_to_f32_nhwc(obs: torch.Tensor, lut: torch.Tensor) -> torch.Tensor:
     return out.permute(0, 3, 1, 2)
 
 
+def conv1_u8(obs: torch.Tensor, conv: nn.Conv2d, scale: float) -> torch.Tensor:
+    """relu(conv(obs / scale)) of the trunk's first layer straight from uint8 frame stacks
+    [n, 4, 84, 84] (tsrl_dqn_conv1_fwd: bytes as exact bf16 operands, the weight split into
+    three bf16 planes; f32 GEMM error).  Returns [n, 32, 20, 20] in channels_last memory."""
+    obs = obs.contiguous()
+    n = obs.shape[0]
+    w = conv.weight.detach()
+    if not (w.is_cuda and w.dtype == torch.float32 and w.device == obs.device):
+        raise _C.TsrlError("conv1_u8: the conv weight must be an f32 tensor on the frames' "
+                           "device")
+    out = torch.empty((n, 20, 20, 32), dtype=torch.float32, device=obs.device)
+    b = conv.bias.detach() if conv.bias is not None else None
+    # the weight is addressed through its strides (channels_last needs no copy)
+    _C.check(_C.lib().tsrl_dqn_conv1_fwd(_C.ptr(obs), n, w.data_ptr(), *w.stride(),
+                                         _C.ptr(b) if b is not None else None, float(scale), 1,
+                                         _C.ptr(out), _C.stream_ptr(obs.device)),
+             "tsrl_dqn_conv1_fwd")
+    return out.permute(0, 3, 1, 2)
+
+
+class _Conv1U8(torch.autograd.Function):
+    """conv1 + ReLU from uint8 frames (forward: tsrl_dqn_conv1_fwd).  Backward: the ReLU
+    mask, then the weight and bias gradients from MIOpen over the scaled f32 frames
+    (tsrl_frames_to_f32_nhwc, built only when a gradient is needed); the frames themselves
+    need no gradient."""
+
+    @staticmethod
+    def forward(ctx, obs, weight, bias, conv, lut, scale):
+        z = conv1_u8(obs, conv, scale)
+        ctx.save_for_backward(obs, weight, z)
+        ctx.lut = lut
+        ctx.has_bias = bias is not None
+        return z
+
+    @staticmethod
+    def backward(ctx, gz):
+        obs, weight, z = ctx.saved_tensors
+        gy = torch.ops.aten.threshold_backward(gz, z, 0.0)
+        x = frames_to_f32_nhwc(obs, ctx.lut)
+        _, gw, gb = torch.ops.aten.convolution_backward(
+            gy, x, weight, [weight.shape[0]] if ctx.has_bias else None, (4, 4), (0, 0), (1, 1),
+            False, (0, 0), 1, (False, True, ctx.has_bias))
+        return None, gw, gb, None, None, None
+
+
 def layer_init(layer: nn.Module, std: float = np.sqrt(2), bias_const: float = 0.0):
     torch.nn.init.orthogonal_(layer.weight, std)
     torch.nn.init.constant_(layer.bias, bias_const)
@@ -70,6 +115,10 @@ class DQN(nn.Module):
         self.channels_last = channels_last
         if channels_last:
             self.net.to(memory_format=torch.channels_last)
+        # uint8 frame stacks on the GPU enter through the hand-written first layer
+        # (conv1_u8); False keeps MIOpen for it
+        self.fused_conv1 = True
+        self._conv1_split = None
 
     def _scale_lut(self, dev) -> torch.Tensor:
         """The 256 scaled byte values, divided on the host: f32 division there is
@@ -82,8 +131,36 @@ class DQN(nn.Module):
             self._lut = lut = (key, t.to(dev).contiguous())
         return lut[1]
 
+    def _conv1_parts(self):
+        """(conv1, rest of the conv stack, outer layers after it) when the trunk starts with
+        Conv2d(4, 32, 8, stride 4) + ReLU over 84x84 frames, else None."""
+        if self._conv1_split is None:
+            outer = None
+            seq = self.net
+            if len(seq) and isinstance(seq[0], nn.Sequential):
+                outer, seq = self.net, self.net[0]
+            conv = seq[0] if len(seq) > 1 else None
+            ok = isinstance(conv, nn.Conv2d) and isinstance(seq[1], nn.ReLU) and \
+                conv.in_channels == 4 and conv.out_channels == 32 and \
+                conv.kernel_size == (8, 8) and conv.stride == (4, 4) and \
+                conv.padding == (0, 0) and conv.dilation == (1, 1) and conv.groups == 1 and \
+                conv.padding_mode == "zeros"
+            self._conv1_split = (conv, seq[2:], outer[1:] if outer is not None else None) \
+                if ok else False
+        return self._conv1_split or None
+
     def forward(self, obs, state: Any = None, info: Dict[str, Any] = {}):
         obs = torch.as_tensor(obs, device=self.device)
+        parts = self._conv1_parts() if self.fused_conv1 else None
+        if parts is not None and obs.dim() == 4 and obs.dtype == torch.uint8 and obs.is_cuda \
+                and tuple(obs.shape[1:]) == (4, 84, 84) and self.scale and \
+                obs.data_ptr() % 4 == 0:
+            conv, rest, outer = parts
+            lut = self._scale_lut(obs.device)
+            h = _Conv1U8.apply(obs.contiguous(), conv.weight, conv.bias, conv, lut,
+                               float(self.scale))
+            h = rest(h)
+            return (outer(h) if outer is not None else h), state
         if self.channels_last and obs.dim() == 4 and obs.dtype == torch.uint8 and \
                 obs.is_cuda and self.scale:
             return self.net(frames_to_f32_nhwc(obs, self._scale_lut(obs.device))), state
