@@ -255,6 +255,15 @@ int tsrl_dqn_conv1_fwd(const uint8_t* frames, int64_t n, const float* w, int64_t
                        int64_t sw1, int64_t sw2, int64_t sw3, const float* bias, float scale,
                        int relu, float* out, void* stream);
 
+/* Data gradient of the trunk's second convolution (Conv2d(32, 64, 4, stride 2), :53-90) with
+ * the ReLU mask of its input fused: dx = (z1 > 0) * conv_transpose(gy, w), gy [n][9][9][64]
+ * f32 NHWC, w [64][32][4][4] f32 through its element strides, z1 [n][20][20][32] f32 NHWC
+ * (the first layer's ReLU output; NULL = no mask), dx [n][20][20][32] f32 NHWC.  Replaces
+ * MIOpen's backward-data + ReLU backward of loss.backward() (ppo.py:146) for the trunk;
+ * bf16x6 products (f32 GEMM error). */
+int tsrl_dqn_conv2_dgrad(const float* gy, int64_t n, const float* w, int64_t sw0, int64_t sw1,
+                         int64_t sw2, int64_t sw3, const float* z1, float* dx, void* stream);
+
 /* ---------------------------------------------------------------------------------
  * np.random.permutation(n) of the global legacy RandomState, bit-exact: the shuffle order
  * of Batch.split (tianshou/data/batch.py:896-912, one permutation per PPO repeat,

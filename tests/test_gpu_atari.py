@@ -199,6 +199,34 @@ def test_dqn_nhwc_trunk_matches_nchw(dev):
                                    atol=1e-4 * float(pb.grad.abs().max()))
 
 
+@pytest.mark.parametrize("n", [1, 37, 300])
+def test_conv2_dgrad_kernel_vs_f64(dev, n):
+    """tsrl_dqn_conv2_dgrad against fp64 conv_transpose (torch's conv2d input gradient) with
+    the ReLU mask of z1: elementwise within 1e-6 of the absolute-value product (f32 GEMM
+    error), masked entries exactly zero, ragged batches (tiles straddle samples)."""
+    from tianshou_amd import _C
+    torch.manual_seed(n)
+    w = torch.randn(64, 32, 4, 4, device=dev).contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(n, 9, 9, 64, device=dev)
+    z1 = torch.relu(torch.randn(n, 20, 20, 32, device=dev))
+    out = torch.empty(n, 20, 20, 32, device=dev)
+    _C.check(_C.lib().tsrl_dqn_conv2_dgrad(_C.ptr(gy), n, w.data_ptr(), *w.stride(),
+                                           _C.ptr(z1), _C.ptr(out), _C.stream_ptr(dev)), "dgrad")
+    g64 = gy.permute(0, 3, 1, 2).double()
+    ref = torch.nn.grad.conv2d_input((n, 32, 20, 20), w.double(), g64, stride=2)
+    mag = torch.nn.grad.conv2d_input((n, 32, 20, 20), w.double().abs(), g64.abs(), stride=2)
+    mask = (z1 > 0).permute(0, 3, 1, 2)
+    got = out.permute(0, 3, 1, 2).double()
+    assert bool((got[~mask] == 0).all())
+    err = (got - ref)[mask].abs()
+    assert bool((err <= 1e-6 * mag[mask] + 1e-12).all()), float((err / mag[mask]).max())
+    # unmasked form
+    _C.check(_C.lib().tsrl_dqn_conv2_dgrad(_C.ptr(gy), n, w.data_ptr(), *w.stride(), None,
+                                           _C.ptr(out), _C.stream_ptr(dev)), "dgrad")
+    err = (out.permute(0, 3, 1, 2).double() - ref).abs()
+    assert bool((err <= 1e-6 * mag + 1e-12).all())
+
+
 @pytest.mark.parametrize("n", [1, 37, 1024])
 def test_conv1_u8_kernel_vs_f64(dev, n):
     """tsrl_dqn_conv1_fwd (uint8 frames, bf16 byte operands x 3-plane split weights) against
@@ -211,6 +239,7 @@ def test_conv1_u8_kernel_vs_f64(dev, n):
     net = DQN(4, 84, 84, (6,), device=dev, features_only=True, output_dim=512,
               layer_init=layer_init).to(dev)
     conv = net._conv1_parts()[0]
+    assert net._conv1_parts()[1] is not None  # conv2 data gradient on the HIP path too
     with torch.no_grad():
         conv.bias.uniform_(-0.5, 0.5)
     x = torch.randint(0, 256, (n, 4, 84, 84), dtype=torch.uint8, device=dev)
@@ -230,8 +259,9 @@ def test_conv1_u8_kernel_vs_f64(dev, n):
 
 def test_dqn_fused_conv1_matches_miopen(dev):
     """The whole trunk with the uint8 first layer (forward: tsrl_dqn_conv1_fwd; backward:
-    ReLU mask + MIOpen weight/bias gradient over the scaled frames) against the same module
-    on MIOpen throughout: outputs and every parameter gradient."""
+    MIOpen weight/bias gradients, conv2's data gradient with conv1's ReLU mask from
+    tsrl_dqn_conv2_dgrad) against the same module on MIOpen throughout: outputs and every
+    parameter gradient."""
     from tianshou_amd.utils.net_atari import DQN, layer_init
     torch.manual_seed(1)
     a = DQN(4, 84, 84, (6,), device=dev, features_only=True, output_dim=512,

@@ -142,6 +142,111 @@ __global__ __launch_bounds__(256, 2) void dqn_conv1_fwd_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// Data gradient of the second convolution (Conv2d(32, 64, 4, stride 2): [n,32,20,20] ->
+// [n,64,9,9]) as a bf16x6 implicit GEMM, the ReLU mask of its input (the first layer's
+// output z1) fused into the epilogue: dX1 = (z1 > 0) * conv_transpose(gy2, W2).
+// Input pixel (ih, iw) receives the 2x2 taps kh = ih%2 + 2 th, kw = iw%2 + 2 tw from output
+// pixel (ih/2 - th, iw/2 - tw) when that lies inside the 9x9 map, so the pixels of one parity
+// class (ih%2, iw%2) share one sub-kernel: D[32 ci][32 px] += Wc[32 ci][16 k] . G[16 k][32 px]
+// with k = (tap, co), 4 taps x 64 channels = 256.  Workgroups of class cls = blockIdx.y stage
+// that class's split sub-kernel (3 planes, 48 KB, same swizzled rows as conv1); a lane's B
+// fragment is 8 consecutive channels of gy2 (NHWC, 32 contiguous bytes) split in registers.
+constexpr int C2_CI = 32, C2_CO = 64, C2_IN = 20, C2_OUT = 9;
+constexpr int C2_CPIX = (C2_IN / 2) * (C2_IN / 2);  // 100 input pixels per class per sample
+
+__global__ __launch_bounds__(256, 2) void dqn_conv2_dgrad_kernel(
+    const float* __restrict__ gy, int64_t n, const float* __restrict__ W, int64_t sw0,
+    int64_t sw1, int64_t sw2, int64_t sw3, const float* __restrict__ z1,
+    float* __restrict__ dx) {
+    __shared__ __attribute__((aligned(16))) char Ws[NPL][C2_CI * C1_ROWB];
+    const int t = threadIdx.x;
+    const int w = t >> 6, l = t & 63, h = l >> 5, c = l & 31;
+    const int cls = blockIdx.y, ph = cls >> 1, pw = cls & 1;
+    // sub-kernel of the class: element (ci, k), k = tap * 64 + co, tap = 2 th + tw
+    for (int i = t; i < C2_CI * 256; i += 256) {
+        const int ci = i >> 8, k = i & 255;
+        const int tap = k >> 6, co = k & 63;
+        const int kh = ph + 2 * (tap >> 1), kw = pw + 2 * (tap & 1);
+        const float v = W[co * sw0 + ci * sw1 + kh * sw2 + kw * sw3];
+        __bf16 a0, a1, a2;
+        x6::split1(v, a0, a1, a2);
+        const int o = c1_off(ci, k >> 3) + 2 * (k & 7);
+        *reinterpret_cast<__bf16*>(&Ws[0][o]) = a0;
+        *reinterpret_cast<__bf16*>(&Ws[1][o]) = a1;
+        *reinterpret_cast<__bf16*>(&Ws[2][o]) = a2;
+    }
+    __syncthreads();
+    const int64_t npix = n * C2_CPIX;
+    const int64_t ntile = (npix + 31) / 32;
+    for (int64_t tl = (int64_t)blockIdx.x * 4 + w; tl < ntile; tl += (int64_t)gridDim.x * 4) {
+        const int64_t p = tl * 32 + c;
+        const bool live = p < npix;
+        const int64_t q = live ? p : 0;
+        const int64_t smp = q / C2_CPIX;
+        const int r = (int)(q - smp * C2_CPIX);
+        const int ih = 2 * (r / 10) + ph, iw = 2 * (r % 10) + pw;
+        // the 4 taps' source rows of gy (clamped to a valid address, zeroed when outside)
+        const float* src[4];
+        bool ok[4];
+#pragma unroll
+        for (int tap = 0; tap < 4; ++tap) {
+            const int oh = (ih >> 1) - (tap >> 1), ow = (iw >> 1) - (tap & 1);
+            ok[tap] = live && oh >= 0 && oh < C2_OUT && ow >= 0 && ow < C2_OUT;
+            src[tap] = gy + ((smp * C2_OUT + (ok[tap] ? oh : 0)) * C2_OUT + (ok[tap] ? ow : 0)) *
+                                C2_CO + 8 * h;
+        }
+        float4 g[32];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const float4* s4 = reinterpret_cast<const float4*>(src[j >> 2] + 16 * (j & 3));
+            g[2 * j] = s4[0];
+            g[2 * j + 1] = s4[1];
+        }
+        f32x16 acc;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[e] = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const bool k_ = ok[j >> 2];
+            bf16x8 b[NPL];
+            const float4 u = g[2 * j], v = g[2 * j + 1];
+            const float f[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                __bf16 a0, a1, a2;
+                x6::split1(k_ ? f[e] : 0.0f, a0, a1, a2);
+                b[0][e] = a0;
+                b[1][e] = a1;
+                b[2][e] = a2;
+            }
+            const int ao = c1_off(c, 2 * j + h);
+            bf16x8 a[NPL];
+#pragma unroll
+            for (int pl = 0; pl < NPL; ++pl) a[pl] = *reinterpret_cast<const bf16x8*>(&Ws[pl][ao]);
+            acc = x6::mfma6(a, b, acc);
+        }
+        if (live) {
+            const int64_t o = ((smp * C2_IN + ih) * C2_IN + iw) * C2_CI;
+            float4* d = reinterpret_cast<float4*>(dx + o);
+            const float4* zm = reinterpret_cast<const float4*>(z1 + o);
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq) {
+                float4 v = make_float4(acc[4 * qq], acc[4 * qq + 1], acc[4 * qq + 2],
+                                       acc[4 * qq + 3]);
+                if (z1) {
+                    const float4 m = zm[2 * qq + h];
+                    v.x = m.x > 0.0f ? v.x : 0.0f;
+                    v.y = m.y > 0.0f ? v.y : 0.0f;
+                    v.z = m.z > 0.0f ? v.z : 0.0f;
+                    v.w = m.w > 0.0f ? v.w : 0.0f;
+                }
+                d[2 * qq + h] = v;
+            }
+        }
+    }
+}
+
 }  // namespace
 }  // namespace tsrl
 
@@ -166,5 +271,25 @@ extern "C" int tsrl_dqn_conv1_fwd(const uint8_t* frames, int64_t n, const float*
                        as_stream(stream), frames, npix, w, sw0, sw1, sw2, sw3, bias, scale, relu,
                        out);
     TSRL_LAUNCH_CHECK("tsrl_dqn_conv1_fwd");
+    return 0;
+}
+
+extern "C" int tsrl_dqn_conv2_dgrad(const float* gy, int64_t n, const float* w, int64_t sw0,
+                                    int64_t sw1, int64_t sw2, int64_t sw3, const float* z1,
+                                    float* dx, void* stream) {
+    TSRL_CHECK_ARG(n >= 0, "tsrl_dqn_conv2_dgrad: n < 0");
+    if (n == 0) return 0;
+    TSRL_CHECK_ARG(gy && w && dx, "tsrl_dqn_conv2_dgrad: null pointer");
+    TSRL_CHECK_ARG(aligned16(gy) && aligned16(dx) && (!z1 || aligned16(z1)),
+                   "tsrl_dqn_conv2_dgrad: gy / dx / z1 must be 16-byte aligned");
+    const int64_t ntile = (n * C2_CPIX + 31) / 32;
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) == hipSuccess)
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    // 4 parity classes x gx workgroups, 2 per CU in total
+    const int64_t gx = std::max<int64_t>(1, std::min<int64_t>((ntile + 3) / 4, (int64_t)ncu / 2));
+    hipLaunchKernelGGL(dqn_conv2_dgrad_kernel, dim3((unsigned)gx, 4), dim3(256), 0,
+                       as_stream(stream), gy, n, w, sw0, sw1, sw2, sw3, z1, dx);
+    TSRL_LAUNCH_CHECK("tsrl_dqn_conv2_dgrad");
     return 0;
 }

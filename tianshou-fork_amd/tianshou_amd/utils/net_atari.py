@@ -78,6 +78,49 @@ class _Conv1U8(torch.autograd.Function):
         return None, gw, gb, None, None, None
 
 
+def _nhwc(t: torch.Tensor) -> torch.Tensor:
+    """The [n, h, w, c] contiguous tensor behind an [n, c, h, w] channels_last tensor (a copy
+    only when it is not channels_last)."""
+    return t.permute(0, 2, 3, 1).contiguous()
+
+
+class _Conv12U8(torch.autograd.Function):
+    """conv1 + ReLU + conv2 + ReLU from uint8 frames.  Forward: tsrl_dqn_conv1_fwd, MIOpen
+    conv2, ReLU.  Backward: ReLU mask of conv2, MIOpen weight/bias gradient of conv2, the
+    conv2 data gradient with conv1's ReLU mask fused (tsrl_dqn_conv2_dgrad), then conv1's
+    weight/bias gradient (MIOpen over the scaled f32 frames)."""
+
+    @staticmethod
+    def forward(ctx, obs, w1, b1, w2, b2, conv1, conv2, lut, scale):
+        z1 = conv1_u8(obs, conv1, scale)
+        z2 = torch.relu_(torch.nn.functional.conv2d(z1, w2, b2, conv2.stride))
+        ctx.save_for_backward(obs, w1, w2, z1, z2)
+        ctx.lut = lut
+        ctx.bias = (b1 is not None, b2 is not None)
+        return z2
+
+    @staticmethod
+    def backward(ctx, gz2):
+        obs, w1, w2, z1, z2 = ctx.saved_tensors
+        n = obs.shape[0]
+        gy2 = torch.ops.aten.threshold_backward(gz2, z2, 0.0)
+        gy2 = gy2.contiguous(memory_format=torch.channels_last)
+        _, gw2, gb2 = torch.ops.aten.convolution_backward(
+            gy2, z1, w2, [w2.shape[0]] if ctx.bias[1] else None, (2, 2), (0, 0), (1, 1), False,
+            (0, 0), 1, (False, True, ctx.bias[1]))
+        gy1 = torch.empty((n, 20, 20, 32), dtype=torch.float32, device=obs.device)
+        g2 = _nhwc(gy2)
+        _C.check(_C.lib().tsrl_dqn_conv2_dgrad(_C.ptr(g2), n, w2.data_ptr(), *w2.stride(),
+                                               _C.ptr(_nhwc(z1)), _C.ptr(gy1),
+                                               _C.stream_ptr(obs.device)),
+                 "tsrl_dqn_conv2_dgrad")
+        x = frames_to_f32_nhwc(obs, ctx.lut)
+        _, gw1, gb1 = torch.ops.aten.convolution_backward(
+            gy1.permute(0, 3, 1, 2), x, w1, [w1.shape[0]] if ctx.bias[0] else None, (4, 4),
+            (0, 0), (1, 1), False, (0, 0), 1, (False, True, ctx.bias[0]))
+        return None, gw1, gb1, gw2, gb2, None, None, None, None
+
+
 def layer_init(layer: nn.Module, std: float = np.sqrt(2), bias_const: float = 0.0):
     torch.nn.init.orthogonal_(layer.weight, std)
     torch.nn.init.constant_(layer.bias, bias_const)
@@ -132,8 +175,9 @@ class DQN(nn.Module):
         return lut[1]
 
     def _conv1_parts(self):
-        """(conv1, rest of the conv stack, outer layers after it) when the trunk starts with
-        Conv2d(4, 32, 8, stride 4) + ReLU over 84x84 frames, else None."""
+        """(conv1, conv2 or None, rest of the conv stack, outer layers after it) when the
+        trunk starts with Conv2d(4, 32, 8, stride 4) + ReLU over 84x84 frames (conv2 when it
+        is followed by the Nature-DQN Conv2d(32, 64, 4, stride 2) + ReLU), else None."""
         if self._conv1_split is None:
             outer = None
             seq = self.net
@@ -145,8 +189,14 @@ class DQN(nn.Module):
                 conv.kernel_size == (8, 8) and conv.stride == (4, 4) and \
                 conv.padding == (0, 0) and conv.dilation == (1, 1) and conv.groups == 1 and \
                 conv.padding_mode == "zeros"
-            self._conv1_split = (conv, seq[2:], outer[1:] if outer is not None else None) \
-                if ok else False
+            conv2 = seq[2] if ok and len(seq) > 3 else None
+            ok2 = isinstance(conv2, nn.Conv2d) and isinstance(seq[3], nn.ReLU) and \
+                conv2.in_channels == 32 and conv2.out_channels == 64 and \
+                conv2.kernel_size == (4, 4) and conv2.stride == (2, 2) and \
+                conv2.padding == (0, 0) and conv2.dilation == (1, 1) and \
+                conv2.groups == 1 and conv2.padding_mode == "zeros"
+            self._conv1_split = (conv, conv2 if ok2 else None, seq[4:] if ok2 else seq[2:],
+                                 outer[1:] if outer is not None else None) if ok else False
         return self._conv1_split or None
 
     def forward(self, obs, state: Any = None, info: Dict[str, Any] = {}):
@@ -155,10 +205,14 @@ class DQN(nn.Module):
         if parts is not None and obs.dim() == 4 and obs.dtype == torch.uint8 and obs.is_cuda \
                 and tuple(obs.shape[1:]) == (4, 84, 84) and self.scale and \
                 obs.data_ptr() % 4 == 0:
-            conv, rest, outer = parts
+            conv, conv2, rest, outer = parts
             lut = self._scale_lut(obs.device)
-            h = _Conv1U8.apply(obs.contiguous(), conv.weight, conv.bias, conv, lut,
-                               float(self.scale))
+            if conv2 is not None:
+                h = _Conv12U8.apply(obs.contiguous(), conv.weight, conv.bias, conv2.weight,
+                                    conv2.bias, conv, conv2, lut, float(self.scale))
+            else:
+                h = _Conv1U8.apply(obs.contiguous(), conv.weight, conv.bias, conv, lut,
+                                   float(self.scale))
             h = rest(h)
             return (outer(h) if outer is not None else h), state
         if self.channels_last and obs.dim() == 4 and obs.dtype == torch.uint8 and \

@@ -76,6 +76,24 @@ def main():
     flop = 2.0 * N * 400 * 32 * 256
     print(f"conv1 from u8: tsrl_dqn_conv1_fwd {t_fused:7.3f} ms ({flop / t_fused / 1e9:6.1f} "
           f"TFLOP/s f32-equivalent) vs frames+MIOpen+ReLU {t_lib:7.3f} ms", flush=True)
+    from tianshou_amd import _C
+    w2 = torch.randn(64, 32, 4, 4, device=dev).contiguous(memory_format=cl)
+    gy2 = torch.randn(N, 9, 9, 64, device=dev)
+    z1 = torch.relu(torch.randn(N, 20, 20, 32, device=dev))
+    dx = torch.empty(N, 20, 20, 32, device=dev)
+    s_ = _C.stream_ptr(dev)
+    t_dg = timed(lambda: _C.lib().tsrl_dqn_conv2_dgrad(_C.ptr(gy2), N, w2.data_ptr(),
+                                                        *w2.stride(), _C.ptr(z1), _C.ptr(dx),
+                                                        s_), a.iters)
+    gy2c = gy2.permute(0, 3, 1, 2)
+    z1c = z1.permute(0, 3, 1, 2)
+    t_lib = timed(lambda: torch.ops.aten.threshold_backward(torch.ops.aten.convolution_backward(
+        gy2c, z1c, w2, None, (2, 2), (0, 0), (1, 1), False, (0, 0), 1,
+        (True, False, False))[0], z1c, 0.0), a.iters)
+    flop = 2.0 * N * 81 * 64 * 32 * 16
+    print(f"conv2 data gradient + conv1 ReLU mask: tsrl_dqn_conv2_dgrad {t_dg:7.3f} ms "
+          f"({flop / t_dg / 1e9:6.1f} TFLOP/s f32-equivalent) vs MIOpen + threshold_backward "
+          f"{t_lib:7.3f} ms", flush=True)
     for fin, fout in ((3136, 512), (512, 7)):
         x = torch.randn(N, fin, device=dev)
         lin = torch.nn.Linear(fin, fout).to(dev)
