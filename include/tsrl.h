@@ -213,6 +213,46 @@ typedef struct tsrl_add_args {
     int64_t obs_next_src_pitch;
 } tsrl_add_args;
 int tsrl_buffer_add(const tsrl_add_args* a, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * One vector step of Collector.collect (collector.py:258-361) in ONE launch, for a
+ * SyntheticVectorEnv with Box observations under VectorEnvNormObs (venv_wrappers.py:77-99)
+ * and the Gaussian MuJoCo actor (utils/models.py:34-97, pg.py:133-171).  Replaces the
+ * launch sequence tsrl_gauss_policy_act_rng -> tsrl_synth_box_step_reset -> tsrl_rms_merge2
+ * -> tsrl_buffer_add of one step, rotated by one: the launch of step i first runs the buffer
+ * add of step i-1 (`add`; add.k == 0: none), then the actor on the new live obs, the env
+ * step + auto-reset, and both obs_rms updates (folded by the last workgroups to finish, no
+ * grid barrier).  The caller issues the add of the LAST step as tsrl_buffer_add(&add).
+ *   w1p: the actor's first-layer weight packed by tsrl_collect_pack_w1 (once per update);
+ *   workspace: tsrl_collect_workspace_bytes(k, dim) bytes, ZEROED once before first use
+ *     (its tickets re-arm themselves);
+ *   totals (data parallel, nullable): the step/reset moments are written there in
+ *     tsrl_rms_sum_partials2's [4*dim+2] layout instead of merged; the caller all-reduces them
+ *     and runs tsrl_rms_merge2(nblk = 1) before the next step.
+ * ------------------------------------------------------------------------------- */
+typedef struct tsrl_collect_args {
+    tsrl_add_args add;       /* pending add of the previous step (add.k == 0: none) */
+    int64_t k;               /* envs (rows) */
+    int64_t dim;             /* observation columns (multiple of 4, <= 512) */
+    float* cur;              /* [k, dim] live normalised observations */
+    /* actor */
+    const float* w1p; const float* b1; const float* w2; const float* b2;
+    const float* w3; const float* b3; const float* log_std; int64_t act_dim;
+    uint64_t act_seed; const int64_t* rng_ctr; int64_t* rng_next; int sample;
+    int bound_method; const float* low; const float* high;
+    float* act; float* act_remap;   /* [k, act_dim] */
+    /* synthetic env (tsrl_synth_box_step_reset's operands) */
+    uint64_t env_seed; int64_t ep_len; int64_t* ep_j; int64_t* ep_t;
+    float* raw; float* reset_raw; double* rew; uint8_t* term; uint8_t* trunc; uint8_t* done;
+    /* obs RunningMeanStd */
+    void* workspace;
+    float* mean; float* var; float* snap_mean; float* snap_var; double* count;
+    double* totals;
+} tsrl_collect_args;
+int64_t tsrl_collect_pack_floats(int64_t dim);
+int tsrl_collect_pack_w1(const float* W, int64_t dim, float* packed, void* stream);
+int64_t tsrl_collect_workspace_bytes(int64_t k, int64_t dim);
+int tsrl_collect_box_step(const tsrl_collect_args* a, void* stream);
 /* *rel_dev = (*rel_dev + 1) % ring_size (device-side ring cursor for graph-captured steps). */
 int tsrl_ring_advance(int64_t* rel_dev, int64_t ring_size, void* stream);
 

@@ -31,15 +31,16 @@ def test_library_exports_every_header_symbol():
 
 
 def test_ctypes_struct_layout_matches_header(tmp_path):
-    """AddArgs / PPOParams mirror the C structs (sizes via a compiled probe)."""
+    """AddArgs / PPOParams / CollectArgs mirror the C structs (sizes via a compiled probe)."""
     import ctypes
     import subprocess
     from tianshou_amd import _C
     src = tmp_path / "probe.c"
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "tsrl.h"\n'
-                   'int main(){printf("%zu %zu %zu %zu\\n", sizeof(tsrl_add_args), '
+                   'int main(){printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(tsrl_add_args), '
                    'sizeof(tsrl_ppo_params), offsetof(tsrl_add_args, stat_idx), '
-                   'offsetof(tsrl_ppo_params, norm_adv));}')
+                   'offsetof(tsrl_ppo_params, norm_adv), sizeof(tsrl_collect_args), '
+                   'offsetof(tsrl_collect_args, sample), offsetof(tsrl_collect_args, totals));}')
     exe = tmp_path / "probe"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)],
                    check=True)
@@ -48,6 +49,9 @@ def test_ctypes_struct_layout_matches_header(tmp_path):
     assert int(out[1]) == ctypes.sizeof(_C.PPOParams)
     assert int(out[2]) == _C.AddArgs.stat_idx.offset
     assert int(out[3]) == _C.PPOParams.norm_adv.offset
+    assert int(out[4]) == ctypes.sizeof(_C.CollectArgs)
+    assert int(out[5]) == _C.CollectArgs.sample.offset
+    assert int(out[6]) == _C.CollectArgs.totals.offset
 
 
 @pytest.mark.parametrize("name", ["manager", "ragged"])

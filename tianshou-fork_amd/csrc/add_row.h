@@ -8,19 +8,20 @@
 
 namespace tsrl {
 
-__device__ __forceinline__ void copy_row(const void* src, void* dst, int64_t bytes, int lane) {
+__device__ __forceinline__ void copy_row(const void* src, void* dst, int64_t bytes, int lane,
+                                         int nl = kWave) {
     const char* s = reinterpret_cast<const char*>(src);
     char* d = reinterpret_cast<char*>(dst);
     if ((bytes & 15) == 0 && aligned16(s) && aligned16(d)) {
         const int4* s4 = reinterpret_cast<const int4*>(s);
         int4* d4 = reinterpret_cast<int4*>(d);
-        for (int64_t i = lane; i < bytes / 16; i += kWave) d4[i] = s4[i];
+        for (int64_t i = lane; i < bytes / 16; i += nl) d4[i] = s4[i];
     } else if ((bytes & 3) == 0 && (((uintptr_t)s | (uintptr_t)d) & 3) == 0) {
         const int* s4 = reinterpret_cast<const int*>(s);
         int* d4 = reinterpret_cast<int*>(d);
-        for (int64_t i = lane; i < bytes / 4; i += kWave) d4[i] = s4[i];
+        for (int64_t i = lane; i < bytes / 4; i += nl) d4[i] = s4[i];
     } else {
-        for (int64_t i = lane; i < bytes; i += kWave) d[i] = s[i];
+        for (int64_t i = lane; i < bytes; i += nl) d[i] = s[i];
     }
 }
 
@@ -30,9 +31,12 @@ __device__ __forceinline__ float norm1(float x, float m, float v, float eps, flo
     return y;
 }
 
-// Row r of one add (urel = the uniform ring position of this step).
+// Row r of one add (urel = the uniform ring position of this step) by nl lanes (lane < nl).
+// lx (nullable): the new live obs row is also written to lx[col * lxp] (the fused collect step
+// keeps it in LDS for the next policy step).
 __device__ __forceinline__ void add_row(const tsrl_add_args& a, int64_t r, int lane,
-                                        int64_t urel) {
+                                        int64_t urel, float* lx = nullptr, int lxp = 0,
+                                        int nl = kWave) {
     const int64_t b = a.ids ? a.ids[r] : r;
     const int64_t ptr = a.ptr ? a.ptr[r] : a.offset[b] + urel;
 
@@ -40,13 +44,13 @@ __device__ __forceinline__ void add_row(const tsrl_add_args& a, int64_t r, int l
     const int64_t next_pitch = a.obs_next_src_pitch ? a.obs_next_src_pitch : a.obs_row_bytes;
     if (a.obs_src && a.obs_dst)
         copy_row((const char*)a.obs_src + r * obs_pitch,
-                 (char*)a.obs_dst + ptr * a.obs_row_bytes, a.obs_row_bytes, lane);
+                 (char*)a.obs_dst + ptr * a.obs_row_bytes, a.obs_row_bytes, lane, nl);
     if (a.act_src && a.act_dst)
         copy_row((const char*)a.act_src + r * a.act_row_bytes,
-                 (char*)a.act_dst + ptr * a.act_row_bytes, a.act_row_bytes, lane);
+                 (char*)a.act_dst + ptr * a.act_row_bytes, a.act_row_bytes, lane, nl);
     if (a.obs_next_src_raw && a.obs_next_dst_raw)
         copy_row((const char*)a.obs_next_src_raw + r * next_pitch,
-                 (char*)a.obs_next_dst_raw + ptr * a.obs_row_bytes, a.obs_row_bytes, lane);
+                 (char*)a.obs_next_dst_raw + ptr * a.obs_row_bytes, a.obs_row_bytes, lane, nl);
     if (a.obs_next_src && (a.obs_next_dst || a.cur_obs)) {
         const float* src = a.obs_next_src + r * a.obs_dim;
         float* dst = a.obs_next_dst ? a.obs_next_dst + ptr * a.obs_dim : nullptr;
@@ -63,7 +67,7 @@ __device__ __forceinline__ void add_row(const tsrl_add_args& a, int64_t r, int l
                                                      aligned16(a.reset_var)))));
         if (v4) {
             const int64_t nq = a.obs_dim >> 2;
-            for (int64_t q = lane; q < nq; q += kWave) {
+            for (int64_t q = lane; q < nq; q += nl) {
                 float4 x = reinterpret_cast<const float4*>(src)[q];
                 if (nrm) {
                     const float4 m = reinterpret_cast<const float4*>(a.norm_mean)[q];
@@ -87,10 +91,16 @@ __device__ __forceinline__ void add_row(const tsrl_add_args& a, int64_t r, int l
                         }
                     }
                     reinterpret_cast<float4*>(cur)[q] = x;
+                    if (lx) {
+                        lx[(4 * q) * lxp] = x.x;
+                        lx[(4 * q + 1) * lxp] = x.y;
+                        lx[(4 * q + 2) * lxp] = x.z;
+                        lx[(4 * q + 3) * lxp] = x.w;
+                    }
                 }
             }
         } else
-        for (int64_t d = lane; d < a.obs_dim; d += kWave) {
+        for (int64_t d = lane; d < a.obs_dim; d += nl) {
             float x = src[d];
             if (nrm) x = norm1(x, a.norm_mean[d], a.norm_var[d], a.norm_eps, a.norm_clip);
             if (dst) dst[d] = x;
@@ -101,6 +111,7 @@ __device__ __forceinline__ void add_row(const tsrl_add_args& a, int64_t r, int l
                         x = norm1(x, a.reset_mean[d], a.reset_var[d], a.norm_eps, a.norm_clip);
                 }
                 cur[d] = x;
+                if (lx) lx[d * lxp] = x;
             }
         }
     }

@@ -4,29 +4,19 @@
 // kernel steps every env of the shard and, while the raw observation rows are still in
 // registers, accumulates the per-column (sum, sumsq) partials VectorEnvNormObs needs for its
 // RunningMeanStd update (venv_wrappers.py:93-99), so the obs rows are read once.
-#include "tsrl_common.h"
+#include "synth.h"
 
 namespace tsrl {
 namespace {
 
+using synth::GOLD;
+using synth::REW_SALT;
+using synth::env_key;
+using synth::box_val;
+using synth::RowState;
+
 constexpr int TPB = 256;
 constexpr int ROWS = 16;  // env rows per workgroup
-constexpr uint64_t GOLD = 0x9E3779B97F4A7C15ull;
-constexpr uint64_t REW_SALT = 0xD1B54A32D192ED03ull;
-
-__device__ __forceinline__ uint64_t env_key(uint64_t s_seed, uint64_t e, int64_t j, int64_t t) {
-    return sm64(sm64(sm64(s_seed ^ e) ^ (uint64_t)j) ^ (uint64_t)t);
-}
-
-__device__ __forceinline__ float box_val(uint64_t k, int64_t d) {
-    const uint64_t h = sm64(k + (uint64_t)d * GOLD);
-    return (float)(h >> 40) * 0x1p-23f - 1.0f;
-}
-
-struct RowState {
-    uint64_t key;
-    int active;
-};
 
 // Rows [r0, r0+ROWS): obs rows + column partials over active rows.
 __device__ void box_rows(const RowState* rs, int64_t r0, int64_t k, int64_t dim, float* obs,

@@ -10,7 +10,7 @@
 // every partial folded in fixed order through LDS.  The first-layer weight is pre-packed
 // once per collect into the per-lane fragment order so every weight load is a contiguous
 // 1 KB wave access.
-#include "tsrl_common.h"
+#include "noise.h"
 
 namespace tsrl {
 namespace {
@@ -53,20 +53,6 @@ struct ActParams {
     int A, bound, scale, sample;
     uint64_t seed;  // rng mode (eps == NULL, sample): counter-based normals
 };
-
-// Two standard normals for (seed, step, row, pair): one splitmix64 counter hash gives two
-// 24-bit uniforms -> Box-Muller (cos and sin branches).  Replaces torch.randn_like(mu) of the
-// torch path (a separate launch).
-__device__ __forceinline__ float2 counter_normal2(uint64_t seed, int64_t step, int64_t row,
-                                                 int pair) {
-    const uint64_t h = sm64(sm64(seed ^ (uint64_t)step) ^ (((uint64_t)row << 5) | (uint64_t)pair));
-    const float u1 = ((float)(h >> 40) + 1.0f) * 0x1p-24f;                // (0, 1]
-    const float u2 = (float)((h >> 16) & 0xFFFFFFu) * 0x1p-24f;          // [0, 1)
-    const float r = sqrtf(-2.0f * logf(u1));
-    float sn, cs;
-    sincospif(2.0f * u2, &sn, &cs);
-    return make_float2(r * cs, r * sn);
-}
 
 constexpr int ANW = 8;  // waves per workgroup: the first layer's K is split 8 ways
 

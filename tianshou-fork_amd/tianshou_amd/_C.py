@@ -40,6 +40,21 @@ class AddArgs(ctypes.Structure):
     ]
 
 
+class CollectArgs(ctypes.Structure):
+    """Mirror of ``tsrl_collect_args`` (field order must match include/tsrl.h)."""
+    _fields_ = [
+        ("add", AddArgs), ("k", _i64), ("dim", _i64), ("cur", _p),
+        ("w1p", _p), ("b1", _p), ("w2", _p), ("b2", _p), ("w3", _p), ("b3", _p),
+        ("log_std", _p), ("act_dim", _i64), ("act_seed", _u64), ("rng_ctr", _p),
+        ("rng_next", _p), ("sample", _i32), ("bound_method", _i32), ("low", _p), ("high", _p),
+        ("act", _p), ("act_remap", _p),
+        ("env_seed", _u64), ("ep_len", _i64), ("ep_j", _p), ("ep_t", _p),
+        ("raw", _p), ("reset_raw", _p), ("rew", _p), ("term", _p), ("trunc", _p), ("done", _p),
+        ("workspace", _p), ("mean", _p), ("var", _p), ("snap_mean", _p), ("snap_var", _p),
+        ("count", _p), ("totals", _p),
+    ]
+
+
 class PPOParams(ctypes.Structure):
     """Mirror of ``tsrl_ppo_params``."""
     _fields_ = [
@@ -93,6 +108,10 @@ _SIGS = {
     "tsrl_rms_norm_rows": ([_p, _p, _i64, _i64, _p, _p, _f, _f, _p, _p], ctypes.c_int),
     "tsrl_buffer_add": ([ctypes.POINTER(AddArgs), _p], ctypes.c_int),
     "tsrl_ring_advance": ([_p, _i64, _p], ctypes.c_int),
+    "tsrl_collect_pack_floats": ([_i64], _i64),
+    "tsrl_collect_pack_w1": ([_p, _i64, _p, _p], ctypes.c_int),
+    "tsrl_collect_workspace_bytes": ([_i64, _i64], _i64),
+    "tsrl_collect_box_step": ([ctypes.POINTER(CollectArgs), _p], ctypes.c_int),
     "tsrl_gather_rows": ([_p, _i64, _p, _i64, _p, _p], ctypes.c_int),
     "tsrl_np_shuffle_draws": ([_p, _p, _i64, _p], ctypes.c_int),
     "tsrl_shuffle_apply_workspace_bytes": ([_i64], _i64),

@@ -371,8 +371,9 @@ class VectorReplayBuffer:
                     rel_dev=None, obs=None, act=None, obs_next=None, obs_next_raw=None,
                     cur_obs=None, norm=None, rew=None, term=None, trunc=None, out=None,
                     stats=True, norm_snapshot=False, reset_src=None, reset_mask=None,
-                    reset_norm=None, rel_next=None) -> None:
-        """One tsrl_buffer_add launch (see include/tsrl.h)."""
+                    reset_norm=None, rel_next=None, launch: bool = True):
+        """One tsrl_buffer_add launch (see include/tsrl.h); returns its argument struct
+        (launch=False: only build it, e.g. as the pending add of the fused collect step)."""
         m = self._meta
         d = self._dev
         a = _C.AddArgs()
@@ -435,7 +436,9 @@ class VectorReplayBuffer:
             a.stat_rew = _C.ptr(d["stat_rew"])
             a.stat_len = _C.ptr(d["stat_len"])
             a.stat_idx = _C.ptr(d["stat_idx"])
-        _C.check(_C.lib().tsrl_buffer_add(a, _C.stream_ptr(self.device)), "tsrl_buffer_add")
+        if launch:
+            _C.check(_C.lib().tsrl_buffer_add(a, _C.stream_ptr(self.device)), "tsrl_buffer_add")
+        return a
 
     def _frame_src(self, x: torch.Tensor, row_bytes: int):
         """(source pointer, row pitch) for a source of stored-row payloads: a plain

@@ -61,6 +61,12 @@ class Collector:
         # run the policy step as the fused HIP kernel when the policy offers one
         self.use_fused_act = True
         self._fused_act_on = False
+        # one launch per vector step (csrc/collect.hip) when env, normalisation and actor
+        # allow it; _pending = the buffer add of the previous step, run by the next step's
+        # launch or by _flush()
+        self.use_fused_step = True
+        self._step_on = False
+        self._pending = None
         from tianshou_amd.dist import default_dp
         self.dp = default_dp()
         if sync_obs_rms and self.dp.active and self._norm is not None:
@@ -244,11 +250,78 @@ class Collector:
             return (), torch.int64
         return tuple(act_space.shape), torch.float32
 
+    def _fused_step_ok(self, n_step, kk) -> bool:
+        """The one-launch step (tsrl_collect_box_step) applies: n_step collects over every env
+        of a SyntheticVectorEnv with Box rows under an updating VectorEnvNormObs, and the
+        fused Gaussian act."""
+        from tianshou_amd.env.synthetic import SyntheticVectorEnv
+        b, norm = self._base, self._norm
+        if not (self.use_fused_step and self._fused_act_on and n_step is not None
+                and kk == self.env_num == self.buffer.buffer_num):
+            return False
+        if not isinstance(b, SyntheticVectorEnv) or b.u8 or norm is None or \
+                not norm.update_obs_rms:
+            return False
+        D = b.obs_numel
+        if D % 4 or D > 512 or self._act_spec()[1] != torch.float32:
+            return False
+        sc = self._scratch["step_ctr"]
+        return bool(self.policy.fused_collect_fill(_C.CollectArgs(), (sc[0, 1:2], sc[1, 1:2])))
+
+    def _fused_box_step(self, cur, kk, add_kw) -> None:
+        """One vector step as one launch: the pending add of the previous step, policy act,
+        env step + auto-reset, both obs_rms updates (csrc/collect.hip).  This step's add is
+        left pending for the next launch or _flush()."""
+        s, b, buf = self._scratch, self._base, self.buffer
+        rms = self._norm.obs_rms
+        rms.ensure_snapshot()
+        ws = s.get("collect_ws")
+        if ws is None:
+            nbytes = int(_C.lib().tsrl_collect_workspace_bytes(kk, b.obs_numel))
+            ws = s["collect_ws"] = torch.zeros(nbytes, dtype=torch.uint8, device=b.device)
+        p, sc = self._parity, s["step_ctr"]
+        c = _C.CollectArgs()
+        if self._pending is not None:
+            c.add = self._pending
+        c.k, c.dim, c.cur = kk, b.obs_numel, _C.ptr(cur)
+        assert self.policy.fused_collect_fill(c, (sc[p, 1:2], sc[1 - p, 1:2]))
+        c.act, c.act_remap = _C.ptr(s["act"]), _C.ptr(s["act_remap"])
+        c.env_seed, c.ep_len = b.seed_, b.ep_len
+        c.ep_j, c.ep_t = _C.ptr(b.ep_j), _C.ptr(b.ep_t)
+        c.raw, c.reset_raw = _C.ptr(s["raw"]), _C.ptr(s["reset_raw"])
+        c.rew, c.term, c.trunc, c.done = (_C.ptr(s[x]) for x in ("rew", "term", "trunc", "done"))
+        c.workspace = _C.ptr(ws)
+        c.mean, c.var, c.count = _C.ptr(rms.mean_t), _C.ptr(rms.var_t), _C.ptr(rms.count_t)
+        c.snap_mean, c.snap_var = _C.ptr(rms.snap_mean_t), _C.ptr(rms.snap_var_t)
+        dp = rms.dp is not None and rms.dp.active
+        if dp:
+            c.totals = _C.ptr(rms.payload())
+        _C.check(_C.lib().tsrl_collect_box_step(c, _C.stream_ptr(b.device)),
+                 "tsrl_collect_box_step")
+        if dp:
+            rms.merge_payload(kk)
+        self._pending = buf._launch_add(
+            ids=None, k=kk, obs=cur, act=s["act"], obs_next=s["raw"], cur_obs=cur, norm=rms,
+            norm_snapshot=True, reset_src=s["reset_raw"], reset_mask=s["done"], reset_norm=rms,
+            rew=s["rew"], term=s["term"], trunc=s["trunc"], launch=False, **add_kw)
+        self._parity ^= 1
+
+    def _flush(self) -> None:
+        """Run the pending buffer add of the last fused step (tsrl_buffer_add)."""
+        if self._pending is not None:
+            a, self._pending = self._pending, None
+            _C.check(_C.lib().tsrl_buffer_add(a, _C.stream_ptr(self.buffer.device)),
+                     "tsrl_buffer_add")
+
     def _device_step(self, cur, kk, ids_t, random, no_grad, add_kw) -> None:
         """All device work of one vector step: policy -> map_action -> env kernel (+ column
         partials) -> obs_rms merge -> buffer add (+ fused obs_next normalisation) -> masked
         reset (+ merge + normalisation).  No host synchronisation, so the sequence can be
         captured in a HIP graph."""
+        if self._step_on and not random and ids_t is None and kk == self.env_num:
+            self._fused_box_step(cur, kk, add_kw)
+            return
+        self._flush()
         s, b, buf = self._scratch, self._base, self.buffer
         act_shape, act_dtype = self._act_spec()
         if self._fused_act_on and not random:
@@ -314,7 +387,7 @@ class Collector:
             ptrs += [r.mean_t.data_ptr(), r.var_t.data_ptr(), r.count_t.data_ptr(),
                      self._norm.update_obs_rms]
         return (G, self.policy.training, self.exploration_noise, self._fused_act_on,
-                tuple(ptrs))
+                self._step_on, tuple(ptrs))
 
     def _replay_steps(self, no_grad, n_steps: int, written: list) -> int:
         """Run up to n_steps uniform steps as replays of captured HIP graphs of G steps
@@ -326,6 +399,7 @@ class Collector:
         if n_steps < 2:
             return 0
         buf = self.buffer
+        self._flush()
         sc = self._scratch["step_ctr"]
         if self._parity:  # the live counters sit in slot 1: the graph starts from slot 0
             sc[0].copy_(sc[1])
@@ -346,6 +420,7 @@ class Collector:
                         self._device_step(self._scratch["cur"], self.env_num, None, False,
                                           no_grad, dict(rel_dev=sc[i % 2, 0:1],
                                                         rel_next=sc[(i + 1) % 2, 0:1]))
+                    self._flush()
                 self._graphs[G] = graph = (key, g)
                 self._parity = 0
             graph[1].replay()
@@ -360,6 +435,7 @@ class Collector:
         prep = getattr(self.policy, "prepare_fused_act", None)
         self._fused_act_on = bool(not random and not self._noise_active() and
                                   self.use_fused_act and prep is not None and prep())
+        self._flush()
         s, b, buf = self._scratch, self._base, self.buffer
         N = self.env_num
         act_shape, act_dtype = self._act_spec()
@@ -367,6 +443,7 @@ class Collector:
         dev = buf.device
         # rows r < kk of the scratch arrays belong to env ready[r] (ready None: env r)
         kk = N if n_step is not None else min(N, n_episode)
+        self._step_on = self._fused_step_ok(n_step, kk)
         ready = None
         ids_t = None
         cur = s["cur"] if kk == N else s["cur"][:kk]
@@ -417,6 +494,7 @@ class Collector:
                     break
             elif step_count >= n_step:
                 break
+        self._flush()
         # one read-back of the episode statistics, in the reference's (step, env) order
         d = buf._dev
         if n_episode:

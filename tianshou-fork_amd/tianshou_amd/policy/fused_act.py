@@ -45,6 +45,7 @@ class FusedGaussAct:
         self.L = layers
         self.D, self.A = layers["D"], layers["A"]
         self.packed = None
+        self.packed_c = None  # layer-1 layout of the fused collect step (tsrl_collect_pack_w1)
         self._eps = None
         # "device": noise drawn in-kernel from a counter hash seeded from torch's CPU
         # generator at each pack() (reproducible under torch.manual_seed); "torch": noise
@@ -64,6 +65,13 @@ class FusedGaussAct:
             self.packed = torch.empty(n, dtype=torch.float32, device=w.device)
         _C.check(lib.tsrl_policy_pack_l1(_C.ptr(w.detach()), self.D, _C.ptr(self.packed),
                                          _C.stream_ptr(w.device)), "tsrl_policy_pack_l1")
+        if self.D <= 512:
+            nc = int(lib.tsrl_collect_pack_floats(self.D))
+            if self.packed_c is None or self.packed_c.numel() != nc or \
+                    self.packed_c.device != w.device:
+                self.packed_c = torch.empty(nc, dtype=torch.float32, device=w.device)
+            _C.check(lib.tsrl_collect_pack_w1(_C.ptr(w.detach()), self.D, _C.ptr(self.packed_c),
+                                              _C.stream_ptr(w.device)), "tsrl_collect_pack_w1")
         if self.rng == "device":
             # one seed per policy, drawn at the first pack from torch's CPU generator: steps
             # replayed from HIP graphs carry the seed captured with them, so a per-collect
@@ -75,6 +83,31 @@ class FusedGaussAct:
                 self._ctr = torch.zeros(2, dtype=torch.int64, device=w.device)
             self._ctr.zero_()
             self._parity = 0
+
+    def fill_collect(self, c, sample: bool, bound_method, low_high, ctr) -> bool:
+        """Actor fields of a ``tsrl_collect_args`` (the fused collect step, csrc/collect.hip):
+        the same operands and noise stream as the ``tsrl_gauss_policy_act_rng`` launch of
+        ``__call__``.  False when that step cannot run this actor (torch-generator noise, or
+        an observation dim beyond its 512 columns)."""
+        if self.packed_c is None or (sample and self.rng != "device"):
+            return False
+        L = self.L
+        low, high = low_high if low_high is not None else (None, None)
+        c.w1p = _C.ptr(self.packed_c)
+        c.b1 = _C.ptr(L["w1"].bias.detach())
+        c.w2 = _C.ptr(L["w2"].weight.detach())
+        c.b2 = _C.ptr(L["w2"].bias.detach())
+        c.w3 = _C.ptr(L["w3"].weight.detach())
+        c.b3 = _C.ptr(L["w3"].bias.detach())
+        c.log_std = _C.ptr(L["sigma"].detach())
+        c.act_dim = self.A
+        c.sample = int(bool(sample))
+        c.act_seed = int(self._seed or 0)
+        c.rng_ctr = _C.ptr(ctr[0]) if sample else None
+        c.rng_next = _C.ptr(ctr[1]) if sample else None
+        c.bound_method = _BOUND[bound_method]
+        c.low, c.high = _C.ptr(low), _C.ptr(high)
+        return True
 
     def __call__(self, obs: torch.Tensor, act_out: torch.Tensor, remap_out: torch.Tensor,
                  sample: bool, bound_method, low_high, ctr=None) -> None:

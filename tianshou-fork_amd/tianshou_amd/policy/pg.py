@@ -74,6 +74,17 @@ class PGPolicy(BasePolicy):
         self._fused_act(obs, act_out, remap_out, sample, self.action_bound_method, low_high,
                         ctr)
 
+    def fused_collect_fill(self, c, ctr) -> bool:
+        """Fill the actor fields of the fused collect step (csrc/collect.hip) after
+        prepare_fused_act(); False if this policy's act must stay a separate launch."""
+        fa = getattr(self, "_fused_act", None)
+        if not fa:
+            return False
+        sample = not (self._deterministic_eval and not self.training)
+        dev = fa.L["w1"].weight.device
+        low_high = self._low_high(dev) if self.action_scaling else None
+        return fa.fill_collect(c, sample, self.action_bound_method, low_high, ctr)
+
     def _get_deterministic_action(self, logits):
         if self.action_type == "discrete":
             return logits.argmax(-1)

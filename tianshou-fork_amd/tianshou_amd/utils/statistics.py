@@ -139,6 +139,30 @@ class DeviceRunningMeanStd:
             _C.ptr(self.snap_mean_t), _C.ptr(self.snap_var_t), _C.ptr(self.ticket_t),
             _C.ptr(k_dev), st), "tsrl_rms_merge2")
 
+    def ensure_snapshot(self) -> None:
+        if self.snap_mean_t is None:
+            self.snap_mean_t = torch.empty_like(self.mean_t)
+            self.snap_var_t = torch.empty_like(self.var_t)
+
+    def payload(self) -> torch.Tensor:
+        """The [4*dim + 2] f64 vector of merge2's data-parallel all-reduce."""
+        if self._payload is None:
+            self._payload = torch.empty(4 * self.dim + 2, dtype=torch.float64,
+                                        device=self.device)
+        return self._payload
+
+    def merge_payload(self, k: int) -> None:
+        """All-reduce this rank's step/reset moments (``payload()``, filled by the fused
+        collect step) over the data-parallel ranks, then apply both updates (merge2)."""
+        self.ensure_snapshot()
+        pl, D = self.payload(), self.dim
+        self.dp.all_reduce_(pl)
+        _C.check(_C.lib().tsrl_rms_merge2(
+            _C.ptr(pl[:2 * D]), _C.ptr(pl[2 * D:4 * D]), _C.ptr(pl[4 * D:]), 1, D, k,
+            _C.ptr(self.mean_t), _C.ptr(self.var_t), _C.ptr(self.count_t),
+            _C.ptr(self.snap_mean_t), _C.ptr(self.snap_var_t), _C.ptr(self.ticket_t),
+            _C.ptr(pl[4 * D + 1:]), _C.stream_ptr()), "tsrl_rms_merge2")
+
     def update(self, x: torch.Tensor, mask: Optional[torch.Tensor] = None) -> None:
         x = x.reshape(len(x), -1)
         if mask is not None:
