@@ -223,6 +223,9 @@ int tsrl_buffer_add(const tsrl_add_args* a, void* stream);
  * add of step i-1 (`add`; add.k == 0: none), then the actor on the new live obs, the env
  * step + auto-reset, and both obs_rms updates (folded by the last workgroups to finish, no
  * grid barrier).  The caller issues the add of the LAST step as tsrl_buffer_add(&add).
+ * The live obs of a step go to the buffer's obs rows from this launch (obs_dst ...), so the
+ * adds copy no obs (add.obs_src = NULL) and write the new live obs to HBM only in that
+ * closing tsrl_buffer_add.
  *   w1p: the actor's first-layer weight packed by tsrl_collect_pack_w1 (once per update);
  *   workspace: tsrl_collect_workspace_bytes(k, dim) bytes, ZEROED once before first use
  *     (its tickets re-arm themselves);
@@ -234,7 +237,13 @@ typedef struct tsrl_collect_args {
     tsrl_add_args add;       /* pending add of the previous step (add.k == 0: none) */
     int64_t k;               /* envs (rows) */
     int64_t dim;             /* observation columns (multiple of 4, <= 512) */
-    float* cur;              /* [k, dim] live normalised observations */
+    float* cur;              /* [k, dim] live normalised observations (read when add.k == 0;
+                                the fused add keeps them on chip) */
+    /* this step's stored obs rows: obs_dst[(obs_offset[r] + ring position) * dim] = live obs
+     * row r, the position read from *obs_rel_dev or obs_uniform_rel; the pending add (and the
+     * closing tsrl_buffer_add) therefore run with obs_src = NULL */
+    float* obs_dst; const int64_t* obs_offset; const int64_t* obs_rel_dev;
+    int64_t obs_uniform_rel;
     /* actor */
     const float* w1p; const float* b1; const float* w2; const float* b2;
     const float* w3; const float* b3; const float* log_std; int64_t act_dim;

@@ -33,10 +33,10 @@ __device__ __forceinline__ float norm1(float x, float m, float v, float eps, flo
 
 // Row r of one add (urel = the uniform ring position of this step) by nl lanes (lane < nl).
 // lx (nullable): the new live obs row is also written to lx[col * lxp] (the fused collect step
-// keeps it in LDS for the next policy step).
+// keeps it in LDS for the next policy step); cur_hbm = false then skips its HBM copy.
 __device__ __forceinline__ void add_row(const tsrl_add_args& a, int64_t r, int lane,
                                         int64_t urel, float* lx = nullptr, int lxp = 0,
-                                        int nl = kWave) {
+                                        int nl = kWave, bool cur_hbm = true) {
     const int64_t b = a.ids ? a.ids[r] : r;
     const int64_t ptr = a.ptr ? a.ptr[r] : a.offset[b] + urel;
 
@@ -66,36 +66,63 @@ __device__ __forceinline__ void add_row(const tsrl_add_args& a, int64_t r, int l
                                   (!a.reset_mean || (aligned16(a.reset_mean) &&
                                                      aligned16(a.reset_var)))));
         if (v4) {
+            // QB float4 per lane per pass, every load of a pass issued before its stores (the
+            // stores may alias the loads, so without this each iteration waited out one full
+            // load latency)
             const int64_t nq = a.obs_dim >> 2;
-            for (int64_t q = lane; q < nq; q += nl) {
-                float4 x = reinterpret_cast<const float4*>(src)[q];
-                if (nrm) {
-                    const float4 m = reinterpret_cast<const float4*>(a.norm_mean)[q];
-                    const float4 v = reinterpret_cast<const float4*>(a.norm_var)[q];
-                    x.x = norm1(x.x, m.x, v.x, a.norm_eps, a.norm_clip);
-                    x.y = norm1(x.y, m.y, v.y, a.norm_eps, a.norm_clip);
-                    x.z = norm1(x.z, m.z, v.z, a.norm_eps, a.norm_clip);
-                    x.w = norm1(x.w, m.w, v.w, a.norm_eps, a.norm_clip);
-                }
-                if (dst) reinterpret_cast<float4*>(dst)[q] = x;
-                if (cur) {
-                    if (rst) {
-                        x = reinterpret_cast<const float4*>(a.reset_src + r * a.obs_dim)[q];
-                        if (a.reset_mean) {
-                            const float4 m = reinterpret_cast<const float4*>(a.reset_mean)[q];
-                            const float4 v = reinterpret_cast<const float4*>(a.reset_var)[q];
-                            x.x = norm1(x.x, m.x, v.x, a.norm_eps, a.norm_clip);
-                            x.y = norm1(x.y, m.y, v.y, a.norm_eps, a.norm_clip);
-                            x.z = norm1(x.z, m.z, v.z, a.norm_eps, a.norm_clip);
-                            x.w = norm1(x.w, m.w, v.w, a.norm_eps, a.norm_clip);
+            constexpr int QB = 4;
+            const float4* s4 = reinterpret_cast<const float4*>(src);
+            const float4* r4 = rst ? reinterpret_cast<const float4*>(a.reset_src + r * a.obs_dim)
+                                   : nullptr;
+            const bool rnrm = rst && a.reset_mean;
+            for (int64_t q0 = lane; q0 < nq; q0 += QB * nl) {
+                float4 xs[QB], ms[QB], vs[QB], xr[QB], mr[QB], vr[QB];
+#pragma unroll
+                for (int j = 0; j < QB; ++j) {
+                    const int64_t q = q0 + j * nl;
+                    const int64_t qc = q < nq ? q : 0;  // in-bounds, branch-free
+                    xs[j] = s4[qc];
+                    if (nrm) {
+                        ms[j] = reinterpret_cast<const float4*>(a.norm_mean)[qc];
+                        vs[j] = reinterpret_cast<const float4*>(a.norm_var)[qc];
+                    }
+                    if (cur && rst) {
+                        xr[j] = r4[qc];
+                        if (rnrm) {
+                            mr[j] = reinterpret_cast<const float4*>(a.reset_mean)[qc];
+                            vr[j] = reinterpret_cast<const float4*>(a.reset_var)[qc];
                         }
                     }
-                    reinterpret_cast<float4*>(cur)[q] = x;
-                    if (lx) {
-                        lx[(4 * q) * lxp] = x.x;
-                        lx[(4 * q + 1) * lxp] = x.y;
-                        lx[(4 * q + 2) * lxp] = x.z;
-                        lx[(4 * q + 3) * lxp] = x.w;
+                }
+#pragma unroll
+                for (int j = 0; j < QB; ++j) {
+                    const int64_t q = q0 + j * nl;
+                    if (q >= nq) break;
+                    float4 x = xs[j];
+                    if (nrm) {
+                        x.x = norm1(x.x, ms[j].x, vs[j].x, a.norm_eps, a.norm_clip);
+                        x.y = norm1(x.y, ms[j].y, vs[j].y, a.norm_eps, a.norm_clip);
+                        x.z = norm1(x.z, ms[j].z, vs[j].z, a.norm_eps, a.norm_clip);
+                        x.w = norm1(x.w, ms[j].w, vs[j].w, a.norm_eps, a.norm_clip);
+                    }
+                    if (dst) reinterpret_cast<float4*>(dst)[q] = x;
+                    if (cur) {
+                        if (rst) {
+                            x = xr[j];
+                            if (rnrm) {
+                                x.x = norm1(x.x, mr[j].x, vr[j].x, a.norm_eps, a.norm_clip);
+                                x.y = norm1(x.y, mr[j].y, vr[j].y, a.norm_eps, a.norm_clip);
+                                x.z = norm1(x.z, mr[j].z, vr[j].z, a.norm_eps, a.norm_clip);
+                                x.w = norm1(x.w, mr[j].w, vr[j].w, a.norm_eps, a.norm_clip);
+                            }
+                        }
+                        if (cur_hbm) reinterpret_cast<float4*>(cur)[q] = x;
+                        if (lx) {
+                            lx[(4 * q) * lxp] = x.x;
+                            lx[(4 * q + 1) * lxp] = x.y;
+                            lx[(4 * q + 2) * lxp] = x.z;
+                            lx[(4 * q + 3) * lxp] = x.w;
+                        }
                     }
                 }
             }
@@ -110,7 +137,7 @@ __device__ __forceinline__ void add_row(const tsrl_add_args& a, int64_t r, int l
                     if (a.reset_mean)
                         x = norm1(x, a.reset_mean[d], a.reset_var[d], a.norm_eps, a.norm_clip);
                 }
-                cur[d] = x;
+                if (cur_hbm) cur[d] = x;
                 if (lx) lx[d * lxp] = x;
             }
         }

@@ -128,6 +128,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
     __shared__ float seps[R][AMAX + 1];
     __shared__ RowState rs[R], rr[R];
     __shared__ int s_nd, s_last;
+    __shared__ int64_t s_row[R];
     const int t = threadIdx.x;
     const int w = t >> 6, l = t & 63;
     const int64_t k = a.k;
@@ -142,8 +143,13 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
 #endif
 #if COLLECT_TRACE
     if (t == 0) {
+        unsigned xcc, hwid;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
         ws.trace[((rng_step & 15) * gridDim.x + blockIdx.x) * 8 + 4] = 0;
         ws.trace[((rng_step & 15) * gridDim.x + blockIdx.x) * 8 + 5] = 0;
+        ws.trace[((rng_step & 15) * gridDim.x + blockIdx.x) * 8 + 6] = xcc;
+        ws.trace[((rng_step & 15) * gridDim.x + blockIdx.x) * 8 + 7] = hwid;
     }
 #endif
     TSTAMP(0)
@@ -183,7 +189,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         const int64_t urel = a.add.rel_dev ? *a.add.rel_dev : a.add.uniform_rel;
         // 32 lanes per row: all 16 rows' loads in flight at once
         const int rw = t >> 5;
-        if (rw < nrows) add_row(a.add, r0 + rw, t & 31, urel, sX + rw, XP, 32);
+        if (rw < nrows) add_row(a.add, r0 + rw, t & 31, urel, sX + rw, XP, 32, false);
         if (a.add.rel_next && blockIdx.x == 0 && t == 0)
             *a.add.rel_next = (urel + 1) % a.add.ring_size;
     } else {
@@ -251,6 +257,26 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
     }
     if (a.rng_next && blockIdx.x == 0 && t == 0) *a.rng_next = rng_step + 1;
     __syncthreads();
+    // this step's stored obs rows (ReplayBuffer obs of step i = the live obs the actor sees):
+    // written here from LDS, so the add of step i (next launch / flush) copies nothing and the
+    // live obs never round-trips through HBM between fused steps
+    if (t < nrows) {
+        // with a pending add this launch's block 0 advances the device cursor concurrently,
+        // so the position is the add's own plus one (the ring's uniform next)
+        int64_t urel;
+        if (a.add.k > 0) {
+            const int64_t up = a.add.rel_dev ? *a.add.rel_dev : a.add.uniform_rel;
+            urel = (up + 1) % a.add.ring_size;
+        } else {
+            urel = a.obs_rel_dev ? *a.obs_rel_dev : a.obs_uniform_rel;
+        }
+        s_row[t] = a.obs_offset[r0 + t] + urel;
+    }
+    __syncthreads();
+    for (int i = t; i < nrows * D; i += NT) {
+        const int rw = i / D, c = i - rw * D;
+        a.obs_dst[s_row[rw] * D + c] = sX[c * XP + rw];
+    }
 #if COLLECT_STOP == 1
     return;
 #endif
@@ -579,6 +605,8 @@ extern "C" int tsrl_collect_box_step(const tsrl_collect_args* a, void* stream) {
     TSRL_CHECK_ARG(a->act_dim > 0 && a->act_dim <= AMAX && a->bound_method >= 0 &&
                        a->bound_method <= 2,
                    "tsrl_collect_box_step: 0 < act_dim <= %d, bound_method 0..2", AMAX);
+    TSRL_CHECK_ARG(a->obs_dst && a->obs_offset && (a->obs_rel_dev || a->obs_uniform_rel >= 0),
+                   "tsrl_collect_box_step: obs_dst / obs_offset / this step's ring position");
     TSRL_CHECK_ARG(a->cur && a->w1p && a->b1 && a->w2 && a->b2 && a->w3 && a->b3 && a->log_std &&
                        a->act && a->act_remap && a->ep_j && a->ep_t && a->raw && a->reset_raw &&
                        a->rew && a->term && a->trunc && a->done && a->workspace && a->mean &&
@@ -609,6 +637,8 @@ extern "C" int tsrl_collect_box_step(const tsrl_collect_args* a, void* stream) {
         TSRL_CHECK_ARG(!ad.rel_next || (ad.rel_dev && ad.rel_next != ad.rel_dev),
                        "tsrl_collect_box_step: add.rel_next needs rel_dev (a different word)");
         TSRL_CHECK_ARG(!ad.reset_mask || ad.reset_src, "tsrl_collect_box_step: add reset_src");
+        TSRL_CHECK_ARG(!ad.obs_src, "tsrl_collect_box_step: the pending add copies no obs (the "
+                                    "launch that produced it stored them)");
     }
     Ws ws;
     ws.nblk = nblk_for(k);

@@ -44,6 +44,7 @@ class CollectArgs(ctypes.Structure):
     """Mirror of ``tsrl_collect_args`` (field order must match include/tsrl.h)."""
     _fields_ = [
         ("add", AddArgs), ("k", _i64), ("dim", _i64), ("cur", _p),
+        ("obs_dst", _p), ("obs_offset", _p), ("obs_rel_dev", _p), ("obs_uniform_rel", _i64),
         ("w1p", _p), ("b1", _p), ("w2", _p), ("b2", _p), ("w3", _p), ("b3", _p),
         ("log_std", _p), ("act_dim", _i64), ("act_seed", _u64), ("rng_ctr", _p),
         ("rng_next", _p), ("sample", _i32), ("bound_method", _i32), ("low", _p), ("high", _p),

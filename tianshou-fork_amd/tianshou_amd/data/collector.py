@@ -265,6 +265,12 @@ class Collector:
         D = b.obs_numel
         if D % 4 or D > 512 or self._act_spec()[1] != torch.float32:
             return False
+        buf = self.buffer
+        buf._alloc_storage(b.obs_shape, b.obs_torch_dtype, *self._act_spec())
+        m = buf._meta
+        if getattr(buf, "stack_num", 1) != 1 or m.obs.dtype != torch.float32 or \
+                m.obs[0].numel() != D:
+            return False
         sc = self._scratch["step_ctr"]
         return bool(self.policy.fused_collect_fill(_C.CollectArgs(), (sc[0, 1:2], sc[1, 1:2])))
 
@@ -284,6 +290,11 @@ class Collector:
         if self._pending is not None:
             c.add = self._pending
         c.k, c.dim, c.cur = kk, b.obs_numel, _C.ptr(cur)
+        # this step's stored obs rows come from the launch itself (the live obs never
+        # round-trips through HBM between fused steps); the adds then copy no obs
+        c.obs_dst, c.obs_offset = _C.ptr(buf._meta.obs), _C.ptr(buf._dev["offset"])
+        c.obs_rel_dev = _C.ptr(add_kw.get("rel_dev"))
+        c.obs_uniform_rel = int(add_kw.get("uniform_rel", 0))
         assert self.policy.fused_collect_fill(c, (sc[p, 1:2], sc[1 - p, 1:2]))
         c.act, c.act_remap = _C.ptr(s["act"]), _C.ptr(s["act_remap"])
         c.env_seed, c.ep_len = b.seed_, b.ep_len
@@ -301,7 +312,7 @@ class Collector:
         if dp:
             rms.merge_payload(kk)
         self._pending = buf._launch_add(
-            ids=None, k=kk, obs=cur, act=s["act"], obs_next=s["raw"], cur_obs=cur, norm=rms,
+            ids=None, k=kk, obs=None, act=s["act"], obs_next=s["raw"], cur_obs=cur, norm=rms,
             norm_snapshot=True, reset_src=s["reset_raw"], reset_mask=s["done"], reset_norm=rms,
             rew=s["rew"], term=s["term"], trunc=s["trunc"], launch=False, **add_kw)
         self._parity ^= 1

@@ -100,9 +100,16 @@ def trace_report(c, E, D):
     j = int(np.argsort(tl[:, 0])[8])  # a median launch: its slowest workgroups
     t0 = tr[j, :, 0].min()
     u = (tr[j, :, :4] - t0) / 100.0
-    for b in np.argsort(u[:, 3])[-6:]:
-        print(f"  launch {j} wg {b:4d}: start {u[b, 0]:6.2f} add {u[b, 1]:6.2f} actor "
-              f"{u[b, 2]:6.2f} env {u[b, 3]:6.2f} us")
+    for b in np.argsort(u[:, 3])[-8:]:
+        print(f"  launch {j} wg {b:4d} xcc {tr[j, b, 6] & 15} hwid {tr[j, b, 7]:#x}: start "
+              f"{u[b, 0]:6.2f} add {u[b, 1]:6.2f} actor {u[b, 2]:6.2f} env {u[b, 3]:6.2f} us")
+    add = u[:, 1] - u[:, 0]
+    xcc = tr[j, :, 6] & 15
+    for x in range(8):
+        m = xcc == x
+        if m.any():
+            print(f"  xcc {x}: {m.sum():3d} wgs, add median {np.median(add[m]):5.2f} max "
+                  f"{add[m].max():5.2f} us")
     print(f"  launch span (first stamp -> last stamp): median {np.median(spans):6.2f} us; "
           f"gap between launches (last stamp -> next first stamp): median {np.median(gaps):6.2f} "
           f"min {np.min(gaps):6.2f} max {np.max(gaps):6.2f} us")
