@@ -23,6 +23,13 @@
 // matrix cores are 28 % busy (SQ_VALU_MFMA_BUSY_CYCLES).  The gathered X rows and the
 // single-buffered chunk loop (two barriers per 32 k) bound it, not the MFMA rate; reading all
 // of a step's LDS operands ahead of its MFMAs (sched_barrier) measured 6 % slower.
+// Round 2 (tools/mlp_kernel_bench.py, 262144 rows): staging the X chunk with 8 consecutive
+// lanes per 128-byte row segment (X6_COAL; two lanes per row before) takes the random-row
+// gather from 285 to 245 us, the same as contiguous rows (240 us).  Tried and dropped: X
+// straight to registers (no X LDS stage) with a 3-chunk register ring, double-buffered
+// weight LDS and one barrier per chunk, paired v_cvt_pk splits: 243 / 280 us contiguous /
+// random -- the LDS fragment reads right before their MFMAs (s_waitcnt per MFMA group) and
+// the split VALU (~400 vector instructions per 48 MFMAs, SQ_INSTS_VALU) pace it, not the loads.
 #include "x6.h"
 
 namespace tsrl {
@@ -97,6 +104,9 @@ __global__ void split_w_kernel(const float* __restrict__ Wa, const float* __rest
 #ifndef X6_IL
 #define X6_IL 1
 #endif
+#ifndef X6_COAL
+#define X6_COAL 1
+#endif
 #ifndef X6_OCC
 #define X6_OCC 2
 #endif
@@ -112,9 +122,23 @@ __global__ __launch_bounds__(256, X6_OCC) void l1_fwd_x6_kernel(
     const int64_t row0 = (int64_t)blockIdx.x * XR;
     if (t < HC) sb[t] = t < H ? ba[t] : bc[t - H];
     const int srow = t >> 1, sq = 2 * (t & 1);
+#if X6_COAL
+    // X staging: thread t loads float4 (t & 7) of rows (t >> 3) + 32 i, i = 0..3: each load
+    // instruction reads 8 whole 128-byte row segments (8 consecutive lanes per row)
+    const int xq = t & 7, xr0 = t >> 3;
+    const float* xs_[4];
+    bool xl_[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int64_t g_ = row0 + xr0 + 32 * i;
+        xl_[i] = g_ < n;
+        xs_[i] = X + (xl_[i] ? (idx ? idx[g_] : g_) : 0) * ldx;
+    }
+#else
     const int64_t gr = row0 + srow;
     const bool live = gr < n;
     const float* xsrc = X + (live ? (idx ? idx[gr] : gr) : 0) * ldx;
+#endif
     const int64_t plane = (int64_t)HC * Kp;
     const __bf16* wsrc = wsp + (int64_t)srow * Kp + 8 * sq;
     const int nch = Kp / KC;
@@ -124,17 +148,48 @@ __global__ __launch_bounds__(256, X6_OCC) void l1_fwd_x6_kernel(
     // staging values are named scalars (no arrays or lambdas that end up in scratch).
     float4 x0, x1, x2, x3;
     uint4 w00, w01, w10, w11, w20, w21;
-#define X6_LOAD(kc)                                                                         \
+#if X6_COAL
+#define X6_XLOAD(kc)                                                                        \
+    {                                                                                       \
+        const int k_ = (kc) * KC + 4 * xq;                                                  \
+        x0 = *reinterpret_cast<const float4*>(xs_[0] + (xl_[0] && k_ < D ? k_ : 0));        \
+        x1 = *reinterpret_cast<const float4*>(xs_[1] + (xl_[1] && k_ < D ? k_ : 0));        \
+        x2 = *reinterpret_cast<const float4*>(xs_[2] + (xl_[2] && k_ < D ? k_ : 0));        \
+        x3 = *reinterpret_cast<const float4*>(xs_[3] + (xl_[3] && k_ < D ? k_ : 0));        \
+    }
+#define X6_XSTORE(kc)                                                                       \
+    {                                                                                       \
+        const int k_ = (kc) * KC + 4 * xq;                                                  \
+        *reinterpret_cast<float4*>(&Xs[swf_off(xr0, xq)]) = keep4(xl_[0] && k_ < D, x0);     \
+        *reinterpret_cast<float4*>(&Xs[swf_off(xr0 + 32, xq)]) = keep4(xl_[1] && k_ < D, x1);\
+        *reinterpret_cast<float4*>(&Xs[swf_off(xr0 + 64, xq)]) = keep4(xl_[2] && k_ < D, x2);\
+        *reinterpret_cast<float4*>(&Xs[swf_off(xr0 + 96, xq)]) = keep4(xl_[3] && k_ < D, x3);\
+    }
+#else
+#define X6_XLOAD(kc)                                                                        \
     {                                                                                       \
         const int k_ = (kc) * KC + 8 * sq;                                                  \
-        /* a float4 that starts inside the row is read whole: its columns >= D are the */    \
-        /* caller's finite padding and meet zero weights (split_w pads W with zeros)  */    \
         const bool i0_ = live && k_ < D, i1_ = live && k_ + 4 < D;                          \
         const bool i2_ = live && k_ + 8 < D, i3_ = live && k_ + 12 < D;                     \
         x0 = *reinterpret_cast<const float4*>(xsrc + (i0_ ? k_ : 0));                       \
         x1 = *reinterpret_cast<const float4*>(xsrc + (i1_ ? k_ + 4 : 0));                   \
         x2 = *reinterpret_cast<const float4*>(xsrc + (i2_ ? k_ + 8 : 0));                   \
         x3 = *reinterpret_cast<const float4*>(xsrc + (i3_ ? k_ + 12 : 0));                  \
+    }
+#define X6_XSTORE(kc)                                                                       \
+    {                                                                                       \
+        const int k_ = (kc) * KC + 8 * sq;                                                  \
+        *reinterpret_cast<float4*>(&Xs[xo0]) = keep4(live && k_ < D, x0);                   \
+        *reinterpret_cast<float4*>(&Xs[xo1]) = keep4(live && k_ + 4 < D, x1);               \
+        *reinterpret_cast<float4*>(&Xs[xo2]) = keep4(live && k_ + 8 < D, x2);               \
+        *reinterpret_cast<float4*>(&Xs[xo3]) = keep4(live && k_ + 12 < D, x3);              \
+    }
+#endif
+#define X6_LOAD(kc)                                                                         \
+    {                                                                                       \
+        X6_XLOAD(kc)                                                                        \
+        /* a float4 that starts inside the row is read whole: its columns >= D are the */    \
+        /* caller's finite padding and meet zero weights (split_w pads W with zeros)  */    \
         const __bf16* wk_ = wsrc + (kc) * KC;                                                \
         w00 = *reinterpret_cast<const uint4*>(wk_);                                         \
         w01 = *reinterpret_cast<const uint4*>(wk_ + 8);                                     \
@@ -145,18 +200,16 @@ __global__ __launch_bounds__(256, X6_OCC) void l1_fwd_x6_kernel(
     }
     const int off0 = sw_off(srow, sq), off1 = sw_off(srow, sq + 1);
     // f32 X rows, 16-B chunk qc = 4 * (t & 1) + i of row srow
+#if !X6_COAL
     const int xo0 = swf_off(srow, 2 * sq), xo1 = swf_off(srow, 2 * sq + 1);
     const int xo2 = swf_off(srow, 2 * sq + 2), xo3 = swf_off(srow, 2 * sq + 3);
+#endif
 // The out-of-range float4s are zeroed here, at the LDS store, not right after their loads:
 // a select next to the load makes the wave wait for the data before the chunk's MFMAs (the
 // whole fetch latency exposed once per chunk).
 #define X6_STORE(kc)                                                                        \
     {                                                                                       \
-        const int k_ = (kc) * KC + 8 * sq;                                                  \
-        *reinterpret_cast<float4*>(&Xs[xo0]) = keep4(live && k_ < D, x0);                   \
-        *reinterpret_cast<float4*>(&Xs[xo1]) = keep4(live && k_ + 4 < D, x1);               \
-        *reinterpret_cast<float4*>(&Xs[xo2]) = keep4(live && k_ + 8 < D, x2);               \
-        *reinterpret_cast<float4*>(&Xs[xo3]) = keep4(live && k_ + 12 < D, x3);              \
+        X6_XSTORE(kc)                                                                       \
         *reinterpret_cast<uint4*>(&Ws[0][off0]) = w00;                                      \
         *reinterpret_cast<uint4*>(&Ws[0][off1]) = w01;                                      \
         *reinterpret_cast<uint4*>(&Ws[1][off0]) = w10;                                      \
