@@ -1,14 +1,28 @@
 """Per-kernel totals from a rocprofv3 rocpd database (the sqlite *_results.db it writes):
-python tools/rocpd_top.py <db> [N]  -> name, calls, total ms, mean us (top N by total)."""
+python tools/rocpd_top.py <db> [N] [--last-ms MS]  -> name, calls, total ms, mean us (top N by
+total); --last-ms keeps only the kernels that start in the last MS milliseconds of the trace
+(a steady-state window: e.g. the last timed iteration, after warm-up and MIOpen's find)."""
 import sqlite3
 import sys
 
-db = sys.argv[1]
-n = int(sys.argv[2]) if len(sys.argv) > 2 else 30
+args = [a for a in sys.argv[1:]]
+last_ms = None
+if "--last-ms" in args:
+    i = args.index("--last-ms")
+    last_ms = float(args[i + 1])
+    del args[i:i + 2]
+db = args[0]
+n = int(args[1]) if len(args) > 1 else 30
 c = sqlite3.connect(db)
-tot = c.execute("select sum(duration)/1e6 from kernels").fetchone()[0]
+where, params = "", ()
+if last_ms is not None:
+    t_end = c.execute("select max(end) from kernels").fetchone()[0]
+    where, params = "where start >= ?", (t_end - last_ms * 1e6,)
+    t0 = c.execute(f"select min(start) from kernels {where}", params).fetchone()[0]
+    print(f"window: last {last_ms:.0f} ms of the trace ({(t_end - t0) / 1e6:.1f} ms of kernels)")
+tot = c.execute(f"select sum(duration)/1e6 from kernels {where}", params).fetchone()[0]
 print(f"total kernel time {tot:.2f} ms")
 for name, cnt, ms, us in c.execute(
-        "select name, count(*), sum(duration)/1e6, avg(duration)/1e3 from kernels "
-        "group by name order by sum(duration) desc limit ?", (n,)):
+        f"select name, count(*), sum(duration)/1e6, avg(duration)/1e3 from kernels {where} "
+        "group by name order by sum(duration) desc limit ?", params + (n,)):
     print(f"{ms:10.2f} ms {cnt:7d} x {us:10.1f} us  {name[:140]}")
