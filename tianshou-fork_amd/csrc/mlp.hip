@@ -1054,14 +1054,21 @@ __global__ __launch_bounds__(256, 2) void dw_kernel(
 __global__ __launch_bounds__(256, DWX6_OCC) void dw_x6_kernel(
     const float* __restrict__ dz, const float* __restrict__ X, int64_t ldx,
     const int64_t* __restrict__ idx, int64_t n, int D, int64_t rows_per_split, int ncolpad,
-    float* __restrict__ part) {
+    int ncolt, float* __restrict__ part) {
     constexpr int PL = 128 * 64;  // bytes per plane: 128 rows of 32 bf16
     __shared__ __attribute__((aligned(16))) char Zi[NPL * PL];
     __shared__ __attribute__((aligned(16))) char Xi[NPL * PL];
     const int t = threadIdx.x;
     const int w = t >> 6, l = t & 63, h = l >> 5, c = l & 31;
-    const int col0 = blockIdx.x * DW_COLS;
-    const int64_t r0 = (int64_t)blockIdx.y * rows_per_split;
+    // 1-D grid of ncolt x nsplit workgroups, remapped XCD-aware: blocks b and b + 8 share an
+    // XCD (and its L2), so logical tile L = (b % 8) * (G / 8) + b / 8 puts the ncolt column
+    // tiles of one row split on one XCD at about the same time and dZ1 (read once per column
+    // tile) comes from HBM once (G % 8 == 0 by construction of dw_nsplit; otherwise L = b).
+    const int G = gridDim.x, b = blockIdx.x;
+    const int L = (G & 7) ? b : (b & 7) * (G >> 3) + (b >> 3);
+    const int colt = L % ncolt, split = L / ncolt;
+    const int col0 = colt * DW_COLS;
+    const int64_t r0 = (int64_t)split * rows_per_split;
     const int64_t r1 = min(n, r0 + rows_per_split);
     const int fc = t & 127;                                  // staged feature / column
     const int rg = __builtin_amdgcn_readfirstlane(t >> 7);   // 8-row groups rg, rg + 2
@@ -1142,7 +1149,7 @@ __global__ __launch_bounds__(256, DWX6_OCC) void dw_x6_kernel(
     }
 #undef DWX6_LOAD
 #undef DWX6_STORE
-    float* o = part + (int64_t)blockIdx.y * HC * ncolpad;
+    float* o = part + (int64_t)split * HC * ncolpad;
 #pragma unroll
     for (int i = 0; i < NT; ++i)
 #pragma unroll
@@ -1197,6 +1204,8 @@ int tail_grid(int64_t n) {
 int dw_nsplit(int64_t n) {
     // ~512 resident workgroups on 256 CUs (3 column tiles at D=376), >= 64 rows per split
     int64_t s = std::max<int64_t>(1, std::min<int64_t>(170, n / 64));
+    // a multiple of 8 (XCD-aware tile order in dw_x6_kernel) once there are 8 or more
+    if (s >= 8) s &= ~int64_t(7);
     return (int)s;
 }
 
@@ -1292,8 +1301,8 @@ extern "C" int tsrl_mlp_dw(const float* dz1, const float* X, int64_t ldx, const 
 #define DW_X6 1
 #endif
     if (DW_X6)
-        hipLaunchKernelGGL(dw_x6_kernel, dim3(ncolt, nsplit), dim3(256), 0, as_stream(stream), dz1,
-                           X, ldx, idx, n, (int)D, rps, ncolpad, part);
+        hipLaunchKernelGGL(dw_x6_kernel, dim3(ncolt * nsplit), dim3(256), 0, as_stream(stream),
+                           dz1, X, ldx, idx, n, (int)D, rps, ncolpad, ncolt, part);
     else
         hipLaunchKernelGGL(dw_kernel, dim3(ncolt, nsplit), dim3(256), 0, as_stream(stream), dz1,
                            X, ldx, idx, n, (int)D, rps, ncolpad, part);

@@ -30,6 +30,12 @@
 // weight LDS and one barrier per chunk, paired v_cvt_pk splits: 243 / 280 us contiguous /
 // random -- the LDS fragment reads right before their MFMAs (s_waitcnt per MFMA group) and
 // the split VALU (~400 vector instructions per 48 MFMAs, SQ_INSTS_VALU) pace it, not the loads.
+// Also tried in round 2 (same tool, one box, random rows; this kernel 241.7 us there): a
+// generalised tiling of NW waves x RT 32-row tiles per wave, so each W fragment read from LDS
+// feeds RT row tiles and each staged W chunk serves 32*NW*RT rows: 4x1 (the same tiling
+// rewritten) 250 us, 8x1 (256 rows, W staging halved per row) 260 us, 4x2 (341 VGPR+AGPR,
+// one wave per SIMD) 296 us -- fewer W bytes per row does not pay for the larger barrier
+// group or the lost second wave per SIMD.
 #include "x6.h"
 
 namespace tsrl {
