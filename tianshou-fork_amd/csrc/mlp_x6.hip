@@ -35,7 +35,11 @@
 // feeds RT row tiles and each staged W chunk serves 32*NW*RT rows: 4x1 (the same tiling
 // rewritten) 250 us, 8x1 (256 rows, W staging halved per row) 260 us, 4x2 (341 VGPR+AGPR,
 // one wave per SIMD) 296 us -- fewer W bytes per row does not pay for the larger barrier
-// group or the lost second wave per SIMD.
+// group or the lost second wave per SIMD.  A two-register-set pipeline (each chunk's loads
+// issued two chunks before its LDS store, 212 VGPRs, still 2 waves/SIMD) does not survive
+// compilation: the IR passes sink the restrict-const loads next to their LDS stores (asm
+// memory clobbers and sched_barrier do not pin them) and volatile loads get a vmcnt(0) each;
+// it needs direct-to-LDS loads (global_load_lds_dwordx4) and an LDS ring instead.
 #include "x6.h"
 
 namespace tsrl {
