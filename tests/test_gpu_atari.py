@@ -177,6 +177,27 @@ def test_frames_to_f32_nhwc_bit_exact(dev):
         assert torch.equal(got.cpu(), want), shape
 
 
+def test_dqn_nchw_input_scaling_bit_exact(dev):
+    """The plain NCHW trunk (channels_last=False) scales uint8 frames through the same host-
+    divided table as the NHWC path: its first layer sees scale_obs's f64 division + f32 cast
+    bit for bit (atari_network.py:18-30, :84), so layout is the only difference between the
+    two trunks."""
+    from tianshou_amd.utils.net_atari import DQN
+    b = DQN(4, 84, 84, (6,), device=dev, features_only=True, channels_last=False).to(dev)
+    b.fused_conv1 = False
+    seen = []
+    h = b.net[0].register_forward_pre_hook(lambda m, inp: seen.append(inp[0].detach().clone()))
+    g = torch.Generator(device="cpu").manual_seed(3)
+    obs = torch.randint(0, 256, (9, 4, 84, 84), generator=g, dtype=torch.uint8)
+    want = torch.as_tensor((obs.numpy() / 255.0).astype(np.float32))
+    b(obs.to(dev))
+    b(obs)  # host frames take the same table
+    h.remove()
+    assert len(seen) == 2
+    for x in seen:
+        assert x.dtype == torch.float32 and torch.equal(x.cpu(), want)
+
+
 def test_dqn_nhwc_trunk_matches_nchw(dev):
     """The NHWC trunk fed by tsrl_frames_to_f32_nhwc against the plain NCHW module with the
     same weights (summation order only)."""
@@ -282,21 +303,67 @@ def test_dqn_fused_conv1_matches_miopen(dev):
 
 
 def test_atari_shared_trunk_process_fn_wrapped_ring(dev):
-    """As above on a ring that has wrapped (collect more steps than the buffer holds) and on
-    a random-index sample: next() positions equal the host next(), and process_fn's V(s')
-    equals the critic on the batch's obs_next rows."""
-    E, T, L = 6, 16, 7
+    """As above on a ring that has wrapped (collect more steps than the buffer holds): the
+    stacked obs / obs_next rows equal the env's FrameStack stream (oracle/synth_env.py) where
+    the stack lies inside the retained window, next() positions equal the host next(), and
+    process_fn's returns/advantages equal the GAE on the critic's V(obs) / V(obs_next).  On a
+    random-index sample with duplicate indices, next() reuse either declines (None) or points
+    at rows whose V(s) equals the critic on the batch's obs_next."""
+    from tianshou_amd.policy.base import gae_device
+    E, T, L, X = 6, 16, 7, 5
     _, policy, buf, coll = _setup(dev, E, T, L, seed=5)
     policy._rew_norm = False
-    coll.collect(n_step=E * (T + 5))  # 5 steps past the end of every sub-buffer
+    coll.collect(n_step=E * (T + X))  # X steps past the end of every sub-buffer
+    ref = synth_env.SynthVecEnvNP(E, (4, 84, 84), 6, L, seed=3, u8=True, frame_stack=4)
+    cur = ref.reset()
+    seen = np.zeros((E, T + X, 4, 84, 84), np.uint8)
+    dones = np.zeros((E, T + X), bool)
+    for t in range(T + X):
+        seen[:, t] = cur
+        nxt, _, term, trunc = ref.step()
+        done = term | trunc
+        dones[:, t] = done
+        if done.any():
+            ids = np.flatnonzero(done)
+            nxt[ids] = ref.reset(ids)
+        cur = nxt
+    seen, dones = seen[:, X:], dones[:, X:]  # the retained window, oldest first
     batch, idx = buf.sample(0)
     assert not np.array_equal(idx, np.arange(E * T))  # ring order, not storage order
+    obs = batch.obs.cpu().numpy().reshape(E, T, 4, 84, 84)
+    on = batch.obs_next.cpu().numpy().reshape(E, T, 4, 84, 84)
+    # rows t >= 3 of the window: their frame stack never reaches past the oldest stored row
+    assert np.array_equal(obs[:, 3:], seen[:, 3:])
+    inner = ~dones[:, 3:-1]
+    assert np.array_equal(on[:, 3:-1][inner], seen[:, 4:][inner])
+    assert np.array_equal(on[:, 3:-1][~inner], seen[:, 3:-1][~inner])
+    assert np.array_equal(on[:, -1], seen[:, -1])  # the newest row: its own observation
     p = policy._next_positions(buf, idx, dev)
     assert p is not None
     assert np.array_equal(idx[p.cpu().numpy()], buf.next(idx))
-    with torch.no_grad():  # as _compute_returns calls it
+    with torch.no_grad():
+        v_ref = policy.critic(batch.obs).flatten()
         vn_ref = policy.critic(batch.obs_next).flatten()
-        v_s, v_s_ = policy._eval_values(batch, batch.obs.to(dev), batch.obs_next.to(dev), buf,
-                                        idx)
-    np.testing.assert_allclose(v_s_.cpu().numpy(), vn_ref.cpu().numpy(), rtol=1e-5,
-                               atol=1e-5 * float(vn_ref.abs().max()))
+    out = policy.process_fn(batch, buf, idx)
+    vmax = float(v_ref.abs().max())
+    np.testing.assert_allclose(out.v_s.cpu().numpy(), v_ref.cpu().numpy(), rtol=1e-5,
+                               atol=1e-5 * vmax)
+    adv, ret, _, _ = gae_device(v_ref.contiguous(), vn_ref.contiguous(),
+                                batch.rew.contiguous(), batch.terminated.contiguous(),
+                                batch.truncated.contiguous(), 0.99, 0.95, T)
+    np.testing.assert_allclose(out.adv.cpu().numpy(), adv.cpu().numpy(), rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(out.returns.cpu().numpy(), ret.cpu().numpy(), rtol=1e-5,
+                               atol=1e-5)
+    # random-index sample with duplicates
+    np.random.seed(11)
+    _, ridx = buf.sample(40)
+    ridx = np.concatenate([ridx, ridx[:8], idx[:4]])
+    rb = buf[ridx]
+    pr = policy._next_positions(buf, ridx, dev)
+    with torch.no_grad():
+        v = policy.critic(rb.obs).flatten()
+        vn = policy.critic(rb.obs_next).flatten()
+    if pr is not None:
+        assert np.array_equal(ridx[pr.cpu().numpy()], buf.next(ridx))
+        np.testing.assert_allclose(v[pr].cpu().numpy(), vn.cpu().numpy(), rtol=1e-5,
+                                   atol=1e-5 * float(vn.abs().max()))

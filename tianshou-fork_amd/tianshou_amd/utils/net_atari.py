@@ -221,6 +221,11 @@ class DQN(nn.Module):
         if self.channels_last and obs.dim() == 4:
             obs = obs.contiguous(memory_format=torch.channels_last)  # 1-byte frames
         # scale_obs (atari_network.py:18-30) divides the frames in f64 and the trunk casts to
-        # f32 (:84); other inputs (host tensors, non-u8 frames) take torch's division
-        x = (obs / self.scale).to(torch.float32) if self.scale else obs.to(torch.float32)
+        # f32 (:84): uint8 frames go through the same host-divided table as the NHWC path (a
+        # GPU division by the scalar multiplies by its reciprocal, which is not bit-identical),
+        # so the memory layout is the only difference between the two paths
+        if obs.dtype == torch.uint8 and self.scale:
+            x = self._scale_lut(obs.device)[obs.long()]
+        else:
+            x = (obs / self.scale).to(torch.float32) if self.scale else obs.to(torch.float32)
         return self.net(x), state

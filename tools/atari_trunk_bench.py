@@ -33,7 +33,7 @@ def timed(fn, iters):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=8192)
-    ap.add_argument("--eval-rows", type=int, default=38043)
+    ap.add_argument("--eval-rows", type=int, default=32768)  # A2CPolicy._chunks for 4x84x84
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", action="store_true",
                     help="only MIOpen's default choice with channels_last (profiling runs)")
