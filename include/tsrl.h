@@ -313,6 +313,19 @@ int tsrl_dqn_conv1_fwd(const uint8_t* frames, int64_t n, const float* w, int64_t
 int tsrl_dqn_conv2_dgrad(const float* gy, int64_t n, const float* w, int64_t sw0, int64_t sw1,
                          int64_t sw2, int64_t sw3, const float* z1, float* dx, void* stream);
 
+/* Weight and bias gradient of the first convolution straight from the uint8 frames:
+ * gw[co][ci][kh][kw] = sum_p gy[p][co] * frames[p's tap (ci, kh, kw)] / scale (gw contiguous
+ * [32][4][8][8] f32), gb[co] = sum_p gy[p][co] (nullable), gy [n][20][20][32] f32 NHWC (the
+ * gradient w.r.t. conv1's pre-ReLU output, 16-byte aligned), frames [n][4][84][84] u8
+ * (4-byte aligned).  Replaces the MIOpen weight gradient of Conv2d(4, 32, 8, 4) over
+ * scale_obs(frames) (examples/atari/atari_network.py:18-30,53-90) in loss.backward()
+ * (ppo.py:146) and the u8 -> f32 frame conversion it needs: bytes exact in bf16, gy split
+ * into 3 bf16 planes (f32 GEMM error), per-workgroup partials folded in fixed order (f64).
+ * workspace: tsrl_dqn_conv1_wgrad_workspace_bytes(n) bytes. */
+int64_t tsrl_dqn_conv1_wgrad_workspace_bytes(int64_t n);
+int tsrl_dqn_conv1_wgrad(const uint8_t* frames, int64_t n, const float* gy, float scale,
+                         float* gw, float* gb, void* workspace, int64_t ws_bytes, void* stream);
+
 /* ---------------------------------------------------------------------------------
  * np.random.permutation(n) of the global legacy RandomState, bit-exact: the shuffle order
  * of Batch.split (tianshou/data/batch.py:896-912, one permutation per PPO repeat,

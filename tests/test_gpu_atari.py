@@ -248,6 +248,36 @@ def test_conv2_dgrad_kernel_vs_f64(dev, n):
     assert bool((err <= 1e-6 * mag + 1e-12).all())
 
 
+@pytest.mark.parametrize("n", [1, 5, 37, 300])
+def test_conv1_wgrad_u8_vs_f64(dev, n):
+    """tsrl_dqn_conv1_wgrad (bytes exact in bf16, gy split in 3 bf16 planes, per-workgroup
+    partials folded in f64) against fp64 conv2d_weight of (frames / 255, gy): elementwise
+    within 1e-6 of the absolute-value product (f32 GEMM error), bias gradient = sum of gy in
+    f64 within 1e-6 relative; ragged batches (chunks of 32 pixels straddle samples, the last
+    chunk partial); the channels_last weight gets a channels_last gradient."""
+    from tianshou_amd.utils.net_atari import conv1_u8_wgrad
+    torch.manual_seed(100 + n)
+    x = torch.randint(0, 256, (n, 4, 84, 84), dtype=torch.uint8, device=dev)
+    gy = torch.randn(n, 20, 20, 32, device=dev)
+    gy[torch.rand_like(gy) < 0.4] = 0.0  # ReLU-masked rows
+    w = torch.empty(32, 4, 8, 8, device=dev).contiguous(memory_format=torch.channels_last)
+    gw, gb = conv1_u8_wgrad(x, gy, w, 255.0, True)
+    assert gw.shape == (32, 4, 8, 8) and gw.is_contiguous(memory_format=torch.channels_last)
+    x64 = x.double() / 255.0
+    g64 = gy.permute(0, 3, 1, 2).double()
+    ref = torch.nn.grad.conv2d_weight(x64, (32, 4, 8, 8), g64, stride=4)
+    mag = torch.nn.grad.conv2d_weight(x64, (32, 4, 8, 8), g64.abs(), stride=4)
+    err = (gw.double() - ref).abs()
+    assert bool((err <= 1e-6 * mag + 1e-12).all()), float((err / (mag + 1e-30)).max())
+    gb_ref = g64.sum(dim=(0, 2, 3))
+    gb_mag = g64.abs().sum(dim=(0, 2, 3))
+    assert bool(((gb.double() - gb_ref).abs() <= 1e-6 * gb_mag + 1e-12).all())
+    # no bias: gb is None
+    gw2, gb2 = conv1_u8_wgrad(x, gy, w.contiguous(), 255.0, False)
+    assert gb2 is None and gw2.is_contiguous()
+    assert torch.equal(gw2, gw.contiguous())
+
+
 @pytest.mark.parametrize("n", [1, 37, 1024])
 def test_conv1_u8_kernel_vs_f64(dev, n):
     """tsrl_dqn_conv1_fwd (uint8 frames, bf16 byte operands x 3-plane split weights) against
@@ -280,9 +310,9 @@ def test_conv1_u8_kernel_vs_f64(dev, n):
 
 def test_dqn_fused_conv1_matches_miopen(dev):
     """The whole trunk with the uint8 first layer (forward: tsrl_dqn_conv1_fwd; backward:
-    MIOpen weight/bias gradients, conv2's data gradient with conv1's ReLU mask from
-    tsrl_dqn_conv2_dgrad) against the same module on MIOpen throughout: outputs and every
-    parameter gradient."""
+    conv2's data gradient with conv1's ReLU mask from tsrl_dqn_conv2_dgrad, conv1's
+    weight/bias gradient from the frames by tsrl_dqn_conv1_wgrad, MIOpen for the rest)
+    against the same module on MIOpen throughout: outputs and every parameter gradient."""
     from tianshou_amd.utils.net_atari import DQN, layer_init
     torch.manual_seed(1)
     a = DQN(4, 84, 84, (6,), device=dev, features_only=True, output_dim=512,

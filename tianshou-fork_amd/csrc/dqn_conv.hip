@@ -32,6 +32,8 @@ using x6::bf16x8;
 using x6::f32x16;
 using x6::NPL;
 
+__device__ __forceinline__ int rho(int r) { return (r & 3) + 8 * (r >> 2); }
+
 constexpr int C1_CIN = 4, C1_HW = 84, C1_K = 8, C1_S = 4, C1_OUT = 20, C1_OC = 32;
 constexpr int C1_KK = C1_CIN * C1_K * C1_K;       // 256
 constexpr int C1_PIX = C1_OUT * C1_OUT;           // 400 output pixels per sample
@@ -247,6 +249,161 @@ __global__ __launch_bounds__(256, 2) void dqn_conv2_dgrad_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// Weight and bias gradient of the first convolution straight from the uint8 frames:
+// dW1[co][k] = (sum_p gy1[p][co] * u[p][k]) / scale, db1[co] = sum_p gy1[p][co], where p runs
+// over every output pixel of the minibatch and u[p][k] is the frame byte under tap k of pixel
+// p (k = ci*64 + kh*8 + kw, the NCHW order of W1).  The reference's weight gradient
+// (loss.backward(), ppo.py:146, through scale_obs + Conv2d, atari_network.py:18-30,53-90)
+// multiplies gy1 by f32(u / 255); here the bytes are exact bf16 values and gy1 is split exactly
+// into three bf16 planes, so each product is exact in the f32 accumulator and the division
+// by scale happens once per weight (f32 GEMM error, like the forward kernel above).  This also
+// removes the u8 -> f32 frame conversion the MIOpen weight gradient needs.
+// GEMM view: D[32 co][32 k] += G^T[32 co][16 px] . P[16 px][32 k] (v_mfma_f32_32x32x16_bf16,
+// three per 16 pixels: one per plane of G).  A workgroup walks a contiguous range of 32-pixel
+// chunks (flat pixel index over the batch; chunks may straddle samples).  Per chunk it stages
+// the im2col bytes as Pb[k][32 px] (each thread copies 8-byte runs u[p][ci][4oh+kh][4ow..+7])
+// and the gradient rows as split planes Gs[plane][co][32 px]; wave w owns the 64 taps of input
+// channel w (two 32-k tiles).  Partial sums per workgroup, folded in fixed order by
+// dqn_conv1_wgrad_reduce_kernel (f64).
+constexpr int C1W_CH = 32;  // pixels per chunk
+constexpr int C1W_PR = 40;  // Pb row pitch (bytes): 10-dword rows, conflict-free b64 reads
+constexpr int C1W_GR = 80;  // Gs row pitch (bytes): 20-dword rows, conflict-free b128 phases
+
+__global__ __launch_bounds__(256, 2) void dqn_conv1_wgrad_kernel(
+    const uint8_t* __restrict__ X, const float* __restrict__ gy, int64_t npix, int64_t cpw,
+    float* __restrict__ part) {
+    __shared__ __attribute__((aligned(16))) uint8_t Pb[C1_KK * C1W_PR];        // [k][px]
+    __shared__ __attribute__((aligned(16))) uint8_t Gs[NPL][C1_OC * C1W_GR];   // [co][px] bf16
+    const int t = threadIdx.x;
+    const int w = t >> 6, l = t & 63, h = l >> 5, c = l & 31;
+    const int64_t nchunk = (npix + C1W_CH - 1) / C1W_CH;
+    const int64_t c0 = (int64_t)blockIdx.x * cpw;
+    const int64_t c1 = min(nchunk, c0 + cpw);
+    // staging roles: im2col run q = t >> 3 (ci = q >> 3, kh = q & 7) of the 4 pixels
+    // px0 .. px0 + 3, px0 = 4 (t & 7): 8 bytes each, re-packed as 4-pixel dwords of the 8 rows
+    // k = 8q + kw; gradient float4 (t & 7) (channels 4gq..4gq+3) of pixel gp = t >> 3
+    const int q = t >> 3, px0 = 4 * (t & 7);
+    const int gq = t & 7, gp = t >> 3;
+    uint32_t rb[8];
+    float4 gv;
+    float db[4] = {0.f, 0.f, 0.f, 0.f};
+#define C1W_LOAD(ch)                                                                        \
+    {                                                                                       \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                     \
+            const int64_t p_ = (ch) * C1W_CH + px0 + i;                                     \
+            const int64_t pp_ = p_ < npix ? p_ : 0;                                         \
+            const int64_t s_ = pp_ / C1_PIX;                                                \
+            const int rr_ = (int)(pp_ - s_ * C1_PIX), oh_ = rr_ / C1_OUT, ow_ = rr_ - oh_ * C1_OUT; \
+            const uint32_t* a_ = reinterpret_cast<const uint32_t*>(                         \
+                X + s_ * C1_FRAME + (q >> 3) * (C1_HW * C1_HW) + (C1_S * oh_ + (q & 7)) * C1_HW + \
+                C1_S * ow_);                                                                \
+            rb[2 * i] = a_[0];                                                              \
+            rb[2 * i + 1] = a_[1];                                                          \
+        }                                                                                   \
+        {                                                                                   \
+            const int64_t p_ = (ch) * C1W_CH + gp;                                          \
+            gv = *reinterpret_cast<const float4*>(gy + (p_ < npix ? p_ : 0) * C1_OC + 4 * gq); \
+        }                                                                                   \
+    }
+#define C1W_STORE(ch)                                                                       \
+    {                                                                                       \
+        uint32_t m_ = 0u; /* byte mask of the live pixels among px0..px0+3 */               \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i)                                       \
+            m_ |= ((ch) * C1W_CH + px0 + i < npix ? 0xFFu : 0u) << (8 * i);                 \
+        _Pragma("unroll") for (int e = 0; e < 8; ++e) {                                     \
+            const int sh_ = 8 * (e & 3);                                                    \
+            const uint32_t b0_ = (rb[(e >> 2)] >> sh_) & 0xFFu;                             \
+            const uint32_t b1_ = (rb[2 + (e >> 2)] >> sh_) & 0xFFu;                         \
+            const uint32_t b2_ = (rb[4 + (e >> 2)] >> sh_) & 0xFFu;                         \
+            const uint32_t b3_ = (rb[6 + (e >> 2)] >> sh_) & 0xFFu;                         \
+            *reinterpret_cast<uint32_t*>(&Pb[(8 * q + e) * C1W_PR + px0]) =                 \
+                (b0_ | (b1_ << 8) | (b2_ << 16) | (b3_ << 24)) & m_;                        \
+        }                                                                                   \
+        {                                                                                   \
+            const bool ok_ = (ch) * C1W_CH + gp < npix;                                     \
+            const float g_[4] = {ok_ ? gv.x : 0.f, ok_ ? gv.y : 0.f, ok_ ? gv.z : 0.f,       \
+                                 ok_ ? gv.w : 0.f};                                         \
+            _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                 \
+                __bf16 a0_, a1_, a2_;                                                       \
+                x6::split1(g_[e], a0_, a1_, a2_);                                           \
+                const int o_ = (4 * gq + e) * C1W_GR + 2 * gp;                              \
+                *reinterpret_cast<__bf16*>(&Gs[0][o_]) = a0_;                               \
+                *reinterpret_cast<__bf16*>(&Gs[1][o_]) = a1_;                               \
+                *reinterpret_cast<__bf16*>(&Gs[2][o_]) = a2_;                               \
+                db[e] += g_[e];                                                             \
+            }                                                                               \
+        }                                                                                   \
+    }
+    f32x16 acc0, acc1;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0.0f;
+    if (c0 < c1) {
+        C1W_LOAD(c0)
+        C1W_STORE(c0)
+    }
+    __syncthreads();
+    for (int64_t ch = c0; ch < c1; ++ch) {
+        if (ch + 1 < c1) C1W_LOAD(ch + 1)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int po = 16 * s + 8 * h;
+            bf16x8 a[NPL];
+#pragma unroll
+            for (int pl = 0; pl < NPL; ++pl)
+                a[pl] = *reinterpret_cast<const bf16x8*>(&Gs[pl][c * C1W_GR + 2 * po]);
+            const uint2 u0 = *reinterpret_cast<const uint2*>(&Pb[(64 * w + c) * C1W_PR + po]);
+            const uint2 u1 =
+                *reinterpret_cast<const uint2*>(&Pb[(64 * w + 32 + c) * C1W_PR + po]);
+            const bf16x8 b0 = bytes_to_bf16(u0.x, u0.y), b1 = bytes_to_bf16(u1.x, u1.y);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b0, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b1, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b0, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b1, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b0, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b1, acc1, 0, 0, 0);
+        }
+        if (ch + 1 < c1) {
+            __syncthreads();
+            C1W_STORE(ch + 1)
+            __syncthreads();
+        }
+    }
+#undef C1W_LOAD
+#undef C1W_STORE
+    // partial slab of this workgroup: [32 co][256 k] then db[32]
+    float* o = part + (int64_t)blockIdx.x * (C1_OC * C1_KK + C1_OC);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int co = rho(r) + 4 * h;
+        o[co * C1_KK + 64 * w + c] = acc0[r];
+        o[co * C1_KK + 64 * w + 32 + c] = acc1[r];
+    }
+    // db: the 32 pixel slots of each channel, summed in slot order
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(Pb);  // [32 slots][32 co] (4 KB of the 10 KB)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) red[gp * C1_OC + 4 * gq + e] = db[e];
+    __syncthreads();
+    if (t < C1_OC) {
+        float sacc = 0.0f;
+        for (int i = 0; i < C1W_CH; ++i) sacc += red[i * C1_OC + t];
+        o[C1_OC * C1_KK + t] = sacc;
+    }
+}
+
+__global__ __launch_bounds__(256) void dqn_conv1_wgrad_reduce_kernel(
+    const float* __restrict__ part, int nslab, float inv_scale, float* __restrict__ gw,
+    float* __restrict__ gb) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    constexpr int W = C1_OC * C1_KK + C1_OC;
+    if (i >= W) return;
+    double s = 0.0;
+    for (int k = 0; k < nslab; ++k) s += (double)part[(int64_t)k * W + i];
+    if (i < C1_OC * C1_KK) gw[i] = (float)(s * (double)inv_scale);
+    else if (gb) gb[i - C1_OC * C1_KK] = (float)s;
+}
+
 }  // namespace
 }  // namespace tsrl
 
@@ -291,5 +448,44 @@ extern "C" int tsrl_dqn_conv2_dgrad(const float* gy, int64_t n, const float* w, 
     hipLaunchKernelGGL(dqn_conv2_dgrad_kernel, dim3((unsigned)gx, 4), dim3(256), 0,
                        as_stream(stream), gy, n, w, sw0, sw1, sw2, sw3, z1, dx);
     TSRL_LAUNCH_CHECK("tsrl_dqn_conv2_dgrad");
+    return 0;
+}
+
+extern "C" int64_t tsrl_dqn_conv1_wgrad_workspace_bytes(int64_t n) {
+    if (n <= 0) return 0;
+    const int64_t nchunk = (n * C1_PIX + C1W_CH - 1) / C1W_CH;
+    const int64_t nwg = std::min<int64_t>(nchunk, 512);
+    return nwg * (C1_OC * C1_KK + C1_OC) * (int64_t)sizeof(float);
+}
+
+extern "C" int tsrl_dqn_conv1_wgrad(const uint8_t* frames, int64_t n, const float* gy,
+                                    float scale, float* gw, float* gb, void* workspace,
+                                    int64_t ws_bytes, void* stream) {
+    TSRL_CHECK_ARG(n >= 0, "tsrl_dqn_conv1_wgrad: n < 0");
+    TSRL_CHECK_ARG(frames && gy && gw && (n == 0 || workspace), "tsrl_dqn_conv1_wgrad: null pointer");
+    TSRL_CHECK_ARG((((uintptr_t)frames) & 3) == 0 && aligned16(gy),
+                   "tsrl_dqn_conv1_wgrad: frames must be 4-byte and gy 16-byte aligned");
+    TSRL_CHECK_ARG(scale > 0.0f, "tsrl_dqn_conv1_wgrad: scale must be > 0");
+    TSRL_CHECK_ARG(ws_bytes >= tsrl_dqn_conv1_wgrad_workspace_bytes(n),
+                   "tsrl_dqn_conv1_wgrad: workspace too small");
+    constexpr int W = C1_OC * C1_KK + C1_OC;
+    if (n == 0) {
+        (void)hipMemsetAsync(gw, 0, C1_OC * C1_KK * sizeof(float), as_stream(stream));
+        if (gb) (void)hipMemsetAsync(gb, 0, C1_OC * sizeof(float), as_stream(stream));
+        TSRL_LAUNCH_CHECK("tsrl_dqn_conv1_wgrad");
+        return 0;
+    }
+    const int64_t npix = n * C1_PIX;
+    const int64_t nchunk = (npix + C1W_CH - 1) / C1W_CH;
+    const int64_t nwg0 = std::min<int64_t>(nchunk, 512);
+    const int64_t cpw = (nchunk + nwg0 - 1) / nwg0;
+    const int64_t nwg = (nchunk + cpw - 1) / cpw;  // every workgroup has >= 1 chunk
+    float* part = reinterpret_cast<float*>(workspace);
+    hipLaunchKernelGGL(dqn_conv1_wgrad_kernel, dim3((unsigned)nwg), dim3(256), 0,
+                       as_stream(stream), frames, gy, npix, cpw, part);
+    TSRL_LAUNCH_CHECK("tsrl_dqn_conv1_wgrad");
+    hipLaunchKernelGGL(dqn_conv1_wgrad_reduce_kernel, dim3((W + 255) / 256), dim3(256), 0,
+                       as_stream(stream), part, (int)nwg, 1.0f / scale, gw, gb);
+    TSRL_LAUNCH_CHECK("tsrl_dqn_conv1_wgrad(reduce)");
     return 0;
 }

@@ -53,17 +53,44 @@ def conv1_u8(obs: torch.Tensor, conv: nn.Conv2d, scale: float) -> torch.Tensor:
     return out.permute(0, 3, 1, 2)
 
 
+# conv1's weight/bias gradient from the uint8 frames (tsrl_dqn_conv1_wgrad); False: MIOpen over
+# the scaled f32 frames (tsrl_frames_to_f32_nhwc)
+CONV1_WGRAD_U8 = True
+
+
+def conv1_u8_wgrad(obs: torch.Tensor, gy_nhwc: torch.Tensor, weight: torch.Tensor,
+                   scale: float, bias: bool):
+    """(dW1, db1 or None) of relu-masked gradient rows gy [n, 20, 20, 32] (NHWC) w.r.t.
+    conv(obs / scale, W1) + b1, straight from the uint8 frames (tsrl_dqn_conv1_wgrad)."""
+    n = obs.shape[0]
+    dev = obs.device
+    lib = _C.lib()
+    gw = torch.empty((32, 4, 8, 8), dtype=torch.float32, device=dev)
+    gb = torch.empty(32, dtype=torch.float32, device=dev) if bias else None
+    ws = torch.empty(max(1, (int(lib.tsrl_dqn_conv1_wgrad_workspace_bytes(n)) + 3) // 4),
+                     dtype=torch.float32, device=dev)
+    gy_nhwc = gy_nhwc.contiguous()
+    _C.check(lib.tsrl_dqn_conv1_wgrad(_C.ptr(obs.contiguous()), n, _C.ptr(gy_nhwc), float(scale),
+                                      _C.ptr(gw), _C.ptr(gb) if gb is not None else None,
+                                      _C.ptr(ws), ws.numel() * 4, _C.stream_ptr(dev)),
+             "tsrl_dqn_conv1_wgrad")
+    if weight.is_contiguous(memory_format=torch.channels_last) and not weight.is_contiguous():
+        gw = gw.contiguous(memory_format=torch.channels_last)
+    return gw, gb
+
+
 class _Conv1U8(torch.autograd.Function):
     """conv1 + ReLU from uint8 frames (forward: tsrl_dqn_conv1_fwd).  Backward: the ReLU
-    mask, then the weight and bias gradients from MIOpen over the scaled f32 frames
-    (tsrl_frames_to_f32_nhwc, built only when a gradient is needed); the frames themselves
-    need no gradient."""
+    mask, then the weight and bias gradients straight from the frames (tsrl_dqn_conv1_wgrad;
+    with CONV1_WGRAD_U8 off, MIOpen over the scaled f32 frames of tsrl_frames_to_f32_nhwc);
+    the frames themselves need no gradient."""
 
     @staticmethod
     def forward(ctx, obs, weight, bias, conv, lut, scale):
         z = conv1_u8(obs, conv, scale)
         ctx.save_for_backward(obs, weight, z)
         ctx.lut = lut
+        ctx.scale = scale
         ctx.has_bias = bias is not None
         return z
 
@@ -71,6 +98,9 @@ class _Conv1U8(torch.autograd.Function):
     def backward(ctx, gz):
         obs, weight, z = ctx.saved_tensors
         gy = torch.ops.aten.threshold_backward(gz, z, 0.0)
+        if CONV1_WGRAD_U8:
+            gw, gb = conv1_u8_wgrad(obs, _nhwc(gy), weight, ctx.scale, ctx.has_bias)
+            return None, gw, gb, None, None, None
         x = frames_to_f32_nhwc(obs, ctx.lut)
         _, gw, gb = torch.ops.aten.convolution_backward(
             gy, x, weight, [weight.shape[0]] if ctx.has_bias else None, (4, 4), (0, 0), (1, 1),
@@ -88,7 +118,7 @@ class _Conv12U8(torch.autograd.Function):
     """conv1 + ReLU + conv2 + ReLU from uint8 frames.  Forward: tsrl_dqn_conv1_fwd, MIOpen
     conv2, ReLU.  Backward: ReLU mask of conv2, MIOpen weight/bias gradient of conv2, the
     conv2 data gradient with conv1's ReLU mask fused (tsrl_dqn_conv2_dgrad), then conv1's
-    weight/bias gradient (MIOpen over the scaled f32 frames)."""
+    weight/bias gradient straight from the frames (tsrl_dqn_conv1_wgrad)."""
 
     @staticmethod
     def forward(ctx, obs, w1, b1, w2, b2, conv1, conv2, lut, scale):
@@ -96,6 +126,7 @@ class _Conv12U8(torch.autograd.Function):
         z2 = torch.relu_(torch.nn.functional.conv2d(z1, w2, b2, conv2.stride))
         ctx.save_for_backward(obs, w1, w2, z1, z2)
         ctx.lut = lut
+        ctx.scale = scale
         ctx.bias = (b1 is not None, b2 is not None)
         return z2
 
@@ -114,10 +145,13 @@ class _Conv12U8(torch.autograd.Function):
                                                _C.ptr(_nhwc(z1)), _C.ptr(gy1),
                                                _C.stream_ptr(obs.device)),
                  "tsrl_dqn_conv2_dgrad")
-        x = frames_to_f32_nhwc(obs, ctx.lut)
-        _, gw1, gb1 = torch.ops.aten.convolution_backward(
-            gy1.permute(0, 3, 1, 2), x, w1, [w1.shape[0]] if ctx.bias[0] else None, (4, 4),
-            (0, 0), (1, 1), False, (0, 0), 1, (False, True, ctx.bias[0]))
+        if CONV1_WGRAD_U8:
+            gw1, gb1 = conv1_u8_wgrad(obs, gy1, w1, ctx.scale, ctx.bias[0])
+        else:
+            x = frames_to_f32_nhwc(obs, ctx.lut)
+            _, gw1, gb1 = torch.ops.aten.convolution_backward(
+                gy1.permute(0, 3, 1, 2), x, w1, [w1.shape[0]] if ctx.bias[0] else None, (4, 4),
+                (0, 0), (1, 1), False, (0, 0), 1, (False, True, ctx.bias[0]))
         return None, gw1, gb1, gw2, gb2, None, None, None, None
 
 
