@@ -260,15 +260,20 @@ __global__ __launch_bounds__(256, 2) void dqn_conv2_dgrad_kernel(
 // by scale happens once per weight (f32 GEMM error, like the forward kernel above).  This also
 // removes the u8 -> f32 frame conversion the MIOpen weight gradient needs.
 // GEMM view: D[32 co][32 k] += G^T[32 co][16 px] . P[16 px][32 k] (v_mfma_f32_32x32x16_bf16,
-// three per 16 pixels: one per plane of G).  A workgroup walks a contiguous range of 32-pixel
-// chunks (flat pixel index over the batch; chunks may straddle samples).  Per chunk it stages
-// the im2col bytes as Pb[k][32 px] (each thread copies 8-byte runs u[p][ci][4oh+kh][4ow..+7])
-// and the gradient rows as split planes Gs[plane][co][32 px]; wave w owns the 64 taps of input
-// channel w (two 32-k tiles).  Partial sums per workgroup, folded in fixed order by
-// dqn_conv1_wgrad_reduce_kernel (f64).
-constexpr int C1W_CH = 32;  // pixels per chunk
-constexpr int C1W_PR = 40;  // Pb row pitch (bytes): 10-dword rows, conflict-free b64 reads
-constexpr int C1W_GR = 80;  // Gs row pitch (bytes): 20-dword rows, conflict-free b128 phases
+// three per 16 pixels: one per plane of G).  A workgroup walks a contiguous range of
+// 128-pixel chunks (flat pixel index over the batch; chunks may straddle samples).  Per chunk
+// it stages the im2col bytes as Pb[k][128 px] (each thread copies the 8-byte runs
+// u[p][ci][4oh+kh][4ow..+7] of 4 pixels and re-packs them as 4-pixel dwords of 8 k rows) and the
+// gradient rows as split planes Gs[plane][co][128 px]; wave w owns the 64 taps of input channel
+// w (two 32-k tiles).  Partial sums per workgroup, folded in fixed order by
+// dqn_conv1_wgrad_reduce_kernel (f64).  32-pixel chunks: 345 us + a 147 us single-thread-per-
+// output fold per 8192 rows; the chunk size amortises the two barriers per chunk.
+constexpr int C1W_CH = 128;                   // pixels per chunk
+constexpr int C1W_J = C1W_CH / 32;            // staging repeats per thread
+constexpr int C1W_PR = C1W_CH + 8;            // Pb row pitch (bytes; 34 dwords at 128 px:
+                                              // conflict-free b64 fragment reads)
+constexpr int C1W_GR = 2 * C1W_CH + 16;       // Gs row pitch (bytes; 68 dwords: conflict-free
+                                              // b128 phases)
 
 __global__ __launch_bounds__(256, 2) void dqn_conv1_wgrad_kernel(
     const uint8_t* __restrict__ X, const float* __restrict__ gy, int64_t npix, int64_t cpw,
@@ -280,54 +285,58 @@ __global__ __launch_bounds__(256, 2) void dqn_conv1_wgrad_kernel(
     const int64_t nchunk = (npix + C1W_CH - 1) / C1W_CH;
     const int64_t c0 = (int64_t)blockIdx.x * cpw;
     const int64_t c1 = min(nchunk, c0 + cpw);
-    // staging roles: im2col run q = t >> 3 (ci = q >> 3, kh = q & 7) of the 4 pixels
-    // px0 .. px0 + 3, px0 = 4 (t & 7): 8 bytes each, re-packed as 4-pixel dwords of the 8 rows
-    // k = 8q + kw; gradient float4 (t & 7) (channels 4gq..4gq+3) of pixel gp = t >> 3
-    const int q = t >> 3, px0 = 4 * (t & 7);
+    // staging roles: im2col run q = t >> 3 (ci = q >> 3, kh = q & 7) of the pixel quads
+    // 4 (pg + 8 j) .. + 3, pg = t & 7: 8 bytes per pixel, re-packed as 4-pixel dwords of the 8
+    // rows k = 8q + kw; gradient float4 (t & 7) (channels 4gq..4gq+3) of pixels gp + 32 j
+    const int q = t >> 3, pg = t & 7;
     const int gq = t & 7, gp = t >> 3;
-    uint32_t rb[8];
-    float4 gv;
+    const int qoff = (q >> 3) * (C1_HW * C1_HW) + (q & 7) * C1_HW;  // channel + kernel row
+    // A pixel quad 4m..4m+3 never straddles an output row or a sample (20 and 400 are
+    // multiples of 4, and so is npix), so its 4 eight-byte runs are the 20-byte window
+    // u[4 ow0 .. 4 ow0 + 19] of one input row: 5 dword loads, and kernel column kw of pixel i
+    // is byte (kw & 3) of window dword (kw >> 2) + i.
+    uint32_t rb[C1W_J][5];
+    float4 gv[C1W_J];
     float db[4] = {0.f, 0.f, 0.f, 0.f};
 #define C1W_LOAD(ch)                                                                        \
     {                                                                                       \
-        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                     \
-            const int64_t p_ = (ch) * C1W_CH + px0 + i;                                     \
-            const int64_t pp_ = p_ < npix ? p_ : 0;                                         \
-            const int64_t s_ = pp_ / C1_PIX;                                                \
-            const int rr_ = (int)(pp_ - s_ * C1_PIX), oh_ = rr_ / C1_OUT, ow_ = rr_ - oh_ * C1_OUT; \
+        _Pragma("unroll") for (int j = 0; j < C1W_J; ++j) {                                 \
+            /* 32-bit pixel arithmetic (npix < 2^31, checked on the host): the divisions  */ \
+            /* by the constants 400 and 20 become multiply-high + shift                   */ \
+            const uint32_t p_ = (uint32_t)(ch) * C1W_CH + 4u * (pg + 8 * j);                \
+            const uint32_t pp_ = p_ < (uint32_t)npix ? p_ : 0u;                             \
+            const uint32_t s_ = pp_ / (uint32_t)C1_PIX;                                     \
+            const uint32_t rr_ = pp_ - s_ * C1_PIX, oh_ = rr_ / (uint32_t)C1_OUT;           \
+            const uint32_t ow_ = rr_ - oh_ * C1_OUT;                                        \
             const uint32_t* a_ = reinterpret_cast<const uint32_t*>(                         \
-                X + s_ * C1_FRAME + (q >> 3) * (C1_HW * C1_HW) + (C1_S * oh_ + (q & 7)) * C1_HW + \
-                C1_S * ow_);                                                                \
-            rb[2 * i] = a_[0];                                                              \
-            rb[2 * i + 1] = a_[1];                                                          \
-        }                                                                                   \
-        {                                                                                   \
-            const int64_t p_ = (ch) * C1W_CH + gp;                                          \
-            gv = *reinterpret_cast<const float4*>(gy + (p_ < npix ? p_ : 0) * C1_OC + 4 * gq); \
+                X + (int64_t)s_ * C1_FRAME + qoff + C1_S * oh_ * C1_HW + C1_S * ow_);        \
+            _Pragma("unroll") for (int d = 0; d < 5; ++d) rb[j][d] = a_[d];                 \
+            const int64_t g_ = (ch) * C1W_CH + gp + 32 * j;                                 \
+            gv[j] = *reinterpret_cast<const float4*>(gy + (g_ < npix ? g_ : 0) * C1_OC + 4 * gq); \
         }                                                                                   \
     }
 #define C1W_STORE(ch)                                                                       \
     {                                                                                       \
-        uint32_t m_ = 0u; /* byte mask of the live pixels among px0..px0+3 */               \
-        _Pragma("unroll") for (int i = 0; i < 4; ++i)                                       \
-            m_ |= ((ch) * C1W_CH + px0 + i < npix ? 0xFFu : 0u) << (8 * i);                 \
-        _Pragma("unroll") for (int e = 0; e < 8; ++e) {                                     \
-            const int sh_ = 8 * (e & 3);                                                    \
-            const uint32_t b0_ = (rb[(e >> 2)] >> sh_) & 0xFFu;                             \
-            const uint32_t b1_ = (rb[2 + (e >> 2)] >> sh_) & 0xFFu;                         \
-            const uint32_t b2_ = (rb[4 + (e >> 2)] >> sh_) & 0xFFu;                         \
-            const uint32_t b3_ = (rb[6 + (e >> 2)] >> sh_) & 0xFFu;                         \
-            *reinterpret_cast<uint32_t*>(&Pb[(8 * q + e) * C1W_PR + px0]) =                 \
-                (b0_ | (b1_ << 8) | (b2_ << 16) | (b3_ << 24)) & m_;                        \
-        }                                                                                   \
-        {                                                                                   \
-            const bool ok_ = (ch) * C1W_CH + gp < npix;                                     \
-            const float g_[4] = {ok_ ? gv.x : 0.f, ok_ ? gv.y : 0.f, ok_ ? gv.z : 0.f,       \
-                                 ok_ ? gv.w : 0.f};                                         \
+        _Pragma("unroll") for (int j = 0; j < C1W_J; ++j) {                                 \
+            const int px0_ = 4 * (pg + 8 * j);                                              \
+            const uint32_t m_ = (ch) * C1W_CH + px0_ < npix ? 0xFFFFFFFFu : 0u;              \
+            _Pragma("unroll") for (int e = 0; e < 8; ++e) {                                 \
+                const int k0_ = e >> 2;                                                     \
+                const uint32_t b_ = (uint32_t)(e & 3);                                      \
+                const uint32_t lo_ = __builtin_amdgcn_perm(                                 \
+                    rb[j][k0_ + 1], rb[j][k0_], b_ | ((4u + b_) << 8) | 0x0C0C0000u);        \
+                const uint32_t hi_ = __builtin_amdgcn_perm(                                 \
+                    rb[j][k0_ + 3], rb[j][k0_ + 2], 0x00000C0Cu | (b_ << 16) | ((4u + b_) << 24)); \
+                *reinterpret_cast<uint32_t*>(&Pb[(8 * q + e) * C1W_PR + px0_]) =            \
+                    (lo_ | hi_) & m_;                                                       \
+            }                                                                               \
+            const bool ok_ = (ch) * C1W_CH + gp + 32 * j < npix;                            \
+            const float g_[4] = {ok_ ? gv[j].x : 0.f, ok_ ? gv[j].y : 0.f,                  \
+                                 ok_ ? gv[j].z : 0.f, ok_ ? gv[j].w : 0.f};                 \
             _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                 \
                 __bf16 a0_, a1_, a2_;                                                       \
                 x6::split1(g_[e], a0_, a1_, a2_);                                           \
-                const int o_ = (4 * gq + e) * C1W_GR + 2 * gp;                              \
+                const int o_ = (4 * gq + e) * C1W_GR + 2 * (gp + 32 * j);                   \
                 *reinterpret_cast<__bf16*>(&Gs[0][o_]) = a0_;                               \
                 *reinterpret_cast<__bf16*>(&Gs[1][o_]) = a1_;                               \
                 *reinterpret_cast<__bf16*>(&Gs[2][o_]) = a2_;                               \
@@ -346,7 +355,7 @@ __global__ __launch_bounds__(256, 2) void dqn_conv1_wgrad_kernel(
     for (int64_t ch = c0; ch < c1; ++ch) {
         if (ch + 1 < c1) C1W_LOAD(ch + 1)
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
+        for (int s = 0; s < C1W_CH / 16; ++s) {
             const int po = 16 * s + 8 * h;
             bf16x8 a[NPL];
 #pragma unroll
@@ -381,25 +390,42 @@ __global__ __launch_bounds__(256, 2) void dqn_conv1_wgrad_kernel(
     }
     // db: the 32 pixel slots of each channel, summed in slot order
     __syncthreads();
-    float* red = reinterpret_cast<float*>(Pb);  // [32 slots][32 co] (4 KB of the 10 KB)
+    float* red = reinterpret_cast<float*>(Pb);  // [32 slots][32 co]
 #pragma unroll
     for (int e = 0; e < 4; ++e) red[gp * C1_OC + 4 * gq + e] = db[e];
     __syncthreads();
     if (t < C1_OC) {
         float sacc = 0.0f;
-        for (int i = 0; i < C1W_CH; ++i) sacc += red[i * C1_OC + t];
+        for (int i = 0; i < 32; ++i) sacc += red[i * C1_OC + t];
         o[C1_OC * C1_KK + t] = sacc;
     }
 }
 
+// Fixed-order fold of the per-workgroup slabs: block = 64 outputs x 4 lane groups; group g
+// sums slabs g, g + 4, ... in f64 with 4 independent accumulators (loads stay in flight), then
+// the groups combine in order through LDS.
 __global__ __launch_bounds__(256) void dqn_conv1_wgrad_reduce_kernel(
     const float* __restrict__ part, int nslab, float inv_scale, float* __restrict__ gw,
     float* __restrict__ gb) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
     constexpr int W = C1_OC * C1_KK + C1_OC;
-    if (i >= W) return;
-    double s = 0.0;
-    for (int k = 0; k < nslab; ++k) s += (double)part[(int64_t)k * W + i];
+    __shared__ double sh[4][64];
+    const int o = threadIdx.x & 63, g = threadIdx.x >> 6;
+    const int i = blockIdx.x * 64 + o;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    if (i < W) {
+        int k = g;
+        for (; k + 12 < nslab; k += 16) {
+            a0 += (double)part[(int64_t)k * W + i];
+            a1 += (double)part[(int64_t)(k + 4) * W + i];
+            a2 += (double)part[(int64_t)(k + 8) * W + i];
+            a3 += (double)part[(int64_t)(k + 12) * W + i];
+        }
+        for (; k < nslab; k += 4) a0 += (double)part[(int64_t)k * W + i];
+    }
+    sh[g][o] = (a0 + a1) + (a2 + a3);
+    __syncthreads();
+    if (g != 0 || i >= W) return;
+    const double s = ((sh[0][o] + sh[1][o]) + sh[2][o]) + sh[3][o];
     if (i < C1_OC * C1_KK) gw[i] = (float)(s * (double)inv_scale);
     else if (gb) gb[i - C1_OC * C1_KK] = (float)s;
 }
@@ -468,6 +494,7 @@ extern "C" int tsrl_dqn_conv1_wgrad(const uint8_t* frames, int64_t n, const floa
     TSRL_CHECK_ARG(scale > 0.0f, "tsrl_dqn_conv1_wgrad: scale must be > 0");
     TSRL_CHECK_ARG(ws_bytes >= tsrl_dqn_conv1_wgrad_workspace_bytes(n),
                    "tsrl_dqn_conv1_wgrad: workspace too small");
+    TSRL_CHECK_ARG(n * C1_PIX < ((int64_t)1 << 31), "tsrl_dqn_conv1_wgrad: n * 400 >= 2^31");
     constexpr int W = C1_OC * C1_KK + C1_OC;
     if (n == 0) {
         (void)hipMemsetAsync(gw, 0, C1_OC * C1_KK * sizeof(float), as_stream(stream));
@@ -484,7 +511,7 @@ extern "C" int tsrl_dqn_conv1_wgrad(const uint8_t* frames, int64_t n, const floa
     hipLaunchKernelGGL(dqn_conv1_wgrad_kernel, dim3((unsigned)nwg), dim3(256), 0,
                        as_stream(stream), frames, gy, npix, cpw, part);
     TSRL_LAUNCH_CHECK("tsrl_dqn_conv1_wgrad");
-    hipLaunchKernelGGL(dqn_conv1_wgrad_reduce_kernel, dim3((W + 255) / 256), dim3(256), 0,
+    hipLaunchKernelGGL(dqn_conv1_wgrad_reduce_kernel, dim3((W + 63) / 64), dim3(256), 0,
                        as_stream(stream), part, (int)nwg, 1.0f / scale, gw, gb);
     TSRL_LAUNCH_CHECK("tsrl_dqn_conv1_wgrad(reduce)");
     return 0;
