@@ -397,7 +397,9 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
     // Software pipeline over this wave's tiles (one wave per SIMD: nothing else hides
     // latency): while tile bt computes, the NEXT tile's H1 fragments and gathered per-row
     // inputs are in flight, and the index of the tile after that.  Loads are branch-free:
-    // rows past n read row 0 / tile 0 and are discarded by `live`.
+    // rows past n read row 0 / tile 0 and are discarded by `live`.  Two tiles of inputs in
+    // flight (a second register stage, 433 / 321 VGPR+AGPR) measured 1-2 % slower (round 2):
+    // past one tile ahead the dependent MFMA / tanh chain of the tile, not the loads, paces it.
     float nh1[2][16], nav[16];
     float nx0 = 0.f, nx1 = 0.f;  // actor: logp_old, adv; critic: ret, v_s
     auto row_index = [&](int64_t bt_) -> int64_t {
