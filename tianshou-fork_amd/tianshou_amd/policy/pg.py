@@ -9,11 +9,15 @@ from tianshou_amd.policy.base import BasePolicy
 from tianshou_amd.utils.statistics import DeviceScalarRMS
 
 
-def make_dist(dist_fn, logits):
-    """dist_fn(*logits) without torch.distributions argument validation: its checks are
-    device reductions followed by a host-side ``if not valid.all()`` -- a device->host sync
-    per construction, i.e. per collector step.  (The reference validates; invalid
-    parameters here surface as NaN losses instead of ValueError.)"""
+def make_dist(dist_fn, logits, validate: bool = False):
+    """dist_fn(*logits), by default without torch.distributions argument validation: its
+    checks are device reductions followed by a host-side ``if not valid.all()`` -- a
+    device->host sync per construction, i.e. per collector step.  The reference validates
+    (invalid parameters raise ValueError); ``validate=True`` (``PGPolicy(validate_args=True)``)
+    keeps that behaviour at the cost of the sync, otherwise invalid parameters surface as NaN
+    losses.  The global default is restored afterwards either way."""
+    if validate:
+        return dist_fn(*logits) if isinstance(logits, tuple) else dist_fn(logits)
     prev = torch.distributions.Distribution._validate_args
     torch.distributions.Distribution.set_default_validate_args(False)
     try:
@@ -28,7 +32,8 @@ class PGPolicy(BasePolicy):
                  discount_factor: float = 0.99, reward_normalization: bool = False,
                  action_scaling: bool = True,
                  action_bound_method: Optional[Literal["clip", "tanh"]] = "clip",
-                 deterministic_eval: bool = False, **kwargs: Any) -> None:
+                 deterministic_eval: bool = False, validate_args: bool = False,
+                 **kwargs: Any) -> None:
         super().__init__(action_scaling=action_scaling, action_bound_method=action_bound_method,
                          **kwargs)
         self.actor = model
@@ -40,6 +45,9 @@ class PGPolicy(BasePolicy):
         self._ret_rms = None
         self._eps = 1e-8
         self._deterministic_eval = deterministic_eval
+        # torch.distributions argument checks as in the reference (ValueError on invalid
+        # parameters; one host sync per distribution), off by default (see make_dist)
+        self.validate_args = validate_args
 
     @property
     def ret_rms(self) -> DeviceScalarRMS:
@@ -99,14 +107,14 @@ class PGPolicy(BasePolicy):
             # because torch.normal's tensor-std path checks std >= 0 with a host sync.
             mu = self.actor.forward_mu(batch.obs)
             sigma = self.actor.sigma_param.view(1, -1).exp().expand_as(mu)
-            dist = make_dist(self.dist_fn, (mu, sigma))
+            dist = make_dist(self.dist_fn, (mu, sigma), self.validate_args)
             if self._deterministic_eval and not self.training:
                 act = mu
             else:
                 act = torch.randn_like(mu).mul_(sigma).add_(mu)
             return Batch(logits=(mu, sigma), act=act, state=state, dist=dist)
         logits, hidden = self.actor(batch.obs, state=state, info=batch.get("info", {}))
-        dist = make_dist(self.dist_fn, logits)
+        dist = make_dist(self.dist_fn, logits, self.validate_args)
         if self._deterministic_eval and not self.training:
             act = self._get_deterministic_action(logits)
         else:
