@@ -1,4 +1,4 @@
-"""Data-parallel host logic on CPU with a world_size-2 gloo group (no GPU): gradient
+"""Data-parallel host logic on CPU with world_size-2 and -4 gloo groups (no GPU): gradient
 all-reduce (sum and average), all_gather_cat order, and the scaling convention the fused PPO
 loss relies on -- per-rank sums divided by the GLOBAL minibatch size, then summed across
 ranks -- reproduces the single-process full-batch gradient."""
@@ -34,7 +34,7 @@ def _worker(rank, world, port, out):
     assert dp.active and dp.world == world and dp.rank == rank
     # all_gather_cat keeps rank order
     g = dp.all_gather_cat(torch.tensor([float(rank), rank + 0.5]))
-    assert g.tolist() == [0.0, 0.5, 1.0, 1.5]
+    assert g.tolist() == [v for r in range(world) for v in (float(r), r + 0.5)]
     # gradient all-reduce: global-mean convention
     torch.manual_seed(0)
     net = torch.nn.Sequential(torch.nn.Linear(7, 16), torch.nn.Tanh(), torch.nn.Linear(16, 3))
@@ -64,11 +64,12 @@ def _worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_data_parallel_gloo_two_ranks():
+@pytest.mark.parametrize("world", [2, 4])
+def test_data_parallel_gloo_ranks(world):
     port = _free_port()
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(2, port, out), nprocs=2, join=True)
+    mp.spawn(_worker, args=(world, port, out), nprocs=world, join=True)
     torch.manual_seed(0)
     net = torch.nn.Sequential(torch.nn.Linear(7, 16), torch.nn.Tanh(), torch.nn.Linear(16, 3))
     x = torch.randn(64, 7, generator=torch.Generator().manual_seed(1))
@@ -78,7 +79,7 @@ def test_data_parallel_gloo_two_ranks():
     torch.manual_seed(100)
     rep0 = torch.nn.Sequential(torch.nn.Linear(7, 16), torch.nn.Tanh(), torch.nn.Linear(16, 3))
     want = torch.cat([q.detach().reshape(-1) for q in rep0.parameters()])
-    for r in range(2):
+    for r in range(world):
         gs, ga, sums, flat = out[r]
         assert torch.equal(flat, want)
         for a, b in zip(gs, full):
