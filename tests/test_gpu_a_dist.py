@@ -1,12 +1,13 @@
-"""Data-parallel (env-sharded) PPO update with 2 ranks on one MI355X over gloo: one global
+"""Data-parallel (env-sharded) PPO update with 2 and 4 ranks on one MI355X over gloo: one global
 minibatch split across ranks must give the single-process full-batch update (up to
 summation order) -- one minibatch, and several global minibatches of the reference's
 Batch.split over the global batch (every rank draws the same permutation) -- and the default
-global obs_rms must leave both ranks with the statistics of ONE VectorEnvNormObs over both
+global obs_rms must leave every rank with the statistics of ONE VectorEnvNormObs over all
 env shards (checked against the NumPy env and a host RunningMeanStd).
 
-Runs first among the GPU tests (file name) so that this pytest process has not initialised
-HIP when it starts the rank processes."""
+Runs first among the GPU tests (file name), and both rank groups (6 processes) are started
+together by a module fixture before any test body touches the GPU, so that this pytest
+process has not initialised HIP when it starts the rank processes."""
 import os
 import socket
 import subprocess
@@ -29,24 +30,41 @@ def _free_port():
     return p
 
 
-def test_two_rank_update_matches_single_process(tmp_path):
-    port = str(_free_port())
+@pytest.fixture(scope="module")
+def rank_runs(tmp_path_factory):
+    """Both rank groups (2 and 4 ranks, gloo) run concurrently, before the parent process
+    initialises HIP; returns {world: output directory}."""
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
-    procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "dist_worker.py"),
-                               str(r), "2", port, str(tmp_path)], env=env)
-             for r in range(2)]
-    rcs = [p.wait(timeout=240) for p in procs]
-    assert rcs == [0, 0], rcs
-    r0 = torch.load(tmp_path / "rank0.pt", weights_only=True)
-    r1 = torch.load(tmp_path / "rank1.pt", weights_only=True)
-    # identical parameters on both ranks
-    for k in r0["sd"]:
-        assert torch.equal(r0["sd"][k], r1["sd"][k]), k
-    np.testing.assert_allclose(r0["loss"].numpy(), r1["loss"].numpy(), rtol=1e-6)
-    # global obs_rms identical on both ranks, counting both shards' rows
-    assert torch.equal(r0["rms_mean"], r1["rms_mean"])
-    assert torch.equal(r0["rms_var"], r1["rms_var"])
-    assert int(r0["rms_count"]) == int(r1["rms_count"]) > 0
+    dirs, procs = {}, []
+    for world in (2, 4):
+        port = str(_free_port())
+        d = tmp_path_factory.mktemp(f"dp{world}")
+        dirs[world] = d
+        procs += [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "dist_worker.py"),
+                                    str(r), str(world), port, str(d)], env=env)
+                  for r in range(world)]
+    rcs = [p.wait(timeout=300) for p in procs]
+    assert rcs == [0] * len(procs), rcs
+    return dirs
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_rank_update_matches_single_process(rank_runs, world):
+    outs = [torch.load(rank_runs[world] / f"rank{r}.pt", weights_only=True)
+            for r in range(world)]
+    r0 = outs[0]
+    for r1 in outs[1:]:
+        # identical parameters on every rank
+        for k in r0["sd"]:
+            assert torch.equal(r0["sd"][k], r1["sd"][k]), k
+        np.testing.assert_allclose(r0["loss"].numpy(), r1["loss"].numpy(), rtol=1e-6)
+        # global obs_rms identical on every rank, counting every shard's rows
+        assert torch.equal(r0["rms_mean"], r1["rms_mean"])
+        assert torch.equal(r0["rms_var"], r1["rms_var"])
+        assert int(r0["rms_count"]) == int(r1["rms_count"]) > 0
+        for k in r0["sd2"]:
+            assert torch.equal(r0["sd2"][k], r1["sd2"][k]), k
+        torch.testing.assert_close(r0["loss2"], r1["loss2"], rtol=1e-6, atol=0)
     # single-process reference: the whole batch as one minibatch
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import dist_worker as w
@@ -62,15 +80,12 @@ def test_two_rank_update_matches_single_process(tmp_path):
     # near-zero gradient summed in another order can move it differently: atol = lr / 3
     for k, v in r0["sd"].items():
         np.testing.assert_allclose(v.numpy(), sd[k].cpu().numpy(), rtol=1e-4, atol=1e-4)
-    # global minibatches: 8 per epoch x 2 repeats, rank shares of varying size
-    for k in r0["sd2"]:
-        assert torch.equal(r0["sd2"][k], r1["sd2"][k]), k
-    torch.testing.assert_close(r0["loss2"], r1["loss2"], rtol=1e-6, atol=0)
+    # global minibatches of 256 x world rows (rank shares of varying size), 2 repeats
     policy2 = w.build_policy(23, 5, dev)
     np.random.seed(0)
-    res2 = policy2.learn(Batch(**data), batch_size=512, repeat=2)
+    res2 = policy2.learn(Batch(**data), batch_size=256 * world, repeat=2)
     want = np.array([res2[k] for k in ("loss", "loss/clip", "loss/vf", "loss/ent")])
-    assert want.shape == tuple(r0["loss2"].shape) == (4, 16)
+    assert want.shape == tuple(r0["loss2"].shape) == (4, 2 * 4096 // (256 * world))
     np.testing.assert_allclose(r0["loss2"].numpy(), want, rtol=1e-4, atol=1e-5)
     sd2 = policy2.state_dict()
     for k, v in r0["sd2"].items():
@@ -79,7 +94,7 @@ def test_two_rank_update_matches_single_process(tmp_path):
     # and a RunningMeanStd with f64 batch moments stored as f32 (the device recipe)
     from oracle.synth_env import SynthVecEnvNP
     E, T, D = 32, 24, 23
-    envs = [SynthVecEnvNP(E, (D,), 5, 9, seed=r) for r in range(2)]
+    envs = [SynthVecEnvNP(E, (D,), 5, 9, seed=r) for r in range(world)]
     mean, var, count = np.zeros(D, np.float32), np.ones(D, np.float32), 0.0
 
     def upd(x):
