@@ -39,7 +39,12 @@
 // issued two chunks before its LDS store, 212 VGPRs, still 2 waves/SIMD) does not survive
 // compilation: the IR passes sink the restrict-const loads next to their LDS stores (asm
 // memory clobbers and sched_barrier do not pin them) and volatile loads get a vmcnt(0) each;
-// it needs direct-to-LDS loads (global_load_lds_dwordx4) and an LDS ring instead.
+// it needs direct-to-LDS loads (global_load_lds_dwordx4) and an LDS ring instead.  Built and
+// measured that way too (round 2): X rows and W planes by inline-asm LDS-DMA into a two-stage
+// 2 x 40 KB ring, one barrier per chunk, the swizzles on the source addresses, explicit
+// vmcnt(0) drains (hipcc's own LDS-DMA builtin makes every ds_read wait for the next stage):
+// correct, 256-262 us vs 250-256 us for this kernel on the same box -- neither the staging
+// instructions nor the second barrier are what bounds it.
 #include "x6.h"
 
 namespace tsrl {
