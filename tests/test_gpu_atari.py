@@ -332,6 +332,36 @@ def test_dqn_fused_conv1_matches_miopen(dev):
         torch.testing.assert_close(pa, pb, rtol=1e-3, atol=1e-4 * float(pb.abs().max()))
 
 
+def test_dqn_conv1_only_path_matches_miopen(dev):
+    """A trunk whose second convolution is not the Nature-DQN one (here grouped) takes the
+    conv1-only autograd path (_Conv1U8: tsrl_dqn_conv1_fwd forward, ReLU mask +
+    tsrl_dqn_conv1_wgrad backward): outputs and every parameter gradient against the same
+    module on MIOpen throughout."""
+    from torch import nn
+    from tianshou_amd.utils.net_atari import DQN, layer_init
+    torch.manual_seed(3)
+    a = DQN(4, 84, 84, (6,), device=dev, features_only=True, output_dim=512,
+            layer_init=layer_init).to(dev)
+    a.net[0][2] = layer_init(nn.Conv2d(32, 64, 4, stride=2, groups=2)).to(dev).to(
+        memory_format=torch.channels_last)
+    a._conv1_split = None
+    parts = a._conv1_parts()
+    assert parts is not None and parts[1] is None  # conv1 only
+    x = torch.randint(0, 256, (48, 4, 84, 84), dtype=torch.uint8, device=dev)
+    outs = []
+    for fused in (True, False):
+        a.fused_conv1 = fused
+        a.zero_grad(set_to_none=True)
+        y = a(x)[0]
+        g = torch.randn(y.shape, device=dev, generator=torch.Generator(device=dev).manual_seed(4))
+        y.backward(g)
+        outs.append((y.detach(), [p.grad.clone() for p in a.parameters()]))
+    (ya, ga), (yb, gb) = outs
+    torch.testing.assert_close(ya, yb, rtol=1e-4, atol=1e-5 * float(yb.abs().max()))
+    for pa, pb in zip(ga, gb):
+        torch.testing.assert_close(pa, pb, rtol=1e-3, atol=1e-4 * float(pb.abs().max()))
+
+
 def test_atari_shared_trunk_process_fn_wrapped_ring(dev):
     """As above on a ring that has wrapped (collect more steps than the buffer holds): the
     stacked obs / obs_next rows equal the env's FrameStack stream (oracle/synth_env.py) where
