@@ -278,6 +278,29 @@ def test_conv1_wgrad_u8_vs_f64(dev, n):
     assert torch.equal(gw2, gw.contiguous())
 
 
+def test_conv1_wgrad_u8_production_size(dev):
+    """tsrl_dqn_conv1_wgrad at the config-5 minibatch (8192 frame stacks: 512 workgroups x 50
+    chunks, the full partial-slab fold) against MIOpen's f32 weight gradient of the f32 frames:
+    within 2e-6 of the absolute-value product (both are f32 GEMMs of the same data)."""
+    from tianshou_amd.utils.net_atari import conv1_u8_wgrad
+    torch.manual_seed(7)
+    n = 8192
+    x = torch.randint(0, 256, (n, 4, 84, 84), dtype=torch.uint8, device=dev)
+    gy = torch.randn(n, 20, 20, 32, device=dev)
+    gy[torch.rand_like(gy) < 0.5] = 0.0
+    w = torch.empty(32, 4, 8, 8, device=dev)
+    gw, gb = conv1_u8_wgrad(x, gy, w, 255.0, True)
+    xf = (x.float() / 255.0)
+    g = gy.permute(0, 3, 1, 2)
+    ref = torch.nn.grad.conv2d_weight(xf, (32, 4, 8, 8), g, stride=4)
+    mag = torch.nn.grad.conv2d_weight(xf, (32, 4, 8, 8), g.abs(), stride=4)
+    assert bool(((gw - ref).abs() <= 2e-6 * mag + 1e-9).all()), float(((gw - ref).abs() / mag).max())
+    # bias: the f32 sum of 1.6M signed terms, within 1e-6 of the sum of their magnitudes
+    gb_ref = g.double().sum(dim=(0, 2, 3))
+    gb_mag = g.double().abs().sum(dim=(0, 2, 3))
+    assert bool(((gb.double() - gb_ref).abs() <= 1e-6 * gb_mag).all())
+
+
 @pytest.mark.parametrize("n", [1, 37, 1024])
 def test_conv1_u8_kernel_vs_f64(dev, n):
     """tsrl_dqn_conv1_fwd (uint8 frames, bf16 byte operands x 3-plane split weights) against
