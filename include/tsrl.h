@@ -428,6 +428,12 @@ int tsrl_ppo_cat_finalize(const double* sums, tsrl_ppo_params p, float* losses, 
 int tsrl_cat_logp(const float* x, const int64_t* act, int64_t b, int64_t num_actions, int mode,
                   float* out, void* stream);
 
+/* Categorical(logits).sample() of the Collector's policy step (pg.py:133-171): out[r] =
+ * argmax_a(logits[r][a] - log(-log(u[r][a]))) (Gumbel-max; first index on ties), logits and
+ * u [n][num_actions] f32 (u uniform in [0, 1), drawn by the caller), out [n] int64. */
+int tsrl_cat_gumbel_argmax(const float* logits, const float* u, int64_t n, int64_t num_actions,
+                           int64_t* out, void* stream);
+
 /* ---------------------------------------------------------------------------------
  * Fused actor/critic MLP of the PPO minibatch for the MuJoCo network shape
  * (tianshou/utils/models.py:34-97: Net(D, (64, 64), Tanh) trunks, ActorProb mu head

@@ -450,3 +450,26 @@ def test_atari_shared_trunk_process_fn_wrapped_ring(dev):
         assert np.array_equal(ridx[pr.cpu().numpy()], buf.next(ridx))
         np.testing.assert_allclose(v[pr].cpu().numpy(), vn.cpu().numpy(), rtol=1e-5,
                                    atol=1e-5 * float(vn.abs().max()))
+
+
+def test_gumbel_categorical_sample_distribution(dev):
+    """gumbel_sample (tsrl_cat_gumbel_argmax) draws from Categorical(logits): empirical
+    frequencies of 200k draws per row within 5 standard errors of softmax(logits), -inf
+    logits never drawn, and the stream follows torch.manual_seed (reproducible)."""
+    from tianshou_amd.policy.pg import gumbel_sample
+    logits = torch.tensor([[0.0, 1.0, -1.0, 2.0, 0.5, -3.0],
+                           [5.0, 5.0, 5.0, 5.0, 5.0, 5.0],
+                           [0.0, float("-inf"), 1.0, float("-inf"), -2.0, 0.0]], device=dev)
+    lg = torch.distributions.Categorical(logits=logits).logits
+    m = 200000
+    rep = lg.repeat(m, 1)
+    torch.manual_seed(0)
+    a = gumbel_sample(rep).view(m, 3)
+    p = torch.softmax(logits, -1).double()
+    for r in range(3):
+        f = torch.bincount(a[:, r], minlength=6).double() / m
+        se = (p[r] * (1 - p[r]) / m).sqrt()
+        assert bool(((f - p[r]).abs() <= 5 * se + 1e-12).all()), (r, f, p[r])
+    assert not bool(((a[:, 2] == 1) | (a[:, 2] == 3)).any())
+    torch.manual_seed(0)
+    assert torch.equal(gumbel_sample(rep).view(m, 3), a)

@@ -258,6 +258,32 @@ __global__ __launch_bounds__(TPB) void cat_logp_kernel(const float* xin, const i
     }
 }
 
+// Categorical(logits).sample() as one pass (Collector step, pg.py:133-171 -> dist.sample()):
+// the Gumbel-max form argmax_a(logits[a] - log(-log(u[a]))) with u ~ U[0, 1) drawn by the
+// caller (torch.rand_like: torch's own, graph-capturable stream), which samples exactly the
+// categorical distribution of the logits (first index on ties; -inf logits are never drawn).
+// Replaces torch's softmax + multinomial (exponential draw, argmax and its validity
+// reductions): ~14 small kernels per collector step for Atari-sized batches.
+__global__ __launch_bounds__(TPB) void cat_gumbel_argmax_kernel(const float* __restrict__ logits,
+                                                                const float* __restrict__ u,
+                                                                int64_t n, int64_t A,
+                                                                int64_t* __restrict__ out) {
+    const int64_t r = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (r >= n) return;
+    const float* lr = logits + r * A;
+    const float* ur = u + r * A;
+    float best = -INFINITY;
+    int64_t arg = 0;
+    for (int64_t a = 0; a < A; ++a) {
+        const float g = lr[a] - logf(-logf(ur[a]));
+        if (g > best) {
+            best = g;
+            arg = a;
+        }
+    }
+    out[r] = arg;
+}
+
 }  // namespace
 }  // namespace tsrl
 
@@ -308,5 +334,16 @@ extern "C" int tsrl_cat_logp(const float* x, const int64_t* act, int64_t b, int6
     hipLaunchKernelGGL(cat_logp_kernel, dim3((unsigned)grid), dim3(TPB), 0, as_stream(stream), x,
                        act, b, (int)num_actions, mode, out);
     TSRL_LAUNCH_CHECK("tsrl_cat_logp");
+    return 0;
+}
+
+extern "C" int tsrl_cat_gumbel_argmax(const float* logits, const float* u, int64_t n,
+                                      int64_t num_actions, int64_t* out, void* stream) {
+    TSRL_CHECK_ARG(n >= 0 && num_actions > 0, "tsrl_cat_gumbel_argmax: bad sizes");
+    if (n == 0) return 0;
+    TSRL_CHECK_ARG(logits && u && out, "tsrl_cat_gumbel_argmax: null pointer");
+    hipLaunchKernelGGL(cat_gumbel_argmax_kernel, dim3((unsigned)((n + TPB - 1) / TPB)), dim3(TPB),
+                       0, as_stream(stream), logits, u, n, num_actions, out);
+    TSRL_LAUNCH_CHECK("tsrl_cat_gumbel_argmax");
     return 0;
 }
