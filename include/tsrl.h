@@ -322,6 +322,11 @@ int tsrl_dqn_conv2_dgrad(const float* gy, int64_t n, const float* w, int64_t sw0
  * (ppo.py:146) and the u8 -> f32 frame conversion it needs: bytes exact in bf16, gy split
  * into 3 bf16 planes (f32 GEMM error), per-workgroup partials folded in fixed order (f64).
  * workspace: tsrl_dqn_conv1_wgrad_workspace_bytes(n) bytes. */
+/* y = max(y + bias, 0) in place over rows x C f32 (NHWC activations of a convolution run
+ * without bias; C % 4 == 0, 16-byte aligned; bias nullable): the bias add + ReLU of the
+ * trunk's Conv2d + ReLU pairs (examples/atari/atari_network.py:53-90) in one pass. */
+int tsrl_bias_relu_rows(float* y, const float* bias, int64_t rows, int64_t C, void* stream);
+
 int64_t tsrl_dqn_conv1_wgrad_workspace_bytes(int64_t n);
 int tsrl_dqn_conv1_wgrad(const uint8_t* frames, int64_t n, const float* gy, float scale,
                          float* gw, float* gb, void* workspace, int64_t ws_bytes, void* stream);

@@ -430,6 +430,24 @@ __global__ __launch_bounds__(256) void dqn_conv1_wgrad_reduce_kernel(
     else if (gb) gb[i - C1_OC * C1_KK] = (float)s;
 }
 
+// Bias + ReLU in place over NHWC rows (rows x C, C % 4 == 0): the epilogue of a library
+// convolution run without bias, one pass instead of torch's bias add and ReLU (two passes
+// over the activation).  y = max(y + b, 0) in f32, the same values as add then clamp_min.
+__global__ __launch_bounds__(256) void bias_relu_rows_kernel(float4* __restrict__ y,
+                                                             const float4* __restrict__ b,
+                                                             int64_t n4, int c4) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4;
+         i += (int64_t)gridDim.x * 256) {
+        const float4 bb = b ? b[i % c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 v = y[i];
+        v.x = fmaxf(v.x + bb.x, 0.0f);
+        v.y = fmaxf(v.y + bb.y, 0.0f);
+        v.z = fmaxf(v.z + bb.z, 0.0f);
+        v.w = fmaxf(v.w + bb.w, 0.0f);
+        y[i] = v;
+    }
+}
+
 }  // namespace
 }  // namespace tsrl
 
@@ -514,5 +532,20 @@ extern "C" int tsrl_dqn_conv1_wgrad(const uint8_t* frames, int64_t n, const floa
     hipLaunchKernelGGL(dqn_conv1_wgrad_reduce_kernel, dim3((W + 63) / 64), dim3(256), 0,
                        as_stream(stream), part, (int)nwg, 1.0f / scale, gw, gb);
     TSRL_LAUNCH_CHECK("tsrl_dqn_conv1_wgrad(reduce)");
+    return 0;
+}
+
+extern "C" int tsrl_bias_relu_rows(float* y, const float* bias, int64_t rows, int64_t C,
+                                   void* stream) {
+    TSRL_CHECK_ARG(rows >= 0 && C > 0 && C % 4 == 0, "tsrl_bias_relu_rows: need C %% 4 == 0");
+    if (rows == 0) return 0;
+    TSRL_CHECK_ARG(y && aligned16(y) && (!bias || aligned16(bias)),
+                   "tsrl_bias_relu_rows: y / bias must be 16-byte aligned");
+    const int64_t n4 = rows * C / 4;
+    const unsigned grid = (unsigned)std::min<int64_t>((n4 + 255) / 256, 8192);
+    hipLaunchKernelGGL(bias_relu_rows_kernel, dim3(grid), dim3(256), 0, as_stream(stream),
+                       reinterpret_cast<float4*>(y), reinterpret_cast<const float4*>(bias), n4,
+                       (int)(C / 4));
+    TSRL_LAUNCH_CHECK("tsrl_bias_relu_rows");
     return 0;
 }

@@ -108,6 +108,60 @@ class _Conv1U8(torch.autograd.Function):
         return None, gw, gb, None, None, None
 
 
+def bias_relu_(y: torch.Tensor, bias: Optional[torch.Tensor]) -> torch.Tensor:
+    """relu(y + bias) in place for a channels_last [n, C, h, w] f32 activation on the GPU
+    (tsrl_bias_relu_rows: one pass); other tensors take torch's add + relu."""
+    n, C = y.shape[0], y.shape[1]
+    if (y.is_cuda and y.dtype == torch.float32 and C % 4 == 0 and y.dim() == 4 and
+            y.is_contiguous(memory_format=torch.channels_last) and y.data_ptr() % 16 == 0 and
+            (bias is None or (bias.is_contiguous() and bias.data_ptr() % 16 == 0))):
+        _C.check(_C.lib().tsrl_bias_relu_rows(
+            y.data_ptr(), bias.data_ptr() if bias is not None else None,
+            n * y.shape[2] * y.shape[3], C, _C.stream_ptr(y.device)), "tsrl_bias_relu_rows")
+        return y
+    if bias is not None:
+        y = y.add_(bias.view(1, -1, 1, 1))
+    return torch.relu_(y)
+
+
+class _ConvBiasReLU(torch.autograd.Function):
+    """Conv2d + ReLU with the bias add and the ReLU as one pass (bias_relu_) after the library
+    convolution run without bias.  Backward: the ReLU mask, then the library's data / weight /
+    bias gradients (the same calls as autograd of Conv2d + ReLU)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, conv):
+        z = bias_relu_(torch.nn.functional.conv2d(x, weight, None, conv.stride, conv.padding,
+                                                  conv.dilation, conv.groups), bias)
+        ctx.save_for_backward(x, weight, z)
+        ctx.conv = conv
+        ctx.has_bias = bias is not None
+        return z
+
+    @staticmethod
+    def backward(ctx, gz):
+        x, weight, z = ctx.saved_tensors
+        cv = ctx.conv
+        gy = torch.ops.aten.threshold_backward(gz, z, 0.0)
+        gx, gw, gb = torch.ops.aten.convolution_backward(
+            gy, x, weight, [weight.shape[0]] if ctx.has_bias else None, cv.stride, cv.padding,
+            cv.dilation, False, (0, 0), cv.groups,
+            (ctx.needs_input_grad[0], True, ctx.has_bias))
+        return gx, gw, gb, None
+
+
+def _run_rest(rest: nn.Module, h: torch.Tensor) -> torch.Tensor:
+    """The layers after the fused first block; a leading zero-padding Conv2d + ReLU pair runs
+    as _ConvBiasReLU."""
+    if (len(rest) >= 2 and isinstance(rest[0], nn.Conv2d) and isinstance(rest[1], nn.ReLU) and
+            rest[0].padding_mode == "zeros" and isinstance(rest[0].padding, tuple) and
+            h.is_cuda):
+        cv = rest[0]
+        h = _ConvBiasReLU.apply(h, cv.weight, cv.bias, cv)
+        return rest[2:](h)
+    return rest(h)
+
+
 def _nhwc(t: torch.Tensor) -> torch.Tensor:
     """The [n, h, w, c] contiguous tensor behind an [n, c, h, w] channels_last tensor (a copy
     only when it is not channels_last)."""
@@ -123,7 +177,7 @@ class _Conv12U8(torch.autograd.Function):
     @staticmethod
     def forward(ctx, obs, w1, b1, w2, b2, conv1, conv2, lut, scale):
         z1 = conv1_u8(obs, conv1, scale)
-        z2 = torch.relu_(torch.nn.functional.conv2d(z1, w2, b2, conv2.stride))
+        z2 = bias_relu_(torch.nn.functional.conv2d(z1, w2, None, conv2.stride), b2)
         ctx.save_for_backward(obs, w1, w2, z1, z2)
         ctx.lut = lut
         ctx.scale = scale
@@ -247,7 +301,7 @@ class DQN(nn.Module):
             else:
                 h = _Conv1U8.apply(obs.contiguous(), conv.weight, conv.bias, conv, lut,
                                    float(self.scale))
-            h = rest(h)
+            h = _run_rest(rest, h)
             return (outer(h) if outer is not None else h), state
         if self.channels_last and obs.dim() == 4 and obs.dtype == torch.uint8 and \
                 obs.is_cuda and self.scale:
