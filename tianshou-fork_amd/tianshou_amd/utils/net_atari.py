@@ -150,6 +150,34 @@ class _ConvBiasReLU(torch.autograd.Function):
         return gx, gw, gb, None
 
 
+class _FlattenLinear(torch.autograd.Function):
+    """Flatten + Linear over a channels_last [n, C, h, w] activation without the NCHW copy that
+    Flatten needs: the Linear runs on the NHWC rows (a view) against its weight with the input
+    features permuted to (h, w, C) order -- the same products, summed in another order -- and
+    the input gradient comes back as a channels_last view."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        n, C, H, W = x.shape
+        O = weight.shape[0]
+        xf = x.permute(0, 2, 3, 1).reshape(n, H * W * C)
+        wp = weight.view(O, C, H, W).permute(0, 2, 3, 1).reshape(O, H * W * C)
+        ctx.save_for_backward(xf, wp)
+        ctx.shape = (n, C, H, W)
+        ctx.has_bias = bias is not None
+        return torch.nn.functional.linear(xf, wp, bias)
+
+    @staticmethod
+    def backward(ctx, gy):
+        xf, wp = ctx.saved_tensors
+        n, C, H, W = ctx.shape
+        O = wp.shape[0]
+        gx = (gy @ wp).view(n, H, W, C).permute(0, 3, 1, 2) if ctx.needs_input_grad[0] else None
+        gw = (gy.t() @ xf).view(O, H, W, C).permute(0, 3, 1, 2).reshape(O, C * H * W)
+        gb = gy.sum(0) if ctx.has_bias else None
+        return gx, gw, gb
+
+
 def _run_rest(rest: nn.Module, h: torch.Tensor) -> torch.Tensor:
     """The layers after the fused first block; a leading zero-padding Conv2d + ReLU pair runs
     as _ConvBiasReLU."""
@@ -301,6 +329,15 @@ class DQN(nn.Module):
             else:
                 h = _Conv1U8.apply(obs.contiguous(), conv.weight, conv.bias, conv, lut,
                                    float(self.scale))
+            if (outer is not None and len(rest) and isinstance(rest[-1], nn.Flatten) and
+                    rest[-1].start_dim == 1 and rest[-1].end_dim == -1 and len(outer) and
+                    isinstance(outer[0], nn.Linear)):
+                h = _run_rest(rest[:-1], h)
+                if h.dim() == 4 and h.is_contiguous(memory_format=torch.channels_last):
+                    h = _FlattenLinear.apply(h, outer[0].weight, outer[0].bias)
+                else:
+                    h = outer[0](h.flatten(1))
+                return outer[1:](h), state
             h = _run_rest(rest, h)
             return (outer(h) if outer is not None else h), state
         if self.channels_last and obs.dim() == 4 and obs.dtype == torch.uint8 and \
