@@ -154,6 +154,11 @@ __global__ __launch_bounds__(256, 2) void dqn_conv1_fwd_kernel(
 // with k = (tap, co), 4 taps x 64 channels = 256.  Workgroups of class cls = blockIdx.y stage
 // that class's split sub-kernel (3 planes, 48 KB, same swizzled rows as conv1); a lane's B
 // fragment is 8 consecutive channels of gy2 (NHWC, 32 contiguous bytes) split in registers.
+// Tried and measured (tools/atari_layer_bench.py, 8192 rows): splitting gy2 into bf16 planes
+// once in a separate pass (each element feeds 16 products here) and loading the planes
+// tap by tap, 12 loads ahead of the MFMAs: bit-identical but 0.80 ms against 0.60 ms for
+// this kernel -- the per-product split is not the limit; the 32 gathered 16-byte loads per
+// lane and tile issued up front are what keep the MFMAs fed at 2 waves per SIMD.
 constexpr int C2_CI = 32, C2_CO = 64, C2_IN = 20, C2_OUT = 9;
 constexpr int C2_CPIX = (C2_IN / 2) * (C2_IN / 2);  // 100 input pixels per class per sample
 
