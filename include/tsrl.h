@@ -327,6 +327,17 @@ int tsrl_dqn_conv2_dgrad(const float* gy, int64_t n, const float* w, int64_t sw0
  * trunk's Conv2d + ReLU pairs (examples/atari/atari_network.py:53-90) in one pass. */
 int tsrl_bias_relu_rows(float* y, const float* bias, int64_t rows, int64_t C, void* stream);
 
+/* ReLU backward of the trunk's Conv2d + ReLU pairs fused with the bias gradient:
+ * gy = (z > 0) * gz over rows x C f32 NHWC rows (gy may alias gz; 16-byte aligned;
+ * C % 4 == 0, C / 4 a power of two, C <= 1024) and, when gb is not NULL, gb[c] = sum_r gy[r][c]
+ * (per-workgroup f32 partials folded in f64 in fixed order; ws of
+ * tsrl_relu_bwd_rows_workspace_bytes(rows, C) bytes).  Replaces threshold_backward + the bias
+ * reduction of convolution_backward in loss.backward() (ppo.py:146) for
+ * examples/atari/atari_network.py:53-90. */
+int64_t tsrl_relu_bwd_rows_workspace_bytes(int64_t rows, int64_t C);
+int tsrl_relu_bwd_rows(const float* gz, const float* z, float* gy, int64_t rows, int64_t C,
+                       float* gb, void* ws, int64_t ws_bytes, void* stream);
+
 int64_t tsrl_dqn_conv1_wgrad_workspace_bytes(int64_t n);
 int tsrl_dqn_conv1_wgrad(const uint8_t* frames, int64_t n, const float* gy, float scale,
                          float* gw, float* gb, void* workspace, int64_t ws_bytes, void* stream);

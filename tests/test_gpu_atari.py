@@ -248,6 +248,43 @@ def test_conv2_dgrad_kernel_vs_f64(dev, n):
     assert bool((err <= 1e-6 * mag + 1e-12).all())
 
 
+@pytest.mark.parametrize("rows,C", [(1, 64), (37 * 49, 64), (8192 * 81, 64), (1000, 4),
+                                    (333, 32), (4097, 512)])
+def test_relu_bwd_rows_vs_torch(dev, rows, C):
+    """tsrl_relu_bwd_rows: gy bit-identical to threshold_backward, gb within 1e-6 of the f64
+    column sum relative to the sum of magnitudes (f32 partials, f64 fold); in place
+    (gy aliasing gz) and without gb; through relu_bwd_bias on channels_last activations."""
+    from tianshou_amd import _C
+    from tianshou_amd.utils.net_atari import relu_bwd_bias
+    torch.manual_seed(rows + C)
+    gz = torch.randn(rows, C, device=dev)
+    z = torch.relu(torch.randn(rows, C, device=dev))
+    ref = torch.ops.aten.threshold_backward(gz, z, 0.0)
+    nb = int(_C.lib().tsrl_relu_bwd_rows_workspace_bytes(rows, C))
+    ws = torch.full((nb,), 0xFF, dtype=torch.uint8, device=dev)
+    gy = torch.full_like(gz, float("nan"))
+    gb = torch.full((C,), float("nan"), device=dev)
+    s_ = _C.stream_ptr(dev)
+    _C.check(_C.lib().tsrl_relu_bwd_rows(_C.ptr(gz), _C.ptr(z), _C.ptr(gy), rows, C, _C.ptr(gb),
+                                         ws.data_ptr(), nb, s_), "relu_bwd")
+    assert torch.equal(gy, ref)
+    r64 = ref.double()
+    err = (gb.double() - r64.sum(0)).abs()
+    assert bool((err <= 1e-6 * r64.abs().sum(0) + 1e-30).all()), float(err.max())
+    g2 = gz.clone()
+    _C.check(_C.lib().tsrl_relu_bwd_rows(_C.ptr(g2), _C.ptr(z), _C.ptr(g2), rows, C, None, None,
+                                         0, s_), "relu_bwd in place")
+    assert torch.equal(g2, ref)
+    assert _C.lib().tsrl_relu_bwd_rows(_C.ptr(gz), _C.ptr(z), _C.ptr(gy), rows, C, _C.ptr(gb),
+                                       ws.data_ptr(), nb - 16, s_) != 0
+    if rows % 49 == 0:
+        n = rows // 49
+        to4 = lambda t: t.view(n, 7, 7, C).permute(0, 3, 1, 2)
+        gy4, gb4 = relu_bwd_bias(to4(gz), to4(z), True)
+        assert gy4.is_contiguous(memory_format=torch.channels_last)
+        assert torch.equal(gy4, to4(ref)) and torch.equal(gb4, gb)
+
+
 @pytest.mark.parametrize("n", [1, 5, 37, 300])
 def test_conv1_wgrad_u8_vs_f64(dev, n):
     """tsrl_dqn_conv1_wgrad (bytes exact in bf16, gy split in 3 bf16 planes, per-workgroup

@@ -540,6 +540,113 @@ extern "C" int tsrl_dqn_conv1_wgrad(const uint8_t* frames, int64_t n, const floa
     return 0;
 }
 
+// ReLU backward of the Conv2d + ReLU pairs fused with their bias gradient: gy = (z > 0) * gz
+// over rows x C (NHWC rows) and, per workgroup of a contiguous row range, the column sums of gy
+// (f32, LDS tree over the row lanes) into partials[blk][C]; relu_bwd_fold_kernel adds the
+// partials in f64 in block order (deterministic).  One read of gz and z and one write of gy
+// instead of threshold_backward plus a separate bias reduction over gy.
+__global__ __launch_bounds__(256) void relu_bwd_rows_kernel(const float4* gz,
+                                                            const float4* __restrict__ z,
+                                                            float4* gy, int64_t rows, int c4,
+                                                            int64_t rpb,
+                                                            float4* __restrict__ part) {
+    __shared__ float4 red[256];
+    const int t = threadIdx.x;
+    const int cg = t % c4, rl = t / c4, rstep = 256 / c4;
+    const int64_t r0 = (int64_t)blockIdx.x * rpb;
+    const int64_t r1 = std::min<int64_t>(rows, r0 + rpb);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t r = r0 + rl; r < r1; r += rstep) {
+        const int64_t i = r * c4 + cg;
+        const float4 g = gz[i], m = z[i];
+        float4 v;
+        v.x = m.x > 0.0f ? g.x : 0.0f;
+        v.y = m.y > 0.0f ? g.y : 0.0f;
+        v.z = m.z > 0.0f ? g.z : 0.0f;
+        v.w = m.w > 0.0f ? g.w : 0.0f;
+        gy[i] = v;
+        acc.x += v.x;
+        acc.y += v.y;
+        acc.z += v.z;
+        acc.w += v.w;
+    }
+    if (!part) return;
+    red[t] = acc;
+    __syncthreads();
+    for (int st = 128; st >= c4; st >>= 1) {
+        if (t < st) {
+            const float4 o = red[t + st];
+            red[t].x += o.x;
+            red[t].y += o.y;
+            red[t].z += o.z;
+            red[t].w += o.w;
+        }
+        __syncthreads();
+    }
+    if (t < c4) part[(int64_t)blockIdx.x * c4 + t] = red[t];
+}
+
+// one workgroup per column: strided f64 sums over the partial rows, then a fixed-order LDS tree
+__global__ __launch_bounds__(256) void relu_bwd_fold_kernel(const float* __restrict__ part,
+                                                            int64_t nblk, int64_t C,
+                                                            float* __restrict__ gb) {
+    __shared__ double red[256];
+    const int t = threadIdx.x;
+    const int64_t c = blockIdx.x;
+    double s = 0.0;
+    for (int64_t b = t; b < nblk; b += 256) s += (double)part[b * C + c];
+    red[t] = s;
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+        if (t < st) red[t] += red[t + st];
+        __syncthreads();
+    }
+    if (t == 0) gb[c] = (float)red[0];
+}
+
+static int64_t relu_bwd_nblk(int64_t rows, int64_t C) {
+    const int64_t rstep = 256 / (C / 4);
+    // >= 16 workgroups per CU at the trunk's sizes (memory-level parallelism), ~10 rows each
+    return std::max<int64_t>(1, std::min<int64_t>(4096, (rows + 4 * rstep - 1) / (4 * rstep)));
+}
+
+extern "C" int64_t tsrl_relu_bwd_rows_workspace_bytes(int64_t rows, int64_t C) {
+    if (rows <= 0 || C <= 0 || C % 4 || C > 1024) return 0;
+    return relu_bwd_nblk(rows, C) * C * 4;
+}
+
+extern "C" int tsrl_relu_bwd_rows(const float* gz, const float* z, float* gy, int64_t rows,
+                                  int64_t C, float* gb, void* ws, int64_t ws_bytes,
+                                  void* stream) {
+    const int64_t c4 = C / 4;
+    TSRL_CHECK_ARG(rows >= 0 && C > 0 && C % 4 == 0 && C <= 1024 && (c4 & (c4 - 1)) == 0,
+                   "tsrl_relu_bwd_rows: need C %% 4 == 0, C / 4 a power of two, C <= 1024");
+    if (rows == 0) {
+        if (gb) (void)hipMemsetAsync(gb, 0, C * sizeof(float), as_stream(stream));
+        return 0;
+    }
+    TSRL_CHECK_ARG(gz && z && gy, "tsrl_relu_bwd_rows: null pointer");
+    TSRL_CHECK_ARG(aligned16(gz) && aligned16(z) && aligned16(gy),
+                   "tsrl_relu_bwd_rows: gz / z / gy must be 16-byte aligned");
+    const int64_t nblk = relu_bwd_nblk(rows, C);
+    if (gb)
+        TSRL_CHECK_ARG(ws && aligned16(ws) && ws_bytes >= nblk * C * 4,
+                       "tsrl_relu_bwd_rows: workspace too small");
+    const int64_t rpb = (rows + nblk - 1) / nblk;
+    hipLaunchKernelGGL(relu_bwd_rows_kernel, dim3((unsigned)nblk), dim3(256), 0,
+                       as_stream(stream), reinterpret_cast<const float4*>(gz),
+                       reinterpret_cast<const float4*>(z), reinterpret_cast<float4*>(gy), rows,
+                       (int)c4, rpb, gb ? reinterpret_cast<float4*>(ws) : nullptr);
+    TSRL_LAUNCH_CHECK("tsrl_relu_bwd_rows");
+    if (gb) {
+        hipLaunchKernelGGL(relu_bwd_fold_kernel, dim3((unsigned)C), dim3(256),
+                           0, as_stream(stream), reinterpret_cast<const float*>(ws), nblk, C,
+                           gb);
+        TSRL_LAUNCH_CHECK("tsrl_relu_bwd_rows (fold)");
+    }
+    return 0;
+}
+
 extern "C" int tsrl_bias_relu_rows(float* y, const float* bias, int64_t rows, int64_t C,
                                    void* stream) {
     TSRL_CHECK_ARG(rows >= 0 && C > 0 && C % 4 == 0, "tsrl_bias_relu_rows: need C %% 4 == 0");

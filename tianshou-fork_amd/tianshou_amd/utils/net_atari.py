@@ -124,6 +124,38 @@ def bias_relu_(y: torch.Tensor, bias: Optional[torch.Tensor]) -> torch.Tensor:
     return torch.relu_(y)
 
 
+RELU_BWD_FUSED = True
+
+
+def relu_bwd_bias(gz: torch.Tensor, z: torch.Tensor, want_bias: bool):
+    """(gy, gb): gy = (z > 0) * gz and, when want_bias, gb = gy summed over (n, h, w), in one
+    pass over channels_last f32 [n, C, h, w] activations on the GPU (tsrl_relu_bwd_rows; f64
+    fold of per-workgroup partials).  Other tensors take threshold_backward and return
+    gb = None, leaving the bias gradient to convolution_backward."""
+    C = z.shape[1] if z.dim() == 4 else 0
+    c4 = C // 4
+    cl = torch.channels_last
+    if (RELU_BWD_FUSED and z.is_cuda and z.dtype == torch.float32 and gz.dtype == torch.float32
+            and z.dim() == 4 and gz.shape == z.shape and C % 4 == 0 and 0 < C <= 1024 and
+            (c4 & (c4 - 1)) == 0 and z.is_contiguous(memory_format=cl) and
+            gz.is_contiguous(memory_format=cl) and z.data_ptr() % 16 == 0 and
+            gz.data_ptr() % 16 == 0):
+        rows = z.shape[0] * z.shape[2] * z.shape[3]
+        gy = torch.empty_like(z, memory_format=cl)
+        gb = ws = None
+        nb = 0
+        if want_bias:
+            gb = torch.empty(C, dtype=torch.float32, device=z.device)
+            nb = int(_C.lib().tsrl_relu_bwd_rows_workspace_bytes(rows, C))
+            ws = torch.empty(max(nb, 16), dtype=torch.uint8, device=z.device)
+        _C.check(_C.lib().tsrl_relu_bwd_rows(
+            gz.data_ptr(), z.data_ptr(), gy.data_ptr(), rows, C,
+            gb.data_ptr() if gb is not None else None, ws.data_ptr() if ws is not None else None,
+            nb, _C.stream_ptr(z.device)), "tsrl_relu_bwd_rows")
+        return gy, gb
+    return torch.ops.aten.threshold_backward(gz, z, 0.0), None
+
+
 class _ConvBiasReLU(torch.autograd.Function):
     """Conv2d + ReLU with the bias add and the ReLU as one pass (bias_relu_) after the library
     convolution run without bias.  Backward: the ReLU mask, then the library's data / weight /
@@ -142,12 +174,13 @@ class _ConvBiasReLU(torch.autograd.Function):
     def backward(ctx, gz):
         x, weight, z = ctx.saved_tensors
         cv = ctx.conv
-        gy = torch.ops.aten.threshold_backward(gz, z, 0.0)
-        gx, gw, gb = torch.ops.aten.convolution_backward(
-            gy, x, weight, [weight.shape[0]] if ctx.has_bias else None, cv.stride, cv.padding,
+        gy, gb = relu_bwd_bias(gz, z, ctx.has_bias)
+        lib_bias = ctx.has_bias and gb is None
+        gx, gw, gb2 = torch.ops.aten.convolution_backward(
+            gy, x, weight, [weight.shape[0]] if lib_bias else None, cv.stride, cv.padding,
             cv.dilation, False, (0, 0), cv.groups,
-            (ctx.needs_input_grad[0], True, ctx.has_bias))
-        return gx, gw, gb, None
+            (ctx.needs_input_grad[0], True, lib_bias))
+        return gx, gw, gb if gb is not None else gb2, None
 
 
 class _FlattenLinear(torch.autograd.Function):
@@ -216,11 +249,14 @@ class _Conv12U8(torch.autograd.Function):
     def backward(ctx, gz2):
         obs, w1, w2, z1, z2 = ctx.saved_tensors
         n = obs.shape[0]
-        gy2 = torch.ops.aten.threshold_backward(gz2, z2, 0.0)
+        gy2, gb2 = relu_bwd_bias(gz2, z2, ctx.bias[1])
         gy2 = gy2.contiguous(memory_format=torch.channels_last)
-        _, gw2, gb2 = torch.ops.aten.convolution_backward(
-            gy2, z1, w2, [w2.shape[0]] if ctx.bias[1] else None, (2, 2), (0, 0), (1, 1), False,
-            (0, 0), 1, (False, True, ctx.bias[1]))
+        lib_bias = ctx.bias[1] and gb2 is None
+        _, gw2, gb2_ = torch.ops.aten.convolution_backward(
+            gy2, z1, w2, [w2.shape[0]] if lib_bias else None, (2, 2), (0, 0), (1, 1), False,
+            (0, 0), 1, (False, True, lib_bias))
+        if gb2 is None:
+            gb2 = gb2_
         gy1 = torch.empty((n, 20, 20, 32), dtype=torch.float32, device=obs.device)
         g2 = _nhwc(gy2)
         _C.check(_C.lib().tsrl_dqn_conv2_dgrad(_C.ptr(g2), n, w2.data_ptr(), *w2.stride(),

@@ -58,6 +58,10 @@ def main():
         res["relu_"] = timed(lambda: torch.relu_(y), a.iters)
         res["relu_bwd"] = timed(lambda: torch.ops.aten.threshold_backward(gy, y, 0.0), a.iters)
         res["bias_grad"] = timed(lambda: gy.sum((0, 2, 3)), a.iters)
+        from tianshou_amd.utils.net_atari import relu_bwd_bias
+        gyc = gy.contiguous(memory_format=cl)
+        yc = y.contiguous(memory_format=cl)
+        res["relu_bwd+bias_grad fused"] = timed(lambda: relu_bwd_bias(gyc, yc, True), a.iters)
         line = " ".join(f"{kk} {v:7.3f} ms" for kk, v in res.items())
         print(f"conv {cin}->{cout} k{k} s{s} out {ho}x{ho}: {line}  | fwd "
               f"{flop / res['fwd'] / 1e9:6.1f} dgrad {flop / res['dgrad'] / 1e9:6.1f} "
