@@ -392,6 +392,43 @@ def test_dqn_fused_conv1_matches_miopen(dev):
         torch.testing.assert_close(pa, pb, rtol=1e-3, atol=1e-4 * float(pb.abs().max()))
 
 
+def test_dqn_relu_bwd_fused_path_taken(dev, monkeypatch):
+    """The production trunk's conv2 and conv3 ReLU backward + bias gradient go through
+    tsrl_relu_bwd_rows (one call each, NHWC rows n*81 and n*49 of 64 channels), and the result
+    matches threshold_backward + the library bias gradient: outputs bit-identical, every
+    gradient within f32 summation error (the same gy; the library's split-K weight gradients
+    and the bias sums add in another order)."""
+    from tianshou_amd import _C
+    from tianshou_amd.utils import net_atari
+    torch.manual_seed(3)
+    a = net_atari.DQN(4, 84, 84, (6,), device=dev, features_only=True, output_dim=512,
+                      layer_init=net_atari.layer_init).to(dev)
+    x = torch.randint(0, 256, (96, 4, 84, 84), dtype=torch.uint8, device=dev)
+    lib = _C.lib()
+    real = lib.tsrl_relu_bwd_rows
+    calls = []
+
+    def spy(*args):
+        calls.append((args[3], args[4]))
+        return real(*args)
+
+    monkeypatch.setattr(lib, "tsrl_relu_bwd_rows", spy)
+    outs = []
+    for fused in (True, False):
+        monkeypatch.setattr(net_atari, "RELU_BWD_FUSED", fused)
+        a.zero_grad(set_to_none=True)
+        y = a(x)[0]
+        g = torch.randn(y.shape, device=dev, generator=torch.Generator(device=dev).manual_seed(4))
+        y.backward(g)
+        outs.append((y.detach(), [(n_, p.grad.clone()) for n_, p in a.named_parameters()]))
+    assert sorted(calls) == [(96 * 49, 64), (96 * 81, 64)]
+    (ya, ga), (yb, gb) = outs
+    assert torch.equal(ya, yb)
+    for (name, pa), (_, pb) in zip(ga, gb):
+        torch.testing.assert_close(pa, pb, rtol=1e-5, atol=1e-6 * float(pb.abs().max()),
+                                   msg=name)
+
+
 def test_dqn_conv1_only_path_matches_miopen(dev):
     """A trunk whose second convolution is not the Nature-DQN one (here grouped) takes the
     conv1-only autograd path (_Conv1U8: tsrl_dqn_conv1_fwd forward, ReLU mask +
