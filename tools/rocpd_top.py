@@ -2,6 +2,7 @@
 python tools/rocpd_top.py <db> [N] [--last-ms MS]  -> name, calls, total ms, mean us (top N by
 total); --last-ms keeps only the kernels that start in the last MS milliseconds of the trace
 (a steady-state window: e.g. the last timed iteration, after warm-up and MIOpen's find)."""
+import os
 import sqlite3
 import sys
 
@@ -12,6 +13,8 @@ if "--last-ms" in args:
     last_ms = float(args[i + 1])
     del args[i:i + 2]
 db = args[0]
+if not os.path.isfile(db):
+    sys.exit(__doc__)
 n = int(args[1]) if len(args) > 1 else 30
 c = sqlite3.connect(db)
 where, params = "", ()
