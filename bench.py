@@ -131,6 +131,28 @@ class GaeTimer:
         return float(np.mean(ts)) if ts else float("nan")
 
 
+def gae_pmc_traffic(E: int, T: int):
+    """(HBM bytes per GAE launch, note) from the committed rocprofv3 --pmc FETCH_SIZE /
+    WRITE_SIZE passes of the same kernel and shape (FETCH doubled per the gfx950
+    calibration).  PMC collection needs the profiler, so the bench does not re-measure it;
+    the record names the sha256 of the kernel source it was measured on, and a different
+    csrc/gae.hip makes the figure stale: then traffic is null and the note says why."""
+    import hashlib
+    import glob
+    if (E, T) != (4096, 2048):
+        return None, "no PMC record for this shape"
+    src = os.path.join(ROOT, "tianshou-fork_amd", "csrc", "gae.hip")
+    with open(src, "rb") as f:
+        sha = hashlib.sha256(f.read()).hexdigest()
+    for pmc in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_gae_pmc.json")), reverse=True):
+        with open(pmc) as f:
+            d = json.load(f)["derived"]
+        if d.get("source_sha256") == sha:
+            return d["traffic_bytes"], f"{os.path.relpath(pmc, ROOT)} (gae.hip sha256 {sha[:12]})"
+    return None, (f"stale: no profiles/r*_gae_pmc.json measured on this gae.hip "
+                  f"(sha256 {sha[:12]}); re-run tools/pmc_gae.py")
+
+
 def build_atari(args, dev, rank):
     """BASELINE config 5: examples/atari/atari_ppo.py's PPO (shared Nature-DQN trunk,
     Categorical(logits), frame-stack buffer with save_only_last_obs / ignore_obs_next) on the
@@ -319,14 +341,7 @@ def main():
     gae_ms = timer.mean_ms()
     gae_bytes = GAE_BYTES_PER_TRANSITION * n
     achieved = gae_bytes / (gae_ms * 1e-3) / 1e9
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "r01_gae_pmc.json")
-    if os.path.exists(pmc) and E == 4096 and T == 2048:
-        # HBM bytes per launch of the same kernel/shape from rocprofv3 --pmc FETCH_SIZE /
-        # WRITE_SIZE passes (FETCH doubled per the gfx950 calibration), committed under
-        # profiles/; PMC collection needs the profiler, so it is not re-measured here.
-        with open(pmc) as f:
-            traffic = json.load(f)["derived"]["traffic_bytes"]
+    traffic, traffic_note = gae_pmc_traffic(E, T)
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -368,6 +383,7 @@ def main():
             "roofline": {"kernel": "tsrl_gae (gae_rows_staged_kernel)", "bound": "hbm",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": traffic_note,
                          "launch_us": gae_ms * 1e3,
                          "launch_us_each": [round(t * 1e3, 2) for t in timer.each_ms()],
                          "bytes_per_launch": gae_bytes},

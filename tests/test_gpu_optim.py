@@ -93,3 +93,68 @@ def test_clip_adam_split_epilogue_equals_split_w(D):
         assert torch.equal(got.view(torch.int32), want.view(torch.int32)), f"step {step}"
         for p, r in zip(ac.parameters(), raw):
             assert torch.equal(p.grad, r)
+
+
+def test_clip_adam_resumes_loaded_state():
+    """optim.load_state_dict() on an optimiser whose storage the flat Adam pass owns: the
+    loaded moments / step counts (not the flat buffers' later values) are what the next
+    clip_adam continues from -- the same trajectory as torch Adam resumed from that state."""
+    import copy
+    from tianshou_amd.policy import fused_mlp
+    from tianshou_amd.utils.models import get_actor_critic, init_actor_critic
+    from tianshou_amd.utils.net import ActorCritic
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(2)
+    nets = []
+    for _ in range(2):
+        a, c = get_actor_critic((24,), (64, 64), (5,), dev)
+        nets.append((a.to(dev), c.to(dev)))
+    init_actor_critic(*nets[0])
+    ac0, ac1 = ActorCritic(*nets[0]), ActorCritic(*nets[1])
+    ac1.load_state_dict(ac0.state_dict())
+    opt_ref = torch.optim.Adam(ac0.parameters(), lr=3e-4)
+    opt = torch.optim.Adam(ac1.parameters(), lr=3e-4)
+    fm = fused_mlp.FusedActorCritic(fused_mlp.match(*nets[1]), ac1.parameters())
+    assert fm.bind_adam(opt)
+    g = torch.Generator(device=dev).manual_seed(7)
+
+    def grads():
+        return [torch.randn(p.shape, device=dev, generator=g) for p in ac0.parameters()]
+
+    def ref_step(gs):
+        for p, gr in zip(ac0.parameters(), gs):
+            p.grad = gr.clone()
+        torch.nn.utils.clip_grad_norm_(ac0.parameters(), max_norm=0.5)
+        opt_ref.step()
+
+    def flat_step(gs):
+        assert fm.adam_bound(opt)
+        fm.bind_grads()
+        for p, gr in zip(ac1.parameters(), gs):
+            p.grad.copy_(gr)
+        fm.clip_adam(0.5)
+
+    for _ in range(3):
+        gs = grads()
+        ref_step(gs)
+        flat_step(gs)
+    torch.cuda.synchronize()
+    saved_opt = copy.deepcopy(opt.state_dict())
+    saved_par = copy.deepcopy(ac1.state_dict())
+    for _ in range(2):  # steps the flat storage takes and then forgets
+        flat_step(grads())
+    ac1.load_state_dict(saved_par)
+    opt.load_state_dict(saved_opt)
+    assert fm.adam_bound(opt)  # re-binds the loaded state into the flat storage
+    for p in ac1.parameters():
+        assert opt.state[p]["exp_avg"].data_ptr() != 0
+    for _ in range(3):
+        gs = grads()
+        ref_step(gs)
+        flat_step(gs)
+    torch.cuda.synchronize()
+    for (n0, p0), p1 in zip(ac0.named_parameters(), ac1.parameters()):
+        np.testing.assert_allclose(p1.detach().cpu().numpy(), p0.detach().cpu().numpy(),
+                                   rtol=1e-5, atol=1e-7, err_msg=n0)
+    for p0, p1 in zip(ac0.parameters(), ac1.parameters()):
+        assert float(opt.state[p1]["step"]) == float(opt_ref.state[p0]["step"]) == 6.0

@@ -17,8 +17,14 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("tag", ["recompute", "graph"])
+@pytest.mark.parametrize("tag", ["recompute", "graph", "graph_torch_adam"])
 def test_scheduled_updates_match_reference(golden_dir, tag):
+    """graph_torch_adam: the "graph" golden with the flat Adam pass off, so torch's capturable
+    fused Adam runs inside the captured learn graph with its float lr baked in: each schedule
+    step must re-capture (the lr is part of the graph key), or later updates would replay the
+    first update's lr."""
+    torch_adam = tag == "graph_torch_adam"
+    tag = "graph" if torch_adam else tag
     from tianshou_amd.data import Batch, VectorReplayBuffer
     from tianshou_amd.env import Box
     from tianshou_amd.policy import PPOPolicy
@@ -36,6 +42,7 @@ def test_scheduled_updates_match_reference(golden_dir, tag):
                        ent_coef=0.01, reward_normalization=True, advantage_normalization=True,
                        recompute_advantage=cfg["recompute"], eps_clip=0.2).to(dev)
     assert policy._fused and policy._mlp is not None
+    policy.fused_adam = not torch_adam
     policy.load_state_dict({k[len(p + "init_"):]: torch.as_tensor(z[k]) for k in z.files
                             if k.startswith(p + "init_")})
     policy.lr_scheduler = get_linear_lr_schedular(optim, step_per_epoch=3000,
@@ -61,7 +68,11 @@ def test_scheduled_updates_match_reference(golden_dir, tag):
         assert policy.ret_rms.var == pytest.approx(rr[1], rel=1e-5)
         assert policy.ret_rms.count == int(rr[2])
         graphs.append(policy._learn_graph["graph"] if policy._learn_graph else None)
-    if tag == "graph":
+    if torch_adam:
+        # update 0 runs eagerly (no Adam state yet); the lr changes every update
+        assert graphs[1] is not None and graphs[2] is not None and graphs[1] is not graphs[2]
+        assert not policy._mlp.adam_bound(optim)
+    elif tag == "graph":
         assert graphs[0] is not None and graphs[0] is graphs[1] is graphs[2]
     else:
         assert graphs == [None] * 3  # recompute_advantage runs the epochs eagerly

@@ -146,9 +146,10 @@ using namespace tsrl;
 
 extern "C" int tsrl_np_shuffle_draws(uint32_t* key, int32_t* pos, int64_t n, uint32_t* draws) {
     TSRL_CHECK_ARG(key && pos && (draws || n <= 0), "tsrl_np_shuffle_draws: null argument");
-    TSRL_CHECK_ARG(n >= 0 && n <= (int64_t)0xFFFFFFFFll,
-                   "tsrl_np_shuffle_draws: n=%lld outside [0, 2^32) (64-bit draws unsupported)",
-                   (long long)n);
+    // n <= INT_MAX: the device side (tsrl_shuffle_apply) sorts n - 1 keys with an int count
+    TSRL_CHECK_ARG(n >= 0 && n <= (int64_t)INT_MAX,
+                   "tsrl_np_shuffle_draws: n=%lld outside [0, 2^31) (the shuffle's radix sort "
+                   "takes an int count)", (long long)n);
     TSRL_CHECK_ARG(*pos >= 0 && *pos <= kMtN, "tsrl_np_shuffle_draws: pos=%d", (int)*pos);
     if (n == 0) return 0;
     draws[0] = 0;
@@ -189,7 +190,8 @@ extern "C" int64_t tsrl_shuffle_apply_workspace_bytes(int64_t n) {
 
 extern "C" int tsrl_shuffle_apply(const uint32_t* draws, int64_t n, int64_t* out,
                                   void* workspace, int64_t workspace_bytes, void* stream) {
-    TSRL_CHECK_ARG(n >= 0 && n <= (int64_t)0xFFFFFFFFll, "tsrl_shuffle_apply: n=%lld",
+    TSRL_CHECK_ARG(n >= 0 && n <= (int64_t)INT_MAX,
+                   "tsrl_shuffle_apply: n=%lld outside [0, 2^31) (hipcub radix sort int count)",
                    (long long)n);
     if (n == 0) return 0;
     TSRL_CHECK_ARG(draws && out, "tsrl_shuffle_apply: null argument");

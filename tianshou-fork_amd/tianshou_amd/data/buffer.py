@@ -224,10 +224,14 @@ class VectorReplayBuffer:
             self._reserved_keys), "Input batch doesn't meet ReplayBuffer's data form requirement."
         self._alloc_state()
         meta = Batch()
+        def nested(b: Batch) -> Batch:
+            # every level of a nested Batch (info / policy sub-dicts) moves to the device
+            return Batch({kk: nested(vv) if isinstance(vv, Batch) else self._to_dev(vv)
+                          for kk, vv in b.items()})
+
         for k, v in batch.items():
             if isinstance(v, Batch):
-                meta.__dict__[k] = Batch({kk: self._to_dev(vv) for kk, vv in v.items()
-                                          if not isinstance(vv, Batch)})
+                meta.__dict__[k] = nested(v)
                 continue
             t = self._to_dev(v)
             if k == "rew":

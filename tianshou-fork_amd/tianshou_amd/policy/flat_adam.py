@@ -6,8 +6,9 @@ parameters -- the parameters and their Adam moments become views into flat buffe
 make a whole epoch of minibatches capturable as one HIP graph: no host-side optimiser logic,
 no allocation, no synchronisation.
 
-``optim.state[p]`` entries are views too, so ``optim.state_dict()`` / ``load_state_dict``
-and torch's own ``optim.step()`` keep working on the same storage.
+``optim.state[p]`` entries are views too, so ``optim.state_dict()`` and torch's own
+``optim.step()`` work on the same storage; after ``optim.load_state_dict()`` the next
+``adam_bound`` check copies the loaded moments and step counts into the flat storage.
 
 Used by the fused Gaussian MLP (policy/fused_mlp.py, which adds its kernels' pointers) and by
 the Categorical learn path of PPOPolicy (any torch actor / critic networks).
@@ -78,9 +79,55 @@ class FlatAdam:
             all(a is b for a, b in zip(g["params"], params))
 
     def adam_bound(self, optim) -> bool:
+        """The flat storage serves ``optim``: same optimiser, parameters still views into the
+        flat buffer.  If ``optim.state`` no longer holds the flat views (``load_state_dict``
+        installs new exp_avg / exp_avg_sq / step tensors), the loaded moments and step counts
+        are copied into the flat storage and the views re-installed, so a restored state is
+        what the next clip_adam pass continues from."""
         st = self._adam
-        return st is not None and st["optim"] is optim and all(
-            p.data_ptr() == v.data_ptr() for p, v in zip(self.params, st["pviews"]))
+        if st is None or st["optim"] is not optim or not all(
+                p.data_ptr() == v.data_ptr() for p, v in zip(self.params, st["pviews"])):
+            return False
+        if not self._state_is_flat(optim):
+            self._rebind_state(optim)
+        return True
+
+    def _state_is_flat(self, optim) -> bool:
+        st = self._adam
+        for i, p in enumerate(self.params):
+            s = optim.state.get(p)
+            if s is None:
+                return False
+            m, v, k = s.get("exp_avg"), s.get("exp_avg_sq"), s.get("step")
+            if not (isinstance(m, torch.Tensor) and isinstance(v, torch.Tensor) and
+                    isinstance(k, torch.Tensor)):
+                return False
+            if m.data_ptr() != st["mviews"][i].data_ptr() or \
+                    v.data_ptr() != st["vviews"][i].data_ptr() or \
+                    k.data_ptr() != st["steps"][i].data_ptr():
+                return False
+        return True
+
+    def _rebind_state(self, optim) -> None:
+        """Copy whatever ``optim.state`` now holds into the flat moments / step counts (zeros
+        for a parameter without state) and point ``optim.state`` back at the flat views."""
+        st = self._adam
+        o = 0
+        for i, p in enumerate(self.params):
+            k = p.numel()
+            s = optim.state.get(p, {})
+            if "exp_avg" in s:
+                st["m"][o:o + k].copy_(s["exp_avg"].reshape(-1))
+                st["v"][o:o + k].copy_(s["exp_avg_sq"].reshape(-1))
+                st["steps"][i].copy_(torch.as_tensor(s["step"], dtype=torch.float32))
+            else:
+                st["m"][o:o + k].zero_()
+                st["v"][o:o + k].zero_()
+                st["steps"][i].zero_()
+            optim.state[p] = {"step": st["steps"][i], "exp_avg": st["mviews"][i],
+                              "exp_avg_sq": st["vviews"][i]}
+            o += k
+        st["lr_host"] = None  # load_state_dict may also have changed the param-group lr
 
     def bind_adam(self, optim) -> bool:
         """Move every parameter and its Adam moments into flat buffers (parameter .data and
@@ -97,7 +144,7 @@ class FlatAdam:
         flat_m = torch.zeros(n, dtype=torch.float32, device=dev)
         flat_v = torch.zeros(n, dtype=torch.float32, device=dev)
         steps = torch.zeros(len(self.params), dtype=torch.float32, device=dev)
-        pviews = []
+        pviews, mviews, vviews = [], [], []
         o = 0
         for i, p in enumerate(self.params):
             k = p.numel()
@@ -113,9 +160,12 @@ class FlatAdam:
                               "exp_avg": flat_m[o:o + k].view_as(p),
                               "exp_avg_sq": flat_v[o:o + k].view_as(p)}
             pviews.append(p.data)
+            mviews.append(optim.state[p]["exp_avg"])
+            vviews.append(optim.state[p]["exp_avg_sq"])
             o += k
         steps.fill_(float(steps.max()) if len(steps) else 0.0)
         self._adam = dict(optim=optim, p=flat_p, m=flat_m, v=flat_v, steps=steps, pviews=pviews,
+                          mviews=mviews, vviews=vviews,
                           ticket=torch.zeros(1, dtype=torch.int32, device=dev),
                           partials=torch.zeros(
                               max(int(_C.lib().tsrl_clip_adam_partials(n)), 1),

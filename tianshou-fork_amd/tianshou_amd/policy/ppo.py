@@ -421,9 +421,14 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
         returns the [n_minibatch, 4] loss terms, or None if the capture failed (the caller
         then runs the epoch eagerly, and later epochs do too)."""
         n = perm.numel()
+        flat_opt = self._mlp.adam_bound(self.optim)
+        # the flat Adam pass reads lr from a device word (set_lr), so a schedule needs no
+        # re-capture; any other (capturable torch) optimiser bakes the float lr into the
+        # captured step, so the lrs are part of the key and a schedule step re-captures
+        lrs = None if flat_opt else tuple(float(g["lr"]) for g in self.optim.param_groups)
         key = (n, tuple(chunks), obs_all.data_ptr(), tuple(obs_all.shape),
                tuple(a.shape for a in arrays), self._mlp.flat_grad is not None and
-               self._mlp.flat_grad.data_ptr(), self._mlp.adam_bound(self.optim))
+               self._mlp.flat_grad.data_ptr(), flat_opt, lrs)
         st = self._learn_graph
         if st is None or st["key"] != key:
             st = None
