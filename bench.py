@@ -71,6 +71,9 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=None,
                     help="T' of the bounded CPU-baseline sample (envs x T')")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--exact-obs-rms", action="store_true",
+                    help="VectorEnvNormObs with the reference's f32 obs_rms arithmetic bit for "
+                         "bit (sequential f32 column sums; opt-in, measures its cost)")
     ap.add_argument("--force-dp", action="store_true",
                     help="diagnostic: under torch.distributed.run with ONE rank, run the "
                          "data-parallel code path (RCCL collectives over a one-rank "
@@ -275,7 +278,7 @@ def main():
         coll, policy, buf = build_cartpole(args, dev, rank)
     else:
         env = VectorEnvNormObs(SyntheticVectorEnv(E, (D,), A, ep_len=args.ep_len, seed=rank,
-                                                  device=dev))
+                                                  device=dev), exact_obs_rms=args.exact_obs_rms)
         actor, critic = get_actor_critic((D,), (64, 64), (A,), dev)
         # to the device before the optimiser: fused + capturable Adam
         actor, critic = actor.to(dev), critic.to(dev)
@@ -376,6 +379,8 @@ def main():
                        "permutation": args.perm + (" (per-rank stream)" if world > 1 else ""),
                        "rccl_world_size": world if distributed else None,
                        "learn_graph": args.graph_learn,
+                       "obs_rms": "exact f32 (reference arithmetic)" if args.exact_obs_rms
+                       else "f64 moments",
                        "learn_graph_capture_failed": bool(getattr(policy, "_graph_failed",
                                                                   False)),
                        "collect_s": phase["collect"] / args.steps,

@@ -154,6 +154,17 @@ int tsrl_rms_sum_partials2(const double* partials_step, const double* partials_r
 int tsrl_rms_norm_rows(const float* x, const uint8_t* mask, int64_t k, int64_t dim,
                        const float* mean, const float* var, float eps, float clip,
                        float* out, void* stream);
+/* Exact (opt-in) form of RunningMeanStd.update: the reference's f32 arithmetic bit for bit --
+ * np.mean / np.var over axis 0 (sequential row-order f32 column sums) and the f32 update with
+ * the counts as NEP-50 f32 scalars (statistics.py:93-114).  Updates mean / var / *count with
+ * the rows of x taken by mask (all when NULL); snap_mean / snap_var (nullable, both or none)
+ * receive the state after it; then, when x2 is non-NULL, a second update with x2's rows taken
+ * by mask2 (the reset rows of the same vector step).  `ticket`: a zero-initialised device word
+ * of the statistics object (re-armed by the call).  One thread per column, latency-bound. */
+int tsrl_rms_exact_update(const float* x, const uint8_t* mask, int64_t k, const float* x2,
+                          const uint8_t* mask2, int64_t k2, int64_t dim, float* mean, float* var,
+                          double* count, float* snap_mean, float* snap_var,
+                          unsigned int* ticket, void* stream);
 
 /* ---------------------------------------------------------------------------------
  * VectorReplayBuffer add for one vector step (ReplayBufferManager.add,

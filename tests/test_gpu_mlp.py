@@ -103,6 +103,55 @@ def test_l1_fwd_x6_f32_accuracy(dev, D, n):
         np.testing.assert_allclose(frag_to_rows(frag, n), want.cpu(), rtol=1e-5, atol=1e-5)
 
 
+def frag_to_rows_dev(frag, n, nt=4):
+    """frag_to_rows on the device (for large n)."""
+    ntile = (n + 31) // 32
+    f = frag[:ntile * nt * 64 * 16].view(ntile, nt, 64, 16)
+    lane = torch.arange(64, device=frag.device)
+    r = torch.arange(16, device=frag.device)
+    feat = (r[None, :] & 3) + 8 * (r[None, :] >> 2) + 4 * (lane[:, None] >> 5)  # [64, 16]
+    rows = (lane & 31)[:, None].expand(64, 16)
+    out = torch.empty(ntile, 32, nt * 32, device=frag.device)
+    for ft in range(nt):
+        out[:, rows, 32 * ft + feat] = f[:, ft]
+    return out.view(-1, nt * 32)[:n]
+
+
+@pytest.mark.parametrize("D,n,use_idx", [(376, 262144 + 77, True), (376, 1000, True),
+                                         (17, 5000, True), (8, 33, False), (128, 256, True),
+                                         (376, 4 * 256 * 9 + 300, False), (24, 1, True)])
+def test_l1_ring_kernel_bitwise_equals_staged_kernel(dev, D, n, use_idx):
+    """The LDS-DMA pipelined layer-1 kernel (fragment output, l1_ring_kernel) accumulates
+    exactly as the register-staged kernel (row-major output, l1_fwd_x6_kernel): same
+    k-steps, same six-product order per accumulator -> bit-identical results, for partial
+    tiles, partial workgroups, padded rows (ldx > D) and both index modes."""
+    from tianshou_amd import _C
+    g = torch.Generator(device=dev).manual_seed(D * 7 + n)
+    ldx = (D + 3) // 4 * 4
+    N = n + 300
+    X = torch.zeros(N, ldx, device=dev)
+    X[:, :D] = torch.randn(N, D, device=dev, generator=g) * 2
+    idx = torch.randperm(N, device=dev, generator=g)[:n] if use_idx else None
+    Wa = torch.randn(64, D, device=dev, generator=g) * 0.1
+    Wc = torch.randn(64, D, device=dev, generator=g) * 0.1
+    ba, bc = torch.randn(64, device=dev, generator=g), torch.randn(64, device=dev, generator=g)
+    L = _C.lib()
+    s = _C.stream_ptr(dev)
+    ws = torch.empty((int(L.tsrl_mlp_split_bytes(D)) + 3) // 4, device=dev)
+    _C.check(L.tsrl_mlp_split_w(_C.ptr(Wa), _C.ptr(Wc), D, _C.ptr(ws), s))
+    for act in (1, 0):
+        rows = torch.empty(n, 128, device=dev)
+        _C.check(L.tsrl_mlp_l1_fwd_x6(_C.ptr(X), ldx, _C.ptr(idx), n, D, _C.ptr(ws), _C.ptr(ba),
+                                      _C.ptr(bc), act, _C.ptr(rows), 0, s))
+        frag = torch.full((int(L.tsrl_mlp_frag_floats(n)) + 4096,), 7.0, device=dev)
+        _C.check(L.tsrl_mlp_l1_fwd_x6(_C.ptr(X), ldx, _C.ptr(idx), n, D, _C.ptr(ws), _C.ptr(ba),
+                                      _C.ptr(bc), act, _C.ptr(frag), 1, s))
+        got = frag_to_rows_dev(frag, n)
+        assert torch.equal(got.view(torch.int32), rows.view(torch.int32)), act
+        # nothing written past tsrl_mlp_frag_floats(n)
+        assert bool((frag[int(L.tsrl_mlp_frag_floats(n)):] == 7.0).all())
+
+
 @pytest.mark.parametrize("D,n", [(376, 1000), (24, 4096), (8, 33), (128, 128)])
 def test_l1_fwd_matches_torch(dev, D, n):
     from tianshou_amd import _C

@@ -172,6 +172,38 @@ def test_collector_matches_reference(golden_dir, dev):
     assert env3.get_obs_rms().count == int(z["c3_rms_count"])
 
 
+@pytest.mark.parametrize("tag", ["d8", "d376"])
+def test_fused_collect_step_matches_reference(golden_dir, dev, tag):
+    """The production one-launch collect step (collect_box_step_kernel: previous step's
+    buffer add, Gaussian actor, env step + auto-reset, both obs_rms updates; taken when
+    D % 4 == 0) against the reference Collector + VectorEnvNormObs at D = 8 and the
+    headline's D = 376 (tools/gen_goldens.py gen_collector_fused; collector.py:258-361,
+    venv_wrappers.py:77-99): rew / flags / env_id / episode statistics bit-exact, obs and
+    obs_next rtol 2e-4 (f64 device moments vs NumPy's f32 sums), obs_rms moments rtol 1e-5,
+    counts exact -- over two n_step collects with reset_buffer(keep_statistics=True)."""
+    z = np.load(os.path.join(golden_dir, f"collector_{tag}.npz"))
+    env, policy, buf, c, (E, D, A, L, T) = _collector_setup(z, dev)
+    assert D % 4 == 0
+    res1 = c.collect(n_step=E * T)
+    assert c._step_on, "the fused one-launch step did not run"
+    _check_stats(z, "c1_", res1)
+    _check_buf(z, "c1_buf_", buf, D)
+    rms = env.get_obs_rms()
+    np.testing.assert_allclose(rms.mean, z["c1_rms_mean"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(rms.var, z["c1_rms_var"], rtol=1e-5, atol=1e-6)
+    assert rms.count == int(z["c1_rms_count"])
+    np.testing.assert_allclose(c.data.obs.cpu().numpy(), z["c1_data_obs"], rtol=2e-4, atol=2e-5)
+    c.reset_buffer(keep_statistics=True)
+    res2 = c.collect(n_step=E * T // 2)
+    assert c._step_on
+    _check_stats(z, "c2_", res2)
+    _check_buf(z, "c2_buf_", buf, D)
+    rms = env.get_obs_rms()
+    np.testing.assert_allclose(rms.mean, z["c2_rms_mean"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(rms.var, z["c2_rms_var"], rtol=1e-5, atol=1e-6)
+    assert rms.count == int(z["c2_rms_count"])
+
+
 def test_process_fn_matches_reference(golden_dir, dev):
     """PPOPolicy.process_fn on the reference's collected buffer: critic values, GAE with
     rew_norm (f64 path), logp_old, ret_rms (ppo.py:87-97, a2c.py:83-117).  returns / adv at
@@ -228,3 +260,47 @@ def test_process_fn_on_reference_values(golden_dir, dev):
     assert policy.ret_rms.var == pytest.approx(float(z["pf_ret_rms_var"]), rel=1e-9)
     assert policy.ret_rms.count == int(z["pf_ret_rms_count"])
 
+
+
+def test_exact_rms_update_matches_reference_bitwise(golden_dir, dev):
+    """tsrl_rms_exact_update (DeviceRunningMeanStd(exact=True)) reproduces the reference
+    RunningMeanStd bit for bit over the golden update sequence (statistics.py:93-114;
+    tests/golden/rms.npz, batches of 5, 3, 1, 8, 2, 64 and 1 rows): mean, var, count and the
+    normalised batch."""
+    from tianshou_amd.utils.statistics import DeviceRunningMeanStd
+    z = np.load(os.path.join(golden_dir, "rms.npz"))
+    rms = DeviceRunningMeanStd(6, dev, exact=True)
+    for i in range(int(z["n"])):
+        x = torch.as_tensor(z[f"x{i}"]).to(dev)
+        rms.update(x)
+        assert np.array_equal(rms.mean, z[f"mean{i}"]), i
+        assert np.array_equal(rms.var, z[f"var{i}"]), i
+        assert rms.count == int(z[f"count{i}"])
+        assert np.array_equal(rms.norm(x).cpu().numpy(), z[f"norm{i}"]), i
+
+
+@pytest.mark.parametrize("name", ["collector", "collector_d8", "collector_d376"])
+def test_exact_obs_rms_collect_bitwise(golden_dir, dev, name):
+    """VectorEnvNormObs(exact_obs_rms=True): the collected rollout is the reference's bit for
+    bit -- obs_rms mean / var, the stored normalised obs and obs_next, and the live obs --
+    on the generic device path (D = 5) and on the one-launch fused step (D = 8, 376)."""
+    from tianshou_amd.data import Collector, VectorReplayBuffer
+    from tianshou_amd.env import SyntheticVectorEnv, VectorEnvNormObs
+    z = np.load(os.path.join(golden_dir, name + ".npz"))
+    _, policy, _, _, (E, D, A, L, T) = _collector_setup(z, dev)
+    env = VectorEnvNormObs(SyntheticVectorEnv(E, (D,), A, ep_len=L, device=dev),
+                           exact_obs_rms=True)
+    buf = VectorReplayBuffer(E * T, E, device=dev)
+    c = Collector(policy, env, buf)
+    c.graph_steps = 4
+    res1 = c.collect(n_step=E * T)
+    assert c._step_on == (D % 4 == 0)
+    _check_stats(z, "c1_", res1)
+    rms = env.get_obs_rms()
+    assert np.array_equal(rms.mean, z["c1_rms_mean"])
+    assert np.array_equal(rms.var, z["c1_rms_var"])
+    assert rms.count == int(z["c1_rms_count"])
+    m = buf._meta
+    assert np.array_equal(m.obs.cpu().numpy(), z["c1_buf_obs"])
+    assert np.array_equal(m.obs_next.cpu().numpy(), z["c1_buf_obs_next"])
+    assert np.array_equal(c.data.obs.cpu().numpy(), z["c1_data_obs"])

@@ -36,7 +36,11 @@ def test_scheduled_updates_match_reference(golden_dir, tag):
     cfg = json.loads(str(z[p + "cfg"]))
     E, T, D, A, bs = cfg["E"], cfg["T"], cfg["D"], cfg["A"], cfg["bs"]
     actor, critic = get_actor_critic((D,), (64, 64), (A,), dev)
+    if torch_adam:  # on the device first: init_and_get_optim then builds a capturable Adam
+        actor, critic = actor.to(dev), critic.to(dev)
     optim = init_and_get_optim(actor, critic, 3e-4)
+    if torch_adam:
+        assert optim.defaults["capturable"]
     policy = PPOPolicy(actor, critic, optim, fixed_std_normal, action_space=Box(-1.0, 1.0, (A,)),
                        discount_factor=0.99, gae_lambda=0.95, max_grad_norm=0.5, vf_coef=0.25,
                        ent_coef=0.01, reward_normalization=True, advantage_normalization=True,

@@ -325,6 +325,261 @@ __global__ __launch_bounds__(256, X6_OCC) void l1_fwd_x6_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// l1_ring_kernel: the same product (bit-identical accumulators: each accumulator sees the
+// same k-steps and the same six-product order as l1_fwd_x6_kernel) with an LDS-DMA pipeline
+// deep enough to keep the gathered rows streaming from HBM.
+//
+// Workgroup = 8 waves (2 per SIMD) x 32 rows = 256 rows per tile, all 128 features, up to
+// RTPW tiles per workgroup (one row index per lane and piece loaded before the pipeline
+// starts, so the K loop issues no ordinary global load).  Per 32-k chunk c (flattened over
+// the workgroup's tiles):
+//   X(c): every wave copies ITS OWN 32 rows x 128 B by global_load_lds_dwordx4 (4 wave-
+//         instructions of 8 rows x 128 B; XOR swizzle applied on the source address, so the
+//         lane-linear LDS image is swf_off's), into a 3-stage ring -- issued two chunks ahead
+//         and waited for by the issuing wave only (nobody else reads them);
+//   W(c): the three split-weight planes of the chunk (24 KB, 3 wave-instructions per wave,
+//         x6::sw_off image), into a 2-stage ring -- issued one chunk ahead; one raw s_barrier
+//         per chunk publishes them and retires the stage read in chunk c - 1.
+// Waits are counted `s_waitcnt vmcnt(N)` in inline asm (the LDS-DMA loads are inline asm
+// too, so the compiler inserts no drain of its own); the per-tile epilogue stores count in
+// vmcnt and are skipped by the count of the wait that follows them.
+// ---------------------------------------------------------------------------------------
+#ifndef RING_VARIANT
+#define RING_VARIANT 0  // diagnostic builds only: 1 = no LDS-DMA in the loop, 2 = no MFMAs
+#endif
+constexpr int RNW = 8;                   // waves per workgroup
+constexpr int RROWS = 32 * RNW;          // rows per tile
+constexpr int RTPW = 4;                  // tiles per workgroup (at most)
+constexpr int RXS = 3, RWS = 2;          // X / W ring stages
+constexpr int RXSTAGE = RROWS * XROWB;   // 32 KB
+constexpr int RWSTAGE = NPL * HC * ROWB;  // 24 KB
+constexpr int RWOFF = RXS * RXSTAGE;
+constexpr int RBOFF = RWOFF + RWS * RWSTAGE;
+constexpr int RLDS = RBOFF + HC * 4;
+
+// One LDS-DMA wave-instruction: lane l copies 16 bytes from src to LDS byte lds + 16 l (M0 is
+// set and restored inside the statement; lds is wave-uniform).
+__device__ __forceinline__ void glds16(const void* src, uint32_t lds) {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(src), "s"(lds)
+        : "memory");
+}
+
+template <bool TANH>
+__global__ __launch_bounds__(RNW * 64, 1) void l1_ring_kernel(
+    const float* __restrict__ X, int64_t ldx, const int64_t* __restrict__ idx, int64_t n,
+    int64_t ntiles, int Kp, const __bf16* __restrict__ wsp, const float* __restrict__ ba,
+    const float* __restrict__ bc, float* __restrict__ out, int64_t frag_tiles) {
+    __shared__ __attribute__((aligned(16))) char sm[RLDS];
+    const int t = threadIdx.x;
+    const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int l = t & 63, h = l >> 5, c = l & 31;
+    const int64_t tile0 = (int64_t)blockIdx.x * RTPW;
+    const int ntl = (int)min((int64_t)RTPW, ntiles - tile0);
+    const int nch = Kp / KC;
+    const int C = ntl * nch;
+    float* sb = reinterpret_cast<float*>(sm + RBOFF);
+    if (t < HC) sb[t] = t < H ? ba[t] : bc[t - H];
+    // source rows of this lane's X pieces: tile tl, instruction i -> local row 32w + 8i + l/8
+    // (rows past n, and tiles past ntl, read a real row; the index loads are unconditional)
+    uint32_t rid[RTPW][4];
+#pragma unroll
+    for (int tl = 0; tl < RTPW; ++tl)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int64_t g = (tile0 + tl) * RROWS + 32 * w + 8 * i + (l >> 3);
+            rid[tl][i] = (uint32_t)(g < n ? g : n - 1);
+        }
+    if (idx) {
+#pragma unroll
+        for (int tl = 0; tl < RTPW; ++tl)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) rid[tl][i] = (uint32_t)idx[rid[tl][i]];
+    }
+    __syncthreads();
+    const uint32_t lds0 = (uint32_t)(uintptr_t)sm;
+    // Issue cursors (wave-uniform): the next X chunk (tile px_tl, chunk px_kc, ring slot px_s)
+    // and the next W chunk (chunk pw_kc, slot pw_s).  Per lane: the 4 row bases of the X
+    // tile being issued and the lane's piece offsets (XOR swizzle on the source address, so
+    // the lane-linear LDS image is swf_off's), the 3 weight-plane sources of the lane.
+    int px_tl = 0, px_kc = 0, px_s = 0, pw_kc = 0, pw_s = 0;
+    const float* xb[4];
+    int xoff[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = 32 * w + 8 * i + (l >> 3);
+        xoff[i] = 4 * ((l & 7) ^ ((r >> 1) & 7));
+        xb[i] = X;
+    }
+    const __bf16* wb[3];
+    uint32_t wdst[3];
+#pragma unroll
+    for (int jj = 0; jj < 3; ++jj) {
+        const int j = 3 * w + jj;  // instruction j of the 24: plane j / 8, rows 16 (j % 8) ..
+        const int p = j >> 3, row = 16 * (j & 7) + (l >> 2);
+        const int q = (l & 3) ^ ((row >> 2) & 3);
+        wb[jj] = wsp + p * (int64_t)HC * Kp + (int64_t)row * Kp + 8 * q;
+        wdst[jj] = (uint32_t)(RWOFF + p * HC * ROWB + 16 * (j & 7) * ROWB);
+    }
+    auto issue_x = [&]() {
+        if (px_kc == 0) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                uint32_t ri = 0;
+#pragma unroll
+                for (int u = 0; u < RTPW; ++u) ri = u == px_tl ? rid[u][i] : ri;
+                xb[i] = X + (int64_t)ri * ldx;
+            }
+        }
+        const uint32_t st = lds0 + (uint32_t)(px_s * RXSTAGE + (32 * w) * XROWB);
+        const bool last = px_kc == nch - 1;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            int k = px_kc * KC + xoff[i];
+            // past the row (last chunk only): a finite value that meets zero weights
+            if (last) k = k < ldx ? k : 0;
+            glds16(xb[i] + k, st + (uint32_t)(i * 8 * XROWB));
+        }
+        px_s = px_s == RXS - 1 ? 0 : px_s + 1;
+        if (++px_kc == nch) {
+            px_kc = 0;
+            ++px_tl;
+        }
+    };
+    auto issue_w = [&]() {
+        const uint32_t st = lds0 + (uint32_t)(pw_s * RWSTAGE);
+#pragma unroll
+        for (int jj = 0; jj < 3; ++jj) glds16(wb[jj] + pw_kc * KC, st + wdst[jj]);
+        pw_s ^= 1;
+        if (++pw_kc == nch) pw_kc = 0;
+    };
+    f32x16 acc[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][r] = 0.0f;
+    if (C > 0) {
+        issue_w();
+        issue_x();
+        if (C > 1) issue_x();
+    }
+#if RING_VARIANT == 3
+    if (w >= 4) __builtin_amdgcn_s_setprio(1);  // static priority for the second-dispatched half
+#endif
+    bool epi_prev = false;
+    int cs_x = 0, cs_w = 0;  // ring slots of the chunk being computed
+    for (int cc = 0, tl = 0, kc = 0; cc < C; ++cc) {
+        // retire W(cc) and X(cc): younger in flight are X(cc + 1) (4) and the previous tile's
+        // epilogue stores (16), when they were issued
+        const bool nx = cc + 1 < C;
+        if (epi_prev) {
+            if (nx) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        } else {
+            if (nx) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();
+#if RING_VARIANT != 1
+        if (nx) issue_w();
+        if (cc + 2 < C) issue_x();
+#endif
+        const char* Xs = sm + cs_x * RXSTAGE;
+        const char* Ws = sm + RWOFF + cs_w * RWSTAGE;
+        cs_x = cs_x == RXS - 1 ? 0 : cs_x + 1;
+        cs_w ^= 1;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            bf16x8 b[NPL];
+            {
+                const int xr = 32 * w + c;
+                const float4 u = *reinterpret_cast<const float4*>(&Xs[swf_off(xr, 4 * s + 2 * h)]);
+                const float4 v = *reinterpret_cast<const float4*>(
+                    &Xs[swf_off(xr, 4 * s + 2 * h + 1)]);
+                split4(u, b[0], b[1], b[2], 0);
+                split4(v, b[0], b[1], b[2], 4);
+            }
+#pragma unroll
+            for (int ip = 0; ip < NT; ip += 2) {
+                bf16x8 a0[NPL], a1[NPL];
+                const int ao0 = sw_off(32 * ip + c, 2 * s + h);
+                const int ao1 = sw_off(32 * (ip + 1) + c, 2 * s + h);
+#pragma unroll
+                for (int p = 0; p < NPL; ++p) {
+                    a0[p] = *reinterpret_cast<const bf16x8*>(&Ws[p * HC * ROWB + ao0]);
+                    a1[p] = *reinterpret_cast<const bf16x8*>(&Ws[p * HC * ROWB + ao1]);
+                }
+#if RING_VARIANT == 2
+#define RX6_PAIR(pa, pb)                                                                    \
+    asm volatile("" ::"v"(a0[pa]), "v"(a1[pa]), "v"(b[pb]));
+#else
+#define RX6_PAIR(pa, pb)                                                                    \
+    acc[ip] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[pa], b[pb], acc[ip], 0, 0, 0);     \
+    acc[ip + 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[pa], b[pb], acc[ip + 1], 0, 0, 0);
+#endif
+                RX6_PAIR(0, 0)
+                RX6_PAIR(0, 1)
+                RX6_PAIR(1, 0)
+                RX6_PAIR(0, 2)
+                RX6_PAIR(1, 1)
+                RX6_PAIR(2, 0)
+#undef RX6_PAIR
+            }
+#if RING_VARIANT == 4
+            // interleave: per MFMA one LDS read and three VALU of the neighbouring split
+#pragma unroll
+            for (int g = 0; g < 24; ++g) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+                __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // VALU
+            }
+#endif
+        }
+        epi_prev = kc == nch - 1;
+        if (epi_prev) {
+            // bias + tanh -> fragment layout [row tile][feature tile][lane][16]
+            const int64_t bt = (tile0 + tl) * (RROWS / 32) + w;
+            const bool keep = bt < frag_tiles;
+#pragma unroll
+            for (int i = 0; i < NT; ++i) {
+                float v[16];
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const float4 bb = *reinterpret_cast<const float4*>(&sb[32 * i + 8 * g + 4 * h]);
+                    const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const float z = acc[i][4 * g + e] + bv[e];
+                        v[4 * g + e] = TANH ? tanh_nb(z) : z;
+                        acc[i][4 * g + e] = 0.0f;
+                    }
+                }
+                if (keep) {
+                    float4* o = reinterpret_cast<float4*>(out + ((bt * NT + i) * 64 + l) * 16);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        o[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+                }
+            }
+            // a tile whose fragments lie past the buffer issues no stores: keep the counted
+            // waits exact
+            epi_prev = keep;
+        }
+        if (++kc == nch) {
+            kc = 0;
+            ++tl;
+        }
+    }
+}
+
 inline int64_t kpad32(int64_t D) { return (D + KC - 1) / KC * KC; }
 
 }  // namespace
@@ -359,6 +614,23 @@ extern "C" int tsrl_mlp_l1_fwd_x6(const float* X, int64_t ldx, const int64_t* id
                        aligned16(wsplit),
                    "tsrl_mlp_l1_fwd_x6: X/out/wsplit must be 16-byte aligned, ldx a multiple "
                    "of 4 and >= roundup(D, 4) (X columns D..roundup(D,4) finite: zero padding)");
+    if (frag_out) {
+        // the LDS-DMA pipelined kernel (fragment layout only); frag_tiles = the 32-row tiles
+        // of tsrl_mlp_frag_floats(n)
+        const int64_t ntiles = (n + RROWS - 1) / RROWS;
+        const int64_t frag_tiles = (n + XR - 1) / XR * (XR / 32);
+        const unsigned grid = (unsigned)((ntiles + RTPW - 1) / RTPW);
+        if (act_tanh)
+            hipLaunchKernelGGL(l1_ring_kernel<true>, dim3(grid), dim3(RNW * 64), 0,
+                               as_stream(stream), X, ldx, idx, n, ntiles, (int)kpad32(D),
+                               reinterpret_cast<const __bf16*>(wsplit), ba, bc, out, frag_tiles);
+        else
+            hipLaunchKernelGGL(l1_ring_kernel<false>, dim3(grid), dim3(RNW * 64), 0,
+                               as_stream(stream), X, ldx, idx, n, ntiles, (int)kpad32(D),
+                               reinterpret_cast<const __bf16*>(wsplit), ba, bc, out, frag_tiles);
+        TSRL_LAUNCH_CHECK("tsrl_mlp_l1_fwd_x6(ring)");
+        return 0;
+    }
     const unsigned grid = (unsigned)((n + XR - 1) / XR);
     hipLaunchKernelGGL(l1_fwd_x6_kernel, dim3(grid), dim3(256), 0, as_stream(stream), X, ldx,
                        idx, n, (int)D, (int)kpad32(D),

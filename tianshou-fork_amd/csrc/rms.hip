@@ -317,3 +317,233 @@ extern "C" int tsrl_rms_norm_rows(const float* x, const uint8_t* mask, int64_t k
     TSRL_LAUNCH_CHECK("tsrl_rms_norm_rows");
     return 0;
 }
+
+// ---------------------------------------------------------------------------------------
+// Exact RunningMeanStd (opt-in, VectorEnvNormObs(exact_obs_rms=True)): the reference's own f32
+// arithmetic, bit for bit.  np.mean / np.var over axis 0 of a C-contiguous [k, D] f32 array
+// sum each column SEQUENTIALLY in row order in f32 (the reduction axis is not the contiguous
+// one, so no pairwise summation): S = x0 + x1 + ...; mean = S / k; var = sum((x - mean)^2)
+// / k, every operation rounded to f32 (statistics.py:93-101).  The update then runs in f32
+// with the python-int counts converted to f32 (NEP 50), in the reference's operation order
+// (statistics.py:103-114).  One thread per column: two dependent f32 chains of k adds each
+// -- latency-bound by construction (the price of the reference's summation order).
+// ---------------------------------------------------------------------------------------
+namespace tsrl {
+namespace {
+
+struct ExactRows {
+    const float* x;       // [k, dim]
+    const uint8_t* mask;  // rows taken (NULL: all), in row order
+    int64_t k;
+};
+
+// Workgroup = 64 columns; 4 waves load blocks of EXB selected rows (64 columns each, 256 B
+// per row) into LDS while wave 0 runs the columns' ordered f32 chains over the previous
+// block, so the chains, not the memory latency, set the pace.  Selected rows are listed in
+// row order per span of EXSPAN rows (ballot prefix counts over the mask).
+constexpr int EXT = 256;    // threads
+constexpr int EXB = 128;    // rows per LDS block
+constexpr int EXSPAN = 4096;
+
+struct ExactSmem {
+    float blk[2][EXB][64];
+    int list[EXSPAN];
+    int nsel;
+    int wcnt[EXT / 64];
+};
+
+// Rows [s0, s0 + span) selected by the mask -> sm.list (row order), sm.nsel.
+__device__ void exact_list(const ExactRows& b, int64_t s0, int span, ExactSmem& sm) {
+    const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    int base = 0;
+    for (int c0 = 0; c0 < span; c0 += EXT) {
+        const int r = c0 + t;
+        const bool sel = r < span && (!b.mask || b.mask[s0 + r]);
+        const uint64_t bal = __ballot(sel);
+        const int before = __popcll(bal & ((1ull << l) - 1));
+        if (l == 0) sm.wcnt[w] = __popcll(bal);
+        __syncthreads();
+        int off = base;
+        for (int u = 0; u < w; ++u) off += sm.wcnt[u];
+        if (sel) sm.list[off + before] = r;
+        int tot = 0;
+        for (int u = 0; u < EXT / 64; ++u) tot += sm.wcnt[u];
+        base += tot;
+        __syncthreads();
+    }
+    if (t == 0) sm.nsel = base;
+    __syncthreads();
+}
+
+// One ordered pass over the selected rows of b: acc = (((acc + f(x_r0)) + f(x_r1)) + ...) in
+// f32 for the workgroup's 64 columns, f(x) = x (MEAN) or (x - bm)^2 (VAR).  Returns the
+// number of rows taken; acc is valid in wave 0.
+template <bool VAR>
+__device__ int64_t exact_pass(const ExactRows& b, int64_t dim, int64_t c0, float bm, float& acc,
+                              ExactSmem& sm) {
+#pragma clang fp contract(off)
+    const int t = threadIdx.x;
+    const int64_t col = c0 + (t & 63);
+    int64_t total = 0;
+    for (int64_t s0 = 0; s0 < b.k; s0 += EXSPAN) {
+        const int span = (int)min((int64_t)EXSPAN, b.k - s0);
+        exact_list(b, s0, span, sm);
+        const int nsel = sm.nsel;
+        total += nsel;
+        // block q of the list: thread t loads rows (t >> 6) + 4j, j < EXB / 4, column t & 63
+        auto load = [&](int q, float (&v)[EXB / 4]) {
+#pragma unroll
+            for (int j = 0; j < EXB / 4; ++j) {
+                const int e = q * EXB + (t >> 6) + 4 * j;
+                const int64_t r = s0 + (e < nsel ? sm.list[e] : 0);
+                v[j] = col < dim ? b.x[r * dim + col] : 0.0f;
+            }
+        };
+        auto store = [&](int buf, const float (&v)[EXB / 4]) {
+#pragma unroll
+            for (int j = 0; j < EXB / 4; ++j) sm.blk[buf][(t >> 6) + 4 * j][t & 63] = v[j];
+        };
+        const int nb = (nsel + EXB - 1) / EXB;
+        float v[EXB / 4];
+        if (nb > 0) {
+            load(0, v);
+            store(0, v);
+        }
+        __syncthreads();
+        for (int q = 0; q < nb; ++q) {
+            if (q + 1 < nb) load(q + 1, v);
+            if (t < 64) {
+                const int n = min(EXB, nsel - q * EXB);
+                int e = 0;
+                // software pipeline: the next 16 rows' LDS reads are in flight while the
+                // current 16 are added in order
+                if (n >= 32) {
+                    float x[16], y[16];
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) x[u] = sm.blk[q & 1][u][t];
+                    for (; e + 32 <= n; e += 16) {
+#pragma unroll
+                        for (int u = 0; u < 16; ++u) y[u] = sm.blk[q & 1][e + 16 + u][t];
+#pragma unroll
+                        for (int u = 0; u < 16; ++u) {
+                            if (VAR) {
+                                const float dv = x[u] - bm;
+                                const float sq = dv * dv;
+                                acc = acc + sq;
+                            } else {
+                                acc = acc + x[u];
+                            }
+                        }
+#pragma unroll
+                        for (int u = 0; u < 16; ++u) x[u] = y[u];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) {
+                        if (VAR) {
+                            const float dv = x[u] - bm;
+                            const float sq = dv * dv;
+                            acc = acc + sq;
+                        } else {
+                            acc = acc + x[u];
+                        }
+                    }
+                    e += 16;
+                }
+                for (; e < n; ++e) {
+                    const float x = sm.blk[q & 1][e][t];
+                    if (VAR) {
+                        const float dv = x - bm;
+                        const float sq = dv * dv;
+                        acc = acc + sq;
+                    } else {
+                        acc = acc + x;
+                    }
+                }
+            }
+            __syncthreads();
+            if (q + 1 < nb) store((q + 1) & 1, v);
+            __syncthreads();
+        }
+    }
+    return total;
+}
+
+__device__ void exact_update(const ExactRows& b, int64_t dim, int64_t c0, double cnt_old,
+                             float& mean, float& var, double& cnt_new, ExactSmem& sm) {
+#pragma clang fp contract(off)
+    float S = 0.0f;
+    const int64_t cnt = exact_pass<false>(b, dim, c0, 0.0f, S, sm);
+    cnt_new = cnt_old;
+    if (cnt == 0) return;  // the reference updates only with rows (Collector resets none)
+    const float kf = (float)cnt;
+    const float bm = S / kf;
+    float Q = 0.0f;
+    exact_pass<true>(b, dim, c0, bm, Q, sm);
+    const float bv = Q / kf;
+    const double tot = cnt_old + (double)cnt;
+    const float cf = (float)cnt_old, tf = (float)tot;
+    const float delta = bm - mean;
+    const float new_mean = mean + (delta * kf) / tf;
+    const float m_a = var * cf;
+    const float m_b = bv * kf;
+    const float m_2 = (m_a + m_b) + (((delta * delta) * cf) * kf) / tf;
+    mean = new_mean;
+    var = m_2 / tf;
+    cnt_new = tot;
+}
+
+// First update with b1's rows, the state after it to snap_* (when given), then b2's rows
+// (when b2.x is given).  Every workgroup reads the old count first; the last to finish
+// (agent-scope ticket, re-armed) publishes the new one.
+__global__ __launch_bounds__(EXT) void rms_exact_kernel(ExactRows b1, ExactRows b2, int64_t dim,
+                                                       float* mean, float* var, double* count,
+                                                       float* snap_mean, float* snap_var,
+                                                       unsigned int* ticket) {
+    __shared__ ExactSmem sm;
+    const int t = threadIdx.x;
+    const int64_t c0 = (int64_t)blockIdx.x * 64;
+    const int64_t d = c0 + t;
+    const bool own = t < 64 && d < dim;
+    const double cold = *count;
+    float m = own ? mean[d] : 0.0f, v = own ? var[d] : 1.0f;
+    double c1, c2;
+    exact_update(b1, dim, c0, cold, m, v, c1, sm);
+    if (own && snap_mean) {
+        snap_mean[d] = m;
+        snap_var[d] = v;
+    }
+    c2 = c1;
+    if (b2.x) exact_update(b2, dim, c0, c1, m, v, c2, sm);
+    if (own) {
+        mean[d] = m;
+        var[d] = v;
+    }
+    if (t == 0) {
+        const unsigned int prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL,
+                                                         __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == gridDim.x - 1) {
+            *count = c2;
+            __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+}  // namespace
+}  // namespace tsrl
+
+extern "C" int tsrl_rms_exact_update(const float* x, const uint8_t* mask, int64_t k,
+                                     const float* x2, const uint8_t* mask2, int64_t k2,
+                                     int64_t dim, float* mean, float* var, double* count,
+                                     float* snap_mean, float* snap_var, unsigned int* ticket,
+                                     void* stream) {
+    TSRL_CHECK_ARG(x && mean && var && count && ticket && dim > 0 && k >= 0 && k2 >= 0 &&
+                       (snap_mean == nullptr) == (snap_var == nullptr),
+                   "tsrl_rms_exact_update: bad arguments");
+    const ExactRows b1{x, mask, k};
+    const ExactRows b2{x2, mask2, x2 ? k2 : 0};
+    const unsigned grid = (unsigned)((dim + 63) / 64);
+    hipLaunchKernelGGL(rms_exact_kernel, dim3(grid), dim3(EXT), 0, as_stream(stream), b1, b2,
+                       dim, mean, var, count, snap_mean, snap_var, ticket);
+    TSRL_LAUNCH_CHECK("tsrl_rms_exact_update");
+    return 0;
+}

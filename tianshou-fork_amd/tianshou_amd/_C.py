@@ -155,6 +155,8 @@ _SIGS = {
     "tsrl_ppo_cat_finalize": ([_p, PPOParams, _p, _p], ctypes.c_int),
     "tsrl_cat_logp": ([_p, _p, _i64, _i64, ctypes.c_int, _p, _p], ctypes.c_int),
     "tsrl_cat_gumbel_argmax": ([_p, _p, _i64, _i64, _p, _p], ctypes.c_int),
+    "tsrl_rms_exact_update": ([_p, _p, _i64, _p, _p, _i64, _i64, _p, _p, _p, _p, _p, _p, _p],
+                              ctypes.c_int),
     "tsrl_mlp_l1_fwd": ([_p, _i64, _p, _i64, _i64, _p, _p, _p, _p, ctypes.c_int, _p,
                          ctypes.c_int, _p], ctypes.c_int),
     "tsrl_mlp_frag_floats": ([_i64], _i64),

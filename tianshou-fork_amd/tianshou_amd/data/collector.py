@@ -157,7 +157,10 @@ class Collector:
         if self._norm is not None and not self._base.u8:
             rms = self._norm.obs_rms
             if self._norm.update_obs_rms:
-                rms.merge_partials(partials, self._base.nblk_for(k), mask, k)
+                if rms.exact:
+                    rms.exact_update(raw[:k], None if mask is None else mask[:k])
+                else:
+                    rms.merge_partials(partials, self._base.nblk_for(k), mask, k)
             rms.norm_rows(raw.reshape(k, -1), cur.reshape(k, -1), mask)
         elif mask is None:
             cur.copy_(raw)
@@ -305,11 +308,17 @@ class Collector:
         c.mean, c.var, c.count = _C.ptr(rms.mean_t), _C.ptr(rms.var_t), _C.ptr(rms.count_t)
         c.snap_mean, c.snap_var = _C.ptr(rms.snap_mean_t), _C.ptr(rms.snap_var_t)
         dp = rms.dp is not None and rms.dp.active
-        if dp:
+        if dp or rms.exact:
+            # the launch writes this step's moments instead of folding them
             c.totals = _C.ptr(rms.payload())
         _C.check(_C.lib().tsrl_collect_box_step(c, _C.stream_ptr(b.device)),
                  "tsrl_collect_box_step")
-        if dp:
+        if rms.exact:
+            # both updates from the raw step / reset rows the launch wrote, in the
+            # reference's f32 arithmetic
+            rms.exact_update(s["raw"][:kk], None, s["reset_raw"][:kk], s["done"][:kk],
+                             snapshot=True)
+        elif dp:
             rms.merge_payload(kk)
         self._pending = buf._launch_add(
             ids=None, k=kk, obs=None, act=s["act"], obs_next=s["raw"], cur_obs=cur, norm=rms,
@@ -359,7 +368,9 @@ class Collector:
                               s["part"] if upd else None, s["part2"] if upd else None,
                               blk if upd else None)
             rms = norm_obj.obs_rms if norm_obj is not None else None
-            if upd:
+            if upd and rms.exact:
+                rms.exact_update(raw, None, s["reset_raw"][:kk], done, snapshot=True)
+            elif upd:
                 rms.merge2(s["part"], s["part2"], blk, b.nblk_for(kk), kk)
             kw = dict(add_kw)
             buf._launch_add(ids=None, k=kk, obs=cur, act=act, obs_next=raw, cur_obs=cur,
@@ -372,7 +383,10 @@ class Collector:
         norm = None
         if self._norm is not None and not b.u8:
             if self._norm.update_obs_rms:
-                self._norm.obs_rms.merge_partials(s["part"], b.nblk_for(kk), None, kk)
+                if self._norm.obs_rms.exact:
+                    self._norm.obs_rms.exact_update(raw)
+                else:
+                    self._norm.obs_rms.merge_partials(s["part"], b.nblk_for(kk), None, kk)
             norm = self._norm.obs_rms
         if b.u8:
             buf._launch_add(ids=ids_t, k=kk, obs=cur, act=act, obs_next_raw=raw, rew=rew,

@@ -9,11 +9,13 @@ from tianshou_amd.utils.statistics import DeviceRunningMeanStd
 class VectorEnvNormObs:
     is_async = False
 
-    def __init__(self, venv, update_obs_rms: bool = True) -> None:
+    def __init__(self, venv, update_obs_rms: bool = True, exact_obs_rms: bool = False) -> None:
+        """``exact_obs_rms`` (build option, default off): obs_rms with the reference's f32
+        arithmetic bit for bit (DeviceRunningMeanStd(exact=True)) instead of f64 moments."""
         self.venv = venv
         self.update_obs_rms = update_obs_rms
         dim = int(getattr(venv, "obs_numel"))
-        self.obs_rms = DeviceRunningMeanStd(dim, venv.device)
+        self.obs_rms = DeviceRunningMeanStd(dim, venv.device, exact=exact_obs_rms)
 
     def __len__(self) -> int:
         return len(self.venv)

@@ -44,10 +44,17 @@ class RunningMeanStd:
 
 
 class DeviceRunningMeanStd:
-    """Column RunningMeanStd over rows of a [k, dim] f32 device tensor (obs_rms)."""
+    """Column RunningMeanStd over rows of a [k, dim] f32 device tensor (obs_rms).
+
+    Default: batch moments accumulated in f64 (deterministic parallel folds), the merge
+    rounded to f32 like the reference -- normalised obs agree with the reference to ~1e-6
+    relative (f64 moments are more accurate than NumPy's f32 sums).  ``exact=True``: the
+    reference's own f32 arithmetic bit for bit (sequential row-order f32 column sums of
+    np.mean / np.var, tsrl_rms_exact_update), at the cost of two k-long dependent f32 add
+    chains per column on every update (single process only)."""
 
     def __init__(self, dim: int, device, clip_max: Optional[float] = 10.0,
-                 epsilon: float = np.finfo(np.float32).eps.item()) -> None:
+                 epsilon: float = np.finfo(np.float32).eps.item(), exact: bool = False) -> None:
         self.dim = int(dim)
         self.device = torch.device(device)
         self.mean_t = torch.zeros(self.dim, dtype=torch.float32, device=self.device)
@@ -56,13 +63,39 @@ class DeviceRunningMeanStd:
         self.ticket_t = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.clip_max = clip_max
         self.eps = epsilon
+        self.exact = bool(exact)
         self.dp = None  # tianshou_amd.dist.DataParallel: sync the moments over ranks
         self.snap_mean_t = None  # state after the step-batch update of merge2
         self.snap_var_t = None
         self._payload = None  # data-parallel merge2 all-reduce vector
 
     def sync_with(self, dp) -> None:
+        if self.exact and dp is not None and dp.active:
+            raise ValueError("exact obs_rms keeps the reference's sequential f32 row order, "
+                             "which a sum over data-parallel ranks cannot reproduce")
         self.dp = dp
+
+    def exact_update(self, x: torch.Tensor, mask: Optional[torch.Tensor] = None,
+                     x2: Optional[torch.Tensor] = None, mask2: Optional[torch.Tensor] = None,
+                     snapshot: bool = False) -> None:
+        """RunningMeanStd.update (statistics.py:93-114) with the reference's f32 arithmetic on
+        the rows of x taken by mask (all when None); with x2, a second update on x2's rows
+        taken by mask2 (the reset rows of the same vector step); ``snapshot`` stores the
+        state after the first update in snap_mean_t / snap_var_t (merge2's contract)."""
+        if snapshot:
+            self.ensure_snapshot()
+        x = x.reshape(len(x), -1)
+        assert x.dtype == torch.float32 and x.is_contiguous() and x.shape[1] == self.dim
+        if x2 is not None:
+            x2 = x2.reshape(len(x2), -1)
+            assert x2.dtype == torch.float32 and x2.is_contiguous() and x2.shape[1] == self.dim
+        u8 = lambda m: None if m is None else m.reshape(-1).view(torch.uint8)  # noqa: E731
+        _C.check(_C.lib().tsrl_rms_exact_update(
+            _C.ptr(x), _C.ptr(u8(mask)), len(x), _C.ptr(x2), _C.ptr(u8(mask2)),
+            0 if x2 is None else len(x2), self.dim, _C.ptr(self.mean_t), _C.ptr(self.var_t),
+            _C.ptr(self.count_t), _C.ptr(self.snap_mean_t) if snapshot else None,
+            _C.ptr(self.snap_var_t) if snapshot else None, _C.ptr(self.ticket_t),
+            _C.stream_ptr()), "tsrl_rms_exact_update")
 
     # -- reference-compatible views (sync on access) ------------------------------------
     @property
@@ -165,6 +198,9 @@ class DeviceRunningMeanStd:
 
     def update(self, x: torch.Tensor, mask: Optional[torch.Tensor] = None) -> None:
         x = x.reshape(len(x), -1)
+        if self.exact:
+            self.exact_update(x.contiguous().float(), None if mask is None else mask.bool())
+            return
         if mask is not None:
             xs = x[mask.bool()]
         else:

@@ -517,6 +517,39 @@ def gen_collector():
     _save("collector.npz", **out)
 
 
+def gen_collector_fused():
+    """The same Collector + VectorEnvNormObs path at observation widths that take the build's
+    one-launch fused collect step (tsrl_collect_box_step needs D % 4 == 0): D = 8 and the
+    headline's D = 376, 16 envs x 24 steps, both done kinds (even envs terminate, odd ones
+    truncate), two n_step collects with reset_buffer(keep_statistics=True) between them."""
+    for D, A, L, tag in ((8, 3, 7, "d8"), (376, 17, 9, "d376")):
+        E, T = 16, 24
+        out = dict(E=np.array(E), D=np.array(D), A=np.array(A), L=np.array(L), T=np.array(T))
+        venv = VectorEnvNormObs(DummyVectorEnv(
+            [lambda e=e: SynthGymEnv(e, D, A, L) for e in range(E)]))
+        policy = _make_policy(D, A, seed=4, reward_normalization=True, ent_coef=0.0)
+        out.update(_sd_arrays("init_", policy))
+        buf = VectorReplayBuffer(E * T, E)
+        torch.manual_seed(1)
+        np.random.seed(1)
+        c = Collector(policy, venv, buf)
+        res1 = c.collect(n_step=E * T)
+        out.update(_stats_arrays("c1_", res1))
+        out.update(_buf_arrays("c1_buf_", buf))
+        rms = venv.get_obs_rms()
+        out["c1_rms_mean"], out["c1_rms_var"], out["c1_rms_count"] = \
+            np.asarray(rms.mean), np.asarray(rms.var), np.array(rms.count)
+        out["c1_data_obs"] = np.asarray(c.data.obs)
+        c.reset_buffer(keep_statistics=True)
+        res2 = c.collect(n_step=E * T // 2)
+        out.update(_stats_arrays("c2_", res2))
+        out.update(_buf_arrays("c2_buf_", buf))
+        rms = venv.get_obs_rms()
+        out["c2_rms_mean"], out["c2_rms_var"], out["c2_rms_count"] = \
+            np.asarray(rms.mean), np.asarray(rms.var), np.array(rms.count)
+        _save(f"collector_{tag}.npz", **out)
+
+
 # --------------------------------------------------------------------------------------
 # 8. Frame-stack storage (SURVEY.md §8 A9): VectorReplayBuffer(stack_num, save_only_last_obs,
 #    ignore_obs_next, sample_avail) -- manager.py:104-161 (last-frame store),
@@ -1001,10 +1034,12 @@ def gen_cartpole():
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     which = sys.argv[1:] or ["returns", "gae", "buffer", "split", "rms", "ppo", "collector",
+                             "collector_fused",
                              "stack", "ppo_discrete", "npg", "replay", "cartpole", "sched",
                              "persist"]
     table = dict(returns=gen_returns_known, gae=gen_gae_random, buffer=gen_buffer_traces,
                  split=gen_split, rms=gen_rms, ppo=gen_ppo, collector=gen_collector,
+                 collector_fused=gen_collector_fused,
                  stack=gen_stack, ppo_discrete=gen_ppo_discrete, npg=gen_npg, replay=gen_replay,
                  cartpole=gen_cartpole, sched=gen_sched,
                  persist=gen_persist)

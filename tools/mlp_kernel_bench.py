@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default=None,
                     help="time one kernel only (l1_fwd, l1_fwd_x6, tail, dw, minibatch): PMC passes")
+    ap.add_argument("--act", type=int, default=1, help="layer-1 activation: 1 tanh, 0 identity")
     ap.add_argument("--contig", action="store_true",
                     help="minibatch rows contiguous (no permutation gather)")
     ap.add_argument("--sorted", action="store_true",
@@ -77,8 +78,15 @@ def main():
         _C.check(L.tsrl_mlp_split_w(_C.ptr(W["w1a"].weight), _C.ptr(W["w1c"].weight), D,
                                     _C.ptr(wsx), s))
         _C.check(L.tsrl_mlp_l1_fwd_x6(_C.ptr(obs), D, _C.ptr(idx), B, D, _C.ptr(wsx),
-                                      _C.ptr(W["w1a"].bias), _C.ptr(W["w1c"].bias), 1,
+                                      _C.ptr(W["w1a"].bias), _C.ptr(W["w1c"].bias), a.act,
                                       _C.ptr(h1), 1, s))
+
+    rows_out = torch.empty(B, 128, device=dev)
+
+    def l1x6_staged():  # the register-staged kernel (row-major output path)
+        _C.check(L.tsrl_mlp_l1_fwd_x6(_C.ptr(obs), D, _C.ptr(idx), B, D, _C.ptr(wsx),
+                                      _C.ptr(W["w1a"].bias), _C.ptr(W["w1c"].bias), 1,
+                                      _C.ptr(rows_out), 0, s))
 
     def tail():
         _C.check(L.tsrl_ppo_tail(_C.ptr(h1), B, _C.ptr(idx), fm._tail_w, A, _C.ptr(act),
@@ -96,6 +104,7 @@ def main():
         fm.minibatch(obs, idx, B, act, logp_old, adv, ret, v_s, p, dp)
 
     for name, fn, flop in (("l1_fwd", l1, flop_l1), ("l1_fwd_x6(+split)", l1x6, flop_l1),
+                           ("l1_x6_staged(rows)", l1x6_staged, flop_l1),
                            ("tail(+reduce)", tail, flop_tail),
                            ("dw(+reduce)", dw, flop_l1), ("minibatch", whole, None)):
         if a.only and not name.startswith(a.only):
