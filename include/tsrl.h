@@ -369,6 +369,15 @@ int tsrl_dqn_conv1_wgrad(const uint8_t* frames, int64_t n, const float* gy, floa
  *   from tsrl_shuffle_apply_workspace_bytes(n).
  * ------------------------------------------------------------------------------- */
 int tsrl_np_shuffle_draws(uint32_t* key, int32_t* pos, int64_t n, uint32_t* draws);
+/* The same draws and final state computed by host threads (csrc/np_perm_mt.cpp): MT19937 jump
+ * ahead (x^J mod the generator's minimal polynomial) so each thread generates its own stretch of
+ * the stream, and the masked rejection resolved chunk-parallel (every word classified for a window
+ * of possible starting i, only the uncertain words walked in order, then the draws written per
+ * chunk from the exact starts).  For the global permutation of a data-parallel update
+ * (batch.py:896-912 over world x n rows).  n < 2^21 runs tsrl_np_shuffle_draws; nthreads <= 0:
+ * hardware concurrency (at most 32).  The first call builds the jump table (~1 s, cached). */
+int tsrl_np_shuffle_draws_mt(uint32_t* key, int32_t* pos, int64_t n, uint32_t* draws,
+                             int nthreads);
 int64_t tsrl_shuffle_apply_workspace_bytes(int64_t n);
 int tsrl_shuffle_apply(const uint32_t* draws, int64_t n, int64_t* out, void* workspace,
                        int64_t workspace_bytes, void* stream);

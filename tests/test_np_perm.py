@@ -62,3 +62,27 @@ def test_draws_reject_bad_arguments():
     assert _C.lib().tsrl_np_shuffle_draws(key.ctypes.data, ctypes.addressof(pos), 4,
                                           d.ctypes.data) != 0
     assert b"pos" in _C.lib().tsrl_last_error()
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+def test_threaded_draws_equal_sequential(threads):
+    """tsrl_np_shuffle_draws_mt (MT19937 jump-ahead + chunk-parallel masked rejection) gives
+    exactly the sequential loop's draws and final RandomState, over successive calls at sizes
+    above its 2^21 threshold (the sequential loop is pinned to np.random.permutation above)."""
+    import ctypes
+
+    from tianshou_amd import _C
+    L = _C.lib()
+    rng = np.random.RandomState(2024)
+    for n in (1 << 21, 3_000_017, 12_582_912):
+        st = rng.get_state()
+        out = []
+        for fn, extra in ((L.tsrl_np_shuffle_draws, ()), (L.tsrl_np_shuffle_draws_mt, (threads,))):
+            k = np.ascontiguousarray(st[1], dtype=np.uint32).copy()
+            p = ctypes.c_int32(int(st[2]))
+            d = np.empty(n, np.uint32)
+            _C.check(fn(k.ctypes.data, ctypes.addressof(p), n, d.ctypes.data, *extra))
+            out.append((k, p.value, d))
+        assert np.array_equal(out[0][2], out[1][2]), n
+        assert np.array_equal(out[0][0], out[1][0]) and out[0][1] == out[1][1], n
+        rng.set_state(("MT19937", out[0][0], out[0][1], 0, 0.0))

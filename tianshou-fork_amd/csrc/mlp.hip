@@ -179,6 +179,9 @@ struct TailParams {
     double inv_b64;
 };
 
+#ifndef TAIL_VARIANT
+#define TAIL_VARIANT 0  // diagnostic builds only: 1 = no layer-2/3 weight-gradient MFMAs
+#endif
 constexpr int WS2 = 65;   // LDS row stride of the staged weights (odd: conflict-free reads)
 // per-workgroup slab of weight-gradient partial sums (floats) and loss partial sums (doubles)
 constexpr int SL_W2A = 0, SL_B2A = SL_W2A + H * H, SL_W2C = SL_B2A + H, SL_B2C = SL_W2C + H * H,
@@ -226,7 +229,8 @@ __device__ __forceinline__ int rs_reg(int l) {
 // critic outputs, so the halves are independent and each keeps half the live state.
 constexpr int SH = 18;   // half-tile transpose scratch: [64 features][16 rows], stride 18
 constexpr int T_B2 = 0, T_B3 = T_B2 + H, T_W3C = T_B3 + AMAX, T_VAR = T_W3C + H,
-              T_LS = T_VAR + AMAX, T_SCR = T_LS + AMAX, T_END = T_SCR + 4 * 2 * H * SH;
+              T_LS = T_VAR + AMAX, T_IV = T_LS + AMAX, T_IV2 = T_IV + AMAX,
+              T_SCR = T_IV2 + AMAX, T_END = T_SCR + 4 * 2 * H * SH;
 
 // The chain products (layer 2, mu head, dZ2 = W3^T dMu, dZ1 = W2^T dZ2) run as bf16x6 (x6.h):
 // their activation operand is the C-layout tile itself -- registers 8s..8s+7 of a 32x32 tile
@@ -362,6 +366,11 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
                 const float sig = t < A ? expf(wt.log_std[t]) : 1.0f;
                 sm[T_VAR + t] = sig * sig;
                 sm[T_LS + t] = logf(sig);
+                // reciprocals once per workgroup: the per-row terms multiply (a correctly
+                // rounded f32 division is ~10 VALU; the products differ from the divisions
+                // by at most one rounding)
+                sm[T_IV + t] = 1.0f / (sig * sig);
+                sm[T_IV2 + t] = 1.0f / (2.0f * (sig * sig));
             }
         } else if (t < H) {
             sm[T_W3C + t] = wt.w3c[t];
@@ -496,7 +505,7 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
                 diff[r] = 0.0f;
                 if (a < A && live) {
                     diff[r] = av[r] - (mu[r] + sm[T_B3 + a]);
-                    lp += -(diff[r] * diff[r]) / (2.0f * sm[T_VAR + a]) - sm[T_LS + a] -
+                    lp += -(diff[r] * diff[r]) * sm[T_IV2 + a] - sm[T_LS + a] -
                           LOG_SQRT_2PI;
                 }
             }
@@ -545,9 +554,9 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int a = rho(r) + 4 * h;
-                const float var = sm[T_VAR + a];
-                dmu[0][r] = g_logp * diff[r] / var;
-                dls[r] = (a < A && live) ? g_logp * (diff[r] * diff[r] / var - 1.0f) : 0.0f;
+                const float iv = sm[T_IV + a];
+                dmu[0][r] = g_logp * diff[r] * iv;
+                dls[r] = (a < A && live) ? g_logp * (diff[r] * diff[r] * iv - 1.0f) : 0.0f;
             }
             dls_acc += (double)rs_sum16(dls, l);
             gb3 += rs_sum16(dmu[0], l);
@@ -561,7 +570,9 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
                 put_half<1>(S1, dmu, c, h, half);
                 put_half<2>(S2, h2, c, h, half);
                 wave_sync_lds();
+#if TAIL_VARIANT != 1
                 acc_wgrad<1, 2>(gW3, S1, S2, c, h);
+#endif
             }
             // dZ2 = (W3a^T dMu) * (1 - H2^2)
             __builtin_amdgcn_sched_barrier(0);
@@ -701,7 +712,9 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
             put_half<2>(S1, dz2, c, h, half);
             put_half<2>(S2, h1, c, h, half);
             wave_sync_lds();
+#if TAIL_VARIANT != 1
             acc_wgrad<2, 2>(gW2, S1, S2, c, h);
+#endif
         }
     }
 #undef TAIL_PREFETCH

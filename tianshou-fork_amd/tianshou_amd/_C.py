@@ -157,6 +157,7 @@ _SIGS = {
     "tsrl_cat_gumbel_argmax": ([_p, _p, _i64, _i64, _p, _p], ctypes.c_int),
     "tsrl_rms_exact_update": ([_p, _p, _i64, _p, _p, _i64, _i64, _p, _p, _p, _p, _p, _p, _p],
                               ctypes.c_int),
+    "tsrl_np_shuffle_draws_mt": ([_p, _p, _i64, _p, ctypes.c_int], ctypes.c_int),
     "tsrl_mlp_l1_fwd": ([_p, _i64, _p, _i64, _i64, _p, _p, _p, _p, ctypes.c_int, _p,
                          ctypes.c_int, _p], ctypes.c_int),
     "tsrl_mlp_frag_floats": ([_i64], _i64),

@@ -5,10 +5,13 @@ Batch.split (tianshou/data/batch.py:896-912) shuffles every PPO repeat with
 Fisher-Yates over MT19937 words: 0.2-0.3 s of single-threaded host time at 8.4M indices,
 plus a 67 MB host-to-device copy.  Here the work is split (csrc/perm.hip):
 
-* ``tsrl_np_shuffle_draws`` (host C++, no HIP call, releases the GIL through ctypes): the
-  MT19937 stream and the masked rejection loop, ~20 ms at 8.4M, advancing a copy of the
-  global state that is written back with ``np.random.set_state`` -- the global RandomState
-  ends exactly where NumPy's own call would leave it;
+* ``tsrl_np_shuffle_draws_mt`` (host C++, no HIP call, releases the GIL through ctypes): the
+  MT19937 stream and the masked rejection loop, advancing a copy of the global state that is
+  written back with ``np.random.set_state`` -- the global RandomState ends exactly where
+  NumPy's own call would leave it.  Sequential below 2^21 elements (~10 ms at 8.4M on the
+  MI355X box host); above, host threads (MT19937 jump-ahead + chunk-parallel rejection, exact:
+  csrc/np_perm_mt.cpp), ~30 ms instead of 75 ms at 67M -- the global permutation of an 8-rank
+  update;
 * ``tsrl_shuffle_apply`` (device): the swap sequence resolved in parallel from the draws.
 
 ``prefetch(n, count)`` starts a host thread that computes the draws of the next ``count``
@@ -17,6 +20,7 @@ prefetched permutation is only used if the global state is still the one it was 
 from; otherwise it is discarded and recomputed, so results never depend on timing.
 """
 import ctypes
+import os
 import threading
 from typing import List, Optional
 
@@ -33,13 +37,18 @@ def _state_key():
     return st
 
 
+# host threads for the draws of large permutations (tsrl_np_shuffle_draws_mt; below 2^21
+# elements it runs the sequential loop)
+THREADS = int(os.environ.get("TSRL_PERM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+
+
 def _draws(key: np.ndarray, pos: int, n: int, out: np.ndarray):
     """Fill out[:n] with the shuffle draws; return the advanced (key, pos)."""
     key = np.ascontiguousarray(key, dtype=np.uint32).copy()
     cpos = ctypes.c_int32(int(pos))
-    _C.check(_C.lib().tsrl_np_shuffle_draws(key.ctypes.data, ctypes.addressof(cpos), int(n),
-                                            out.ctypes.data if n > 0 else None),
-             "tsrl_np_shuffle_draws")
+    _C.check(_C.lib().tsrl_np_shuffle_draws_mt(key.ctypes.data, ctypes.addressof(cpos), int(n),
+                                               out.ctypes.data if n > 0 else None, THREADS),
+             "tsrl_np_shuffle_draws_mt")
     return key, cpos.value
 
 

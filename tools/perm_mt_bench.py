@@ -1,0 +1,83 @@
+"""Host timing of the threaded np.random.permutation draws (tsrl_np_shuffle_draws_mt) against
+the sequential loop (tsrl_np_shuffle_draws), with equality checks:
+    python tools/perm_mt_bench.py [n ...] [--threads T]"""
+import argparse
+import ctypes
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tianshou-fork_amd"))
+import numpy as np  # noqa: E402
+
+from tianshou_amd import _C  # noqa: E402
+
+
+def run(fn, key, pos, n, *extra):
+    k = np.ascontiguousarray(key, dtype=np.uint32).copy()
+    p = ctypes.c_int32(int(pos))
+    d = np.empty(n, np.uint32)
+    t = time.perf_counter()
+    _C.check(fn(k.ctypes.data, ctypes.addressof(p), n, d.ctypes.data, *extra))
+    return k, p.value, d, time.perf_counter() - t
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("n", type=int, nargs="*", default=[8388608, 67108864])
+    ap.add_argument("--threads", type=int, default=0)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--device", action="store_true", help="device permutation end to end")
+    a = ap.parse_args()
+    if a.device:
+        device_bench(a.n)
+        return
+    L = _C.lib()
+    rng = np.random.RandomState(7)
+    print("cpus", os.cpu_count(), "affinity", len(os.sched_getaffinity(0)), flush=True)
+    for n in a.n:
+        for r in range(a.reps):
+            st = rng.get_state()
+            k1, p1, d1, t1 = run(L.tsrl_np_shuffle_draws, st[1], st[2], n)
+            k2, p2, d2, t2 = run(L.tsrl_np_shuffle_draws_mt, st[1], st[2], n, a.threads)
+            ok = np.array_equal(d1, d2) and np.array_equal(k1, k2) and p1 == p2
+            print(f"n={n} rep {r}: sequential {t1 * 1e3:.1f} ms, threaded {t2 * 1e3:.1f} ms, "
+                  f"equal {ok}", flush=True)
+            rng.set_state(("MT19937", k1, p1, 0, 0.0))
+
+
+def device_bench(n_list, world=8):
+    """End-to-end np_permutation(n) on the device (host draws + copy + tsrl_shuffle_apply) and
+    the data-parallel share selection of _minibatch_plan for rank 0 of `world`."""
+    import torch
+    from tianshou_amd.utils.np_perm import LegacyPermutation
+    dev = torch.device("cuda", 0)
+    lp = LegacyPermutation()
+    for n in n_list:
+        np.random.seed(1)
+        ref_state = np.random.get_state()
+        for r in range(3):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            perm = lp(n, dev)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            nl, B = n // world, n // 32
+            pos = torch.nonzero((perm >= 0) & (perm < nl)).squeeze(1)
+            idx = (perm[pos]).contiguous()
+            lab = torch.div(pos, B, rounding_mode="floor")
+            counts = torch.bincount(lab, minlength=32).cpu()
+            t2 = time.perf_counter()
+            print(f"device n={n} rep {r}: permutation {1e3 * (t1 - t0):.1f} ms, rank share "
+                  f"selection + counts {1e3 * (t2 - t1):.1f} ms", flush=True)
+        if n <= 8388608:
+            np.random.set_state(ref_state)
+            want = np.random.permutation(n)
+            np.random.set_state(ref_state)
+            got = lp(n, dev).cpu().numpy()
+            print("  equals np.random.permutation:", np.array_equal(want, got), flush=True)
+
+
+if __name__ == "__main__":
+    main()
