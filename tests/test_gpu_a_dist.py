@@ -43,7 +43,13 @@ def rank_runs(tmp_path_factory):
         procs += [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "dist_worker.py"),
                                     str(r), str(world), port, str(d)], env=env)
                   for r in range(world)]
-    rcs = [p.wait(timeout=300) for p in procs]
+    # BASELINE config 4's per-rank shape, 2 ranks (dist_c4_worker.py)
+    port = str(_free_port())
+    d = tmp_path_factory.mktemp("c4")
+    dirs["c4"] = d
+    procs += [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "dist_c4_worker.py"),
+                                str(r), "2", port, str(d)], env=env) for r in range(2)]
+    rcs = [p.wait(timeout=600) for p in procs]
     assert rcs == [0] * len(procs), rcs
     return dirs
 
@@ -122,3 +128,17 @@ def test_rank_update_matches_single_process(rank_runs, world):
     assert int(r0["rms_count"]) == int(count)
     np.testing.assert_allclose(r0["rms_mean"].numpy(), mean, rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(r0["rms_var"].numpy(), var, rtol=1e-5, atol=1e-6)
+
+
+def test_config4_shape_dp_update(rank_runs):
+    """2 ranks x 512 envs x 2048 steps x D = 376 (config 4's per-rank shape): global obs_rms
+    collect + one update with the global-batch split equals the single process over the
+    union of both ranks' envs (dist_c4_worker.py)."""
+    r = torch.load(rank_runs["c4"] / "c4.pt", weights_only=True)
+    assert r["rms_count"] >= 2 * 512 * 2049  # both shards' reset + step rows (+ auto-resets)
+    assert r["loss"].shape == r["loss_ref"].shape == (4, 32)
+    np.testing.assert_allclose(r["loss"].numpy(), r["loss_ref"].numpy(), rtol=1e-4, atol=1e-6)
+    for k, v in r["sd"].items():
+        # one Adam step moves a weight by up to lr = 3e-4: atol = lr / 3
+        np.testing.assert_allclose(v.numpy(), r["sd_ref"][k].numpy(), rtol=1e-4, atol=1e-4,
+                                   err_msg=k)

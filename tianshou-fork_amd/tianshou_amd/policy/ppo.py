@@ -9,6 +9,7 @@ values are accumulated on device (no per-minibatch .item() syncs; the returned l
 read back once at the end).  Other actor/dist combinations run the reference's torch
 formulation on the GPU.
 """
+import contextlib
 import zlib
 from typing import Any, Callable, Dict, List, Optional
 
@@ -161,6 +162,7 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
         # utils/np_perm.py); True: torch.randperm on the GPU.
         self.perm_device = perm_device
         self._np_perm = LegacyPermutation()
+        self._plan_stream = None
         self._np_perm_used, self._np_perm_n = False, 0
         # data-parallel minibatch composition (see _minibatch_plan): "global" = the
         # reference's split of the global batch, "local" = every rank splits its own rows
@@ -260,6 +262,9 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
         n = len(batch.v_s)
         terms = []
         f32 = dict(device=dev, dtype=torch.float32)
+        mlp_ok = self._mlp is not None and batch.obs.is_cuda and \
+            batch.obs.dtype == torch.float32 and batch.obs.dim() == 2
+        plans = self._plan_pipeline(n, dev, batch_size, repeat, mlp_ok)
         for step in range(repeat):
             if self._recompute_adv and step > 0:
                 batch = self._compute_returns(batch, self._buffer, self._indices)
@@ -268,9 +273,7 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
             adv = batch.adv.reshape(-1).to(**f32).contiguous()
             ret = batch.returns.reshape(-1).to(**f32).contiguous()
             v_s = batch.v_s.reshape(-1).to(**f32).contiguous()
-            mlp_ok = self._mlp is not None and batch.obs.is_cuda and \
-                batch.obs.dtype == torch.float32 and batch.obs.dim() == 2
-            perm, chunks = self._minibatch_plan(n, dev, batch_size, allow_global=mlp_ok)
+            perm, chunks = plans(step)
             if mlp_ok and self.fused_adam and self._mlp.bind_adam(self.optim):
                 self._mlp.set_lr()
             obs_all = self._mlp.rows(batch.obs) if mlp_ok else None
@@ -330,8 +333,47 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
         all ranks' envs) with global minibatches of world * batch_size rows, and keeps its
         own rows of each, in permutation order.  ``"local"``: each rank splits its own n rows
         (weak scaling: the sequential host draws stay O(n) per rank)."""
+        return self._take_plan(self._issue_plan(n, dev, batch_size, allow_global, None), dev)
+
+    def _plan_pipeline(self, n: int, dev, batch_size: int, repeat: int, allow_global: bool):
+        """plans(k) -> repeat k's (idx, chunks).  With the np.random permutation on a HIP
+        device, each repeat's permutation (pinned draws -> device copy -> swap resolution ->
+        this rank's share) is enqueued on a side stream, and the next repeat's too as soon as
+        its prefetched host draws exist, so the copy and the resolution overlap the previous
+        repeat's minibatches instead of serialising with them.  The global RandomState is
+        consumed in the same order as repeat sequential calls."""
+        if self.perm_device or dev.type != "cuda":
+            return lambda k: self._minibatch_plan(n, dev, batch_size, allow_global)
+        if self._plan_stream is None or self._plan_stream.device != dev:
+            self._plan_stream = torch.cuda.Stream(dev)
+        side = self._plan_stream
         W = self.dp.world if self.dp.active else 1
-        if W > 1 and allow_global and self.dp_permutation == "global" and not self.perm_device:
+        pn = n * W if self._global_perm(n, dev, allow_global) else n
+        issued = {}
+
+        def plans(k):
+            if k not in issued:
+                issued[k] = self._issue_plan(n, dev, batch_size, allow_global, side)
+            if k + 1 < repeat and k + 1 not in issued and self._np_perm.next_ready(pn):
+                issued[k + 1] = self._issue_plan(n, dev, batch_size, allow_global, side)
+            return self._take_plan(issued.pop(k), dev)
+        return plans
+
+    def _global_perm(self, n: int, dev, allow_global: bool) -> bool:
+        W = self.dp.world if self.dp.active else 1
+        return W > 1 and allow_global and self.dp_permutation == "global" and \
+            not self.perm_device
+
+    def _issue_plan(self, n: int, dev, batch_size: int, allow_global: bool, stream):
+        """Enqueue one repeat's minibatch plan on ``stream`` (None: the current stream) and
+        return it pending; _take_plan orders the current stream after it.  No host
+        synchronisation here: the data-parallel share selection is a compaction by prefix
+        sum whose size is known (every rank owns exactly n of the global rows), and the
+        per-minibatch share counts travel back to pinned host memory behind an event."""
+        W = self.dp.world if self.dp.active else 1
+        ctx = torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+        cuda = dev.type == "cuda"
+        if self._global_perm(n, dev, allow_global):
             N, B = n * W, batch_size * W
             gb = split_bounds(N, B, merge_last=True)
             if not self._np_perm_used:  # once per learn(): every rank holds the same stream
@@ -345,21 +387,48 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
                         "dp_permutation='global' needs the same global np.random state and "
                         "the same number of rows on every rank (seed np.random identically, "
                         "or set dp_permutation='local')")
-            perm_g = self._np_perm(N, dev)
             self._np_perm_used = True
             self._np_perm_n = N
-            lo = self.dp.rank * n
-            pos = torch.nonzero((perm_g >= lo) & (perm_g < lo + n)).squeeze(1)
-            idx = (perm_g[pos] - lo).contiguous()
-            lab = torch.div(pos, B, rounding_mode="floor").clamp_(max=len(gb) - 1)
-            counts = torch.bincount(lab, minlength=len(gb)).cpu().tolist()
-            chunks, o = [], 0
-            for (gs, ge), c in zip(gb, counts):
-                chunks.append((o, o + c, ge - gs))
-                o += c
-            return idx, chunks
-        perm = self._permutation(n, dev, batch_size)
-        return perm, [(s, e, (e - s) * W) for s, e in split_bounds(n, batch_size, True)]
+            ends = torch.tensor([ge - 1 for _, ge in gb], dtype=torch.int64)
+            with ctx:
+                perm_g = self._np_perm(N, dev)
+                lo = self.dp.rank * n
+                mine = (perm_g >= lo) & (perm_g < lo + n)
+                cs = torch.cumsum(mine, 0)
+                # this rank's rows in permutation order: row perm_g[p] - lo goes to slot
+                # cs[p] - 1; every other position writes the spare slot n
+                tgt = cs.sub(1).masked_fill_(~mine, n)
+                idx = torch.empty(n + 1, dtype=torch.int64, device=dev)
+                idx.scatter_(0, tgt, perm_g.sub_(lo))
+                cum_dev = cs[ends.to(dev, non_blocking=True)]
+                cum = torch.empty(len(gb), dtype=torch.int64, pin_memory=cuda)
+                cum.copy_(cum_dev, non_blocking=cuda)
+                ev = torch.cuda.Event() if cuda else None
+                if ev is not None:
+                    ev.record()
+            return {"idx": idx[:n], "cum": cum, "gb": gb, "ev": ev}
+        with ctx:
+            perm = self._permutation(n, dev, batch_size)
+            ev = torch.cuda.Event() if cuda else None
+            if ev is not None:
+                ev.record()
+        return {"idx": perm, "ev": ev,
+                "chunks": [(s, e, (e - s) * W) for s, e in split_bounds(n, batch_size, True)]}
+
+    def _take_plan(self, rec, dev):
+        if rec["ev"] is not None:
+            cur = torch.cuda.current_stream(dev)
+            cur.wait_event(rec["ev"])
+            rec["idx"].record_stream(cur)
+        if "chunks" in rec:
+            return rec["idx"], rec["chunks"]
+        if rec["ev"] is not None:
+            rec["ev"].synchronize()  # the share counts (pinned host): long done by now
+        chunks, o = [], 0
+        for (gs, ge), c in zip(rec["gb"], rec["cum"].tolist()):
+            chunks.append((o, c, ge - gs))
+            o = c
+        return rec["idx"], chunks
 
     def _dev_bounds(self, chunks, dev):
         """Device int64 [n_minibatch + 1] start offsets of the chunks (cached per plan)."""

@@ -60,6 +60,7 @@ class _Prefetch:
         self.bufs = [torch.empty(max(n, 1), dtype=torch.int32, pin_memory=True)
                      for _ in range(count)]
         self.states: List = [None] * count
+        self.ready = [threading.Event() for _ in range(count)]
         self.error: Optional[BaseException] = None
         self.thread = threading.Thread(target=self._run, name="tsrl-np-perm", daemon=True)
         self.thread.start()
@@ -70,14 +71,17 @@ class _Prefetch:
             for i, b in enumerate(self.bufs):
                 key, pos = _draws(key, pos, self.n, b.numpy().view(np.uint32))
                 self.states[i] = (key, pos)
+                self.ready[i].set()
         except BaseException as e:  # surfaced to the consumer
             self.error = e
+            for ev in self.ready:
+                ev.set()
 
-    def wait(self):
-        self.thread.join()
+    def wait(self, i: int):
+        """Block until permutation i's draws exist (not the later ones)."""
+        self.ready[i].wait()
         if self.error is not None:
             raise self.error
-
 
 class LegacyPermutation:
     """Callable: ``perm(n, device) -> int64 device tensor`` equal to
@@ -86,7 +90,7 @@ class LegacyPermutation:
     def __init__(self):
         self._pf: Optional[_Prefetch] = None
         self._pf_next = 0
-        self._ws = None
+        self._ws = {}  # per (device, stream): a workspace is only reused in its stream's order
 
     # -- device side ----------------------------------------------------------------------
     def _apply(self, host_draws: torch.Tensor, n: int, device) -> torch.Tensor:
@@ -95,34 +99,50 @@ class LegacyPermutation:
             return out
         L = _C.lib()
         wsb = int(L.tsrl_shuffle_apply_workspace_bytes(n))
-        if self._ws is None or self._ws.numel() < wsb or self._ws.device != out.device:
-            self._ws = torch.empty(wsb, dtype=torch.uint8, device=device)
+        wkey = (out.device, torch.cuda.current_stream(out.device).cuda_stream)
+        ws = self._ws.get(wkey)
+        if ws is None or ws.numel() < wsb:
+            ws = self._ws[wkey] = torch.empty(wsb, dtype=torch.uint8, device=device)
         d = torch.empty(n, dtype=torch.int32, device=device)
         d.copy_(host_draws[:n], non_blocking=host_draws.is_pinned())
-        _C.check(L.tsrl_shuffle_apply(_C.ptr(d), n, _C.ptr(out), _C.ptr(self._ws), wsb,
+        _C.check(L.tsrl_shuffle_apply(_C.ptr(d), n, _C.ptr(out), _C.ptr(ws), wsb,
                                       _C.stream_ptr(out.device)), "tsrl_shuffle_apply")
         return out
 
     # -- host stream ----------------------------------------------------------------------
-    def __call__(self, n: int, device) -> torch.Tensor:
+    def __call__(self, n: int, device, stream=None) -> torch.Tensor:
+        """The permutation as an int64 tensor on ``device``.  With ``stream`` the copy and the
+        device resolution are enqueued there (the caller orders its own stream after it and
+        owns the tensor's cross-stream lifetime); otherwise on the current stream."""
         st = _state_key()
         pf = self._pf
         if pf is not None and pf.n == n and self._pf_next < len(pf.bufs):
             i = self._pf_next
-            want = pf.start if i == 0 else None
-            pf.wait()
-            if want is None:
-                want = pf.states[i - 1]
+            pf.wait(i)
+            want = pf.start if i == 0 else pf.states[i - 1]
             if int(st[2]) == want[1] and np.array_equal(st[1], want[0]):
                 key, pos = pf.states[i]
                 np.random.set_state(("MT19937", key, pos, st[3], st[4]))
                 self._pf_next += 1
-                return self._apply(pf.bufs[i], n, device)
+                return self._apply_on(pf.bufs[i], n, device, stream)
         self._drop()
         buf = torch.empty(max(n, 1), dtype=torch.int32, pin_memory=True)
         key, pos = _draws(st[1], st[2], n, buf.numpy().view(np.uint32))
         np.random.set_state(("MT19937", key, pos, st[3], st[4]))
-        return self._apply(buf, n, device)
+        return self._apply_on(buf, n, device, stream)
+
+    def _apply_on(self, buf, n, device, stream):
+        if stream is None:
+            return self._apply(buf, n, device)
+        with torch.cuda.stream(stream):
+            return self._apply(buf, n, device)
+
+    def next_ready(self, n: int) -> bool:
+        """True if the next call with size ``n`` would not wait for host draws."""
+        pf = self._pf
+        if pf is None or pf.n != n or self._pf_next >= len(pf.bufs):
+            return False
+        return pf.ready[self._pf_next].is_set()
 
     def prefetch(self, n: int, count: int) -> None:
         """Start computing the draws of the next ``count`` permutations of size ``n`` from
