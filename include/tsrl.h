@@ -267,12 +267,20 @@ typedef struct tsrl_collect_args {
     /* obs RunningMeanStd */
     void* workspace;
     float* mean; float* var; float* snap_mean; float* snap_var; double* count;
-    double* totals;
+    double* totals;          /* data parallel / exact obs_rms: this step's f64 moments (the
+                                merge2 vector); NULL: the deferred merge below */
+    int64_t rms_step;        /* index of this launch in its chain of deferred steps (0: the
+                                first after tsrl_collect_rms_finalize or a fresh workspace) */
 } tsrl_collect_args;
 int64_t tsrl_collect_pack_floats(int64_t dim);
 int tsrl_collect_pack_w1(const float* W, int64_t dim, float* packed, void* stream);
 int64_t tsrl_collect_workspace_bytes(int64_t k, int64_t dim);
 int tsrl_collect_box_step(const tsrl_collect_args* a, void* stream);
+/* After the last deferred step of a chain (rms_step = that step's index): its integer
+ * obs_rms moments merged into mean / var / count, snap_mean / snap_var = the statistics after
+ * its step rows (what the closing tsrl_buffer_add normalises obs_next with).  Replaces the
+ * obs_rms update of VectorEnvNormObs.step (env/venv_wrappers.py:93-99) for that step. */
+int tsrl_collect_rms_finalize(const tsrl_collect_args* a, void* stream);
 /* *rel_dev = (*rel_dev + 1) % ring_size (device-side ring cursor for graph-captured steps). */
 int tsrl_ring_advance(int64_t* rel_dev, int64_t ring_size, void* stream);
 

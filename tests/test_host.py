@@ -37,10 +37,11 @@ def test_ctypes_struct_layout_matches_header(tmp_path):
     from tianshou_amd import _C
     src = tmp_path / "probe.c"
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "tsrl.h"\n'
-                   'int main(){printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(tsrl_add_args), '
+                   'int main(){printf("%zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(tsrl_add_args), '
                    'sizeof(tsrl_ppo_params), offsetof(tsrl_add_args, stat_idx), '
                    'offsetof(tsrl_ppo_params, norm_adv), sizeof(tsrl_collect_args), '
-                   'offsetof(tsrl_collect_args, sample), offsetof(tsrl_collect_args, totals));}')
+                   'offsetof(tsrl_collect_args, sample), offsetof(tsrl_collect_args, totals), '
+                   'offsetof(tsrl_collect_args, rms_step));}')
     exe = tmp_path / "probe"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)],
                    check=True)
@@ -52,6 +53,7 @@ def test_ctypes_struct_layout_matches_header(tmp_path):
     assert int(out[4]) == ctypes.sizeof(_C.CollectArgs)
     assert int(out[5]) == _C.CollectArgs.sample.offset
     assert int(out[6]) == _C.CollectArgs.totals.offset
+    assert int(out[7]) == _C.CollectArgs.rms_step.offset
 
 
 @pytest.mark.parametrize("name", ["manager", "ragged"])

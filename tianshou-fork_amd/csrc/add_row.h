@@ -31,15 +31,9 @@ __device__ __forceinline__ float norm1(float x, float m, float v, float eps, flo
     return y;
 }
 
-// Row r of one add (urel = the uniform ring position of this step) by nl lanes (lane < nl).
-// lx (nullable): the new live obs row is also written to lx[col * lxp] (the fused collect step
-// keeps it in LDS for the next policy step); cur_hbm = false then skips its HBM copy.
-__device__ __forceinline__ void add_row(const tsrl_add_args& a, int64_t r, int lane,
-                                        int64_t urel, float* lx = nullptr, int lxp = 0,
-                                        int nl = kWave, bool cur_hbm = true) {
-    const int64_t b = a.ids ? a.ids[r] : r;
-    const int64_t ptr = a.ptr ? a.ptr[r] : a.offset[b] + urel;
-
+// The payload copies of add_row (obs, act, raw obs_next rows) by nl lanes.
+__device__ __forceinline__ void add_row_copies(const tsrl_add_args& a, int64_t r, int lane,
+                                               int64_t ptr, int nl) {
     const int64_t obs_pitch = a.obs_src_pitch ? a.obs_src_pitch : a.obs_row_bytes;
     const int64_t next_pitch = a.obs_next_src_pitch ? a.obs_next_src_pitch : a.obs_row_bytes;
     if (a.obs_src && a.obs_dst)
@@ -51,6 +45,75 @@ __device__ __forceinline__ void add_row(const tsrl_add_args& a, int64_t r, int l
     if (a.obs_next_src_raw && a.obs_next_dst_raw)
         copy_row((const char*)a.obs_next_src_raw + r * next_pitch,
                  (char*)a.obs_next_dst_raw + ptr * a.obs_row_bytes, a.obs_row_bytes, lane, nl);
+}
+
+// The lane-0 part of add_row: flags, env id and the episode bookkeeping of row r, split
+// into its loads (RowTail::load) and the stores that use them (RowTail::apply), so a caller
+// can issue the loads early and apply them later.
+struct RowTail {
+    double rew, ep_rew;
+    int64_t ep_len, ep_idx, off, next_rel;
+    uint8_t tm, tr;
+
+    __device__ __forceinline__ void load(const tsrl_add_args& a, int64_t r, int64_t b) {
+        rew = a.rew ? a.rew[r] : 0.0;
+        tm = a.term ? a.term[r] : 0;
+        tr = a.trunc ? a.trunc[r] : 0;
+        ep_rew = a.ep_rew[b];
+        ep_len = a.ep_len[b];
+        ep_idx = a.ep_idx[b];
+        off = a.offset[b];
+        next_rel = a.next_rel ? a.next_rel[r] : 0;
+    }
+    __device__ __forceinline__ void apply(const tsrl_add_args& a, int64_t r, int64_t urel,
+                                          int64_t b, int64_t ptr) const {
+        const uint8_t done = (uint8_t)((tm != 0) | (tr != 0));
+        if (a.rew_dst) a.rew_dst[ptr] = rew;
+        if (a.term_dst) a.term_dst[ptr] = (uint8_t)(tm != 0);
+        if (a.trunc_dst) a.trunc_dst[ptr] = (uint8_t)(tr != 0);
+        if (a.done_dst) a.done_dst[ptr] = done;
+        if (a.env_id_dst) a.env_id_dst[ptr] = b;
+        // ReplayBuffer._add_index episode bookkeeping (base.py:205-214)
+        const double er = ep_rew + rew;
+        const int64_t el = ep_len + 1;
+        const int64_t ei = ep_idx + off;
+        if (a.out_ep_rew) a.out_ep_rew[r] = done ? er : er * 0.0;
+        if (a.out_ep_len) a.out_ep_len[r] = done ? el : 0;
+        if (a.out_ep_idx) a.out_ep_idx[r] = ei;
+        if (done) {
+            if (a.stat_rew) a.stat_rew[ptr] = er;
+            if (a.stat_len) a.stat_len[ptr] = el;
+            if (a.stat_idx) a.stat_idx[ptr] = ei;
+            a.ep_rew[b] = 0.0;
+            a.ep_len[b] = 0;
+            a.ep_idx[b] = a.next_rel ? next_rel
+                                     : (a.rel_dev ? (urel + 1) % a.ring_size : a.uniform_next);
+        } else {
+            a.ep_rew[b] = er;
+            a.ep_len[b] = el;
+        }
+    }
+};
+
+__device__ __forceinline__ void add_row_tail(const tsrl_add_args& a, int64_t r, int lane,
+                                             int64_t urel, int64_t b, int64_t ptr) {
+    if (lane == 0) {
+        RowTail rt;
+        rt.load(a, r, b);
+        rt.apply(a, r, urel, b, ptr);
+    }
+}
+
+// Row r of one add (urel = the uniform ring position of this step) by nl lanes (lane < nl).
+// lx (nullable): the new live obs row is also written to lx[col * lxp] (the fused collect step
+// keeps it in LDS for the next policy step); cur_hbm = false then skips its HBM copy.
+__device__ __forceinline__ void add_row(const tsrl_add_args& a, int64_t r, int lane,
+                                        int64_t urel, float* lx = nullptr, int lxp = 0,
+                                        int nl = kWave, bool cur_hbm = true) {
+    const int64_t b = a.ids ? a.ids[r] : r;
+    const int64_t ptr = a.ptr ? a.ptr[r] : a.offset[b] + urel;
+
+    add_row_copies(a, r, lane, ptr, nl);
     if (a.obs_next_src && (a.obs_next_dst || a.cur_obs)) {
         const float* src = a.obs_next_src + r * a.obs_dim;
         float* dst = a.obs_next_dst ? a.obs_next_dst + ptr * a.obs_dim : nullptr;
@@ -142,36 +205,7 @@ __device__ __forceinline__ void add_row(const tsrl_add_args& a, int64_t r, int l
             }
         }
     }
-    if (lane == 0) {
-        const double rew = a.rew ? a.rew[r] : 0.0;
-        const uint8_t tm = a.term ? a.term[r] : 0;
-        const uint8_t tr = a.trunc ? a.trunc[r] : 0;
-        const uint8_t done = (uint8_t)((tm != 0) | (tr != 0));
-        if (a.rew_dst) a.rew_dst[ptr] = rew;
-        if (a.term_dst) a.term_dst[ptr] = (uint8_t)(tm != 0);
-        if (a.trunc_dst) a.trunc_dst[ptr] = (uint8_t)(tr != 0);
-        if (a.done_dst) a.done_dst[ptr] = done;
-        if (a.env_id_dst) a.env_id_dst[ptr] = b;
-        // ReplayBuffer._add_index episode bookkeeping (base.py:205-214)
-        const double er = a.ep_rew[b] + rew;
-        const int64_t el = a.ep_len[b] + 1;
-        const int64_t ei = a.ep_idx[b] + a.offset[b];
-        if (a.out_ep_rew) a.out_ep_rew[r] = done ? er : er * 0.0;
-        if (a.out_ep_len) a.out_ep_len[r] = done ? el : 0;
-        if (a.out_ep_idx) a.out_ep_idx[r] = ei;
-        if (done) {
-            if (a.stat_rew) a.stat_rew[ptr] = er;
-            if (a.stat_len) a.stat_len[ptr] = el;
-            if (a.stat_idx) a.stat_idx[ptr] = ei;
-            a.ep_rew[b] = 0.0;
-            a.ep_len[b] = 0;
-            a.ep_idx[b] = a.next_rel ? a.next_rel[r]
-                                      : (a.rel_dev ? (urel + 1) % a.ring_size : a.uniform_next);
-        } else {
-            a.ep_rew[b] = er;
-            a.ep_len[b] = el;
-        }
-    }
+    add_row_tail(a, r, lane, urel, b, ptr);
 }
 
 }  // namespace tsrl

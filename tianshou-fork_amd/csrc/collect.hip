@@ -17,12 +17,20 @@
 //      and map_action exactly as policy.hip;
 //   C. the env step + auto-reset of these rows (synth.h, as env.hip's box_step_reset_kernel)
 //      with the column moments of the step rows and of the reset rows;
-//   D. obs_rms: the moments are folded deterministically without a grid barrier -- the last
-//      of each group of GS workgroups to finish (agent-scope ticket) sums its group's partials
-//      in index order, the last group sums the group partials in index order and applies both
-//      RunningMeanStd updates (rms.hip's merge2 arithmetic), re-arming every ticket.  With
-//      `totals` set (data parallel) it writes the step/reset moments instead and the caller
-//      all-reduces them and runs tsrl_rms_merge2(nblk = 1).
+//   D. obs_rms: the synthetic env's values are x = m 2^-23 with integer |m| <= 2^23
+//      (synth.h), so the column moments are summed EXACTLY as integers (sum m, sum m^2 <
+//      2^59 over any step) by 64-bit atomics into a per-step totals slot -- exact sums are
+//      independent of the summation order, so no ordered fold is needed.  The merge of those
+//      totals into the RunningMeanStd (rms.hip's merge2 arithmetic) is DEFERRED to the next
+//      launch: every workgroup of launch i+1 merges step i's totals into the state left by
+//      launch i (its pending add needs exactly those statistics) in its prologue, workgroup
+//      0 publishes the merged state into the other state slot, and the last workgroup to
+//      take a ticket re-zeroes the consumed totals slot.  The launch therefore ends with its
+//      env rows, with no grid-wide hand-off; tsrl_collect_rms_finalize merges the last
+//      step's totals into the caller's state before the closing tsrl_buffer_add.  With
+//      `totals` set (data parallel / exact obs_rms) the last arriver converts this step's
+//      integer totals into the f64 moments vector instead; the caller all-reduces it and runs
+//      tsrl_rms_merge2(nblk = 1).
 #include "add_row.h"
 #include "noise.h"
 #include "synth.h"
@@ -42,7 +50,6 @@ constexpr int NW = 8;          // waves per workgroup
 constexpr int NT = NW * 64;
 constexpr int H = 64;          // actor hidden width
 constexpr int AMAX = 32;
-constexpr int GS = 16;         // workgroups per obs_rms group
 constexpr int KMAX = 512;      // observation columns handled (padded to 128)
 constexpr int XP = 17;         // LDS pitch of the live-obs tile sX[col][row]
 constexpr int HP = 16;         // h1 / h2 tiles [feature][row]
@@ -60,9 +67,22 @@ constexpr int WP = 68;         // W2 / W3 rows (4i + k banks: conflict-free A fr
 #if COLLECT_TRACE
 #define TSTAMP(i) \
     if (t == 0) ws.trace[((rng_step & 15) * gridDim.x + blockIdx.x) * 8 + (i)] = __builtin_amdgcn_s_memrealtime();
+// detail stamps of the prologue, in a second area of the same shape
+#define TSTAMP2(i) \
+    if (t == 0) ws.trace[(16 + (rng_step & 15)) * gridDim.x * 8 + blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime();
 #else
 #define TSTAMP(i)
+#define TSTAMP2(i)
 #endif
+
+// Workgroup barrier that orders LDS only: outstanding global loads and stores stay in flight
+// (__syncthreads also waits for every global store's acknowledgement and every pending load)
+#define LDS_SYNC()                                                                          \
+    do {                                                                                    \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                  \
+        __builtin_amdgcn_s_barrier();                                                       \
+        asm volatile("" ::: "memory");                                                      \
+    } while (0)
 
 __host__ __device__ inline int64_t kpad(int64_t dim) { return (dim + 127) / 128 * 128; }
 
@@ -88,35 +108,71 @@ __global__ void pack_w1_kernel(const float* __restrict__ W, int64_t dim, float* 
     }
 }
 
-// Write-through (sc1) 16-byte stores and L1-bypassing (sc1) 16-byte loads of the handed-off
-// obs_rms partials (buffer instructions, aux 16 = sc1), byte offsets into one descriptor.
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void st2_sc1(__amdgpu_buffer_rsrc_t r, int off, double x, double y) {
-    const uint64_t a = __double_as_longlong(x), b = __double_as_longlong(y);
-    u32x4 v;
-    v.x = (unsigned)a;
-    v.y = (unsigned)(a >> 32);
-    v.z = (unsigned)b;
-    v.w = (unsigned)(b >> 32);
-    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16);
-}
-__device__ __forceinline__ double2 ld2_sc1(__amdgpu_buffer_rsrc_t r, int off) {
-    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
-    return make_double2(__longlong_as_double(((uint64_t)v.y << 32) | v.x),
-                        __longlong_as_double(((uint64_t)v.w << 32) | v.z));
-}
-
+// Workspace: tickets, three integer-totals slots (step i of a chain accumulates slot i % 3,
+// reads slot (i - 1) % 3, zeroes slot (i + 1) % 3) and two RunningMeanStd state slots (read
+// i % 2, write (i + 1) % 2), the diagnostic trace.  Totals slot (int64): [0, D) sum m of the step rows per
+// column, [D, 2D) sum m^2, [2D, 3D) / [3D, 4D) the same over the reset rows, [4D] reset rows.
+constexpr int TOT_N = 4 * KMAX + 2;
+struct RmsState {
+    float mean[KMAX];
+    float var[KMAX];
+    double count;
+    double pad[7];
+};
 struct Ws {
-    unsigned int* tickets;  // [ngroups + 1]
-    double* part;           // [nblk][PSTRIDE]
-    double* gpart;          // [ngroups][PSTRIDE]
-    int64_t pstride;        // 4 * dim + 4 (s1, q1, s2, q2 per column; reset-row count, pad)
+    unsigned int* tickets;  // [1] data-parallel last arriver
+    long long* tot[3];
+    RmsState* st[2];
     int64_t nblk;
-    int ngroups;
     uint64_t* trace;
 };
-// Partial slab of one workgroup / group (doubles): [0, 2D) step rows (s, q) per column,
-// [2D, 4D) reset rows (s, q) per column (zeros without reset rows), [4D] reset-row count.
+
+// m such that the synthetic env value is x = m 2^-23 exactly (box_val, synth.h)
+__device__ __forceinline__ int box_m(uint64_t key, int64_t d) {
+    const uint64_t h = sm64(key + (uint64_t)d * synth::GOLD);
+    return (int)(h >> 40) - (1 << 23);
+}
+
+__device__ __forceinline__ void atomic_add_i64(long long* p, long long v) {
+    __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// rms.hip rms_merge2_kernel's two RunningMeanStd updates for one column from exact integer
+// moments: (m0, v0, count) -> snapshot after the k step rows -> state after the nd reset rows.
+__device__ __forceinline__ void merge_column(double m0, double v0, double old_count, double k,
+                                             long long s1i, long long q1i, double nd,
+                                             long long s2i, long long q2i, float& snap_m,
+                                             float& snap_v, float& fin_m, float& fin_v) {
+#pragma clang fp contract(off)
+    const double tot1 = old_count + k, tot2 = tot1 + nd;
+    if (k > 0.0) {
+        const double S1 = (double)s1i * 0x1p-23, Q1 = (double)q1i * 0x1p-46;
+        const double bm = S1 / k;
+        double bv = Q1 / k - bm * bm;
+        bv = bv < 0.0 ? 0.0 : bv;
+        const double delta = bm - m0;
+        const double nm = m0 + delta * k / tot1;
+        const double m2 = v0 * old_count + bv * k + delta * delta * old_count * k / tot1;
+        m0 = (double)(float)nm;
+        v0 = (double)(float)(m2 / tot1);
+    }
+    snap_m = (float)m0;
+    snap_v = (float)v0;
+    if (nd > 0.0) {
+        const double S2 = (double)s2i * 0x1p-23, Q2 = (double)q2i * 0x1p-46;
+        const double bm = S2 / nd;
+        double bv = Q2 / nd - bm * bm;
+        bv = bv < 0.0 ? 0.0 : bv;
+        const double delta = bm - m0;
+        const double nm = m0 + delta * nd / tot2;
+        const double m2 = v0 * tot1 + bv * nd + delta * delta * tot1 * nd / tot2;
+        m0 = (double)(float)nm;
+        v0 = (double)(float)(m2 / tot2);
+    }
+    fin_m = (float)m0;
+    fin_v = (float)v0;
+}
 
 __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_args a, Ws ws) {
 #pragma clang fp contract(off)
@@ -129,6 +185,10 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
     __shared__ RowState rs[R], rr[R];
     __shared__ int s_nd, s_last;
     __shared__ int64_t s_row[R];
+    // deferred obs_rms merge: the statistics after the previous step's step rows (obs_next
+    // normalisation) and after its reset rows (reset rows, state)
+    __shared__ __attribute__((aligned(16))) float sSnapM[KMAX], sSnapV[KMAX], sFinM[KMAX],
+        sFinV[KMAX];
     const int t = threadIdx.x;
     const int w = t >> 6, l = t & 63;
     const int64_t k = a.k;
@@ -138,6 +198,8 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
     const int nrows = (int)min((int64_t)R, k - r0);
     const int Kp = (int)kpad(D), KW = Kp / NW, SQ = KW / 16;
     const int64_t rng_step = a.rng_ctr ? *a.rng_ctr : 0;
+    // this step's ring position of the pending add (first load: nothing waits behind it)
+    const int64_t urel = a.add.k > 0 ? (a.add.rel_dev ? *a.add.rel_dev : a.add.uniform_rel) : 0;
 #if COLLECT_STOP == 9
     if (t >= 0) return;  // launch overhead only
 #endif
@@ -154,7 +216,117 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
 #endif
     TSTAMP(0)
 
-    // small actor weights: loads in flight during the add phase, LDS stores after it
+    // ---- deferred obs_rms merge of the previous step (see D) ----------------------------------
+    const bool defer = a.totals == nullptr;
+    const int step = a.rms_step;  // index of this launch in its chain of deferred steps
+    const int par = step & 1;
+    const int tcur = step % 3, tprev = (step + 2) % 3, tnext = (step + 1) % 3;
+    const bool merge = defer && step > 0;
+    tsrl_add_args ad = a.add;
+    // A1 (merge chain): every load of the pending add (raw rows, reset flag, act row, flags
+    // and episode counters) and of the merge is issued first; they are consumed after the
+    // merge, so one memory latency covers all of them.  32 lanes per row, float4 pieces
+    // q = lane + 32 j of the row.
+    constexpr int AQ = (KMAX / 4 + 31) / 32;
+    const int arw = t >> 5, aln = t & 31;
+    const int nq = D >> 2;
+    const int act_n = (int)(ad.act_row_bytes >> 2);
+    const bool fast = merge && ad.k > 0 && ad.obs_next_src && ad.obs_next_dst &&
+                      ad.norm_mean && ad.reset_mean && ad.reset_src && ad.reset_mask &&
+                      !ad.obs_src && !ad.obs_next_src_raw && ad.act_src && ad.act_dst &&
+                      (ad.act_row_bytes & 3) == 0 && act_n <= 32 &&
+                      aligned16(ad.obs_next_src) && aligned16(ad.obs_next_dst) &&
+                      aligned16(ad.reset_src);
+    const int64_t ar = r0 + arw;
+    const bool arow = fast && arw < nrows;
+    float4 axs[AQ], axr[AQ];
+    uint8_t amask = 0;
+    float aact = 0.0f;
+    int64_t aptr_ld = 0;
+    RowTail atail;
+    if (arow) {
+        amask = ad.reset_mask[ar];  // first: waiting for it below waits for nothing later
+        const float4* s4 = reinterpret_cast<const float4*>(ad.obs_next_src + ar * D);
+#pragma unroll
+        for (int j = 0; j < AQ; ++j) {
+            const int q = aln + 32 * j;
+            axs[j] = s4[q < nq ? q : 0];
+        }
+        if (aln < act_n) aact = reinterpret_cast<const float*>(ad.act_src)[ar * act_n + aln];
+        // the row's storage position (every lane: it addresses the lane's stores)
+        aptr_ld = ad.ptr ? ad.ptr[ar] : ad.offset[ar] + urel;
+        if (aln == 0) atail.load(ad, ar, ar);
+    }
+    TSTAMP2(0)
+    float mm0 = 0.f, mv0 = 0.f;
+    long long ms1 = 0, mq1 = 0, ms2 = 0, mq2 = 0;
+    double mcount = 0.0, mnd = 0.0;
+    if (merge) {
+        const RmsState* sin = ws.st[par];
+        const long long* tp = ws.tot[tprev];
+        mcount = sin->count;
+        mnd = (double)tp[4 * D];
+        if (t < D) {  // D <= KMAX = NT: one column per thread
+            mm0 = sin->mean[t];
+            mv0 = sin->var[t];
+            ms1 = tp[t];
+            mq1 = tp[D + t];
+            ms2 = tp[2 * D + t];
+            mq2 = tp[3 * D + t];
+        }
+    }
+    TSTAMP2(1)
+    // the reset rows of envs that finished (their flag has arrived with the other loads)
+    if (arow && amask) {
+        const float4* r4 = reinterpret_cast<const float4*>(ad.reset_src + ar * D);
+#pragma unroll
+        for (int j = 0; j < AQ; ++j) {
+            const int q = aln + 32 * j;
+            axr[j] = r4[q < nq ? q : 0];
+        }
+    }
+    TSTAMP2(2)
+    if (merge) {
+        const double kp = (double)k;  // the chain's steps all cover the same k envs
+        if (t < D)
+            merge_column((double)mm0, (double)mv0, mcount, kp, ms1, mq1, mnd, ms2, mq2,
+                         sSnapM[t], sSnapV[t], sFinM[t], sFinV[t]);
+        TSTAMP2(3)
+        LDS_SYNC();
+        TSTAMP2(4)
+        if (blockIdx.x == 0) {
+            RmsState* so = ws.st[par ^ 1];
+            if (t < D) {
+                so->mean[t] = sFinM[t];
+                so->var[t] = sFinV[t];
+            }
+            if (t == 0) so->count = mcount + kp + mnd;
+            // the slot the next launch accumulates: read by the launch before this one
+            long long* tz = ws.tot[tnext];
+            for (int i = t; i <= 4 * D; i += NT) tz[i] = 0;
+        }
+        if (ad.norm_mean) {
+            ad.norm_mean = sSnapM;
+            ad.norm_var = sSnapV;
+        }
+        if (ad.reset_mean) {
+            ad.reset_mean = sFinM;
+            ad.reset_var = sFinV;
+        }
+    } else if (defer && blockIdx.x == 0) {
+        // first step of a chain: the caller's state seeds the state slot (slot 1 of the
+        // totals ring is zero: tsrl_collect_rms_finalize cleared the ring)
+        RmsState* so = ws.st[par ^ 1];
+        for (int d = t; d < D; d += NT) {
+            so->mean[d] = a.mean[d];
+            so->var[d] = a.var[d];
+        }
+        if (t == 0) so->count = *a.count;
+    }
+
+    // actor weights: issued after every load the add and the merge wait for (vmcnt retires
+    // in order, so a wait for an earlier load would also wait for these), in flight during
+    // the add and the env step
     float4 w2r[2], w3r;
 #pragma unroll
     for (int j = 0; j < 2; ++j) w2r[j] = reinterpret_cast<const float4*>(a.w2)[t + NT * j];
@@ -184,16 +356,53 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
                 wall[sq][ft] = wp[((sq < SQ ? sq : 0) * 4 + ft) * 64];
     }
 
+    TSTAMP(4)
     // ---- A. pending add of the previous step -> buffer rows + live obs (HBM and sX) ---------
-    if (a.add.k > 0) {
-        const int64_t urel = a.add.rel_dev ? *a.add.rel_dev : a.add.uniform_rel;
-        // 32 lanes per row: all 16 rows' loads in flight at once
-        const int rw = t >> 5;
-        if (rw < nrows) add_row(a.add, r0 + rw, t & 31, urel, sX + rw, XP, 32, false);
+    if (ad.k > 0) {
+        if (fast) {
+            // A2: normalise the prefetched rows: obs_next with the statistics after the step
+            // rows, the live obs of a reset env with those after the reset rows (add_row)
+            if (arow) {
+                const int64_t aptr = aptr_ld;
+                float4* dst = reinterpret_cast<float4*>(ad.obs_next_dst + aptr * D);
+                const float eps = ad.norm_eps, clip = ad.norm_clip;
+#pragma unroll
+                for (int j = 0; j < AQ; ++j) {
+                    const int q = aln + 32 * j;
+                    if (q >= nq) break;
+                    const float4 m = *reinterpret_cast<const float4*>(&sSnapM[4 * q]);
+                    const float4 v = *reinterpret_cast<const float4*>(&sSnapV[4 * q]);
+                    float4 x = axs[j];
+                    x.x = norm1(x.x, m.x, v.x, eps, clip);
+                    x.y = norm1(x.y, m.y, v.y, eps, clip);
+                    x.z = norm1(x.z, m.z, v.z, eps, clip);
+                    x.w = norm1(x.w, m.w, v.w, eps, clip);
+                    dst[q] = x;
+                    if (amask) {
+                        const float4 mr = *reinterpret_cast<const float4*>(&sFinM[4 * q]);
+                        const float4 vr = *reinterpret_cast<const float4*>(&sFinV[4 * q]);
+                        x = axr[j];
+                        x.x = norm1(x.x, mr.x, vr.x, eps, clip);
+                        x.y = norm1(x.y, mr.y, vr.y, eps, clip);
+                        x.z = norm1(x.z, mr.z, vr.z, eps, clip);
+                        x.w = norm1(x.w, mr.w, vr.w, eps, clip);
+                    }
+                    float* lx = sX + arw;
+                    lx[(4 * q) * XP] = x.x;
+                    lx[(4 * q + 1) * XP] = x.y;
+                    lx[(4 * q + 2) * XP] = x.z;
+                    lx[(4 * q + 3) * XP] = x.w;
+                }
+                if (aln < act_n) reinterpret_cast<float*>(ad.act_dst)[aptr * act_n + aln] = aact;
+                if (aln == 0) atail.apply(ad, ar, urel, ar, aptr);
+            }
+        } else {
+            // 32 lanes per row: all 16 rows' loads in flight at once
+            if (arw < nrows) add_row(ad, r0 + arw, aln, urel, sX + arw, XP, 32, false);
+        }
         if (a.add.rel_next && blockIdx.x == 0 && t == 0)
             *a.add.rel_next = (urel + 1) % a.add.ring_size;
     } else {
-        const int nq = D >> 2;
         for (int i = t; i < nrows * nq; i += NT) {
             const int rw = i / nq, q = i - rw * nq;
             const float4 x = reinterpret_cast<const float4*>(a.cur + (r0 + rw) * D)[q];
@@ -204,7 +413,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         }
     }
     TSTAMP(1)
-    // the env rows' episode counters: loaded now, used after the actor phase
+    // the env rows' episode counters: loaded now, used by the env step
     int64_t ej = 0, et = 0;
     if (t < nrows) {
         ej = a.ep_j[r0 + t];
@@ -256,7 +465,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         shi[t] = vhi;
     }
     if (a.rng_next && blockIdx.x == 0 && t == 0) *a.rng_next = rng_step + 1;
-    __syncthreads();
+    LDS_SYNC();
     // this step's stored obs rows (ReplayBuffer obs of step i = the live obs the actor sees):
     // written here from LDS, so the add of step i (next launch / flush) copies nothing and the
     // live obs never round-trips through HBM between fused steps
@@ -272,11 +481,72 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         }
         s_row[t] = a.obs_offset[r0 + t] + urel;
     }
-    __syncthreads();
+    LDS_SYNC();
     for (int i = t; i < nrows * D; i += NT) {
         const int rw = i / D, c = i - rw * D;
         a.obs_dst[s_row[rw] * D + c] = sX[c * XP + rw];
     }
+    // ---- C. env step + auto-reset of these rows (env.hip box_step_reset_kernel) -------------
+    // The synthetic env's transition does not read the action, so the step runs before the
+    // actor: its obs_rms atomics drain while the actor computes.  Phase A of this launch has
+    // consumed the previous step's env rows of this workgroup (the __syncthreads above).
+    if (t == 0) s_nd = 0;
+    LDS_SYNC();
+    if (t < R) {
+        const int64_t r = r0 + t;
+        RowState st = {0ull, 0}, sr = {0ull, 0};
+        if (t < nrows) {
+            const int64_t e = r;
+            int64_t j = ej;
+            int64_t tt = et + 1;
+            st.key = env_key(a.env_seed, (uint64_t)e, j, tt);
+            st.active = 1;
+            const uint64_t h = sm64(st.key ^ REW_SALT);
+            a.rew[r] = (double)(h >> 40) * 0x1p-24;
+            const bool dn = tt >= a.ep_len;
+            a.term[r] = (uint8_t)(dn && (e % 2 == 0));
+            a.trunc[r] = (uint8_t)(dn && (e % 2 == 1));
+            a.done[r] = (uint8_t)dn;
+            if (dn) {
+                j += 1;
+                tt = (j == 0) ? (e % a.ep_len) : 0;
+                a.ep_j[e] = j;
+                sr.key = env_key(a.env_seed, (uint64_t)e, j, tt);
+                sr.active = 1;
+                atomicAdd(&s_nd, 1);
+            }
+            a.ep_t[e] = tt;
+        }
+        rs[t] = st;
+        rr[t] = sr;
+    }
+    LDS_SYNC();
+    const int nd = s_nd;
+    long long* tc = ws.tot[tcur];
+    for (int d = t; d < D; d += NT) {
+        long long s1 = 0, q1 = 0, s2 = 0, q2 = 0;
+        for (int r = 0; r < nrows; ++r) {
+            const int m = box_m(rs[r].key, d);
+            a.raw[(r0 + r) * D + d] = (float)m * 0x1p-23f;  // == box_val(key, d), exactly
+            s1 += m;
+            q1 += (long long)m * m;
+        }
+        atomic_add_i64(tc + d, s1);
+        atomic_add_i64(tc + D + d, q1);
+        if (nd > 0) {
+            for (int r = 0; r < nrows; ++r) {
+                if (!rr[r].active) continue;
+                const int m = box_m(rr[r].key, d);
+                a.reset_raw[(r0 + r) * D + d] = (float)m * 0x1p-23f;
+                s2 += m;
+                q2 += (long long)m * m;
+            }
+            atomic_add_i64(tc + 2 * D + d, s2);
+            atomic_add_i64(tc + 3 * D + d, q2);
+        }
+    }
+    if (t == 0 && nd > 0) atomic_add_i64(tc + 4 * D, nd);
+    TSTAMP(2)
 #if COLLECT_STOP == 1
     return;
 #endif
@@ -306,7 +576,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
 #pragma unroll
             for (int r = 0; r < 4; ++r) red[((w * 4 + ft) * 4 + r) * 64 + l] = acc[ft][r];
     }
-    __syncthreads();
+    LDS_SYNC();
     // h1 = tanh(sum over the 8 waves in order + b1) -> sH1[f][row]
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -318,7 +588,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         const int f = 16 * ft + 4 * (ln >> 4) + r;
         sH1[f * HP + (ln & 15)] = tanh_nb(z + sb1[f]);
     }
-    __syncthreads();
+    LDS_SYNC();
     // layer 2: wave w -> feature tile w & 3 over k half w >> 2 (8 steps of 4)
     {
         const int ft = w & 3, kh = w >> 2;
@@ -330,7 +600,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
 #pragma unroll
         for (int r = 0; r < 4; ++r) red[(w * 4 + r) * 64 + l] = z[r];
     }
-    __syncthreads();
+    LDS_SYNC();
     // h2 = tanh(half 0 + half 1 + b2) -> sH2
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -340,7 +610,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         const int f = 16 * ft + 4 * (ln >> 4) + r;
         sH2[f * HP + (ln & 15)] = tanh_nb(z + sb2[f]);
     }
-    __syncthreads();
+    LDS_SYNC();
     // mu head: wave w -> action tile w & 1 over k quarter w >> 1 (4 steps of 4)
     {
         const int at = w & 1, kq = w >> 1;
@@ -352,7 +622,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
 #pragma unroll
         for (int r = 0; r < 4; ++r) red[(w * 4 + r) * 64 + l] = z[r];
     }
-    __syncthreads();
+    LDS_SYNC();
     // mu = sum of the 4 quarters + b3; act = randn * sigma + mu; map_action -> act_remap
     {
         const int ln = t & 63, r = (t >> 6) & 3, at = t >> 8;  // 2 x 4 x 64 = 512 threads
@@ -380,201 +650,86 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
 #if COLLECT_STOP == 2
     return;
 #endif
-    // ---- C. env step + auto-reset of these rows (env.hip box_step_reset_kernel) -------------
-    TSTAMP(2)
-    if (t == 0) s_nd = 0;
-    __syncthreads();
-    if (t < R) {
-        const int64_t r = r0 + t;
-        RowState st = {0ull, 0}, sr = {0ull, 0};
-        if (t < nrows) {
-            const int64_t e = r;
-            int64_t j = ej;
-            int64_t tt = et + 1;
-            st.key = env_key(a.env_seed, (uint64_t)e, j, tt);
-            st.active = 1;
-            const uint64_t h = sm64(st.key ^ REW_SALT);
-            a.rew[r] = (double)(h >> 40) * 0x1p-24;
-            const bool dn = tt >= a.ep_len;
-            a.term[r] = (uint8_t)(dn && (e % 2 == 0));
-            a.trunc[r] = (uint8_t)(dn && (e % 2 == 1));
-            a.done[r] = (uint8_t)dn;
-            if (dn) {
-                j += 1;
-                tt = (j == 0) ? (e % a.ep_len) : 0;
-                a.ep_j[e] = j;
-                sr.key = env_key(a.env_seed, (uint64_t)e, j, tt);
-                sr.active = 1;
-                atomicAdd(&s_nd, 1);
-            }
-            a.ep_t[e] = tt;
-        }
-        rs[t] = st;
-        rr[t] = sr;
-    }
-    __syncthreads();
-    const int nd = s_nd;
-    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
-        ws.part + (int64_t)blockIdx.x * ws.pstride, 0, (int)(ws.pstride * 8), 0x00020000);
-    for (int d = t; d < D; d += NT) {
-        double s1 = 0.0, q1 = 0.0, s2 = 0.0, q2 = 0.0;
-        for (int r = 0; r < nrows; ++r) {
-            const float x = box_val(rs[r].key, d);
-            a.raw[(r0 + r) * D + d] = x;
-            s1 += (double)x;
-            q1 += (double)x * (double)x;
-        }
-        if (nd > 0)
-            for (int r = 0; r < nrows; ++r) {
-                if (!rr[r].active) continue;
-                const float x = box_val(rr[r].key, d);
-                a.reset_raw[(r0 + r) * D + d] = x;
-                s2 += (double)x;
-                q2 += (double)x * (double)x;
-            }
-        st2_sc1(prs, 16 * d, s1, q1);
-        st2_sc1(prs, 16 * (D + d), s2, q2);
-    }
-    if (t == 0) st2_sc1(prs, 32 * D, (double)nd, 0.0);
+    TSTAMP(3)
+    if (defer) return;
 
 #if COLLECT_STOP == 3
     return;
 #endif
-    // ---- D. obs_rms: deterministic two-level fold by the last workgroups ---------------------
-    // Hand-off (cdna_hip_programming.md Guideline 16, counter form with write-through data):
-    // partials stored sc1 and drained by every wave, ONE relaxed agent-scope ticket add per
-    // workgroup; the last arriver reads them with sc1 loads only (no L2 write-back / L1
-    // invalidate fences: a __threadfence() in every thread cost ~100 us per step).
+    // ---- D (data parallel / exact obs_rms): the last arriver writes the f64 moments ----------
+    // Hand-off (cdna_hip_programming.md Guideline 16, counter form): every wave's atomics are
+    // performed (vmcnt 0) before the workgroup's one relaxed agent-scope ticket add; the last
+    // arriver reads the totals with agent-scope atomic loads.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    TSTAMP(3)
-    const int g = (int)(blockIdx.x / GS);
-    const int64_t gb0 = (int64_t)g * GS, gb1 = min(gb0 + GS, ws.nblk);
     if (t == 0) {
-        const unsigned int prev = __hip_atomic_fetch_add(&ws.tickets[g], 1u, __ATOMIC_RELAXED,
+        const unsigned int prev = __hip_atomic_fetch_add(&ws.tickets[1], 1u, __ATOMIC_RELAXED,
                                                          __HIP_MEMORY_SCOPE_AGENT);
-        s_last = prev == (unsigned int)(gb1 - gb0 - 1);
+        s_last = prev == (unsigned int)(ws.nblk - 1);
     }
     __syncthreads();
     if (!s_last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // the group's slabs, every load of an entry issued before its (index-ordered) sum; entry
-    // i < D: step column i, D <= i < 2D: reset column i - D, i = 2D: (reset-row count, 0)
-    const int gn = (int)(gb1 - gb0);
-    const int64_t sb = ws.pstride * 8;  // slab bytes
-    const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc(
-        ws.part + gb0 * ws.pstride, 0, (int)(sb * gn), 0x00020000);
-    const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
-        ws.gpart + (int64_t)g * ws.pstride, 0, (int)sb, 0x00020000);
-    for (int i = t; i <= 2 * D; i += NT) {
-        double2 v[GS];
-#pragma unroll
-        for (int b = 0; b < GS; ++b)
-            v[b] = b < gn ? ld2_sc1(grs, (int)(b * sb + 16 * i)) : make_double2(0.0, 0.0);
-        double x = 0.0, y = 0.0;
-#pragma unroll
-        for (int b = 0; b < GS; ++b) {
-            x += v[b].x;
-            y += v[b].y;
-        }
-        st2_sc1(ors, 16 * i, x, y);
+    for (int i = t; i <= 4 * D; i += NT) {
+        const long long v = __hip_atomic_load(tc + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int blk = i / D;  // 0, 2: sums (2^-23); 1, 3: sums of squares (2^-46); 4: count
+        double x = (double)v;
+        if (i < 4 * D) x *= (blk & 1) ? 0x1p-46 : 0x1p-23;
+        // payload layout of merge2: [2D) (s, q) per column of the step rows, [2D, 4D) reset
+        // rows, [4D] reset-row count, [4D + 1] step rows
+        const int d = i - blk * D;
+        if (i == 4 * D) a.totals[4 * D] = x;
+        else a.totals[(blk >> 1) * 2 * D + 2 * d + (blk & 1)] = x;
+        tc[i] = 0;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    TSTAMP(4)
     if (t == 0) {
-        __hip_atomic_store(&ws.tickets[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned int prev = __hip_atomic_fetch_add(&ws.tickets[ws.ngroups], 1u,
-                                                         __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT);
-        s_last = prev == (unsigned int)(ws.ngroups - 1);
-    }
-    __syncthreads();
-    if (!s_last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // the last group: totals over the groups in index order, then both updates per column
-    const __amdgpu_buffer_rsrc_t trs = __builtin_amdgcn_make_buffer_rsrc(
-        ws.gpart, 0, (int)(ws.pstride * 8 * ws.ngroups), 0x00020000);
-    const int64_t gsb = ws.pstride * 8;
-    const double old_count = *a.count;
-    const double bc1 = (double)k;
-    double ND = 0.0;
-    for (int d = t; d < D; d += NT) {  // D > 0: thread 0 always runs (its ND sets count)
-        double S1 = 0.0, Q1 = 0.0, S2 = 0.0, Q2 = 0.0;
-        const int dc = d;
-        ND = 0.0;
-        for (int g0 = 0; g0 < ws.ngroups; g0 += GS) {
-            double2 v1[GS], v2[GS], vn[GS];
-#pragma unroll
-            for (int j = 0; j < GS; ++j) {
-                const bool in = g0 + j < ws.ngroups;
-                const int base = (int)((g0 + j) * gsb);
-                v1[j] = in ? ld2_sc1(trs, base + 16 * dc) : make_double2(0.0, 0.0);
-                v2[j] = in ? ld2_sc1(trs, base + 16 * (D + dc)) : make_double2(0.0, 0.0);
-                vn[j] = in ? ld2_sc1(trs, base + 32 * D) : make_double2(0.0, 0.0);
-            }
-#pragma unroll
-            for (int j = 0; j < GS; ++j) {
-                S1 += v1[j].x;
-                Q1 += v1[j].y;
-                S2 += v2[j].x;
-                Q2 += v2[j].y;
-                ND += vn[j].x;
-            }
-        }
-        const double tot1 = old_count + bc1, tot2 = tot1 + ND;
-        if (a.totals) {
-            a.totals[2 * d] = S1;
-            a.totals[2 * d + 1] = Q1;
-            a.totals[2 * D + 2 * d] = S2;
-            a.totals[2 * D + 2 * d + 1] = Q2;
-            continue;
-        }
-        // rms.hip rms_merge2_kernel's arithmetic
-        double m0 = (double)a.mean[d], v0 = (double)a.var[d];
-        if (bc1 > 0.0) {
-            const double bm = S1 / bc1;
-            double bv = Q1 / bc1 - bm * bm;
-            bv = bv < 0.0 ? 0.0 : bv;
-            const double delta = bm - m0;
-            const double nm = m0 + delta * bc1 / tot1;
-            const double m2 = v0 * old_count + bv * bc1 + delta * delta * old_count * bc1 / tot1;
-            m0 = (double)(float)nm;
-            v0 = (double)(float)(m2 / tot1);
-        }
-        a.snap_mean[d] = (float)m0;
-        a.snap_var[d] = (float)v0;
-        if (ND > 0.0) {
-            const double bm = S2 / ND;
-            double bv = Q2 / ND - bm * bm;
-            bv = bv < 0.0 ? 0.0 : bv;
-            const double delta = bm - m0;
-            const double nm = m0 + delta * ND / tot2;
-            const double m2 = v0 * tot1 + bv * ND + delta * delta * tot1 * ND / tot2;
-            m0 = (double)(float)nm;
-            v0 = (double)(float)(m2 / tot2);
-        }
-        a.mean[d] = (float)m0;
-        a.var[d] = (float)v0;
-    }
-    __syncthreads();  // every thread has read *count
-    TSTAMP(5)
-    if (t == 0) {
-        if (a.totals) {
-            a.totals[4 * D] = ND;
-            a.totals[4 * D + 1] = bc1;
-        } else {
-            *a.count = old_count + bc1 + ND;
-        }
-        __hip_atomic_store(&ws.tickets[ws.ngroups], 0u, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+        a.totals[4 * D + 1] = (double)k;
+        __hip_atomic_store(&ws.tickets[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
+// tsrl_collect_rms_finalize: the last deferred step's totals merged into the caller's state
+// (mean / var / count and the snapshot after its step rows), the totals slot re-zeroed.
+__global__ __launch_bounds__(NT) void rms_finalize_kernel(tsrl_collect_args a, Ws ws) {
+#pragma clang fp contract(off)
+    const int t = threadIdx.x;
+    const int D = (int)a.dim;
+    const int step = a.rms_step;  // the chain's last launch
+    const RmsState* sin = ws.st[(step + 1) & 1];  // the state the last launch published
+    long long* tp = ws.tot[step % 3];
+    const double old_count = sin->count, nd = (double)tp[4 * D], kp = (double)a.k;
+    for (int d = t; d < D; d += NT) {
+        float sm, sv, fm, fv;
+        merge_column((double)sin->mean[d], (double)sin->var[d], old_count, kp, tp[d],
+                     tp[D + d], nd, tp[2 * D + d], tp[3 * D + d], sm, sv, fm, fv);
+        a.snap_mean[d] = sm;
+        a.snap_var[d] = sv;
+        a.mean[d] = fm;
+        a.var[d] = fv;
+    }
+    __syncthreads();  // every thread has read the totals
+    for (int j = 0; j < 3; ++j)
+        for (int i = t; i <= 4 * D; i += NT) ws.tot[j][i] = 0;
+    if (t == 0) *a.count = old_count + kp + nd;
+}
+
 inline int64_t nblk_for(int64_t k) { return (k + R - 1) / R; }
-inline int ngroups_for(int64_t k) { return (int)((nblk_for(k) + GS - 1) / GS); }
-inline int64_t ticket_bytes(int64_t k) { return ((ngroups_for(k) + 1) * 4 + 255) / 256 * 256; }
-inline int64_t trace_bytes(int64_t k) { return COLLECT_TRACE ? 16 * nblk_for(k) * 64 : 0; }
+constexpr int64_t TICKET_BYTES = 256;
+constexpr int64_t TOT_BYTES = (TOT_N * 8 + 255) / 256 * 256;
+constexpr int64_t ST_BYTES = (sizeof(RmsState) + 255) / 256 * 256;
+inline int64_t trace_bytes(int64_t k) { return COLLECT_TRACE ? 2 * 16 * nblk_for(k) * 64 : 0; }
+
+Ws make_ws(const tsrl_collect_args* a) {
+    Ws ws;
+    ws.nblk = nblk_for(a->k);
+    char* base = reinterpret_cast<char*>(a->workspace);
+    ws.tickets = reinterpret_cast<unsigned int*>(base);
+    for (int i = 0; i < 3; ++i)
+        ws.tot[i] = reinterpret_cast<long long*>(base + TICKET_BYTES + i * TOT_BYTES);
+    for (int i = 0; i < 2; ++i)
+        ws.st[i] = reinterpret_cast<RmsState*>(base + TICKET_BYTES + 3 * TOT_BYTES + i * ST_BYTES);
+    ws.trace = reinterpret_cast<uint64_t*>(base + TICKET_BYTES + 3 * TOT_BYTES + 2 * ST_BYTES);
+    return ws;
+}
 
 }  // namespace
 }  // namespace tsrl
@@ -594,7 +749,7 @@ extern "C" int tsrl_collect_pack_w1(const float* W, int64_t dim, float* packed, 
 
 extern "C" int64_t tsrl_collect_workspace_bytes(int64_t k, int64_t dim) {
     if (k <= 0 || dim <= 0) return 0;
-    return ticket_bytes(k) + (nblk_for(k) + ngroups_for(k)) * (4 * dim + 4) * 8 + trace_bytes(k);
+    return TICKET_BYTES + 3 * TOT_BYTES + 2 * ST_BYTES + trace_bytes(k);
 }
 
 extern "C" int tsrl_collect_box_step(const tsrl_collect_args* a, void* stream) {
@@ -640,20 +795,23 @@ extern "C" int tsrl_collect_box_step(const tsrl_collect_args* a, void* stream) {
         TSRL_CHECK_ARG(!ad.obs_src, "tsrl_collect_box_step: the pending add copies no obs (the "
                                     "launch that produced it stored them)");
     }
-    Ws ws;
-    ws.nblk = nblk_for(k);
-    ws.ngroups = ngroups_for(k);
-    ws.pstride = 4 * D + 4;
-    char* base = reinterpret_cast<char*>(a->workspace);
-    ws.tickets = reinterpret_cast<unsigned int*>(base);
-    ws.part = reinterpret_cast<double*>(base + ticket_bytes(k));
-    ws.gpart = ws.part + ws.nblk * ws.pstride;
-    ws.trace = reinterpret_cast<uint64_t*>(ws.gpart + ws.ngroups * ws.pstride);
+    TSRL_CHECK_ARG(k <= (int64_t)1 << 24, "tsrl_collect_box_step: k <= 2^24 (exact int64 moments)");
+    const Ws ws = make_ws(a);
     tsrl_collect_args p = *a;
     p.act_seed = sm64(a->act_seed);
     p.env_seed = sm64(a->env_seed);
     hipLaunchKernelGGL(collect_box_step_kernel, dim3((unsigned)ws.nblk), dim3(NT), 0,
                        as_stream(stream), p, ws);
     TSRL_LAUNCH_CHECK("tsrl_collect_box_step");
+    return 0;
+}
+
+extern "C" int tsrl_collect_rms_finalize(const tsrl_collect_args* a, void* stream) {
+    TSRL_CHECK_ARG(a != nullptr && a->workspace && a->mean && a->var && a->count &&
+                       a->snap_mean && a->snap_var && a->k > 0 && a->dim > 0 && a->dim <= KMAX,
+                   "tsrl_collect_rms_finalize: bad arguments");
+    hipLaunchKernelGGL(rms_finalize_kernel, dim3(1), dim3(NT), 0, as_stream(stream), *a,
+                       make_ws(a));
+    TSRL_LAUNCH_CHECK("tsrl_collect_rms_finalize");
     return 0;
 }

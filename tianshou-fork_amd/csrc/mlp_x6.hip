@@ -345,6 +345,9 @@ __global__ __launch_bounds__(256, X6_OCC) void l1_fwd_x6_kernel(
 // too, so the compiler inserts no drain of its own); the per-tile epilogue stores count in
 // vmcnt and are skipped by the count of the wait that follows them.
 // ---------------------------------------------------------------------------------------
+#ifndef RING_PREFETCH
+#define RING_PREFETCH 0  // 1: all of a chunk's LDS operands read ahead of its MFMAs
+#endif
 #ifndef RING_VARIANT
 #define RING_VARIANT 0  // diagnostic builds only: 1 = no LDS-DMA in the loop, 2 = no MFMAs
 #endif
@@ -496,6 +499,65 @@ __global__ __launch_bounds__(RNW * 64, 1) void l1_ring_kernel(
         const char* Ws = sm + RWOFF + cs_w * RWSTAGE;
         cs_x = cs_x == RXS - 1 ? 0 : cs_x + 1;
         cs_w ^= 1;
+#if RING_PREFETCH
+        // every LDS operand of the chunk (both k-steps: 2 x 2 f32 X pieces, 2 x 4 x 3 weight
+        // fragments) read up front, then the two k-steps' splits and MFMAs: the reads' latency
+        // is exposed once per chunk instead of before every MFMA group
+        {
+            typedef float f32x4v __attribute__((ext_vector_type(4)));
+            f32x4v xu[2], xv[2];
+            bf16x8 af[2][NT][NPL];
+            const int xr = 32 * w + c;
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                xu[s] = *reinterpret_cast<const f32x4v*>(&Xs[swf_off(xr, 4 * s + 2 * h)]);
+                xv[s] = *reinterpret_cast<const f32x4v*>(&Xs[swf_off(xr, 4 * s + 2 * h + 1)]);
+#pragma unroll
+                for (int i = 0; i < NT; ++i) {
+                    const int ao = sw_off(32 * i + c, 2 * s + h);
+#pragma unroll
+                    for (int p = 0; p < NPL; ++p)
+                        af[s][i][p] = *reinterpret_cast<const bf16x8*>(&Ws[p * HC * ROWB + ao]);
+                }
+            }
+            // pin the reads here (the IR passes otherwise sink each next to its MFMA, with a
+            // wait before every group): one wait per chunk
+            auto pin = [&](int s) {
+                asm volatile("" : "+v"(xu[s]), "+v"(xv[s]));
+#pragma unroll
+                for (int i = 0; i < NT; ++i)
+#pragma unroll
+                    for (int p = 0; p < NPL; ++p) asm volatile("" : "+v"(af[s][i][p]));
+            };
+#if RING_PREFETCH == 1
+            pin(0);
+            pin(1);
+#endif
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+#if RING_PREFETCH == 2
+                pin(s);  // k-step 1's reads still in flight during k-step 0's MFMAs
+#endif
+                bf16x8 b[NPL];
+                split4(make_float4(xu[s].x, xu[s].y, xu[s].z, xu[s].w), b[0], b[1], b[2], 0);
+                split4(make_float4(xv[s].x, xv[s].y, xv[s].z, xv[s].w), b[0], b[1], b[2], 4);
+#pragma unroll
+                for (int ip = 0; ip < NT; ip += 2) {
+#define RX6_PAIR(pa, pb)                                                                    \
+    acc[ip] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s][ip][pa], b[pb], acc[ip], 0, 0, 0); \
+    acc[ip + 1] =                                                                           \
+        __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s][ip + 1][pa], b[pb], acc[ip + 1], 0, 0, 0);
+                    RX6_PAIR(0, 0)
+                    RX6_PAIR(0, 1)
+                    RX6_PAIR(1, 0)
+                    RX6_PAIR(0, 2)
+                    RX6_PAIR(1, 1)
+                    RX6_PAIR(2, 0)
+#undef RX6_PAIR
+                }
+            }
+        }
+#else
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             bf16x8 b[NPL];
@@ -543,6 +605,7 @@ __global__ __launch_bounds__(RNW * 64, 1) void l1_ring_kernel(
             }
 #endif
         }
+#endif
         epi_prev = kc == nch - 1;
         if (epi_prev) {
             // bias + tanh -> fragment layout [row tile][feature tile][lane][16]

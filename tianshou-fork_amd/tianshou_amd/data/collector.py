@@ -66,6 +66,9 @@ class Collector:
         # launch or by _flush()
         self.use_fused_step = True
         self._step_on = False
+        # CollectArgs of the last fused step whose obs_rms merge is still deferred (None: none)
+        self._rms_chain = None
+        self._rms_step = 0  # index of the next deferred launch in its chain
         self._pending = None
         from tianshou_amd.dist import default_dp
         self.dp = default_dp()
@@ -309,10 +312,16 @@ class Collector:
         c.snap_mean, c.snap_var = _C.ptr(rms.snap_mean_t), _C.ptr(rms.snap_var_t)
         dp = rms.dp is not None and rms.dp.active
         if dp or rms.exact:
-            # the launch writes this step's moments instead of folding them
+            # the launch writes this step's moments; the caller merges them (all-reduce +
+            # merge2, or the exact f32 update)
             c.totals = _C.ptr(rms.payload())
+        c.rms_step = self._rms_step if not (dp or rms.exact) else 0
         _C.check(_C.lib().tsrl_collect_box_step(c, _C.stream_ptr(b.device)),
                  "tsrl_collect_box_step")
+        # deferred merge: the next launch (or _flush's tsrl_collect_rms_finalize) merges this
+        # step's obs_rms moments
+        self._rms_chain = None if (dp or rms.exact) else c
+        self._rms_step = 0 if (dp or rms.exact) else self._rms_step + 1
         if rms.exact:
             # both updates from the raw step / reset rows the launch wrote, in the
             # reference's f32 arithmetic
@@ -327,7 +336,13 @@ class Collector:
         self._parity ^= 1
 
     def _flush(self) -> None:
-        """Run the pending buffer add of the last fused step (tsrl_buffer_add)."""
+        """Run the pending buffer add of the last fused step (tsrl_buffer_add), after merging
+        that step's deferred obs_rms moments (tsrl_collect_rms_finalize)."""
+        if self._rms_chain is not None:
+            c, self._rms_chain = self._rms_chain, None
+            self._rms_step = 0
+            _C.check(_C.lib().tsrl_collect_rms_finalize(c, _C.stream_ptr(self.buffer.device)),
+                     "tsrl_collect_rms_finalize")
         if self._pending is not None:
             a, self._pending = self._pending, None
             _C.check(_C.lib().tsrl_buffer_add(a, _C.stream_ptr(self.buffer.device)),

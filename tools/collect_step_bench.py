@@ -64,13 +64,24 @@ def trace_report(c, E, D):
     import numpy as np
     ws = c._scratch["collect_ws"].cpu().numpy()
     nblk = -(-E // 16)
-    ng = -(-nblk // 16)
-    tb = -(-((ng + 1) * 4) // 256) * 256
-    off = tb + (nblk + ng) * (4 * D + 4) * 8
+    rup = lambda x: -(-x // 256) * 256  # noqa: E731
+    # collect.hip make_ws: tickets, 2 totals slots, 2 state slots, then the trace
+    off = 256 + 3 * rup((4 * 512 + 2) * 8) + 2 * rup(2 * 512 * 4 + 8 * 8)
     tr = ws[off:off + 16 * nblk * 64].view(np.uint64).reshape(16, nblk, 8).astype(np.int64)
+    tr2 = ws[off + 16 * nblk * 64:off + 32 * nblk * 64].view(np.uint64).reshape(16, nblk, 8)
+    tr2 = tr2.astype(np.int64)
+    if tr2.any():
+        # prologue detail stamps (wave 0): relative to the workgroup's own start stamp
+        rel = (tr2[:, :, :5] - tr[:, :, :1]) / 100.0
+        chained = tr2[:, :, 3].min(axis=1) > 0
+        rel = rel[chained]
+        for i, nm in enumerate(["A1 loads issued", "merge loads issued", "reset rows issued",
+                                "merge math done", "after LDS barrier"]):
+            print(f"  prologue {nm:>20s}: median {np.median(rel[:, :, i]):5.2f} p90 "
+                  f"{np.percentile(rel[:, :, i], 90):5.2f} us after the workgroup start")
     order = np.argsort(tr[:, :, 0].min(1))
     tr = tr[order]
-    names = ["start", "add", "actor", "env", "groupfold", "merge"]
+    names = ["start", "add", "env", "actor", "unused", "unused"]
     spans, gaps = [], []
     for j in range(16):
         t0 = tr[j, :, 0].min()
@@ -85,6 +96,16 @@ def trace_report(c, E, D):
     for i in range(1, 4):
         d = us[:, i] - us[:, i - 1]
         print(f"  phase {names[i]:>9}: median {np.median(d):6.2f}  max {d.max():6.2f} us")
+    allu = (tr[:, :, :6] - tr[:, :, :1].min(axis=1, keepdims=True)) / 100.0
+    mg = allu[:, :, 4] - allu[:, :, 0]
+    ad = allu[:, :, 1] - allu[:, :, 4]
+    print(f"  all launches: prologue merge median {np.median(mg):5.2f} p90 {np.percentile(mg, 90):5.2f}"
+          f" max {mg.max():5.2f} us; add after merge median {np.median(ad):5.2f} p90 "
+          f"{np.percentile(ad, 90):5.2f} max {ad.max():5.2f} us")
+    for j in range(16):
+        print(f"   launch {j:2d}: span {spans[j]:6.2f} us, merge max {mg[j].max():5.2f}, add max "
+              f"{ad[j].max():5.2f}, env end max {allu[j, :, 2].max():6.2f}" +
+              (f", gap before {gaps[j - 1]:6.2f}" if j else ""))
     tl = []
     for j in range(16):
         t0 = tr[j, :, 0].min()
