@@ -271,6 +271,9 @@ typedef struct tsrl_collect_args {
                                 merge2 vector); NULL: the deferred merge below */
     int64_t rms_step;        /* index of this launch in its chain of deferred steps (0: the
                                 first after tsrl_collect_rms_finalize or a fresh workspace) */
+    int64_t rms_rows;        /* step rows behind the previous step's totals (0: k); data
+                                parallel: world * k, the caller having summed the totals slot
+                                (tsrl_collect_totals_offset) over the ranks */
 } tsrl_collect_args;
 int64_t tsrl_collect_pack_floats(int64_t dim);
 int tsrl_collect_pack_w1(const float* W, int64_t dim, float* packed, void* stream);
@@ -281,6 +284,9 @@ int tsrl_collect_box_step(const tsrl_collect_args* a, void* stream);
  * its step rows (what the closing tsrl_buffer_add normalises obs_next with).  Replaces the
  * obs_rms update of VectorEnvNormObs.step (env/venv_wrappers.py:93-99) for that step. */
 int tsrl_collect_rms_finalize(const tsrl_collect_args* a, void* stream);
+/* Byte offset in the workspace of the int64 [4 * dim + 1] totals slot that step `step` of a
+ * chain accumulates (data parallel: all-reduce it with SUM before the next launch). */
+int64_t tsrl_collect_totals_offset(int64_t step);
 /* *rel_dev = (*rel_dev + 1) % ring_size (device-side ring cursor for graph-captured steps). */
 int tsrl_ring_advance(int64_t* rel_dev, int64_t ring_size, void* stream);
 

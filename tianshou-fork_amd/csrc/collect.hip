@@ -287,7 +287,9 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
     }
     TSTAMP2(2)
     if (merge) {
-        const double kp = (double)k;  // the chain's steps all cover the same k envs
+        // the step rows behind the totals: k, or every rank's k when the totals were
+        // all-reduced (data parallel)
+        const double kp = (double)(a.rms_rows > 0 ? a.rms_rows : k);
         if (t < D)
             merge_column((double)mm0, (double)mv0, mcount, kp, ms1, mq1, mnd, ms2, mq2,
                          sSnapM[t], sSnapV[t], sFinM[t], sFinV[t]);
@@ -696,7 +698,8 @@ __global__ __launch_bounds__(NT) void rms_finalize_kernel(tsrl_collect_args a, W
     const int step = a.rms_step;  // the chain's last launch
     const RmsState* sin = ws.st[(step + 1) & 1];  // the state the last launch published
     long long* tp = ws.tot[step % 3];
-    const double old_count = sin->count, nd = (double)tp[4 * D], kp = (double)a.k;
+    const double old_count = sin->count, nd = (double)tp[4 * D];
+    const double kp = (double)(a.rms_rows > 0 ? a.rms_rows : a.k);
     for (int d = t; d < D; d += NT) {
         float sm, sv, fm, fv;
         merge_column((double)sin->mean[d], (double)sin->var[d], old_count, kp, tp[d],
@@ -804,6 +807,10 @@ extern "C" int tsrl_collect_box_step(const tsrl_collect_args* a, void* stream) {
                        as_stream(stream), p, ws);
     TSRL_LAUNCH_CHECK("tsrl_collect_box_step");
     return 0;
+}
+
+extern "C" int64_t tsrl_collect_totals_offset(int64_t step) {
+    return TICKET_BYTES + (step % 3) * TOT_BYTES;
 }
 
 extern "C" int tsrl_collect_rms_finalize(const tsrl_collect_args* a, void* stream) {

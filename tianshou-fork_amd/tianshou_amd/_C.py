@@ -52,7 +52,7 @@ class CollectArgs(ctypes.Structure):
         ("env_seed", _u64), ("ep_len", _i64), ("ep_j", _p), ("ep_t", _p),
         ("raw", _p), ("reset_raw", _p), ("rew", _p), ("term", _p), ("trunc", _p), ("done", _p),
         ("workspace", _p), ("mean", _p), ("var", _p), ("snap_mean", _p), ("snap_var", _p),
-        ("count", _p), ("totals", _p), ("rms_step", _i64),
+        ("count", _p), ("totals", _p), ("rms_step", _i64), ("rms_rows", _i64),
     ]
 
 
@@ -114,6 +114,7 @@ _SIGS = {
     "tsrl_collect_workspace_bytes": ([_i64, _i64], _i64),
     "tsrl_collect_box_step": ([ctypes.POINTER(CollectArgs), _p], ctypes.c_int),
     "tsrl_collect_rms_finalize": ([ctypes.POINTER(CollectArgs), _p], ctypes.c_int),
+    "tsrl_collect_totals_offset": ([_i64], _i64),
     "tsrl_gather_rows": ([_p, _i64, _p, _i64, _p, _p], ctypes.c_int),
     "tsrl_np_shuffle_draws": ([_p, _p, _i64, _p], ctypes.c_int),
     "tsrl_shuffle_apply_workspace_bytes": ([_i64], _i64),

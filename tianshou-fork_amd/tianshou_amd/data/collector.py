@@ -311,24 +311,30 @@ class Collector:
         c.mean, c.var, c.count = _C.ptr(rms.mean_t), _C.ptr(rms.var_t), _C.ptr(rms.count_t)
         c.snap_mean, c.snap_var = _C.ptr(rms.snap_mean_t), _C.ptr(rms.snap_var_t)
         dp = rms.dp is not None and rms.dp.active
-        if dp or rms.exact:
-            # the launch writes this step's moments; the caller merges them (all-reduce +
-            # merge2, or the exact f32 update)
+        if rms.exact:
+            # the launch writes this step's moments; the caller applies the exact f32 update
             c.totals = _C.ptr(rms.payload())
-        c.rms_step = self._rms_step if not (dp or rms.exact) else 0
+        c.rms_step = 0 if rms.exact else self._rms_step
+        if dp:
+            c.rms_rows = kk * rms.dp.world
         _C.check(_C.lib().tsrl_collect_box_step(c, _C.stream_ptr(b.device)),
                  "tsrl_collect_box_step")
+        if dp and not rms.exact:
+            # the step's exact integer moments summed over the ranks (one all-reduce per env
+            # step, a graph node under RCCL); the next launch merges the GLOBAL batch, as the
+            # reference's single VectorEnvNormObs over every env shard (venv_wrappers.py:93-99)
+            off = int(_C.lib().tsrl_collect_totals_offset(self._rms_step))
+            n = 4 * b.obs_numel + 1
+            rms.dp.all_reduce_(ws[off:off + 8 * n].view(torch.int64))
         # deferred merge: the next launch (or _flush's tsrl_collect_rms_finalize) merges this
         # step's obs_rms moments
-        self._rms_chain = None if (dp or rms.exact) else c
-        self._rms_step = 0 if (dp or rms.exact) else self._rms_step + 1
+        self._rms_chain = None if rms.exact else c
+        self._rms_step = 0 if rms.exact else self._rms_step + 1
         if rms.exact:
             # both updates from the raw step / reset rows the launch wrote, in the
             # reference's f32 arithmetic
             rms.exact_update(s["raw"][:kk], None, s["reset_raw"][:kk], s["done"][:kk],
                              snapshot=True)
-        elif dp:
-            rms.merge_payload(kk)
         self._pending = buf._launch_add(
             ids=None, k=kk, obs=None, act=s["act"], obs_next=s["raw"], cur_obs=cur, norm=rms,
             norm_snapshot=True, reset_src=s["reset_raw"], reset_mask=s["done"], reset_norm=rms,
