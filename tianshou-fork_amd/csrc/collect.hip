@@ -56,6 +56,9 @@ constexpr int HP = 16;         // h1 / h2 tiles [feature][row]
 constexpr int WP = 68;         // W2 / W3 rows (4i + k banks: conflict-free A fragments)
 // diagnostic builds only (tools/collect_step_bench.py): return after phase 1 (add), 2 (actor)
 // or 3 (env); 0 = the whole step
+#ifndef COLLECT_ATOMIC_LATE
+#define COLLECT_ATOMIC_LATE 0  // 1: the obs_rms atomics after the actor (measured slower)
+#endif
 #ifndef COLLECT_STOP
 #define COLLECT_STOP 0
 #endif
@@ -174,6 +177,9 @@ __device__ __forceinline__ void merge_column(double m0, double v0, double old_co
     fin_v = (float)v0;
 }
 
+// SQC = kpad(dim) / 128: the 128-column groups of an observation row (a compile-time bound, so
+// the layer-1 weight fragments and the prefetched rows take only the registers dim needs)
+template <int SQC>
 __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_args a, Ws ws) {
 #pragma clang fp contract(off)
     __shared__ float sX[KMAX * XP];
@@ -227,7 +233,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
     // and episode counters) and of the merge is issued first; they are consumed after the
     // merge, so one memory latency covers all of them.  32 lanes per row, float4 pieces
     // q = lane + 32 j of the row.
-    constexpr int AQ = (KMAX / 4 + 31) / 32;
+    constexpr int AQ = SQC;  // float4 pieces per lane: ceil(dim / 128) = SQC
     const int arw = t >> 5, aln = t & 31;
     const int nq = D >> 2;
     const int act_n = (int)(ad.act_row_bytes >> 2);
@@ -253,8 +259,9 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
             axs[j] = s4[q < nq ? q : 0];
         }
         if (aln < act_n) aact = reinterpret_cast<const float*>(ad.act_src)[ar * act_n + aln];
-        // the row's storage position (every lane: it addresses the lane's stores)
-        aptr_ld = ad.ptr ? ad.ptr[ar] : ad.offset[ar] + urel;
+        // the row's storage position (every lane: it addresses the lane's stores); the ring
+        // position urel is added at A2, so no load here waits for it
+        aptr_ld = ad.ptr ? ad.ptr[ar] : ad.offset[ar];
         if (aln == 0) atail.load(ad, ar, ar);
     }
     TSTAMP2(0)
@@ -346,16 +353,15 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
             vhi = a.high[t];
         }
     }
-    // layer-1 weight fragments of this wave (SQ <= KMAX / 128 = 4) and the env rows' episode
-    // counters: independent of the add phase, so their latency hides behind it
-    float4 wall[KMAX / 128][4];
+    // layer-1 weight fragments of this wave (SQ == SQC): independent of the add phase, so
+    // their latency hides behind it
+    float4 wall[SQC][4];
     {
         const float4* wp = reinterpret_cast<const float4*>(a.w1p) + (int64_t)w * SQ * 4 * 64 + l;
 #pragma unroll
-        for (int sq = 0; sq < KMAX / 128; ++sq)
+        for (int sq = 0; sq < SQC; ++sq)
 #pragma unroll
-            for (int ft = 0; ft < 4; ++ft)
-                wall[sq][ft] = wp[((sq < SQ ? sq : 0) * 4 + ft) * 64];
+            for (int ft = 0; ft < 4; ++ft) wall[sq][ft] = wp[(sq * 4 + ft) * 64];
     }
 
     TSTAMP(4)
@@ -365,7 +371,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
             // A2: normalise the prefetched rows: obs_next with the statistics after the step
             // rows, the live obs of a reset env with those after the reset rows (add_row)
             if (arow) {
-                const int64_t aptr = aptr_ld;
+                const int64_t aptr = ad.ptr ? aptr_ld : aptr_ld + urel;
                 float4* dst = reinterpret_cast<float4*>(ad.obs_next_dst + aptr * D);
                 const float eps = ad.norm_eps, clip = ad.norm_clip;
 #pragma unroll
@@ -525,29 +531,40 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
     LDS_SYNC();
     const int nd = s_nd;
     long long* tc = ws.tot[tcur];
-    for (int d = t; d < D; d += NT) {
-        long long s1 = 0, q1 = 0, s2 = 0, q2 = 0;
+    // this thread's column (D <= KMAX = NT): its exact integer moments, added to the totals
+    // slot by atomics after the actor (their issue would otherwise delay it)
+    long long cs1 = 0, cq1 = 0, cs2 = 0, cq2 = 0;
+    if (t < D) {
+        const int d = t;
         for (int r = 0; r < nrows; ++r) {
             const int m = box_m(rs[r].key, d);
             a.raw[(r0 + r) * D + d] = (float)m * 0x1p-23f;  // == box_val(key, d), exactly
-            s1 += m;
-            q1 += (long long)m * m;
+            cs1 += m;
+            cq1 += (long long)m * m;
         }
-        atomic_add_i64(tc + d, s1);
-        atomic_add_i64(tc + D + d, q1);
-        if (nd > 0) {
+        if (nd > 0)
             for (int r = 0; r < nrows; ++r) {
                 if (!rr[r].active) continue;
                 const int m = box_m(rr[r].key, d);
                 a.reset_raw[(r0 + r) * D + d] = (float)m * 0x1p-23f;
-                s2 += m;
-                q2 += (long long)m * m;
+                cs2 += m;
+                cq2 += (long long)m * m;
             }
-            atomic_add_i64(tc + 2 * D + d, s2);
-            atomic_add_i64(tc + 3 * D + d, q2);
-        }
     }
-    if (t == 0 && nd > 0) atomic_add_i64(tc + 4 * D, nd);
+    auto add_totals = [&]() {
+        if (t < D) {
+            atomic_add_i64(tc + t, cs1);
+            atomic_add_i64(tc + D + t, cq1);
+            if (nd > 0) {
+                atomic_add_i64(tc + 2 * D + t, cs2);
+                atomic_add_i64(tc + 3 * D + t, cq2);
+            }
+        }
+        if (t == 0 && nd > 0) atomic_add_i64(tc + 4 * D, nd);
+    };
+#if !COLLECT_ATOMIC_LATE
+    add_totals();
+#endif
     TSTAMP(2)
 #if COLLECT_STOP == 1
     return;
@@ -560,8 +577,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         for (int ft = 0; ft < 4; ++ft) acc[ft] = f32x4{0.f, 0.f, 0.f, 0.f};
         const float* xb = sX + (w * KW + (l >> 4)) * XP + (l & 15);
 #pragma unroll
-        for (int sq = 0; sq < KMAX / 128; ++sq) {
-            if (sq >= SQ) break;
+        for (int sq = 0; sq < SQC; ++sq) {
             const float* xs = xb + 16 * sq * XP;
             const float b0 = xs[0], b1 = xs[4 * XP], b2 = xs[8 * XP], b3 = xs[12 * XP];
 #pragma unroll
@@ -579,6 +595,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
             for (int r = 0; r < 4; ++r) red[((w * 4 + ft) * 4 + r) * 64 + l] = acc[ft][r];
     }
     LDS_SYNC();
+    TSTAMP2(5)
     // h1 = tanh(sum over the 8 waves in order + b1) -> sH1[f][row]
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -591,6 +608,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         sH1[f * HP + (ln & 15)] = tanh_nb(z + sb1[f]);
     }
     LDS_SYNC();
+    TSTAMP2(6)
     // layer 2: wave w -> feature tile w & 3 over k half w >> 2 (8 steps of 4)
     {
         const int ft = w & 3, kh = w >> 2;
@@ -625,6 +643,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         for (int r = 0; r < 4; ++r) red[(w * 4 + r) * 64 + l] = z[r];
     }
     LDS_SYNC();
+    TSTAMP2(7)
     // mu = sum of the 4 quarters + b3; act = randn * sigma + mu; map_action -> act_remap
     {
         const int ln = t & 63, r = (t >> 6) & 3, at = t >> 8;  // 2 x 4 x 64 = 512 threads
@@ -653,6 +672,9 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
     return;
 #endif
     TSTAMP(3)
+#if COLLECT_ATOMIC_LATE
+    add_totals();
+#endif
     if (defer) return;
 
 #if COLLECT_STOP == 3
@@ -803,8 +825,24 @@ extern "C" int tsrl_collect_box_step(const tsrl_collect_args* a, void* stream) {
     tsrl_collect_args p = *a;
     p.act_seed = sm64(a->act_seed);
     p.env_seed = sm64(a->env_seed);
-    hipLaunchKernelGGL(collect_box_step_kernel, dim3((unsigned)ws.nblk), dim3(NT), 0,
-                       as_stream(stream), p, ws);
+    switch (kpad(D) / 128) {
+        case 1:
+            hipLaunchKernelGGL(collect_box_step_kernel<1>, dim3((unsigned)ws.nblk), dim3(NT), 0,
+                               as_stream(stream), p, ws);
+            break;
+        case 2:
+            hipLaunchKernelGGL(collect_box_step_kernel<2>, dim3((unsigned)ws.nblk), dim3(NT), 0,
+                               as_stream(stream), p, ws);
+            break;
+        case 3:
+            hipLaunchKernelGGL(collect_box_step_kernel<3>, dim3((unsigned)ws.nblk), dim3(NT), 0,
+                               as_stream(stream), p, ws);
+            break;
+        default:
+            hipLaunchKernelGGL(collect_box_step_kernel<4>, dim3((unsigned)ws.nblk), dim3(NT), 0,
+                               as_stream(stream), p, ws);
+            break;
+    }
     TSRL_LAUNCH_CHECK("tsrl_collect_box_step");
     return 0;
 }

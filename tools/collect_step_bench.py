@@ -69,14 +69,19 @@ def trace_report(c, E, D):
     off = 256 + 3 * rup((4 * 512 + 2) * 8) + 2 * rup(2 * 512 * 4 + 8 * 8)
     tr = ws[off:off + 16 * nblk * 64].view(np.uint64).reshape(16, nblk, 8).astype(np.int64)
     tr2 = ws[off + 16 * nblk * 64:off + 32 * nblk * 64].view(np.uint64).reshape(16, nblk, 8)
+    stamp_rel = (tr[:, :, :4] - tr[:, :, :1]) / 100.0
+    print("  stamps (all launches, median after the workgroup start): add "
+          f"{np.median(stamp_rel[:, :, 1]):5.2f}, env {np.median(stamp_rel[:, :, 2]):5.2f}, "
+          f"actor {np.median(stamp_rel[:, :, 3]):5.2f} us")
     tr2 = tr2.astype(np.int64)
     if tr2.any():
         # prologue detail stamps (wave 0): relative to the workgroup's own start stamp
-        rel = (tr2[:, :, :5] - tr[:, :, :1]) / 100.0
+        rel = (tr2[:, :, :8] - tr[:, :, :1]) / 100.0
         chained = tr2[:, :, 3].min(axis=1) > 0
         rel = rel[chained]
         for i, nm in enumerate(["A1 loads issued", "merge loads issued", "reset rows issued",
-                                "merge math done", "after LDS barrier"]):
+                                "merge math done", "after LDS barrier", "actor layer 1 done",
+                                "h1 in LDS", "mu head done"]):
             print(f"  prologue {nm:>20s}: median {np.median(rel[:, :, i]):5.2f} p90 "
                   f"{np.percentile(rel[:, :, i], 90):5.2f} us after the workgroup start")
     order = np.argsort(tr[:, :, 0].min(1))

@@ -23,6 +23,9 @@ def main():
     ap.add_argument("--only", default=None,
                     help="time one kernel only (l1_fwd, l1_fwd_x6, tail, dw, minibatch): PMC passes")
     ap.add_argument("--act", type=int, default=1, help="layer-1 activation: 1 tanh, 0 identity")
+    ap.add_argument("--ld", type=int, default=0,
+                    help="row pitch of the observation array in floats (0: D; e.g. 384 = "
+                         "128-byte-aligned rows)")
     ap.add_argument("--contig", action="store_true",
                     help="minibatch rows contiguous (no permutation gather)")
     ap.add_argument("--sorted", action="store_true",
@@ -40,7 +43,8 @@ def main():
     layers = fused_mlp.match(actor, critic)
     fm = fused_mlp.FusedActorCritic(layers, ActorCritic(actor, critic).parameters())
     N, B, D, A = a.N, a.rows, a.D, a.A
-    obs = torch.randn(N, D, device=dev)
+    ld = a.ld or D
+    obs = torch.randn(N, ld, device=dev)
     act = torch.randn(N, A, device=dev)
     logp_old = torch.randn(N, device=dev) - A
     adv = torch.randn(N, device=dev)
@@ -53,7 +57,8 @@ def main():
     p.eps_clip, p.dual_clip, p.vf_coef, p.ent_coef, p.adv_eps = 0.2, 0.0, 0.25, 0.0, 1e-8
     p.b_global, p.value_clip, p.norm_adv = float(B), 0, 1
     dp = DataParallel()
-    fm.minibatch(obs, idx, B, act, logp_old, adv, ret, v_s, p, dp)
+    fm.minibatch(obs[:, :D].contiguous() if ld != D else obs, idx, B, act, logp_old, adv, ret,
+                 v_s, p, dp)
     torch.cuda.synchronize()
     L = _C.lib()
     s = _C.stream_ptr(dev)
@@ -77,7 +82,7 @@ def main():
     def l1x6():
         _C.check(L.tsrl_mlp_split_w(_C.ptr(W["w1a"].weight), _C.ptr(W["w1c"].weight), D,
                                     _C.ptr(wsx), s))
-        _C.check(L.tsrl_mlp_l1_fwd_x6(_C.ptr(obs), D, _C.ptr(idx), B, D, _C.ptr(wsx),
+        _C.check(L.tsrl_mlp_l1_fwd_x6(_C.ptr(obs), ld, _C.ptr(idx), B, D, _C.ptr(wsx),
                                       _C.ptr(W["w1a"].bias), _C.ptr(W["w1c"].bias), a.act,
                                       _C.ptr(h1), 1, s))
 
@@ -95,7 +100,7 @@ def main():
                                  _C.ptr(sums), _C.ptr(ws), ws.numel(), s))
 
     def dw():
-        _C.check(L.tsrl_mlp_dw(_C.ptr(dz1), _C.ptr(obs), D, _C.ptr(idx), B, D,
+        _C.check(L.tsrl_mlp_dw(_C.ptr(dz1), _C.ptr(obs), ld, _C.ptr(idx), B, D,
                                _C.ptr(W["w1a"].weight.grad), _C.ptr(W["w1a"].bias.grad),
                                _C.ptr(W["w1c"].weight.grad), _C.ptr(W["w1c"].bias.grad),
                                _C.ptr(ws2), ws2.numel(), s))
@@ -108,6 +113,8 @@ def main():
                            ("tail(+reduce)", tail, flop_tail),
                            ("dw(+reduce)", dw, flop_l1), ("minibatch", whole, None)):
         if a.only and not name.startswith(a.only):
+            continue
+        if ld != D and name in ("l1_fwd", "l1_x6_staged(rows)", "minibatch"):
             continue
         fn()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
