@@ -188,7 +188,47 @@ constexpr int SL_W2A = 0, SL_B2A = SL_W2A + H * H, SL_W2C = SL_B2A + H, SL_B2C =
               SL_W3A = SL_B2C + H, SL_B3A = SL_W3A + AMAX * H, SL_W3C = SL_B3A + AMAX,
               SL_B3C = SL_W3C + H, SL_F = SL_B3C + 4;
 constexpr int SL_D = 4 + AMAX;  // clip, vf, count, 0, d/dlog_std[AMAX]
-constexpr int TAIL_TPB = 256;
+// Waves per workgroup (one workgroup per CU).  Measured round 3 (tools/mlp_kernel_bench.py
+// --only tail, both nets + reduce, 262144 rows; per-phase s_memtime stamps with TAIL_TRACE):
+// round 2's kernel 234 us (actor tile 29.7k cycles: head + loss 9.5k of them, 89
+// ds_bpermute per tile); bf16x6 weight gradients 226; + deferred column sums and H1 kept
+// live 210-213 (actor tile 24.4k: head + loss 7.7k, ~1.5k instructions issued one after the
+// other by the only wave of the SIMD).  Two waves per SIMD do not pay: 8 waves each with its
+// own accumulators spill (256 VGPRs) 220-222 us; a lockstep form in which the 8 waves of a
+// round share the weight-gradient MFMAs through LDS (2 accumulator tiles per wave, 8
+// workgroup barriers per round) still spills 20 VGPRs and ran 226-229 us.
+#ifndef TAIL_WAVES
+#define TAIL_WAVES 4
+#endif
+// Column sums over the minibatch rows (db2, db3, dlog_std, the critic's dW3) accumulated per
+// lane across the wave's tiles and reduced across lanes once at the end (1: default), instead
+// of a 16-shuffle reduce-scatter per tile and sum (ds_bpermute chains: 89 per tile in the
+// actor, where they were most of the 9.5k-cycle head + loss phase).
+#ifndef TAIL_DEFER
+#define TAIL_DEFER (TAIL_WAVES == 4)
+#endif
+// keep H1 in registers through the tile (1) or re-read it from L2 for dZ1 (0: fewer VGPRs)
+#ifndef TAIL_KEEP_H1
+#define TAIL_KEEP_H1 (TAIL_WAVES == 4)
+#endif
+// next tile's inputs prefetched into registers during the current tile (needed at one wave
+// per SIMD; at two the partner wave covers the loads and the registers are better spent)
+#ifndef TAIL_PF
+#define TAIL_PF (TAIL_WAVES == 4)
+#endif
+// layer-2/3 weight gradients as bf16x6 products (f32 MFMA, 1/16 of the bf16 rate, before)
+#ifndef TAIL_WG_X6
+#define TAIL_WG_X6 1
+#endif
+// diagnostic builds only (tools/mlp_kernel_bench.py --tail-trace): s_memtime stamps per wave
+// and tile at the phase boundaries, stored behind the workspace slabs
+#ifndef TAIL_TRACE
+#define TAIL_TRACE 0
+#endif
+constexpr int TAIL_NSTAMP = 8;
+constexpr int TAIL_TRACE_TILES = 8;  // first tiles of each wave
+constexpr int TAIL_NW = TAIL_WAVES;
+constexpr int TAIL_TPB = 64 * TAIL_NW;
 
 struct TailWeights {
     const float *w2a, *b2a, *w2c, *b2c, *w3a, *b3a, *w3c, *b3c, *log_std;
@@ -227,10 +267,14 @@ __device__ __forceinline__ int rs_reg(int l) {
 // backward), blockIdx.y == 1 the critic half (layer 2, value head, value loss, backward):
 // the loss gradient w.r.t. mu depends only on actor outputs and w.r.t. the value only on
 // critic outputs, so the halves are independent and each keeps half the live state.
-constexpr int SH = 18;   // half-tile transpose scratch: [64 features][16 rows], stride 18
+// half-tile transpose scratch: [64 features][16 rows]; stride 20 floats (80 B) keeps the
+// 8-row float4 reads of the bf16x6 weight gradients 16-byte aligned and spreads the 16 lanes
+// of a read phase over all 16 bank groups (5 is odd)
+constexpr int SH = TAIL_WG_X6 ? 20 : 18;
 constexpr int T_B2 = 0, T_B3 = T_B2 + H, T_W3C = T_B3 + AMAX, T_VAR = T_W3C + H,
               T_LS = T_VAR + AMAX, T_IV = T_LS + AMAX, T_IV2 = T_IV + AMAX,
-              T_SCR = T_IV2 + AMAX, T_END = T_SCR + 4 * 2 * H * SH;
+              T_SCR = T_IV2 + AMAX, T_END = T_SCR + TAIL_NW * 2 * H * SH;
+static_assert(T_END >= TAIL_NW * 32 * H, "fold scratch");
 
 // The chain products (layer 2, mu head, dZ2 = W3^T dMu, dZ1 = W2^T dZ2) run as bf16x6 (x6.h):
 // their activation operand is the C-layout tile itself -- registers 8s..8s+7 of a 32x32 tile
@@ -250,9 +294,9 @@ __device__ __forceinline__ int img_off(int p, int kc, int row, int q, int nkc, i
 }
 
 // Split M(row, k) (k < 32*nkc) into the image; every thread writes whole 16-byte chunks.
-template <typename F>
-__device__ __forceinline__ void build_img(char* img, int rows, int nkc, F val) {
-    for (int i = threadIdx.x; i < rows * nkc * 4; i += TAIL_TPB) {
+template <int TPB, typename F>
+__device__ __forceinline__ void build_img_n(char* img, int rows, int nkc, F val) {
+    for (int i = threadIdx.x; i < rows * nkc * 4; i += TPB) {
         const int q = i & 3, kc = (i >> 2) % nkc, row = (i >> 2) / nkc;
         bf16x8 p0, p1, p2;
 #pragma unroll
@@ -268,6 +312,11 @@ __device__ __forceinline__ void build_img(char* img, int rows, int nkc, F val) {
         *reinterpret_cast<bf16x8*>(img + img_off(1, kc, row, q, nkc, rows)) = p1;
         *reinterpret_cast<bf16x8*>(img + img_off(2, kc, row, q, nkc, rows)) = p2;
     }
+}
+
+template <typename F>
+__device__ __forceinline__ void build_img(char* img, int rows, int nkc, F val) {
+    build_img_n<TAIL_TPB>(img, rows, nkc, val);
 }
 
 // The 3 planes of one operand fragment: row `row`, 32-k chunk kc, k-step s, lane half h.
@@ -314,6 +363,47 @@ __device__ __forceinline__ void acc_wgrad(f32x16 (&g)[NOT][NFT], const float* S1
     }
 }
 
+// bf16x6 form of acc_wgrad: one 16-deep k-step of v_mfma_f32_32x32x16_bf16 covers the 16
+// rows; lane (c, h) reads rows 8h..8h+7 of feature c of each tile (two float4 reads) and
+// splits them into the three planes in registers.  The C layout of g is acc_wgrad's.
+template <int NOT, int NFT>
+__device__ __forceinline__ void acc_wgrad_x6(f32x16 (&g)[NOT][NFT], const float* S1,
+                                             const float* S2, int c, int h) {
+    bf16x8 b[NFT][NPL];
+    auto ld8 = [&](const float* S, int tile, bf16x8 (&p)[NPL]) {
+        const float4* src = reinterpret_cast<const float4*>(&S[(32 * tile + c) * SH + 8 * h]);
+        const float4 u = src[0], v = src[1];
+        const float e[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            __bf16 x0, x1, x2;
+            split1(e[j], x0, x1, x2);
+            p[0][j] = x0;
+            p[1][j] = x1;
+            p[2][j] = x2;
+        }
+    };
+#pragma unroll
+    for (int i = 0; i < NFT; ++i) ld8(S2, i, b[i]);
+#pragma unroll
+    for (int ot = 0; ot < NOT; ++ot) {
+        bf16x8 a[NPL];
+        ld8(S1, ot, a);
+#pragma unroll
+        for (int ft = 0; ft < NFT; ++ft) g[ot][ft] = mfma6(a, b[ft], g[ot][ft]);
+    }
+}
+
+template <int NOT, int NFT>
+__device__ __forceinline__ void acc_wgrad_any(f32x16 (&g)[NOT][NFT], const float* S1,
+                                              const float* S2, int c, int h) {
+#if TAIL_WG_X6
+    acc_wgrad_x6<NOT, NFT>(g, S1, S2, c, h);
+#else
+    acc_wgrad<NOT, NFT>(g, S1, S2, c, h);
+#endif
+}
+
 // Write a C-layout activation (NT32 tiles of 32 features) rows [16*half, 16*half+16) into
 // feature-major scratch [feature][row - 16*half].
 template <int NT32>
@@ -341,9 +431,26 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
     const float* __restrict__ adv, const float* __restrict__ ret, const float* __restrict__ v_s,
     const double* __restrict__ adv_sums, TailParams p, float* __restrict__ dz1,
     float* __restrict__ slab_f, double* __restrict__ slab_d) {
+#if TAIL_TRACE
+    uint64_t* trace = reinterpret_cast<uint64_t*>(
+        (reinterpret_cast<uintptr_t>(slab_d + (int64_t)gridDim.x * SL_D) + 255) & ~uintptr_t(255)) +
+        (int64_t)NET * gridDim.x * TAIL_NW * TAIL_TRACE_TILES * TAIL_NSTAMP;
+    int tr_tile = 0;
+#define TAIL_STAMP(i)                                                                       \
+    {                                                                                       \
+        __builtin_amdgcn_sched_barrier(0);                                                  \
+        const uint64_t ts_ = __builtin_amdgcn_s_memtime();                                  \
+        if (l == 0 && tr_tile < TAIL_TRACE_TILES)                                           \
+            trace[(((int64_t)blockIdx.x * TAIL_NW + w) * TAIL_TRACE_TILES + tr_tile) *      \
+                      TAIL_NSTAMP + (i)] = ts_;                                             \
+        __builtin_amdgcn_sched_barrier(0);                                                  \
+    }
+#else
+#define TAIL_STAMP(i)
+#endif
     __shared__ __attribute__((aligned(16))) float sm[T_END];
     __shared__ __attribute__((aligned(16))) char img[NET == 0 ? IMG_ACTOR : IMG_CRITIC];
-    __shared__ double sred[4][SL_D];
+    __shared__ double sred[TAIL_NW][SL_D];
     const int t = threadIdx.x;
     const int w = t >> 6, l = t & 63, h = l >> 5, c = l & 31;
     const int A = p.A;
@@ -400,9 +507,18 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
     float gb2[2] = {0.f, 0.f}, gw3c[2] = {0.f, 0.f};
     float gb3 = 0.f;
     double dls_acc = 0.0, loss_acc = 0.0, cnt_acc = 0.0;
+#if TAIL_DEFER
+    // per-lane partial column sums (lane = row c, register r = feature rho(r) + 4h)
+    float gb2_l[2][16], gw3c_l[2][16], gb3_l[16], dls_l[16], gv_l = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        gb2_l[0][r] = gb2_l[1][r] = gw3c_l[0][r] = gw3c_l[1][r] = 0.f;
+        gb3_l[r] = dls_l[r] = 0.f;
+    }
+#endif
 
     const int64_t ntiles = (n + 31) / 32;
-    const int64_t gw = (int64_t)blockIdx.x * 4 + w, nw = (int64_t)gridDim.x * 4;
+    const int64_t gw = (int64_t)blockIdx.x * TAIL_NW + w, nw = (int64_t)gridDim.x * TAIL_NW;
     // Software pipeline over this wave's tiles (one wave per SIMD: nothing else hides
     // latency): while tile bt computes, the NEXT tile's H1 fragments and gathered per-row
     // inputs are in flight, and the index of the tile after that.  Loads are branch-free:
@@ -415,6 +531,9 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
         const int64_t br_ = bt_ * 32 + c;
         return (bt_ < ntiles && br_ < n) ? (idx ? idx[br_] : br_) : 0;
     };
+    // per-row inputs addressed by 32-bit element offsets from the (uniform) base pointers:
+    // one VGPR per address instead of two (the 16 act gathers were spilling)
+    const uint32_t A_u = (uint32_t)A;
 #define TAIL_PREFETCH(BT, J)                                                                \
     {                                                                                       \
         const int64_t bts_ = (BT) < ntiles ? (BT) : 0;                                      \
@@ -429,24 +548,35 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
                 nh1[i_][4 * q_ + 3] = v_.w;                                                 \
             }                                                                               \
         }                                                                                   \
+        const uint32_t j32_ = (uint32_t)(J);                                                \
         if constexpr (actor) {                                                              \
+            const uint32_t ab_ = j32_ * A_u;                                                \
             _Pragma("unroll") for (int r_ = 0; r_ < 16; ++r_) {                             \
-                const int a_ = rho(r_) + 4 * h;                                             \
-                nav[r_] = act[(J) * A + (a_ < A ? a_ : 0)];                                 \
+                const uint32_t a_ = (uint32_t)(rho(r_) + 4 * h);                            \
+                nav[r_] = act[ab_ + (a_ < A_u ? a_ : 0u)];                                  \
             }                                                                               \
-            nx0 = logp_old[J];                                                              \
-            nx1 = adv[J];                                                                   \
+            nx0 = logp_old[j32_];                                                           \
+            nx1 = adv[j32_];                                                                \
         } else {                                                                            \
-            nx0 = ret[J];                                                                   \
-            nx1 = p.value_clip ? v_s[J] : 0.0f;                                             \
+            nx0 = ret[j32_];                                                                \
+            nx1 = p.value_clip ? v_s[j32_] : 0.0f;                                          \
         }                                                                                   \
     }
+#if TAIL_PF
     int64_t j_next = row_index(gw);
     TAIL_PREFETCH(gw, j_next)
     j_next = row_index(gw + nw);
+#endif
     for (int64_t bt = gw; bt < ntiles; bt += nw) {
         const int64_t brow = bt * 32 + c;
         const bool live = brow < n;
+        TAIL_STAMP(0)
+#if !TAIL_PF
+        {
+            const int64_t jc = row_index(bt);
+            TAIL_PREFETCH(bt, jc)
+        }
+#endif
         // ---- this tile's inputs (prefetched), then the next tile's loads --------------------
         float h1[2][16], av[16];
 #pragma unroll
@@ -456,13 +586,15 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
 #pragma unroll
         for (int r = 0; r < 16; ++r) av[r] = nav[r];
         const float x0 = nx0, x1 = nx1;
+#if TAIL_PF
         {
             const int64_t jn = j_next;
             TAIL_PREFETCH(bt + nw, jn)
             j_next = row_index(bt + 2 * nw);
         }
+#endif
         // ---- layer 2 -----------------------------------------------------------------------
-        __builtin_amdgcn_sched_barrier(0);
+        TAIL_STAMP(1)
         float h2[2][16];
         {
             f32x16 z0 = zero16(), z1 = zero16();
@@ -486,7 +618,7 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
         float dz2[2][16];
         if constexpr (actor) {
             // ---- mu head + clipped surrogate ----------------------------------------------
-            __builtin_amdgcn_sched_barrier(0);
+            TAIL_STAMP(2)
             f32x16 mu = zero16();
 #pragma unroll
             for (int kc = 0; kc < 2; ++kc)
@@ -501,13 +633,14 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
             float lp = 0.0f;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
+                // branch-free (the LDS vectors are padded to AMAX): a branch per element
+                // made 16 dependent LDS round trips
                 const int a = rho(r) + 4 * h;
-                diff[r] = 0.0f;
-                if (a < A && live) {
-                    diff[r] = av[r] - (mu[r] + sm[T_B3 + a]);
-                    lp += -(diff[r] * diff[r]) * sm[T_IV2 + a] - sm[T_LS + a] -
-                          LOG_SQRT_2PI;
-                }
+                const bool in = a < A && live;
+                const float d = av[r] - (mu[r] + sm[T_B3 + a]);
+                const float term = -(d * d) * sm[T_IV2 + a] - sm[T_LS + a] - LOG_SQRT_2PI;
+                diff[r] = in ? d : 0.0f;
+                lp += in ? term : 0.0f;
             }
             const float logp = lp + __shfl_xor(lp, 32, 64);
             float g_logp = 0.0f;
@@ -558,11 +691,19 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
                 dmu[0][r] = g_logp * diff[r] * iv;
                 dls[r] = (a < A && live) ? g_logp * (diff[r] * diff[r] * iv - 1.0f) : 0.0f;
             }
+#if TAIL_DEFER
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                dls_l[r] += dls[r];
+                gb3_l[r] += dmu[0][r];
+            }
+#else
             dls_acc += (double)rs_sum16(dls, l);
             gb3 += rs_sum16(dmu[0], l);
+#endif
             __builtin_amdgcn_sched_barrier(0);
             // dW3a = dMu^T . H2a over the 32 rows, two half passes
-            __builtin_amdgcn_sched_barrier(0);
+            TAIL_STAMP(3)
 #pragma unroll
             for (int half = 0; half < 2; ++half) {
                 __builtin_amdgcn_sched_barrier(0);
@@ -571,11 +712,11 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
                 put_half<2>(S2, h2, c, h, half);
                 wave_sync_lds();
 #if TAIL_VARIANT != 1
-                acc_wgrad<1, 2>(gW3, S1, S2, c, h);
+                acc_wgrad_any<1, 2>(gW3, S1, S2, c, h);
 #endif
             }
             // dZ2 = (W3a^T dMu) * (1 - H2^2)
-            __builtin_amdgcn_sched_barrier(0);
+            TAIL_STAMP(4)
             {
                 bf16x8 bd0[NPL], bd1[NPL];
                 split_frag(dmu[0], 0, bd0);
@@ -634,6 +775,13 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
                 if (h == 0) loss_acc += (double)vf;
             }
             {
+#if TAIL_DEFER
+#pragma unroll
+                for (int it = 0; it < 2; ++it)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) gw3c_l[it][r] += gv * h2[it][r];
+                gv_l += h == 0 ? gv : 0.0f;
+#else
                 float gvh[16];
 #pragma unroll
                 for (int it = 0; it < 2; ++it) {
@@ -645,6 +793,7 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
 #pragma unroll
                 for (int off = 32; off > 0; off >>= 1) gsum += __shfl_xor(gsum, off, 64);
                 gb3 += gsum;
+#endif
             }
 #pragma unroll
             for (int ft = 0; ft < 2; ++ft)
@@ -654,7 +803,8 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
                                  (1.0f - h2[ft][r] * h2[ft][r]);
         }
         // ---- dZ1 = (W2^T dZ2) * (1 - H1^2) -> HBM (row-major [n][128]) -------------------
-        __builtin_amdgcn_sched_barrier(0);
+        TAIL_STAMP(5)
+#if !TAIL_KEEP_H1
         {
             // re-read this tile's H1 (L2-hot) instead of keeping it live through the loss and
             // head phases: an opaque zero offset stops the compiler from reusing the first load
@@ -674,6 +824,7 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
                 }
             }
         }
+#endif
         f32x16 dd0 = zero16(), dd1 = zero16();
 #pragma unroll
         for (int kc = 0; kc < 2; ++kc)
@@ -702,9 +853,16 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
             }
         }
         // ---- db2, dW2 = dZ2^T . H1 ---------------------------------------------------------
-        __builtin_amdgcn_sched_barrier(0);
+        TAIL_STAMP(6)
 #pragma unroll
-        for (int ot = 0; ot < 2; ++ot) gb2[ot] += rs_sum16(dz2[ot], l);
+        for (int ot = 0; ot < 2; ++ot) {
+#if TAIL_DEFER
+#pragma unroll
+            for (int r = 0; r < 16; ++r) gb2_l[ot][r] += dz2[ot][r];
+#else
+            gb2[ot] += rs_sum16(dz2[ot], l);
+#endif
+        }
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
             __builtin_amdgcn_sched_barrier(0);
@@ -713,14 +871,41 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
             put_half<2>(S2, h1, c, h, half);
             wave_sync_lds();
 #if TAIL_VARIANT != 1
-            acc_wgrad<2, 2>(gW2, S1, S2, c, h);
+            acc_wgrad_any<2, 2>(gW2, S1, S2, c, h);
 #endif
         }
+        TAIL_STAMP(7)
+#if TAIL_TRACE
+        ++tr_tile;
+#endif
     }
 #undef TAIL_PREFETCH
-    // ---- fold the 4 waves (fixed order) into this workgroup's slab --------------------------
+#if TAIL_DEFER
+    // the deferred column sums: one reduce-scatter each (rs_sum16's lane ownership)
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+        gb2[it] = rs_sum16(gb2_l[it], l);
+        if constexpr (!actor) gw3c[it] = rs_sum16(gw3c_l[it], l);
+    }
+    if constexpr (actor) {
+        gb3 = rs_sum16(gb3_l, l);
+        dls_acc = (double)rs_sum16(dls_l, l);
+    } else {
+        float gsum = gv_l;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) gsum += __shfl_xor(gsum, off, 64);
+        gb3 = gsum;
+    }
+#endif
+    // ---- fold the TAIL_NW waves (fixed order) into this workgroup's slab ---------------------
     __syncthreads();
-    float* red = sm;  // T_END >= 4 * 32 * 64 floats
+    float* red = sm;  // T_END >= TAIL_NW * 32 * 64 floats
+    auto wsum = [&](int stride, int i) {
+        float v = red[i];
+#pragma unroll
+        for (int ww = 1; ww < TAIL_NW; ++ww) v += red[ww * stride + i];
+        return v;
+    };
     float* slab = slab_f + (int64_t)blockIdx.x * SL_F;
     auto fold = [&](const f32x16 (&g)[2], int o0, int base) {
         // rows [o0, o0+32) of a [rows][64] matrix held as C layout (o = rho(r)+4h, f = 32ft+c)
@@ -731,8 +916,7 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
                 red[w * 32 * H + (rho(r) + 4 * h) * H + 32 * ft + c] = g[ft][r];
         __syncthreads();
         for (int i = t; i < 32 * H; i += TAIL_TPB)
-            slab[base + o0 * H + i] =
-                ((red[i] + red[32 * H + i]) + red[2 * 32 * H + i]) + red[3 * 32 * H + i];
+            slab[base + o0 * H + i] = wsum(32 * H, i);
         __syncthreads();
     };
     const int base2 = actor ? SL_W2A : SL_W2C;
@@ -752,7 +936,7 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
     }
     __syncthreads();
     if (t < VW) {
-        const float v = ((red[t] + red[VW + t]) + red[2 * VW + t]) + red[3 * VW + t];
+        const float v = wsum(VW, t);
         if (t < H) {
             slab[(actor ? SL_B2A : SL_B2C) + t] = v;
         } else if (t < 2 * H) {
@@ -763,7 +947,7 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
     }
     if (!actor && t == 0) {
         // every lane of a critic wave holds the same gb3 (full-wave sum)
-        slab[SL_B3C] = ((red[2 * H] + red[VW + 2 * H]) + red[2 * VW + 2 * H]) + red[3 * VW + 2 * H];
+        slab[SL_B3C] = wsum(VW, 2 * H);
     }
     loss_acc = wave_sum(loss_acc);
     cnt_acc = wave_sum(cnt_acc);
@@ -775,7 +959,9 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
     __syncthreads();
     double* sd = slab_d + (int64_t)blockIdx.x * SL_D;
     if (t < SL_D) {
-        const double v = ((sred[0][t] + sred[1][t]) + sred[2][t]) + sred[3][t];
+        double v = sred[0][t];
+#pragma unroll
+        for (int ww = 1; ww < TAIL_NW; ++ww) v += sred[ww][t];
         if (actor) {
             if (t == 0) sd[0] = v;            // clip sum
             else if (t == 1) sd[2] = v;       // row count
@@ -1210,9 +1396,9 @@ TailParams make_tail_params(const tsrl_ppo_params& q, int A) {
 }
 
 int tail_grid(int64_t n) {
-    // workgroups per net (grid.y = 2: actor, critic); 2 resident per CU
+    // workgroups per net (one launch per net), one resident per CU
     const int64_t tiles = (n + 31) / 32;
-    const int64_t g = (tiles + 3) / 4;
+    const int64_t g = (tiles + TAIL_NW - 1) / TAIL_NW;
     return (int)std::min<int64_t>(g, 256);
 }
 
@@ -1252,7 +1438,8 @@ extern "C" int64_t tsrl_mlp_frag_floats(int64_t n) {
 
 extern "C" int64_t tsrl_ppo_tail_workspace_bytes(int64_t n) {
     const int g = tail_grid(n);
-    return (int64_t)g * (SL_F * (int64_t)sizeof(float) + SL_D * (int64_t)sizeof(double)) + 256;
+    return (int64_t)g * (SL_F * (int64_t)sizeof(float) + SL_D * (int64_t)sizeof(double)) + 256 +
+           (TAIL_TRACE ? 256 + 2 * (int64_t)g * TAIL_NW * TAIL_TRACE_TILES * TAIL_NSTAMP * 8 : 0);
 }
 
 extern "C" int tsrl_ppo_tail(const float* h1frag, int64_t n, const int64_t* idx,
@@ -1279,11 +1466,11 @@ extern "C" int tsrl_ppo_tail(const float* h1frag, int64_t n, const int64_t* idx,
     TailWeights w{wt->w2a, wt->b2a, wt->w2c, wt->b2c, wt->w3a, wt->b3a, wt->w3c, wt->b3c,
                   wt->log_std};
     const TailParams tp = make_tail_params(prm, (int)act_dim);
-    hipLaunchKernelGGL(ppo_tail_kernel<0>, dim3(g), dim3(TAIL_TPB), 0, as_stream(stream), h1frag, n,
-                       idx, w, act, logp_old, adv, ret, v_s, adv_sums, tp, dz1, slab_f, slab_d);
+    hipLaunchKernelGGL(ppo_tail_kernel<0>, dim3(g), dim3(TAIL_TPB), 0, as_stream(stream), h1frag,
+                       n, idx, w, act, logp_old, adv, ret, v_s, adv_sums, tp, dz1, slab_f, slab_d);
     TSRL_LAUNCH_CHECK("tsrl_ppo_tail(actor)");
-    hipLaunchKernelGGL(ppo_tail_kernel<1>, dim3(g), dim3(TAIL_TPB), 0, as_stream(stream), h1frag, n,
-                       idx, w, act, logp_old, adv, ret, v_s, adv_sums, tp, dz1, slab_f, slab_d);
+    hipLaunchKernelGGL(ppo_tail_kernel<1>, dim3(g), dim3(TAIL_TPB), 0, as_stream(stream), h1frag,
+                       n, idx, w, act, logp_old, adv, ret, v_s, adv_sums, tp, dz1, slab_f, slab_d);
     TSRL_LAUNCH_CHECK("tsrl_ppo_tail");
     TailGrads gg{grads->w2a, grads->b2a, grads->w2c, grads->b2c, grads->w3a, grads->b3a,
                  grads->w3c, grads->b3c};
