@@ -1,7 +1,9 @@
 #!/bin/bash
-# Collect-step store-form A/B (COLLECT_ROW_STORE variants) at the headline shape.
+# Collect-step A/B at the headline shape: the in-tree library, then each variant named on the
+# command line (variants/libtsrl_<name>.so from tools/build_variant.sh, e.g. a
+# -DCOLLECT_ROW_STORE=1 build of collect.hip in round 3).
 set -o pipefail
-for v in main crs1 crs2; do
+for v in main "$@"; do
   if [ $v = main ]; then unset TSRL_LIB_PATH; else export TSRL_LIB_PATH=variants/libtsrl_$v.so; fi
   echo "== $v"
   timeout -k 10 150 python tools/collect_step_bench.py --steps 256 --reps 3 || exit $?
