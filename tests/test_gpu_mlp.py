@@ -223,6 +223,9 @@ CASES = [
     (8, 1, 257, dict(value_clip=True)),
     (376, 17, 2048, dict(norm_adv=False, ent_coef=0.0)),
     (64, 32, 4096, dict(dual_clip=5.0, value_clip=True, eps_clip=0.1, ent_coef=0.05)),
+    # a partial last 32-row chunk of the dW1 split, the db1 ones column in the third 128-column tile
+    (300, 7, 1000, dict(value_clip=True)),
+    (380, 3, 777, {}),
 ]
 
 

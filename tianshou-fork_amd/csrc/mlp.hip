@@ -1249,6 +1249,10 @@ __global__ __launch_bounds__(256, 2) void dw_kernel(
 // Staging: thread t owns feature / column (t & 127) and the 8-row groups {rg, rg + 2} of the
 // chunk (rg = t >> 7, wave-uniform, so the row indices come in through scalar loads); the
 // next chunk's 32 values are loaded into registers during the current chunk's MFMAs.
+// Round 3, measured and dropped (tools/dw_ab.sh, 262144 rows, same box): one workgroup per
+// CU covering all 384 columns, so each dZ1 element is loaded and split once instead of three
+// times -- 4 waves with 12 accumulator tiles each 311-317 us vs 264-267 for this kernel; 8
+// waves with 6 tiles each, MFMAs issued ahead of the next chunk's split 258-261 vs 246.
 #ifndef DWX6_OCC
 #define DWX6_OCC 2
 #endif
@@ -1482,7 +1486,8 @@ extern "C" int tsrl_ppo_tail(const float* h1frag, int64_t n, const int64_t* idx,
 
 extern "C" int64_t tsrl_mlp_dw_workspace_bytes(int64_t n, int64_t D) {
     const int ncolpad = (int)(((D + 1 + DW_COLS - 1) / DW_COLS) * DW_COLS);
-    return (int64_t)dw_nsplit(n) * HC * ncolpad * (int64_t)sizeof(float);
+    const int nsplit = dw_nsplit(n);
+    return (int64_t)nsplit * HC * ncolpad * (int64_t)sizeof(float);
 }
 
 extern "C" int tsrl_mlp_dw(const float* dz1, const float* X, int64_t ldx, const int64_t* idx,
