@@ -562,7 +562,10 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         }
         if (t == 0 && nd > 0) atomic_add_i64(tc + 4 * D, nd);
     };
-#if !COLLECT_ATOMIC_LATE
+#ifndef COLLECT_NO_TOTALS
+#define COLLECT_NO_TOTALS 0  // diagnostic builds only: skip the obs_rms atomics (wrong stats)
+#endif
+#if !COLLECT_ATOMIC_LATE && !COLLECT_NO_TOTALS
     add_totals();
 #endif
     TSTAMP(2)
