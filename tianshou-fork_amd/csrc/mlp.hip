@@ -182,7 +182,6 @@ struct TailParams {
 #ifndef TAIL_VARIANT
 #define TAIL_VARIANT 0  // diagnostic builds only: 1 = no layer-2/3 weight-gradient MFMAs
 #endif
-constexpr int WS2 = 65;   // LDS row stride of the staged weights (odd: conflict-free reads)
 // per-workgroup slab of weight-gradient partial sums (floats) and loss partial sums (doubles)
 constexpr int SL_W2A = 0, SL_B2A = SL_W2A + H * H, SL_W2C = SL_B2A + H, SL_B2C = SL_W2C + H * H,
               SL_W3A = SL_B2C + H, SL_B3A = SL_W3A + AMAX * H, SL_W3C = SL_B3A + AMAX,
@@ -978,9 +977,14 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
 // with LOGP, the Gaussian log-prob of the stored actions (logp_old, ppo.py:95-96), from the
 // layer-1 activations of tsrl_mlp_l1_fwd.  One wave = 32 rows.
 // ---------------------------------------------------------------------------------------
-constexpr int E_W2A = 0, E_W2C = E_W2A + H * WS2, E_W3 = E_W2C + H * WS2, E_B2A = E_W3 + AMAX * WS2,
-              E_B2C = E_B2A + H, E_B3 = E_B2C + H, E_W3C = E_B3 + AMAX, E_VAR = E_W3C + H,
+constexpr int E_B2A = 0, E_B2C = E_B2A + H, E_B3 = E_B2C + H, E_W3C = E_B3 + AMAX, E_VAR = E_W3C + H,
               E_LS = E_VAR + AMAX, E_END = E_LS + AMAX;
+
+// Round 3: layer 2 and the mu head as bf16x6 products against split weight images (the
+// learn tail's IMG_W2 / IMG_W3 layouts) instead of v_mfma_f32_32x32x2_f32 with one LDS read
+// per MFMA: 2.7x fewer matrix-core cycles per tile.
+constexpr int EV_W2A = 0, EV_W2C = EV_W2A + NPL * 2 * H * 64, EV_W3 = EV_W2C + NPL * 2 * H * 64,
+              EV_IMG = EV_W3 + NPL * 2 * AMAX * 64;  // 60 KB: two workgroups per CU
 
 template <bool LOGP>
 __global__ __launch_bounds__(256, 2) void eval_tail_kernel(const float* __restrict__ h1f,
@@ -989,17 +993,14 @@ __global__ __launch_bounds__(256, 2) void eval_tail_kernel(const float* __restri
                                                            float* __restrict__ value_out,
                                                            float* __restrict__ logp_out) {
     __shared__ float sm[E_END];
+    __shared__ __attribute__((aligned(16))) char img[EV_IMG];
     const int t = threadIdx.x;
     const int w = t >> 6, l = t & 63, h = l >> 5, c = l & 31;
-    for (int i = t; i < H * H; i += 256) {
-        sm[E_W2C + (i >> 6) * WS2 + (i & 63)] = wt.w2c[i];
-        if (LOGP) sm[E_W2A + (i >> 6) * WS2 + (i & 63)] = wt.w2a[i];
-    }
+    build_img_n<256>(img + EV_W2C, H, 2, [=](int r, int k) { return wt.w2c[r * H + k]; });
     if (LOGP) {
-        for (int i = t; i < AMAX * H; i += 256) {
-            const int a = i >> 6;
-            sm[E_W3 + a * WS2 + (i & 63)] = a < A ? wt.w3a[i] : 0.0f;
-        }
+        build_img_n<256>(img + EV_W2A, H, 2, [=](int r, int k) { return wt.w2a[r * H + k]; });
+        build_img_n<256>(img + EV_W3, AMAX, 2,
+                         [=](int r, int k) { return r < A ? wt.w3a[r * H + k] : 0.0f; });
     }
     if (t < H) {
         sm[E_B2C + t] = wt.b2c[t];
@@ -1035,19 +1036,27 @@ __global__ __launch_bounds__(256, 2) void eval_tail_kernel(const float* __restri
                     h1[i][4 * q + 3] = v.w;
                 }
             }
-            const float* sW2 = sm + (net ? E_W2C : E_W2A);
+            const char* iw2 = img + (net ? EV_W2C : EV_W2A);
             const float* sb2 = sm + (net ? E_B2C : E_B2A);
             float h2[2][16];
+            {
+                f32x16 z0 = zero16(), z1 = zero16();
 #pragma unroll
-            for (int ot = 0; ot < 2; ++ot) {
-                f32x16 z = zero16();
-                const float* wa = sW2 + (32 * ot + c) * WS2 + 4 * h;
+                for (int kc = 0; kc < 2; ++kc)
 #pragma unroll
-                for (int it = 0; it < 2; ++it)
+                    for (int s = 0; s < 2; ++s) {
+                        bf16x8 b[NPL], a[NPL];
+                        split_frag(h1[kc], s, b);
+                        ld_img(iw2, 2, H, kc, c, s, h, a);
+                        z0 = mfma6(a, b, z0);
+                        ld_img(iw2, 2, H, kc, 32 + c, s, h, a);
+                        z1 = mfma6(a, b, z1);
+                    }
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) z = mfma(wa[32 * it + rho(r)], h1[it][r], z);
-#pragma unroll
-                for (int r = 0; r < 16; ++r) h2[ot][r] = tanh_nb(z[r] + sb2[32 * ot + rho(r) + 4 * h]);
+                for (int r = 0; r < 16; ++r) {
+                    h2[0][r] = tanh_nb(z0[r] + sb2[rho(r) + 4 * h]);
+                    h2[1][r] = tanh_nb(z1[r] + sb2[32 + rho(r) + 4 * h]);
+                }
             }
             if (net == 1) {
                 float vpart = 0.0f;
@@ -1060,11 +1069,15 @@ __global__ __launch_bounds__(256, 2) void eval_tail_kernel(const float* __restri
                 if (live && h == 0) value_out[brow] = value;
             } else {
                 f32x16 mu = zero16();
-                const float* wa = sm + E_W3 + c * WS2 + 4 * h;
 #pragma unroll
-                for (int it = 0; it < 2; ++it)
+                for (int kc = 0; kc < 2; ++kc)
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) mu = mfma(wa[32 * it + rho(r)], h2[it][r], mu);
+                    for (int s = 0; s < 2; ++s) {
+                        bf16x8 b[NPL], a[NPL];
+                        split_frag(h2[kc], s, b);
+                        ld_img(img + EV_W3, 2, AMAX, kc, c, s, h, a);
+                        mu = mfma6(a, b, mu);
+                    }
                 float lp = 0.0f;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {

@@ -111,13 +111,20 @@ def main():
     def whole():
         fm.minibatch(obs, idx, B, act, logp_old, adv, ret, v_s, p, dp)
 
+    EV = min(N, fm.EVAL_CHUNK)
+    flop_eval = 2.0 * EV * (D * 128 + 64 * 64 * 2 + 64 * (A + 1))
+
+    def evaluate():  # process_fn: V(s) + logp_old of one 2M-row chunk (l1 + eval tail)
+        fm.evaluate(obs[:EV], act[:EV])
+
     if a.tail_trace:
         tail_trace_report(tail, ws, B, a.tail_trace)
         return
     for name, fn, flop in (("l1_fwd", l1, flop_l1), ("l1_fwd_x6(+split)", l1x6, flop_l1),
                            ("l1_x6_staged(rows)", l1x6_staged, flop_l1),
                            ("tail(+reduce)", tail, flop_tail),
-                           ("dw(+reduce)", dw, flop_l1), ("minibatch", whole, None)):
+                           ("dw(+reduce)", dw, flop_l1), ("minibatch", whole, None),
+                           ("eval(2M rows)", evaluate, flop_eval)):
         if a.only and not name.startswith(a.only):
             continue
         if ld != D and name in ("l1_fwd", "l1_x6_staged(rows)", "minibatch"):
