@@ -57,6 +57,63 @@ def test_clip_adam_matches_torch(max_norm):
     assert len(sd["state"]) == len(list(ac1.parameters()))
 
 
+@pytest.mark.parametrize("max_norm", [0.5, None])
+def test_clip_adam_nan_gradient_matches_torch(max_norm):
+    """A NaN gradient element (what an invalid mu / sigma produces with validate_args=False,
+    DESIGN.md section 7) takes the flat Adam state exactly where torch's takes it: with
+    clipping the NaN norm reaches every gradient and every parameter (clip_grad_norm_'s
+    clamp keeps the NaN), without clipping only that element's parameter, moments and later
+    updates; finite elements stay equal to torch, the step counter advances the same way and
+    the flat storage still backs the parameters afterwards."""
+    from tianshou_amd.policy import fused_mlp
+    from tianshou_amd.utils.models import get_actor_critic, init_actor_critic
+    from tianshou_amd.utils.net import ActorCritic
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    nets = []
+    for _ in range(2):
+        a, c = get_actor_critic((24,), (64, 64), (5,), dev)
+        nets.append((a.to(dev), c.to(dev)))
+    init_actor_critic(*nets[0])
+    ac0, ac1 = ActorCritic(*nets[0]), ActorCritic(*nets[1])
+    ac1.load_state_dict(ac0.state_dict())
+    opt_ref = torch.optim.Adam(ac0.parameters(), lr=3e-4)
+    opt = torch.optim.Adam(ac1.parameters(), lr=3e-4)
+    fm = fused_mlp.FusedActorCritic(fused_mlp.match(*nets[1]), ac1.parameters())
+    assert fm.bind_adam(opt)
+    g = torch.Generator(device=dev).manual_seed(2)
+    for step in range(3):
+        grads = [torch.randn(p.shape, device=dev, generator=g) for p in ac0.parameters()]
+        if step == 1:
+            grads[2].view(-1)[7] = float("nan")
+        for p, gr in zip(ac0.parameters(), grads):
+            p.grad = gr.clone()
+        if max_norm:
+            torch.nn.utils.clip_grad_norm_(ac0.parameters(), max_norm=max_norm)
+        opt_ref.step()
+        fm.bind_grads()
+        for p, gr in zip(ac1.parameters(), grads):
+            p.grad.copy_(gr)
+        fm.clip_adam(max_norm)
+        torch.cuda.synchronize()
+        for (n0, p0), p1 in zip(ac0.named_parameters(), ac1.parameters()):
+            x0, x1 = p0.detach().cpu().numpy(), p1.detach().cpu().numpy()
+            np.testing.assert_array_equal(np.isnan(x1), np.isnan(x0), err_msg=f"{step} {n0}")
+            np.testing.assert_allclose(x1[~np.isnan(x0)], x0[~np.isnan(x0)], rtol=1e-5,
+                                       atol=1e-7, err_msg=f"step {step} {n0}")
+    n_nan = sum(int(torch.isnan(p).sum()) for p in ac1.parameters())
+    if max_norm:
+        assert n_nan == sum(p.numel() for p in ac1.parameters())
+    else:
+        assert n_nan == 1
+    for p0, p1 in zip(ac0.parameters(), ac1.parameters()):
+        s0, s1 = opt_ref.state[p0], opt.state[p1]
+        assert float(s1["step"]) == float(s0["step"]) == 3.0
+        np.testing.assert_array_equal(torch.isnan(s1["exp_avg"]).cpu().numpy(),
+                                      torch.isnan(s0["exp_avg"]).cpu().numpy())
+    assert fm.adam_bound(opt)
+
+
 @pytest.mark.parametrize("D", [376, 17, 24])
 def test_clip_adam_split_epilogue_equals_split_w(D):
     """clip_adam(split_w1=True) leaves the bf16x6 planes of the UPDATED first-layer weights

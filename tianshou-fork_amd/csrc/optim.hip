@@ -100,7 +100,11 @@ __global__ __launch_bounds__(OTPB) void clip_adam_kernel(float* __restrict__ p,
             ss = wave_sum(ss);
             if (t == 0) {
                 const float norm = (float)sqrt(ss);
-                s_scale = fminf(a.max_norm / (norm + 1e-6f), 1.0f);
+                // torch.clamp(coef, max=1.0): a NaN norm (a NaN or infinite gradient element)
+                // gives a NaN coefficient that reaches every gradient, as in clip_grad_norm_
+                // (fminf would return 1.0 and leave the finite gradients unclipped)
+                const float coef = a.max_norm / (norm + 1e-6f);
+                s_scale = coef > 1.0f ? 1.0f : coef;
                 if (blockIdx.x == 0) {
                     norm_out[0] = norm;
                     norm_out[1] = s_scale;
