@@ -101,8 +101,9 @@ def test_cartpole_config1_matches_reference(golden_dir, dev):
     sd = policy.state_dict()
     for k in z.files:
         if k.startswith("final_actor.") or k.startswith("final_critic."):
-            np.testing.assert_allclose(sd[k[len("final_"):]].cpu().numpy(), z[k], rtol=1e-3,
-                                       atol=1e-5, err_msg=k)
+            # measured (round 3): <= 6e-8 abs after the Adam steps (round 2 asserted 1e-3 / 1e-5)
+            np.testing.assert_allclose(sd[k[len("final_"):]].cpu().numpy(), z[k], rtol=1e-5,
+                                       atol=1e-6, err_msg=k)
     # 3. deterministic evaluation collect with the updated policy (argmax of the probs)
     c.reset_buffer(keep_statistics=True)
     policy.eval()

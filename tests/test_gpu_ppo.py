@@ -109,16 +109,26 @@ def test_learn_matches_reference(golden_dir, dev, tag):
                   returns=t("returns"), v_s=t("v_s"))
     np.random.seed(21)
     res = policy.learn(batch, batch_size=cfg["batch_size"], repeat=cfg["repeat"])
+    def report(tag, g, w):
+        g, w = np.asarray(g, np.float64), np.asarray(w, np.float64)
+        e = np.abs(g - w)
+        print(f"{p}{tag}: max abs err {e.max():.3g}, max rel err "
+              f"{(e / np.maximum(np.abs(w), 1e-30)).max():.3g}")
     for k in ("loss", "loss/clip", "loss/vf", "loss/ent"):
-        np.testing.assert_allclose(res[k], z[p + k.replace("/", "_")], rtol=1e-4, atol=1e-5)
+        report(k, res[k], z[p + k.replace("/", "_")])
+        # measured (round 3): <= 1.3e-5 rel on the clip term (|clip| ~ 0.02), <= 1e-6 abs
+        np.testing.assert_allclose(res[k], z[p + k.replace("/", "_")], rtol=2e-5, atol=1e-6)
     if cfg["repeat"] == 1 and cfg["n"] == cfg["batch_size"]:
         for name, prm in policy.named_parameters():
             key = p + "grad_" + name
             if key in z.files:
-                np.testing.assert_allclose(prm.grad.cpu().numpy(), z[key], rtol=1e-3,
-                                           atol=1e-5)
+                report("grad " + name, prm.grad.cpu().numpy(), z[key])
+                np.testing.assert_allclose(prm.grad.cpu().numpy(), z[key], rtol=1e-4,
+                                           atol=1e-6)
     sd = policy.state_dict()
     for k in z.files:
         if k.startswith(p + "final_actor.") or k.startswith(p + "final_critic."):
+            report(k, sd[k[len(p + "final_"):]].cpu().numpy(), z[k])
+            # measured (round 3): <= 5.7e-7 abs after the Adam steps (parameters ~0.1)
             np.testing.assert_allclose(sd[k[len(p + "final_"):]].cpu().numpy(), z[k],
-                                       rtol=1e-3, atol=1e-5)
+                                       rtol=1e-5, atol=2e-6)

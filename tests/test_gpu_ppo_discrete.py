@@ -130,5 +130,6 @@ def test_learn_discrete_matches_reference(golden_dir, dev, tag):
     sd = policy.state_dict()
     for k in z.files:
         if k.startswith(p + "final_actor.") or k.startswith(p + "final_critic."):
+            # measured (round 3): <= 2.1e-7 abs after the Adam steps (round 2: 1e-3 / 1e-5)
             np.testing.assert_allclose(sd[k[len(p + "final_"):]].cpu().numpy(), z[k],
-                                       rtol=1e-3, atol=1e-5)
+                                       rtol=1e-5, atol=1e-6)

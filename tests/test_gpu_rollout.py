@@ -230,12 +230,20 @@ def test_process_fn_matches_reference(golden_dir, dev):
     assert policy.ret_rms.count == int(z["pf_ret_rms_count"])
     np.random.seed(5)
     res = policy.learn(batch, batch_size=E * T // 4, repeat=2)
-    np.testing.assert_allclose(res["loss"], z["learn_loss"], rtol=2e-3, atol=2e-4)
+    got, want = np.asarray(res["loss"], np.float64), np.asarray(z["learn_loss"], np.float64)
+    rel = np.abs(got - want) / np.maximum(np.abs(want), 1e-30)
+    print("learn loss rel err per minibatch:", np.array2string(rel, precision=2))
+    # measured (round 3): <= 2.4e-7 rel per minibatch (round 2 asserted 2e-3)
+    np.testing.assert_allclose(res["loss"], z["learn_loss"], rtol=1e-5, atol=1e-7)
     sd = policy.state_dict()
     for k in z.files:
         if k.startswith("final_actor.") or k.startswith("final_critic."):
-            np.testing.assert_allclose(sd[k[len("final_"):]].cpu().numpy(), z[k], rtol=1e-3,
-                                       atol=1e-4)
+            g, w = sd[k[len("final_"):]].cpu().numpy(), z[k]
+            e = np.abs(g - w)
+            print(f"{k}: max abs err {e.max():.3g}, max rel err "
+                  f"{(e / np.maximum(np.abs(w), 1e-30)).max():.3g}, "
+                  f"elements beyond 1e-5 rel {(e > 1e-5 * np.abs(w) + 1e-7).sum()} of {w.size}")
+            np.testing.assert_allclose(g, w, rtol=1e-5, atol=1e-6)  # measured <= 2.2e-7 abs
 
 
 def test_process_fn_on_reference_values(golden_dir, dev):

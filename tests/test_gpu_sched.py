@@ -83,5 +83,6 @@ def test_scheduled_updates_match_reference(golden_dir, tag):
     sd = policy.state_dict()
     for k in z.files:
         if k.startswith(p + "final_actor.") or k.startswith(p + "final_critic."):
+            # measured (round 3): <= 7.6e-8 abs after the Adam steps (round 2: 1e-3 / 1e-5)
             np.testing.assert_allclose(sd[k[len(p + "final_"):]].cpu().numpy(), z[k],
-                                       rtol=1e-3, atol=1e-5, err_msg=k)
+                                       rtol=1e-5, atol=1e-6, err_msg=k)
