@@ -538,7 +538,9 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         const int d = t;
         for (int r = 0; r < nrows; ++r) {
             const int m = box_m(rs[r].key, d);
+#if !COLLECT_NO_RAW
             a.raw[(r0 + r) * D + d] = (float)m * 0x1p-23f;  // == box_val(key, d), exactly
+#endif
             cs1 += m;
             cq1 += (long long)m * m;
         }
@@ -562,6 +564,9 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         }
         if (t == 0 && nd > 0) atomic_add_i64(tc + 4 * D, nd);
     };
+#ifndef COLLECT_NO_RAW
+#define COLLECT_NO_RAW 0  // diagnostic builds only: skip the raw env-row stores (wrong rows)
+#endif
 #ifndef COLLECT_NO_TOTALS
 #define COLLECT_NO_TOTALS 0  // diagnostic builds only: skip the obs_rms atomics (wrong stats)
 #endif
