@@ -1262,7 +1262,10 @@ __global__ __launch_bounds__(256, 2) void dw_kernel(
 // Staging: thread t owns feature / column (t & 127) and the 8-row groups {rg, rg + 2} of the
 // chunk (rg = t >> 7, wave-uniform, so the row indices come in through scalar loads); the
 // next chunk's 32 values are loaded into registers during the current chunk's MFMAs.
-// Round 3, measured and dropped (tools/dw_ab.sh, 262144 rows, same box): one workgroup per
+// Round 3, measured and dropped: dZ1 handed over by the tail as split bf16 planes in this
+// kernel's own LDS image (6 16-byte copies per thread per chunk instead of 16 loads + splits):
+// dW1 217 -> 212 us but the tail's transpose + split of dZ1 221 vs 208 us -- a net loss.
+// Also (tools/dw_ab.sh, 262144 rows, same box): one workgroup per
 // CU covering all 384 columns, so each dZ1 element is loaded and split once instead of three
 // times -- 4 waves with 12 accumulator tiles each 311-317 us vs 264-267 for this kernel; 8
 // waves with 6 tiles each, MFMAs issued ahead of the next chunk's split 258-261 vs 246.
