@@ -78,6 +78,33 @@ constexpr int WP = 68;         // W2 / W3 rows (4i + k banks: conflict-free A fr
 #define TSTAMP2(i)
 #endif
 
+// Store form of the replay rows this step writes (obs and obs_next: 12.6 MB per 4096 x 376
+// step, not read again by this collect).  3 (default): write-through `sc1` vector stores
+// (inline asm, s_nop 1 after each so the data VGPRs are read before reuse), which leave no
+// dirty lines for the end-of-kernel write-back: 23.97-24.04 vs 25.66-25.87 us per step with
+// plain stores, two A/B rounds in one call (tools/collect_ab.sh).  4: also the raw env rows
+// (re-read by the next launch): 24.13-24.21.  0: plain.  Measured earlier and dropped: 1 =
+// non-temporal stores (26.2 vs 25.6), 2 = relaxed agent-scope 8-byte atomic stores (28.9).
+#ifndef COLLECT_ROW_STORE
+#define COLLECT_ROW_STORE 3
+#endif
+__device__ __forceinline__ void row_store4(float4* p, float4 x) {
+#if COLLECT_ROW_STORE >= 3
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v v = {x.x, x.y, x.z, x.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+#else
+    *p = x;
+#endif
+}
+__device__ __forceinline__ void row_store1(float* p, float x) {
+#if COLLECT_ROW_STORE >= 3
+    asm volatile("global_store_dword %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(x) : "memory");
+#else
+    *p = x;
+#endif
+}
+
 // Workgroup barrier that orders LDS only: outstanding global loads and stores stay in flight
 // (__syncthreads also waits for every global store's acknowledgement and every pending load)
 #define LDS_SYNC()                                                                          \
@@ -385,7 +412,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
                     x.y = norm1(x.y, m.y, v.y, eps, clip);
                     x.z = norm1(x.z, m.z, v.z, eps, clip);
                     x.w = norm1(x.w, m.w, v.w, eps, clip);
-                    dst[q] = x;
+                    row_store4(&dst[q], x);
                     if (amask) {
                         const float4 mr = *reinterpret_cast<const float4*>(&sFinM[4 * q]);
                         const float4 vr = *reinterpret_cast<const float4*>(&sFinV[4 * q]);
@@ -492,7 +519,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
     LDS_SYNC();
     for (int i = t; i < nrows * D; i += NT) {
         const int rw = i / D, c = i - rw * D;
-        a.obs_dst[s_row[rw] * D + c] = sX[c * XP + rw];
+        row_store1(&a.obs_dst[s_row[rw] * D + c], sX[c * XP + rw]);
     }
     // ---- C. env step + auto-reset of these rows (env.hip box_step_reset_kernel) -------------
     // The synthetic env's transition does not read the action, so the step runs before the
@@ -538,7 +565,9 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         const int d = t;
         for (int r = 0; r < nrows; ++r) {
             const int m = box_m(rs[r].key, d);
-#if !COLLECT_NO_RAW
+#if COLLECT_ROW_STORE == 4
+            row_store1(&a.raw[(r0 + r) * D + d], (float)m * 0x1p-23f);
+#elif !COLLECT_NO_RAW
             a.raw[(r0 + r) * D + d] = (float)m * 0x1p-23f;  // == box_val(key, d), exactly
 #endif
             cs1 += m;
@@ -548,7 +577,11 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
             for (int r = 0; r < nrows; ++r) {
                 if (!rr[r].active) continue;
                 const int m = box_m(rr[r].key, d);
+#if COLLECT_ROW_STORE == 4
+                row_store1(&a.reset_raw[(r0 + r) * D + d], (float)m * 0x1p-23f);
+#else
                 a.reset_raw[(r0 + r) * D + d] = (float)m * 0x1p-23f;
+#endif
                 cs2 += m;
                 cq2 += (long long)m * m;
             }
