@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--tail-trace", type=int, default=0,
                     help="the library is a TAIL_TRACE=1 build with this many waves per workgroup: "
                          "report the tail's per-phase s_memtime cycles")
+    ap.add_argument("--eval-chunk", type=int, default=0,
+                    help="rows per process_fn evaluation chunk (FusedActorCritic.EVAL_CHUNK)")
     a = ap.parse_args()
     from tianshou_amd import _C
     from tianshou_amd.dist import DataParallel
@@ -45,6 +47,8 @@ def main():
     init_actor_critic(actor, critic)
     layers = fused_mlp.match(actor, critic)
     fm = fused_mlp.FusedActorCritic(layers, ActorCritic(actor, critic).parameters())
+    if a.eval_chunk:
+        fm.EVAL_CHUNK = a.eval_chunk
     N, B, D, A = a.N, a.rows, a.D, a.A
     ld = a.ld or D
     obs = torch.randn(N, ld, device=dev)
@@ -111,7 +115,7 @@ def main():
     def whole():
         fm.minibatch(obs, idx, B, act, logp_old, adv, ret, v_s, p, dp)
 
-    EV = min(N, fm.EVAL_CHUNK)
+    EV = min(N, 1 << 21)
     flop_eval = 2.0 * EV * (D * 128 + 64 * 64 * 2 + 64 * (A + 1))
 
     def evaluate():  # process_fn: V(s) + logp_old of one 2M-row chunk (l1 + eval tail)
