@@ -91,6 +91,20 @@ __global__ __launch_bounds__(OTPB) void clip_adam_kernel(float* __restrict__ p,
     const int t = threadIdx.x;
     const bool clip = a.max_norm > 0.0f;
     const float st = step[0] + 1.0f;
+    const int64_t i0 = (int64_t)blockIdx.x * OCHUNK;
+    // every element of this thread's slice loaded first, all in flight together and under the
+    // fold of the partial norms (one memory latency per launch instead of one per element)
+    constexpr int EPT = OCHUNK / OTPB;
+    float gr[EPT], mr[EPT], vr[EPT], pr[EPT];
+#pragma unroll
+    for (int q = 0; q < EPT; ++q) {
+        const int64_t i = i0 + q * OTPB + t;
+        const bool in = i < n;
+        gr[q] = in ? g[i] : 0.0f;
+        mr[q] = in ? m[i] : 0.0f;
+        vr[q] = in ? v[i] : 0.0f;
+        pr[q] = in ? p[i] : 0.0f;
+    }
     if (clip) {
         // the per-slice sums of squares of norm_partials_kernel, folded by wave 0 in the same
         // fixed order in every workgroup (so every workgroup gets the identical coefficient)
@@ -117,22 +131,27 @@ __global__ __launch_bounds__(OTPB) void clip_adam_kernel(float* __restrict__ p,
     const float bc1 = 1.0f - powf(a.beta1, st);
     const float bc2_sqrt = sqrtf(1.0f - powf(a.beta2, st));
     const float step_size = (lr_dev ? *lr_dev : a.lr) / bc1;
-    const int64_t i0 = (int64_t)blockIdx.x * OCHUNK;
-    const int64_t i1 = min(n, i0 + OCHUNK);
     // g is only read here (other workgroups are still summing it); the clipped gradient is
     // written back by clip_scale_kernel, the next launch on the stream
-    for (int64_t i = i0 + t; i < i1; i += OTPB) {
-        const float gi = g[i] * scale;
-        const float mi = a.beta1 * m[i] + (1.0f - a.beta1) * gi;
-        const float vi = a.beta2 * v[i] + (1.0f - a.beta2) * gi * gi;
+#pragma unroll
+    for (int q = 0; q < EPT; ++q) {
+        const int64_t i = i0 + q * OTPB + t;
+        if (i >= n) break;
+        const float gi = gr[q] * scale;
+        const float mi = a.beta1 * mr[q] + (1.0f - a.beta1) * gi;
+        const float vi = a.beta2 * vr[q] + (1.0f - a.beta2) * gi * gi;
         m[i] = mi;
         v[i] = vi;
-        const float pi = p[i] - step_size * mi / (sqrtf(vi) / bc2_sqrt + a.eps);
+        const float pi = pr[q] - step_size * mi / (sqrtf(vi) / bc2_sqrt + a.eps);
         p[i] = pi;
         if (so.out) split_store(so, i, pi);
     }
+    // the ticket orders only reads of step[0] (every wave's has returned: its value was used
+    // above, and the barrier waits for all waves) before the last workgroup's write, so it is
+    // relaxed: an acquire-release at agent scope would write back and invalidate this XCD's L2
+    __syncthreads();
     if (t == 0) {
-        const unsigned int done = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL,
+        const unsigned int done = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED,
                                                          __HIP_MEMORY_SCOPE_AGENT);
         if (done == gridDim.x - 1) {  // every workgroup has read step[0] and the gradients
             for (int64_t i = 0; i < nstep; ++i) step[i] = st;
