@@ -330,6 +330,8 @@ def main():
     for _ in range(args.warmup):
         iteration()
     phase.update(collect=0.0, update=0.0)
+    from tianshou_amd import dist as tdist
+    tdist.LOG.reset()  # collectives of the timed iterations only
     timer.on = True
     barrier()
     t0 = time.perf_counter()
@@ -346,6 +348,32 @@ def main():
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    dp_report = None
+    if distributed:
+        # N > 1 self-report (rank-collective; every rank takes part): per-iteration counts of
+        # each collective kind in the timed region, each kind timed at its payload, the
+        # collect / update split of every rank, and replica consistency (parameter hash
+        # all-reduced MAX == MIN)
+        import torch.distributed as dist
+        calls = {k: v / args.steps for k, v in sorted(tdist.LOG.calls.items())}
+        split = torch.tensor([phase["collect"] / args.steps, phase["update"] / args.steps],
+                             dtype=torch.float64, device=dev)
+        per_rank = [torch.empty_like(split) for _ in range(world)]
+        dist.all_gather(per_rank, split)
+        h = tdist.param_hash(list(policy.parameters()))
+        hmax, hmin = h.clone(), h.clone()
+        dist.all_reduce(hmax, op=dist.ReduceOp.MAX)
+        dist.all_reduce(hmin, op=dist.ReduceOp.MIN)
+        probe = tdist.probe_collectives(tdist.default_dp())
+        dp_report = {
+            "rccl_world_size": dist.get_world_size(),
+            "collectives_per_iter": calls,
+            "collective_timing": probe,
+            "per_rank_s": [{"rank": r, "collect_s": round(float(t[0]), 5),
+                            "update_s": round(float(t[1]), 5)} for r, t in enumerate(per_rank)],
+            "replica_hash_equal": bool(int(hmax) == int(hmin)),
+            "param_hash": int(h),
+        }
     total_steps = n * world * args.steps
     value = total_steps / elapsed
     gae_ms = timer.mean_ms()
@@ -392,7 +420,8 @@ def main():
                        "learn_graph_capture_failed": bool(getattr(policy, "_graph_failed",
                                                                   False)),
                        "collect_s": phase["collect"] / args.steps,
-                       "update_s": phase["update"] / args.steps},
+                       "update_s": phase["update"] / args.steps,
+                       "data_parallel": dp_report},
             "roofline": {"kernel": "tsrl_gae (gae_rows_staged_kernel)", "bound": "hbm",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -240,9 +240,12 @@ int tsrl_buffer_add(const tsrl_add_args* a, void* stream);
  *   w1p: the actor's first-layer weight packed by tsrl_collect_pack_w1 (once per update);
  *   workspace: tsrl_collect_workspace_bytes(k, dim) bytes, ZEROED once before first use
  *     (its tickets re-arm themselves);
- *   totals (data parallel, nullable): the step/reset moments are written there in
- *     tsrl_rms_sum_partials2's [4*dim+2] layout instead of merged; the caller all-reduces them
- *     and runs tsrl_rms_merge2(nblk = 1) before the next step.
+ *   no_moments (exact obs_rms): nonzero = the launch computes no obs_rms moments; the
+ *     caller applies tsrl_rms_exact_update to raw / reset_raw between launches and the
+ *     pending add normalises with mean / var / snap_*.  0: the step's integer moments are
+ *     merged by the next launch of the chain (rms_step) or by tsrl_collect_rms_finalize;
+ *     data parallel: the caller all-reduces the step's totals slot
+ *     (tsrl_collect_totals_offset) in between.
  * ------------------------------------------------------------------------------- */
 typedef struct tsrl_collect_args {
     tsrl_add_args add;       /* pending add of the previous step (add.k == 0: none) */
@@ -267,13 +270,9 @@ typedef struct tsrl_collect_args {
     /* obs RunningMeanStd */
     void* workspace;
     float* mean; float* var; float* snap_mean; float* snap_var; double* count;
-    double* totals;          /* data parallel / exact obs_rms: this step's f64 moments (the
-                                merge2 vector); NULL: the deferred merge below */
+    int64_t no_moments;      /* exact obs_rms: no moments (see above); 0: the deferred merge */
     int64_t rms_step;        /* index of this launch in its chain of deferred steps (0: the
                                 first after tsrl_collect_rms_finalize or a fresh workspace) */
-    int64_t rms_rows;        /* step rows behind the previous step's totals (0: k); data
-                                parallel: world * k, the caller having summed the totals slot
-                                (tsrl_collect_totals_offset) over the ranks */
 } tsrl_collect_args;
 int64_t tsrl_collect_pack_floats(int64_t dim);
 int tsrl_collect_pack_w1(const float* W, int64_t dim, float* packed, void* stream);
@@ -284,8 +283,9 @@ int tsrl_collect_box_step(const tsrl_collect_args* a, void* stream);
  * its step rows (what the closing tsrl_buffer_add normalises obs_next with).  Replaces the
  * obs_rms update of VectorEnvNormObs.step (env/venv_wrappers.py:93-99) for that step. */
 int tsrl_collect_rms_finalize(const tsrl_collect_args* a, void* stream);
-/* Byte offset in the workspace of the int64 [4 * dim + 1] totals slot that step `step` of a
- * chain accumulates (data parallel: all-reduce it with SUM before the next launch). */
+/* Byte offset in the workspace of the int64 [4 * dim + 2] totals slot that step `step` of a
+ * chain accumulates ([4*dim] reset rows, [4*dim + 1] step rows; data parallel: all-reduce it
+ * with SUM before the next launch, world * k <= 2^17 keeps the sums exact). */
 int64_t tsrl_collect_totals_offset(int64_t step);
 /* *rel_dev = (*rel_dev + 1) % ring_size (device-side ring cursor for graph-captured steps). */
 int tsrl_ring_advance(int64_t* rel_dev, int64_t ring_size, void* stream);

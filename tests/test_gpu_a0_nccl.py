@@ -45,3 +45,21 @@ def test_bench_force_dp_one_rank_rccl():
     # whole epochs) and into the collect graphs (global obs_rms), not run eagerly
     assert out["config"]["learn_graph_capture_failed"] is False
     assert "capture failed" not in p.stderr
+    # the N > 1 self-report (bench.py data_parallel): collective counts per iteration by
+    # kind -- graph-replayed collectives counted per replay --, each kind timed at its
+    # payload, per-rank collect / update split, replica consistency
+    dpr = out["config"]["data_parallel"]
+    assert dpr["rccl_world_size"] == 1
+    calls = dpr["collectives_per_iter"]
+    T, mb, repeat = 128, 32, 4
+    assert calls["obs_rms"] == T  # one per env step (fused step: the int64 totals slot)
+    assert calls["grad"] == mb * repeat  # one bucket per minibatch
+    assert calls["adv_moments"] == repeat  # one per epoch
+    assert calls["ret_rms"] == 1  # one per update
+    tim = dpr["collective_timing"]
+    for kind in ("obs_rms", "grad", "adv_moments"):
+        assert tim[kind]["eager_us"] > 0, kind
+        assert tim[kind]["bytes"] > 0, kind
+    assert tim["obs_rms"]["dtype"] == "int64"
+    assert len(dpr["per_rank_s"]) == 1 and dpr["per_rank_s"][0]["update_s"] > 0
+    assert dpr["replica_hash_equal"] is True

@@ -226,6 +226,9 @@ CASES = [
     # a partial last 32-row chunk of the dW1 split, the db1 ones column in the third 128-column tile
     (300, 7, 1000, dict(value_clip=True)),
     (380, 3, 777, {}),
+    # the production shape of the headline bench (config 3: D 376, A 17, 262144-row minibatch)
+    (376, 17, 262144, {}),
+    (376, 17, 262144, dict(dual_clip=3.0, value_clip=True)),
 ]
 
 
@@ -272,7 +275,8 @@ def test_fused_minibatch_matches_autograd(dev, D, A, B, kw):
     torch.cuda.synchronize()
     got = {k: v.grad.detach().cpu().double() for k, v in W.items()}
     mb = [t[idx] for t in (obs, act, logp_old, adv, ret, v_s)]
-    t64, g64 = _ref_minibatch(W, *mb, kw, torch.float64, "cpu")
+    # fp64 autograd on the GPU for the production-size cases (CPU fp64 is minutes there)
+    t64, g64 = _ref_minibatch(W, *mb, kw, torch.float64, dev if B > 65536 else "cpu")
     t32, g32 = _ref_minibatch(W, *mb, kw, torch.float32, dev)
     np.testing.assert_allclose(terms.cpu().double().numpy(), t64.numpy(), rtol=1e-5, atol=1e-6)
     for k in W:
@@ -280,6 +284,7 @@ def test_fused_minibatch_matches_autograd(dev, D, A, B, kw):
         den = ref.norm().item() + 1e-30
         e_fused = (got[k] - ref).norm().item() / den
         e_torch = (g32[k] - ref).norm().item() / den
+        print(f"B={B} {k}: rel L2 err fused {e_fused:.3g}, torch f32 {e_torch:.3g}")
         assert e_fused <= max(4 * e_torch, 2e-6), (k, e_fused, e_torch)
 
 
@@ -346,6 +351,48 @@ def test_process_fn_fused_eval_matches_torch_layers(dev):
     for k in out[0]:
         np.testing.assert_allclose(out[0][k].numpy(), out[1][k].numpy(), rtol=1e-5, atol=1e-5,
                                    err_msg=k)
+
+
+def test_process_fn_fused_eval_headline_width_matches_torch_layers(dev):
+    """The same comparison at the headline width and a production-size row count: D = 376,
+    A = 17, 4096 envs x 512 steps = 2 097 152 rows (one full 2M-row evaluation chunk).  One
+    rollout is collected; process_fn runs on it with the fused evaluation and with the torch
+    layers (same weights, each policy with a fresh ret_rms): v_s, returns, adv, logp_old within
+    rtol 1e-5 / atol 1e-5 (advantages also atol 1e-6 * max); the measured errors are printed."""
+    import copy
+    from tianshou_amd.data import Collector, VectorReplayBuffer
+    from tianshou_amd.env import Box, SyntheticVectorEnv, VectorEnvNormObs
+    from tianshou_amd.policy import PPOPolicy
+    from tianshou_amd.utils.models import fixed_std_normal
+    E, D, A, T = 4096, 376, 17, 512
+    base_a, base_c = _nets(D, A, dev, 13)
+    pols = []
+    for fused in (True, False):
+        actor, critic = copy.deepcopy(base_a), copy.deepcopy(base_c)
+        optim = torch.optim.Adam(list(actor.parameters()) + list(critic.parameters()), lr=1e-4)
+        pol = PPOPolicy(actor, critic, optim, fixed_std_normal, action_space=Box(-1.0, 1.0, (A,)),
+                        reward_normalization=True, fused_mlp=fused)
+        assert (pol._mlp is not None) == fused
+        pols.append(pol)
+    env = VectorEnvNormObs(SyntheticVectorEnv(E, (D,), A, ep_len=300, seed=3, device=dev))
+    buf = VectorReplayBuffer(E * T, E, device=dev)
+    torch.manual_seed(4)
+    Collector(pols[0], env, buf).collect(n_step=E * T)
+    assert buf.obs_chain
+    out = []
+    for pol in pols:
+        batch, idx = buf.sample(0)
+        assert len(idx) == E * T
+        batch = pol.process_fn(batch, buf, idx)
+        out.append({k: batch[k].detach() for k in ("v_s", "returns", "adv", "logp_old")})
+        del batch
+    for k in out[0]:
+        a, b = out[0][k].double(), out[1][k].double()
+        err = (a - b).abs()
+        print(f"{k}: max abs err {float(err.max()):.3g}, max rel err "
+              f"{float((err / b.abs().clamp_min(1e-30)).max()):.3g}")
+        atol = max(1e-5, 1e-6 * float(b.abs().max())) if k == "adv" else 1e-5
+        assert bool((err <= 1e-5 * b.abs() + atol).all()), k
 
 
 def test_learn_graph_replay_matches_eager(dev):

@@ -215,3 +215,43 @@ def test_clip_adam_resumes_loaded_state():
                                    rtol=1e-5, atol=1e-7, err_msg=n0)
     for p0, p1 in zip(ac0.parameters(), ac1.parameters()):
         assert float(opt.state[p1]["step"]) == float(opt_ref.state[p0]["step"]) == 6.0
+
+
+def test_flat_adam_refuses_mixed_step_counts():
+    """A state dict where some parameters have Adam state and others none (per-parameter step
+    counts differ): clip_adam applies ONE bias correction to every parameter, so the flat pass
+    must not claim the optimiser (adam_bound / bind_adam False) -- torch's Adam then steps it,
+    each parameter with its own count.  A uniform state dict still re-binds."""
+    import copy
+    from tianshou_amd.policy import fused_mlp
+    from tianshou_amd.utils.models import get_actor_critic
+    from tianshou_amd.utils.net import ActorCritic
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(3)
+    a, c = get_actor_critic((24,), (64, 64), (5,), dev)
+    a, c = a.to(dev), c.to(dev)
+    ac = ActorCritic(a, c)
+    opt = torch.optim.Adam(ac.parameters(), lr=3e-4)
+    fm = fused_mlp.FusedActorCritic(fused_mlp.match(a, c), ac.parameters())
+    assert fm.bind_adam(opt)
+    fm.bind_grads()
+    for p in ac.parameters():
+        p.grad.copy_(torch.randn_like(p))
+    fm.clip_adam(0.5)
+    torch.cuda.synchronize()
+    full = copy.deepcopy(opt.state_dict())
+    partial = copy.deepcopy(full)
+    first = sorted(partial["state"])[0]
+    del partial["state"][first]  # parameter 0 loses its state: step 0 vs 1 elsewhere
+    opt.load_state_dict(partial)
+    assert not fm.adam_bound(opt)
+    assert not fm.bind_adam(opt)
+    # torch's own Adam continues: parameter 0 from step 0, the others from step 1
+    for p in ac.parameters():
+        p.grad = torch.randn_like(p)
+    opt.step()
+    steps = [float(opt.state[p]["step"]) for p in ac.parameters()]
+    assert steps[0] == 1.0 and all(s == 2.0 for s in steps[1:])
+    # a uniform state dict binds again
+    opt.load_state_dict(full)
+    assert fm.bind_adam(opt)

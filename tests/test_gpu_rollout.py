@@ -312,3 +312,54 @@ def test_exact_obs_rms_collect_bitwise(golden_dir, dev, name):
     assert np.array_equal(m.obs.cpu().numpy(), z["c1_buf_obs"])
     assert np.array_equal(m.obs_next.cpu().numpy(), z["c1_buf_obs_next"])
     assert np.array_equal(c.data.obs.cpu().numpy(), z["c1_data_obs"])
+
+
+def _pf_errors(batch, z, keys):
+    errs = {}
+    for k in keys:
+        got, want = batch[k].detach().cpu().numpy().astype(np.float64), z["pf_" + k]
+        err = np.abs(got - want)
+        errs[k] = (float(err.max()), float((err / np.maximum(np.abs(want), 1e-30)).max()),
+                   float((err / (1e-5 * np.abs(want) + 1e-6 * np.abs(want).max())).max()))
+    return errs
+
+
+@pytest.mark.parametrize("tag", ["d8", "d376"])
+@pytest.mark.parametrize("exact", [False, True])
+def test_headline_path_end_to_end_matches_reference(golden_dir, dev, tag, exact):
+    """The headline path end to end at the headline width, on the build's OWN rollout: the
+    fused one-launch collect step (default integer obs_rms moments, or exact_obs_rms=True) ->
+    sample(0) -> process_fn (fused evaluation: bf16x6 layer 1 + eval tail, V(s') reused along
+    the obs chain, rew_norm GAE) against the reference Collector + VectorEnvNormObs +
+    PPOPolicy.process_fn on the same synthetic env (tools/gen_goldens.py gen_collector_fused;
+    collector.py:258-361, venv_wrappers.py:77-99, statistics.py:93-114, a2c.py:83-117,
+    ppo.py:87-97).  V, returns and advantages do not depend on the sampled actions for this
+    env (its transition ignores them), so they are comparable even though the action streams
+    differ; logp_old is not.  Tolerance: north_star's rtol 1e-5 with atol 1e-6 * max|ref| for
+    returns / adv (and V); the measured errors are printed.  ret_rms rtol 1e-5."""
+    from tianshou_amd.data import Collector, VectorReplayBuffer
+    from tianshou_amd.env import SyntheticVectorEnv, VectorEnvNormObs
+    z = np.load(os.path.join(golden_dir, f"collector_{tag}.npz"))
+    _, policy, _, _, (E, D, A, L, T) = _collector_setup(z, dev)
+    env = VectorEnvNormObs(SyntheticVectorEnv(E, (D,), A, ep_len=L, device=dev),
+                           exact_obs_rms=exact)
+    buf = VectorReplayBuffer(E * T, E, device=dev)
+    c = Collector(policy, env, buf)
+    c.graph_steps = 4
+    res = c.collect(n_step=E * T)
+    assert c._step_on, "the fused one-launch step did not run"
+    _check_stats(z, "c1_", res)
+    batch, idx = buf.sample(0)
+    assert idx.tolist() == z["c1_indices"].tolist()
+    batch = policy.process_fn(batch, buf, idx)
+    errs = _pf_errors(batch, z, ("v_s", "returns", "adv"))
+    for k, (ea, er, ratio) in errs.items():
+        print(f"{tag} exact={exact} {k}: max abs err {ea:.3g}, max rel err {er:.3g}, "
+              f"max err / (rtol 1e-5 + atol 1e-6 max) {ratio:.3g}")
+    for k in ("v_s", "returns", "adv"):
+        want = z["pf_" + k]
+        np.testing.assert_allclose(batch[k].detach().cpu().numpy(), want, rtol=1e-5,
+                                   atol=1e-6 * np.abs(want).max(), err_msg=k)
+    assert policy.ret_rms.mean == pytest.approx(float(z["pf_ret_rms_mean"]), rel=1e-5)
+    assert policy.ret_rms.var == pytest.approx(float(z["pf_ret_rms_var"]), rel=1e-5)
+    assert policy.ret_rms.count == int(z["pf_ret_rms_count"])

@@ -40,7 +40,7 @@ def test_ctypes_struct_layout_matches_header(tmp_path):
                    'int main(){printf("%zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(tsrl_add_args), '
                    'sizeof(tsrl_ppo_params), offsetof(tsrl_add_args, stat_idx), '
                    'offsetof(tsrl_ppo_params, norm_adv), sizeof(tsrl_collect_args), '
-                   'offsetof(tsrl_collect_args, sample), offsetof(tsrl_collect_args, totals), '
+                   'offsetof(tsrl_collect_args, sample), offsetof(tsrl_collect_args, no_moments), '
                    'offsetof(tsrl_collect_args, rms_step));}')
     exe = tmp_path / "probe"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)],
@@ -52,7 +52,7 @@ def test_ctypes_struct_layout_matches_header(tmp_path):
     assert int(out[3]) == _C.PPOParams.norm_adv.offset
     assert int(out[4]) == ctypes.sizeof(_C.CollectArgs)
     assert int(out[5]) == _C.CollectArgs.sample.offset
-    assert int(out[6]) == _C.CollectArgs.totals.offset
+    assert int(out[6]) == _C.CollectArgs.no_moments.offset
     assert int(out[7]) == _C.CollectArgs.rms_step.offset
 
 

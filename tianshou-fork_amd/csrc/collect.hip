@@ -18,19 +18,26 @@
 //   C. the env step + auto-reset of these rows (synth.h, as env.hip's box_step_reset_kernel)
 //      with the column moments of the step rows and of the reset rows;
 //   D. obs_rms: the synthetic env's values are x = m 2^-23 with integer |m| <= 2^23
-//      (synth.h), so the column moments are summed EXACTLY as integers (sum m, sum m^2 <
-//      2^59 over any step) by 64-bit atomics into a per-step totals slot -- exact sums are
-//      independent of the summation order, so no ordered fold is needed.  The merge of those
-//      totals into the RunningMeanStd (rms.hip's merge2 arithmetic) is DEFERRED to the next
-//      launch: every workgroup of launch i+1 merges step i's totals into the state left by
-//      launch i (its pending add needs exactly those statistics) in its prologue, workgroup
-//      0 publishes the merged state into the other state slot, and the last workgroup to
-//      take a ticket re-zeroes the consumed totals slot.  The launch therefore ends with its
-//      env rows, with no grid-wide hand-off; tsrl_collect_rms_finalize merges the last
-//      step's totals into the caller's state before the closing tsrl_buffer_add.  With
-//      `totals` set (data parallel / exact obs_rms) the last arriver converts this step's
-//      integer totals into the f64 moments vector instead; the caller all-reduces it and runs
-//      tsrl_rms_merge2(nblk = 1).
+//      (synth.h), so the column moments are summed EXACTLY as integers by 64-bit atomics into
+//      a per-step totals slot -- exact sums are independent of the summation order, so no
+//      ordered fold is needed.  Bound: one row adds at most 2^46 to a column's sum of m^2, so
+//      the int64 sums are exact while the rows behind one slot (k, or world * k after the
+//      data-parallel all-reduce) stay <= 2^17; tsrl_collect_box_step checks k and the caller
+//      checks world * k.  The slot also counts its step rows ([4D + 1], one atomic per
+//      workgroup), so the merge never assumes equal env shards across ranks.
+//      Totals ring (three slots, `rms_step` = i, the launch's index in its chain): launch i
+//      accumulates slot i % 3, merges slot (i - 1) % 3 (the previous launch's totals) into the
+//      RunningMeanStd in its prologue -- every workgroup does the merge itself, since its
+//      pending add needs exactly those statistics -- and workgroup 0 zeroes slot (i + 1) % 3,
+//      the slot launch i + 1 will accumulate (last read by launch i - 1, finished before
+//      launch i started).  Workgroup 0 also publishes the merged state into state slot
+//      (i + 1) % 2 for launch i + 1.  The first launch of a chain (i = 0) reads the caller's
+//      state and relies on slots 0 and 1 being zero: a fresh (zeroed) workspace or the
+//      previous chain's tsrl_collect_rms_finalize, which merges the last launch's slot and
+//      clears all three.  The launch therefore ends with its env rows, with no grid-wide
+//      hand-off.  With `no_moments` set (exact obs_rms) the launch computes no moments at
+//      all: the caller runs tsrl_rms_exact_update on the raw step / reset rows between
+//      launches, and the pending add normalises with the caller's mean / var / snapshot.
 #include "add_row.h"
 #include "noise.h"
 #include "synth.h"
@@ -216,7 +223,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
     __shared__ float sb1[H], sb2[H], sb3[AMAX], ssig[AMAX], slo[AMAX], shi[AMAX];
     __shared__ float seps[R][AMAX + 1];
     __shared__ RowState rs[R], rr[R];
-    __shared__ int s_nd, s_last;
+    __shared__ int s_nd;
     __shared__ int64_t s_row[R];
     // deferred obs_rms merge: the statistics after the previous step's step rows (obs_next
     // normalisation) and after its reset rows (reset rows, state)
@@ -250,7 +257,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
     TSTAMP(0)
 
     // ---- deferred obs_rms merge of the previous step (see D) ----------------------------------
-    const bool defer = a.totals == nullptr;
+    const bool defer = !a.no_moments;
     const int step = a.rms_step;  // index of this launch in its chain of deferred steps
     const int par = step & 1;
     const int tcur = step % 3, tprev = (step + 2) % 3, tnext = (step + 1) % 3;
@@ -264,7 +271,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
     const int arw = t >> 5, aln = t & 31;
     const int nq = D >> 2;
     const int act_n = (int)(ad.act_row_bytes >> 2);
-    const bool fast = merge && ad.k > 0 && ad.obs_next_src && ad.obs_next_dst &&
+    const bool fast = merge && ad.k > 0 && !ad.ids && ad.obs_next_src && ad.obs_next_dst &&
                       ad.norm_mean && ad.reset_mean && ad.reset_src && ad.reset_mask &&
                       !ad.obs_src && !ad.obs_next_src_raw && ad.act_src && ad.act_dst &&
                       (ad.act_row_bytes & 3) == 0 && act_n <= 32 &&
@@ -294,12 +301,13 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
     TSTAMP2(0)
     float mm0 = 0.f, mv0 = 0.f;
     long long ms1 = 0, mq1 = 0, ms2 = 0, mq2 = 0;
-    double mcount = 0.0, mnd = 0.0;
+    double mcount = 0.0, mnd = 0.0, mk = 0.0;
     if (merge) {
         const RmsState* sin = ws.st[par];
         const long long* tp = ws.tot[tprev];
         mcount = sin->count;
         mnd = (double)tp[4 * D];
+        mk = (double)tp[4 * D + 1];
         if (t < D) {  // D <= KMAX = NT: one column per thread
             mm0 = sin->mean[t];
             mv0 = sin->var[t];
@@ -321,9 +329,9 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
     }
     TSTAMP2(2)
     if (merge) {
-        // the step rows behind the totals: k, or every rank's k when the totals were
-        // all-reduced (data parallel)
-        const double kp = (double)(a.rms_rows > 0 ? a.rms_rows : k);
+        // the step rows behind the totals (counted in the slot: k, or the sum of every
+        // rank's k when the slot was all-reduced)
+        const double kp = mk;
         if (t < D)
             merge_column((double)mm0, (double)mv0, mcount, kp, ms1, mq1, mnd, ms2, mq2,
                          sSnapM[t], sSnapV[t], sFinM[t], sFinV[t]);
@@ -339,7 +347,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
             if (t == 0) so->count = mcount + kp + mnd;
             // the slot the next launch accumulates: read by the launch before this one
             long long* tz = ws.tot[tnext];
-            for (int i = t; i <= 4 * D; i += NT) tz[i] = 0;
+            for (int i = t; i < 4 * D + 2; i += NT) tz[i] = 0;
         }
         if (ad.norm_mean) {
             ad.norm_mean = sSnapM;
@@ -595,7 +603,10 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
                 atomic_add_i64(tc + 3 * D + t, cq2);
             }
         }
-        if (t == 0 && nd > 0) atomic_add_i64(tc + 4 * D, nd);
+        if (t == 0) {
+            if (nd > 0) atomic_add_i64(tc + 4 * D, nd);
+            atomic_add_i64(tc + 4 * D + 1, nrows);
+        }
     };
 #ifndef COLLECT_NO_RAW
 #define COLLECT_NO_RAW 0  // diagnostic builds only: skip the raw env-row stores (wrong rows)
@@ -604,7 +615,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
 #define COLLECT_NO_TOTALS 0  // diagnostic builds only: skip the obs_rms atomics (wrong stats)
 #endif
 #if !COLLECT_ATOMIC_LATE && !COLLECT_NO_TOTALS
-    add_totals();
+    if (defer) add_totals();
 #endif
     TSTAMP(2)
 #if COLLECT_STOP == 1
@@ -714,42 +725,8 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
 #endif
     TSTAMP(3)
 #if COLLECT_ATOMIC_LATE
-    add_totals();
+    if (defer) add_totals();
 #endif
-    if (defer) return;
-
-#if COLLECT_STOP == 3
-    return;
-#endif
-    // ---- D (data parallel / exact obs_rms): the last arriver writes the f64 moments ----------
-    // Hand-off (cdna_hip_programming.md Guideline 16, counter form): every wave's atomics are
-    // performed (vmcnt 0) before the workgroup's one relaxed agent-scope ticket add; the last
-    // arriver reads the totals with agent-scope atomic loads.
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t == 0) {
-        const unsigned int prev = __hip_atomic_fetch_add(&ws.tickets[1], 1u, __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT);
-        s_last = prev == (unsigned int)(ws.nblk - 1);
-    }
-    __syncthreads();
-    if (!s_last) return;
-    for (int i = t; i <= 4 * D; i += NT) {
-        const long long v = __hip_atomic_load(tc + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int blk = i / D;  // 0, 2: sums (2^-23); 1, 3: sums of squares (2^-46); 4: count
-        double x = (double)v;
-        if (i < 4 * D) x *= (blk & 1) ? 0x1p-46 : 0x1p-23;
-        // payload layout of merge2: [2D) (s, q) per column of the step rows, [2D, 4D) reset
-        // rows, [4D] reset-row count, [4D + 1] step rows
-        const int d = i - blk * D;
-        if (i == 4 * D) a.totals[4 * D] = x;
-        else a.totals[(blk >> 1) * 2 * D + 2 * d + (blk & 1)] = x;
-        tc[i] = 0;
-    }
-    if (t == 0) {
-        a.totals[4 * D + 1] = (double)k;
-        __hip_atomic_store(&ws.tickets[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
 }
 
 // tsrl_collect_rms_finalize: the last deferred step's totals merged into the caller's state
@@ -762,7 +739,7 @@ __global__ __launch_bounds__(NT) void rms_finalize_kernel(tsrl_collect_args a, W
     const RmsState* sin = ws.st[(step + 1) & 1];  // the state the last launch published
     long long* tp = ws.tot[step % 3];
     const double old_count = sin->count, nd = (double)tp[4 * D];
-    const double kp = (double)(a.rms_rows > 0 ? a.rms_rows : a.k);
+    const double kp = (double)tp[4 * D + 1];
     for (int d = t; d < D; d += NT) {
         float sm, sv, fm, fv;
         merge_column((double)sin->mean[d], (double)sin->var[d], old_count, kp, tp[d],
@@ -774,7 +751,7 @@ __global__ __launch_bounds__(NT) void rms_finalize_kernel(tsrl_collect_args a, W
     }
     __syncthreads();  // every thread has read the totals
     for (int j = 0; j < 3; ++j)
-        for (int i = t; i <= 4 * D; i += NT) ws.tot[j][i] = 0;
+        for (int i = t; i < 4 * D + 2; i += NT) ws.tot[j][i] = 0;
     if (t == 0) *a.count = old_count + kp + nd;
 }
 
@@ -831,7 +808,7 @@ extern "C" int tsrl_collect_box_step(const tsrl_collect_args* a, void* stream) {
     TSRL_CHECK_ARG(a->cur && a->w1p && a->b1 && a->w2 && a->b2 && a->w3 && a->b3 && a->log_std &&
                        a->act && a->act_remap && a->ep_j && a->ep_t && a->raw && a->reset_raw &&
                        a->rew && a->term && a->trunc && a->done && a->workspace && a->mean &&
-                       a->var && a->count && (a->totals || (a->snap_mean && a->snap_var)),
+                       a->var && a->count && (a->no_moments || (a->snap_mean && a->snap_var)),
                    "tsrl_collect_box_step: null pointer");
     // w1p / workspace are this library's layouts; cur, w2 and w3 are read with 16-byte loads
     // at 4-byte alignment (parameters may be views into a flat parameter buffer)
@@ -861,7 +838,9 @@ extern "C" int tsrl_collect_box_step(const tsrl_collect_args* a, void* stream) {
         TSRL_CHECK_ARG(!ad.obs_src, "tsrl_collect_box_step: the pending add copies no obs (the "
                                     "launch that produced it stored them)");
     }
-    TSRL_CHECK_ARG(k <= (int64_t)1 << 24, "tsrl_collect_box_step: k <= 2^24 (exact int64 moments)");
+    // one row adds <= 2^46 to a column's int64 sum of m^2: exact for <= 2^17 rows per slot (the
+    // data-parallel caller also checks world * k)
+    TSRL_CHECK_ARG(k <= (int64_t)1 << 17, "tsrl_collect_box_step: k <= 2^17 (exact int64 moments)");
     const Ws ws = make_ws(a);
     tsrl_collect_args p = *a;
     p.act_seed = sm64(a->act_seed);

@@ -325,8 +325,19 @@ extern "C" int tsrl_rms_norm_rows(const float* x, const uint8_t* mask, int64_t k
 // one, so no pairwise summation): S = x0 + x1 + ...; mean = S / k; var = sum((x - mean)^2)
 // / k, every operation rounded to f32 (statistics.py:93-101).  The update then runs in f32
 // with the python-int counts converted to f32 (NEP 50), in the reference's operation order
-// (statistics.py:103-114).  One thread per column: two dependent f32 chains of k adds each
-// -- latency-bound by construction (the price of the reference's summation order).
+// (statistics.py:103-114).
+//
+// The two k-long dependent f32 add chains per column cannot be re-associated, so the kernel
+// is built around them: a workgroup owns XC = 8 columns and holds a whole span of up to 4096
+// rows of them in LDS ([column][row], 131 KB), loaded by all 8 waves with every load in
+// flight at once; lanes 0-7 of wave 0 then run the mean chains reading 4 rows per ds_read_b128
+// (32 rows of reads in flight ahead of the adds); the other waves replace the span by
+// (x - mean)^2 in place (the var chain's independent sub / mul, off the chain wave); wave 0
+// runs the var chains.  Per row and pass the chain wave issues 1.25 instructions, so a
+// 4096-row update is ~2 x 4096 x 5 cycles of chain plus one load latency.  Round 3's kernel
+// (64 columns per workgroup, 128-row blocks staged one ahead with two barriers per block) paid
+// a global-load latency per block: ~290 us per 4096 x 376 step vs ~20 here.  Spans past 4096
+// rows (k > 4096: data-parallel global batches, large host collects) are streamed twice.
 // ---------------------------------------------------------------------------------------
 namespace tsrl {
 namespace {
@@ -337,28 +348,26 @@ struct ExactRows {
     int64_t k;
 };
 
-// Workgroup = 64 columns; 4 waves load blocks of EXB selected rows (64 columns each, 256 B
-// per row) into LDS while wave 0 runs the columns' ordered f32 chains over the previous
-// block, so the chains, not the memory latency, set the pace.  Selected rows are listed in
-// row order per span of EXSPAN rows (ballot prefix counts over the mask).
-constexpr int EXT = 256;    // threads
-constexpr int EXB = 128;    // rows per LDS block
-constexpr int EXSPAN = 4096;
+constexpr int XC = 8;        // columns per workgroup
+constexpr int XT = 512;      // threads (8 waves)
+constexpr int XSPAN = 4096;  // rows resident per span
+constexpr int XP = XSPAN + 4;  // LDS pitch of a column (floats): 4-bank skew between columns
 
 struct ExactSmem {
-    float blk[2][EXB][64];
-    int list[EXSPAN];
+    float col[XC][XP];
+    int list[XSPAN];
+    float bm[XC];
     int nsel;
-    int wcnt[EXT / 64];
+    int wcnt[XT / 64];
 };
 
 // Rows [s0, s0 + span) selected by the mask -> sm.list (row order), sm.nsel.
 __device__ void exact_list(const ExactRows& b, int64_t s0, int span, ExactSmem& sm) {
     const int t = threadIdx.x, w = t >> 6, l = t & 63;
     int base = 0;
-    for (int c0 = 0; c0 < span; c0 += EXT) {
+    for (int c0 = 0; c0 < span; c0 += XT) {
         const int r = c0 + t;
-        const bool sel = r < span && (!b.mask || b.mask[s0 + r]);
+        const bool sel = r < span && b.mask[s0 + r];
         const uint64_t bal = __ballot(sel);
         const int before = __popcll(bal & ((1ull << l) - 1));
         if (l == 0) sm.wcnt[w] = __popcll(bal);
@@ -367,7 +376,7 @@ __device__ void exact_list(const ExactRows& b, int64_t s0, int span, ExactSmem& 
         for (int u = 0; u < w; ++u) off += sm.wcnt[u];
         if (sel) sm.list[off + before] = r;
         int tot = 0;
-        for (int u = 0; u < EXT / 64; ++u) tot += sm.wcnt[u];
+        for (int u = 0; u < XT / 64; ++u) tot += sm.wcnt[u];
         base += tot;
         __syncthreads();
     }
@@ -375,110 +384,168 @@ __device__ void exact_list(const ExactRows& b, int64_t s0, int span, ExactSmem& 
     __syncthreads();
 }
 
-// One ordered pass over the selected rows of b: acc = (((acc + f(x_r0)) + f(x_r1)) + ...) in
-// f32 for the workgroup's 64 columns, f(x) = x (MEAN) or (x - bm)^2 (VAR).  Returns the
-// number of rows taken; acc is valid in wave 0.
-template <bool VAR>
-__device__ int64_t exact_pass(const ExactRows& b, int64_t dim, int64_t c0, float bm, float& acc,
-                              ExactSmem& sm) {
-#pragma clang fp contract(off)
-    const int t = threadIdx.x;
-    const int64_t col = c0 + (t & 63);
-    int64_t total = 0;
-    for (int64_t s0 = 0; s0 < b.k; s0 += EXSPAN) {
-        const int span = (int)min((int64_t)EXSPAN, b.k - s0);
-        exact_list(b, s0, span, sm);
-        const int nsel = sm.nsel;
-        total += nsel;
-        // block q of the list: thread t loads rows (t >> 6) + 4j, j < EXB / 4, column t & 63
-        auto load = [&](int q, float (&v)[EXB / 4]) {
+// Load the n selected rows of span s0 (identity when unmasked) into sm.col[c][0, n) for the
+// workgroup's columns [c0, c0 + XC).  Wave w takes column half h = w & 1 and rows
+// (w >> 1) * 64 + lane + 256 j: 64 consecutive rows per store group (conflict-free LDS
+// stores), all of a thread's loads issued before its first store.
+__device__ void exact_load(const ExactRows& b, int64_t dim, int64_t c0, int64_t s0, int n,
+                           bool listed, bool vec4, ExactSmem& sm) {
+    const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    const int h = w & 1;
+    const int rb = (w >> 1) * 64 + l;
+    constexpr int J = XSPAN / 256;  // 16 rows per thread
+    if (vec4) {
+        float4 v[J];
 #pragma unroll
-            for (int j = 0; j < EXB / 4; ++j) {
-                const int e = q * EXB + (t >> 6) + 4 * j;
-                const int64_t r = s0 + (e < nsel ? sm.list[e] : 0);
-                v[j] = col < dim ? b.x[r * dim + col] : 0.0f;
+        for (int j = 0; j < J; ++j) {
+            const int e = rb + 256 * j;
+            v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (e < n) {
+                const int64_t r = s0 + (listed ? sm.list[e] : e);
+                v[j] = *reinterpret_cast<const float4*>(b.x + r * dim + c0 + 4 * h);
             }
-        };
-        auto store = [&](int buf, const float (&v)[EXB / 4]) {
-#pragma unroll
-            for (int j = 0; j < EXB / 4; ++j) sm.blk[buf][(t >> 6) + 4 * j][t & 63] = v[j];
-        };
-        const int nb = (nsel + EXB - 1) / EXB;
-        float v[EXB / 4];
-        if (nb > 0) {
-            load(0, v);
-            store(0, v);
         }
-        __syncthreads();
-        for (int q = 0; q < nb; ++q) {
-            if (q + 1 < nb) load(q + 1, v);
-            if (t < 64) {
-                const int n = min(EXB, nsel - q * EXB);
-                int e = 0;
-                // software pipeline: the next 16 rows' LDS reads are in flight while the
-                // current 16 are added in order
-                if (n >= 32) {
-                    float x[16], y[16];
 #pragma unroll
-                    for (int u = 0; u < 16; ++u) x[u] = sm.blk[q & 1][u][t];
-                    for (; e + 32 <= n; e += 16) {
-#pragma unroll
-                        for (int u = 0; u < 16; ++u) y[u] = sm.blk[q & 1][e + 16 + u][t];
-#pragma unroll
-                        for (int u = 0; u < 16; ++u) {
-                            if (VAR) {
-                                const float dv = x[u] - bm;
-                                const float sq = dv * dv;
-                                acc = acc + sq;
-                            } else {
-                                acc = acc + x[u];
-                            }
-                        }
-#pragma unroll
-                        for (int u = 0; u < 16; ++u) x[u] = y[u];
-                    }
-#pragma unroll
-                    for (int u = 0; u < 16; ++u) {
-                        if (VAR) {
-                            const float dv = x[u] - bm;
-                            const float sq = dv * dv;
-                            acc = acc + sq;
-                        } else {
-                            acc = acc + x[u];
-                        }
-                    }
-                    e += 16;
-                }
-                for (; e < n; ++e) {
-                    const float x = sm.blk[q & 1][e][t];
-                    if (VAR) {
-                        const float dv = x - bm;
-                        const float sq = dv * dv;
-                        acc = acc + sq;
-                    } else {
-                        acc = acc + x;
-                    }
-                }
+        for (int j = 0; j < J; ++j) {
+            const int e = rb + 256 * j;
+            if (e < n) {
+                sm.col[4 * h + 0][e] = v[j].x;
+                sm.col[4 * h + 1][e] = v[j].y;
+                sm.col[4 * h + 2][e] = v[j].z;
+                sm.col[4 * h + 3][e] = v[j].w;
             }
-            __syncthreads();
-            if (q + 1 < nb) store((q + 1) & 1, v);
-            __syncthreads();
+        }
+    } else {
+        // any dim / alignment: 4 scalar loads per row and half (columns past dim read 0)
+#pragma unroll 4
+        for (int j = 0; j < J; ++j) {
+            const int e = rb + 256 * j;
+            if (e >= n) break;
+            const int64_t r = s0 + (listed ? sm.list[e] : e);
+            float v[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int64_t c = c0 + 4 * h + q;
+                v[q] = c < dim ? b.x[r * dim + c] : 0.0f;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) sm.col[4 * h + q][e] = v[q];
         }
     }
-    return total;
+}
+
+// acc = (((acc + v0) + v1) + ... + v_{n-1}) in f32 over column lane's LDS run (wave 0 lanes
+// < XC): ds_read_b128 of 4 rows into two ping-pong register blocks of 32 rows, the reads of one
+// block issued before the 32 adds of the other (no register copies, one wait per block).
+__device__ __forceinline__ void exact_ld(const float* p, float4 (&v)[8]) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(p + 4 * u);
+}
+__device__ __forceinline__ float exact_add(float acc, const float4 (&v)[8]) {
+#pragma clang fp contract(off)
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        acc = acc + v[u].x;
+        acc = acc + v[u].y;
+        acc = acc + v[u].z;
+        acc = acc + v[u].w;
+    }
+    return acc;
+}
+__device__ __forceinline__ float exact_chain(const float* cp, int n, float acc) {
+#pragma clang fp contract(off)
+    int e = 0;
+    if (n >= 64) {
+        float4 A[8], B[8];
+        exact_ld(cp, A);
+        // the scheduling barriers pin each block's reads ahead of the other block's adds
+        // (without them the loop is rotated so that every block's reads are waited for
+        // right after their issue)
+        for (; e + 96 <= n; e += 64) {  // A holds rows [e, e + 32)
+            exact_ld(cp + e + 32, B);
+            __builtin_amdgcn_sched_barrier(0);
+            acc = exact_add(acc, A);
+            exact_ld(cp + e + 64, A);
+            __builtin_amdgcn_sched_barrier(0);
+            acc = exact_add(acc, B);
+        }
+        if (e + 64 <= n) {
+            exact_ld(cp + e + 32, B);
+            __builtin_amdgcn_sched_barrier(0);
+            acc = exact_add(acc, A);
+            acc = exact_add(acc, B);
+            e += 64;
+        } else {
+            acc = exact_add(acc, A);
+            e += 32;
+        }
+    }
+    for (; e < n; ++e) acc = acc + cp[e];
+    return acc;
 }
 
 __device__ void exact_update(const ExactRows& b, int64_t dim, int64_t c0, double cnt_old,
                              float& mean, float& var, double& cnt_new, ExactSmem& sm) {
 #pragma clang fp contract(off)
+    const int t = threadIdx.x;
+    const bool chain = t < XC;
+    const bool vec4 = (dim & 3) == 0 && (reinterpret_cast<uintptr_t>(b.x) & 15) == 0 &&
+                      c0 + XC <= dim;
+    const bool listed = b.mask != nullptr;
+    // pass 1: S = sequential sum of the selected rows, span by span
     float S = 0.0f;
-    const int64_t cnt = exact_pass<false>(b, dim, c0, 0.0f, S, sm);
+    int64_t cnt = 0;
+    int n = 0;
+    const int nspan = (int)((b.k + XSPAN - 1) / XSPAN);
+    for (int sp = 0; sp < nspan; ++sp) {
+        const int64_t s0 = (int64_t)sp * XSPAN;
+        const int span = (int)min((int64_t)XSPAN, b.k - s0);
+        if (listed) {
+            exact_list(b, s0, span, sm);
+            n = sm.nsel;
+        } else {
+            n = span;
+        }
+        exact_load(b, dim, c0, s0, n, listed, vec4, sm);
+        __syncthreads();
+        if (chain) S = exact_chain(&sm.col[t][0], n, S);
+        cnt += n;
+        if (sp + 1 < nspan) __syncthreads();  // the next span overwrites the columns
+    }
     cnt_new = cnt_old;
-    if (cnt == 0) return;  // the reference updates only with rows (Collector resets none)
+    if (cnt == 0) {
+        __syncthreads();
+        return;  // the reference updates only with rows (Collector resets none)
+    }
     const float kf = (float)cnt;
-    const float bm = S / kf;
+    if (chain) sm.bm[t] = S / kf;
+    __syncthreads();
+    // pass 2: Q = sequential sum of (x - bm)^2; the resident span (the last one loaded) is
+    // turned into its squares in place by every thread, earlier spans are reloaded first
     float Q = 0.0f;
-    exact_pass<true>(b, dim, c0, bm, Q, sm);
+    for (int sp = 0; sp < nspan; ++sp) {
+        const int64_t s0 = (int64_t)sp * XSPAN;
+        const int span = (int)min((int64_t)XSPAN, b.k - s0);
+        if (nspan > 1) {
+            if (listed) {
+                exact_list(b, s0, span, sm);
+                n = sm.nsel;
+            } else {
+                n = span;
+            }
+            exact_load(b, dim, c0, s0, n, listed, vec4, sm);
+            __syncthreads();
+        }
+        for (int i = t; i < XC * n; i += XT) {
+            const int c = i / n, e = i - c * n;
+            const float dv = sm.col[c][e] - sm.bm[c];
+            sm.col[c][e] = dv * dv;
+        }
+        __syncthreads();
+        if (chain) Q = exact_chain(&sm.col[t][0], n, Q);
+        __syncthreads();
+    }
+    const float bm = chain ? sm.bm[t] : 0.0f;
     const float bv = Q / kf;
     const double tot = cnt_old + (double)cnt;
     const float cf = (float)cnt_old, tf = (float)tot;
@@ -494,16 +561,17 @@ __device__ void exact_update(const ExactRows& b, int64_t dim, int64_t c0, double
 
 // First update with b1's rows, the state after it to snap_* (when given), then b2's rows
 // (when b2.x is given).  Every workgroup reads the old count first; the last to finish
-// (agent-scope ticket, re-armed) publishes the new one.
-__global__ __launch_bounds__(EXT) void rms_exact_kernel(ExactRows b1, ExactRows b2, int64_t dim,
-                                                       float* mean, float* var, double* count,
-                                                       float* snap_mean, float* snap_var,
-                                                       unsigned int* ticket) {
+// (agent-scope ticket, re-armed) publishes the new one.  Workgroup b owns columns
+// [8 b, 8 b + 8).
+__global__ __launch_bounds__(XT) void rms_exact_kernel(ExactRows b1, ExactRows b2, int64_t dim,
+                                                      float* mean, float* var, double* count,
+                                                      float* snap_mean, float* snap_var,
+                                                      unsigned int* ticket) {
     __shared__ ExactSmem sm;
     const int t = threadIdx.x;
-    const int64_t c0 = (int64_t)blockIdx.x * 64;
+    const int64_t c0 = (int64_t)blockIdx.x * XC;
     const int64_t d = c0 + t;
-    const bool own = t < 64 && d < dim;
+    const bool own = t < XC && d < dim;
     const double cold = *count;
     float m = own ? mean[d] : 0.0f, v = own ? var[d] : 1.0f;
     double c1, c2;
@@ -513,7 +581,10 @@ __global__ __launch_bounds__(EXT) void rms_exact_kernel(ExactRows b1, ExactRows 
         snap_var[d] = v;
     }
     c2 = c1;
-    if (b2.x) exact_update(b2, dim, c0, c1, m, v, c2, sm);
+    if (b2.x) {
+        __syncthreads();
+        exact_update(b2, dim, c0, c1, m, v, c2, sm);
+    }
     if (own) {
         mean[d] = m;
         var[d] = v;
@@ -541,8 +612,8 @@ extern "C" int tsrl_rms_exact_update(const float* x, const uint8_t* mask, int64_
                    "tsrl_rms_exact_update: bad arguments");
     const ExactRows b1{x, mask, k};
     const ExactRows b2{x2, mask2, x2 ? k2 : 0};
-    const unsigned grid = (unsigned)((dim + 63) / 64);
-    hipLaunchKernelGGL(rms_exact_kernel, dim3(grid), dim3(EXT), 0, as_stream(stream), b1, b2,
+    const unsigned grid = (unsigned)((dim + XC - 1) / XC);
+    hipLaunchKernelGGL(rms_exact_kernel, dim3(grid), dim3(XT), 0, as_stream(stream), b1, b2,
                        dim, mean, var, count, snap_mean, snap_var, ticket);
     TSRL_LAUNCH_CHECK("tsrl_rms_exact_update");
     return 0;

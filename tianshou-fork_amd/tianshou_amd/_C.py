@@ -52,7 +52,7 @@ class CollectArgs(ctypes.Structure):
         ("env_seed", _u64), ("ep_len", _i64), ("ep_j", _p), ("ep_t", _p),
         ("raw", _p), ("reset_raw", _p), ("rew", _p), ("term", _p), ("trunc", _p), ("done", _p),
         ("workspace", _p), ("mean", _p), ("var", _p), ("snap_mean", _p), ("snap_var", _p),
-        ("count", _p), ("totals", _p), ("rms_step", _i64), ("rms_rows", _i64),
+        ("count", _p), ("no_moments", _i64), ("rms_step", _i64),
     ]
 
 

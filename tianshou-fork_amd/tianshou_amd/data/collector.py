@@ -21,6 +21,7 @@ import torch
 from tianshou_amd import _C
 from tianshou_amd.data.batch import Batch
 from tianshou_amd.data.buffer import ReplayBuffer, VectorReplayBuffer
+from tianshou_amd.dist import LOG
 from tianshou_amd.env.synthetic import DeviceVectorEnv
 from tianshou_amd.env.wrappers import VectorEnvNormObs
 
@@ -271,6 +272,13 @@ class Collector:
         D = b.obs_numel
         if D % 4 or D > 512 or self._act_spec()[1] != torch.float32:
             return False
+        # the exact int64 obs_rms moments (csrc/collect.hip D): a row adds <= 2^46 to a
+        # column's sum of squares, so the rows summed into one totals slot -- every rank's
+        # after the data-parallel all-reduce -- must stay <= 2^17
+        rms = norm.obs_rms
+        world = rms.dp.world if (rms.dp is not None and rms.dp.active) else 1
+        if kk * world > 1 << 17:
+            return False
         buf = self.buffer
         buf._alloc_storage(b.obs_shape, b.obs_torch_dtype, *self._act_spec())
         m = buf._meta
@@ -312,20 +320,19 @@ class Collector:
         c.snap_mean, c.snap_var = _C.ptr(rms.snap_mean_t), _C.ptr(rms.snap_var_t)
         dp = rms.dp is not None and rms.dp.active
         if rms.exact:
-            # the launch writes this step's moments; the caller applies the exact f32 update
-            c.totals = _C.ptr(rms.payload())
+            # the launch computes no moments; the exact f32 update runs after it (below)
+            c.no_moments = 1
         c.rms_step = 0 if rms.exact else self._rms_step
-        if dp:
-            c.rms_rows = kk * rms.dp.world
         _C.check(_C.lib().tsrl_collect_box_step(c, _C.stream_ptr(b.device)),
                  "tsrl_collect_box_step")
         if dp and not rms.exact:
             # the step's exact integer moments summed over the ranks (one all-reduce per env
             # step, a graph node under RCCL); the next launch merges the GLOBAL batch, as the
             # reference's single VectorEnvNormObs over every env shard (venv_wrappers.py:93-99)
+            # (the slot carries its own step-row count, so unequal env shards merge right)
             off = int(_C.lib().tsrl_collect_totals_offset(self._rms_step))
-            n = 4 * b.obs_numel + 1
-            rms.dp.all_reduce_(ws[off:off + 8 * n].view(torch.int64))
+            n = 4 * b.obs_numel + 2
+            rms.dp.all_reduce_(ws[off:off + 8 * n].view(torch.int64), kind="obs_rms")
         # deferred merge: the next launch (or _flush's tsrl_collect_rms_finalize) merges this
         # step's obs_rms moments
         self._rms_chain = None if rms.exact else c
@@ -461,15 +468,17 @@ class Collector:
             if graph is None or graph[0] != key:
                 g = torch.cuda.CUDAGraph()
                 torch.cuda.synchronize()
+                LOG.capture_begin()
                 with torch.cuda.graph(g):
                     for i in range(G):
                         self._device_step(self._scratch["cur"], self.env_num, None, False,
                                           no_grad, dict(rel_dev=sc[i % 2, 0:1],
                                                         rel_next=sc[(i + 1) % 2, 0:1]))
                     self._flush()
-                self._graphs[G] = graph = (key, g)
+                self._graphs[G] = graph = (key, g, LOG.capture_end())
                 self._parity = 0
             graph[1].replay()
+            LOG.replayed(graph[2])
             for _ in range(G):
                 written.append(int(buf._ring.index[0]))
                 buf._ring.advance(None)

@@ -7,10 +7,52 @@ rank's local minibatch: advantage moments (sum, sum of squares), the loss partia
 the flattened gradients (one all-reduce per minibatch), the obs_rms batch moments per env
 step, and the ret_rms partials per update.
 """
-from typing import Iterable, Optional
+from collections import defaultdict
+from typing import Dict, Iterable, Optional
 
 import torch
 import torch.distributed as dist
+
+
+class CollectiveLog:
+    """What the data-parallel path exchanged, by kind ("obs_rms", "grad", "adv_moments",
+    "loss_sums", "ret_rms", "perm_check", "param_broadcast", ...): logical call counts --
+    a collective captured into a HIP graph counts once per REPLAY of that graph, not at
+    capture -- and the payload (elements, dtype, bytes) of the last call.  bench.py reports
+    it per iteration at N > 1 and times each kind at its payload (``probe_collectives``)."""
+
+    def __init__(self) -> None:
+        self.calls: Dict[str, int] = defaultdict(int)
+        self.payload: Dict[str, tuple] = {}
+        self._capture: Optional[Dict[str, int]] = None
+
+    def note(self, kind: str, t: torch.Tensor, op: str) -> None:
+        self.payload[kind] = (op, t.numel(), str(t.dtype).replace("torch.", ""),
+                              t.numel() * t.element_size())
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            if self._capture is None:
+                self._capture = defaultdict(int)
+            self._capture[kind] += 1
+        else:
+            self.calls[kind] += 1
+
+    def capture_begin(self) -> None:
+        self._capture = defaultdict(int)
+
+    def capture_end(self) -> Dict[str, int]:
+        """The collectives recorded since capture_begin (the graph's tally)."""
+        tally, self._capture = dict(self._capture or {}), None
+        return tally
+
+    def replayed(self, tally: Optional[Dict[str, int]]) -> None:
+        for k, v in (tally or {}).items():
+            self.calls[k] += v
+
+    def reset(self) -> None:
+        self.calls = defaultdict(int)
+
+
+LOG = CollectiveLog()
 
 
 class DataParallel:
@@ -35,15 +77,17 @@ class DataParallel:
         """Collectives of this group can be captured into a HIP graph (RCCL); gloo cannot."""
         return self.enabled and dist.get_backend(self.group) == "nccl"
 
-    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+    def all_reduce_(self, t: torch.Tensor, kind: str = "other") -> torch.Tensor:
         if self.active:
+            LOG.note(kind, t, "all_reduce")
             dist.all_reduce(t, group=self.group)
         return t
 
-    def all_gather_cat(self, t: torch.Tensor) -> torch.Tensor:
+    def all_gather_cat(self, t: torch.Tensor, kind: str = "other") -> torch.Tensor:
         """Concatenate equally-shaped tensors of every rank in rank order."""
         if not self.active:
             return t
+        LOG.note(kind, t, "all_gather")
         out = [torch.empty_like(t) for _ in range(self.world)]
         dist.all_gather(out, t.contiguous(), group=self.group)
         return torch.cat(out)
@@ -58,6 +102,7 @@ class DataParallel:
         if not ps:
             return
         flat = torch.cat([p.detach().reshape(-1) for p in ps])
+        LOG.note("param_broadcast", flat, "broadcast")
         dist.broadcast(flat, src=src, group=self.group)
         o = 0
         with torch.no_grad():
@@ -79,6 +124,7 @@ class DataParallel:
         if self._flat is None or self._flat.numel() != n or self._flat.device != grads[0].device:
             self._flat = torch.empty(n, dtype=grads[0].dtype, device=grads[0].device)
         torch.cat([g.reshape(-1) for g in grads], out=self._flat)
+        LOG.note("grad", self._flat, "all_reduce")
         dist.all_reduce(self._flat, group=self.group)
         if average:
             self._flat.div_(self.world)
@@ -97,3 +143,63 @@ def default_dp() -> DataParallel:
                             and dist.is_initialized()):
         _DEFAULT = DataParallel()
     return _DEFAULT
+
+
+def param_hash(params: Iterable[torch.Tensor]) -> torch.Tensor:
+    """An int64 device hash of the parameters' bit patterns (position-weighted, so a swap
+    or a one-bit change moves it): equal on every rank iff the replicas agree (bench.py
+    compares its all-reduced MAX and MIN)."""
+    h = None
+    for i, p in enumerate(params):
+        bits = p.detach().reshape(-1).contiguous().view(torch.int32).to(torch.int64)
+        w = torch.arange(bits.numel(), device=bits.device, dtype=torch.int64) * 2654435761 \
+            + (i + 1) * 97
+        v = ((bits & 0x7FFFFFFF) * (w % 2147483647 + 1)).remainder(2305843009213693951).sum()
+        h = v if h is None else (h * 31 + v).remainder(2305843009213693951)
+    return h
+
+
+def probe_collectives(dp: DataParallel, reps: int = 30) -> Dict[str, dict]:
+    """Mean HIP-event time of each logged collective kind at its logged payload: `reps`
+    collectives issued eagerly, and the same `reps` captured in one HIP graph and replayed
+    (how the collect steps and the small-minibatch learn epochs issue them)."""
+    out = {}
+    if not dp.active:
+        return out
+    dev = torch.device("cuda", torch.cuda.current_device())
+    for kind, (op, numel, dtype, nbytes) in sorted(LOG.payload.items()):
+        if op != "all_reduce":
+            out[kind] = dict(op=op, numel=numel, dtype=dtype, bytes=nbytes)
+            continue
+        t = torch.zeros(numel, dtype=getattr(torch, dtype), device=dev)
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for _ in range(3):
+            dist.all_reduce(t, group=dp.group)
+        dist.barrier(group=dp.group)
+        torch.cuda.synchronize()
+        s.record()
+        for _ in range(reps):
+            dist.all_reduce(t, group=dp.group)
+        e.record()
+        torch.cuda.synchronize()
+        eager_us = s.elapsed_time(e) * 1e3 / reps
+        graph_us = None
+        try:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(reps):
+                    dist.all_reduce(t, group=dp.group)
+            g.replay()
+            dist.barrier(group=dp.group)
+            torch.cuda.synchronize()
+            s.record()
+            g.replay()
+            e.record()
+            torch.cuda.synchronize()
+            graph_us = s.elapsed_time(e) * 1e3 / reps
+        except RuntimeError:
+            torch.cuda.synchronize()
+        out[kind] = dict(op=op, numel=numel, dtype=dtype, bytes=nbytes,
+                         eager_us=round(eager_us, 2),
+                         graph_us=None if graph_us is None else round(graph_us, 2))
+    return out

@@ -89,8 +89,24 @@ class FlatAdam:
                 p.data_ptr() == v.data_ptr() for p, v in zip(self.params, st["pviews"])):
             return False
         if not self._state_is_flat(optim):
+            if not self._uniform_steps(optim, self.params):
+                # a partial / mixed state dict: torch's Adam keeps one step count per
+                # parameter, the flat pass one for all -- hand the step back to torch
+                self._adam = None
+                return False
             self._rebind_state(optim)
         return True
+
+    @staticmethod
+    def _uniform_steps(optim, params) -> bool:
+        """Every parameter's Adam step count is the same (a parameter without state counts
+        0).  clip_adam applies one bias correction to all parameters, so only then is it the
+        update torch's Adam would make."""
+        ks = set()
+        for p in params:
+            s = optim.state.get(p, {})
+            ks.add(float(s["step"]) if "step" in s else 0.0)
+        return len(ks) <= 1
 
     def _state_is_flat(self, optim) -> bool:
         st = self._adam
@@ -135,7 +151,7 @@ class FlatAdam:
         parameters; then ``clip_adam`` replaces clip_grad_norm_ + optim.step()."""
         if self.adam_bound(optim):
             return True
-        if not self._plain_adam(optim, self.params):
+        if not self._plain_adam(optim, self.params) or not self._uniform_steps(optim, self.params):
             self._adam = None
             return False
         dev = self.params[0].device
@@ -163,7 +179,6 @@ class FlatAdam:
             mviews.append(optim.state[p]["exp_avg"])
             vviews.append(optim.state[p]["exp_avg_sq"])
             o += k
-        steps.fill_(float(steps.max()) if len(steps) else 0.0)
         self._adam = dict(optim=optim, p=flat_p, m=flat_m, v=flat_v, steps=steps, pviews=pviews,
                           mviews=mviews, vviews=vviews,
                           ticket=torch.zeros(1, dtype=torch.int32, device=dev),

@@ -222,7 +222,7 @@ class FusedActorCritic(FlatAdam):
         _C.check(lib.tsrl_adv_moments_seg(_C.ptr(adv), _C.ptr(idx), _C.ptr(bounds), nseg,
                                           max_seg, _C.ptr(pa), _C.ptr(out),
                                           _C.stream_ptr(adv.device)), "tsrl_adv_moments_seg")
-        dp.all_reduce_(out)
+        dp.all_reduce_(out, kind="adv_moments")
         return out
 
     # -- one minibatch --------------------------------------------------------------------------
@@ -257,7 +257,7 @@ class FusedActorCritic(FlatAdam):
             adv_sums = self._buf("adv_sums", 2, torch.float64)[:2]
             _C.check(lib.tsrl_reduce_partials(_C.ptr(pa), nblk, 2, _C.ptr(adv_sums), s),
                      "tsrl_reduce_partials")
-            dp.all_reduce_(adv_sums)
+            dp.all_reduce_(adv_sums, kind="adv_moments")
         h1 = self._buf("h1", int(lib.tsrl_mlp_frag_floats(b)))
         self._l1_fwd(_C.ptr(obs), ldx, ip, b, _C.ptr(h1), 1, split=split_w)
         dz1 = self._buf("dz1", b * 2 * 64)
@@ -292,7 +292,7 @@ class FusedActorCritic(FlatAdam):
             P, k = self._flat.numel(), sums.numel()
             bucket = self._bucket[:P + k]
             bucket[P:].copy_(sums)
-            dp.all_reduce_(bucket)
+            dp.all_reduce_(bucket, kind="grad")
             sums.copy_(bucket[P:])
         terms = torch.empty(4, dtype=torch.float32, device=dev)
         _C.check(lib.tsrl_ppo_gauss_finalize(

@@ -19,6 +19,7 @@ from torch import nn
 
 from tianshou_amd import _C
 from tianshou_amd.data.batch import Batch, gather_rows, split_indices
+from tianshou_amd.dist import LOG
 from tianshou_amd.policy.a2c import A2CPolicy
 from tianshou_amd.policy.flat_adam import FlatAdam
 from tianshou_amd.policy.fused_eval import FusedEvalMixin, cat_logp, cat_mode  # noqa: F401
@@ -63,7 +64,7 @@ class _GaussPPOLoss(torch.autograd.Function):
             adv_sums = torch.empty(2, dtype=torch.float64, device=dev)
             _C.check(L.tsrl_reduce_partials(_C.ptr(pa), nblk, 2, _C.ptr(adv_sums), s),
                      "tsrl_reduce_partials")
-            dp.all_reduce_(adv_sums)
+            dp.all_reduce_(adv_sums, kind="adv_moments")
         grad_mu = torch.empty_like(mu)
         grad_value = torch.empty_like(value)
         partials = torch.empty(nblk * (4 + A), dtype=torch.float64, device=dev)
@@ -75,7 +76,7 @@ class _GaussPPOLoss(torch.autograd.Function):
         sums = torch.empty(4 + A, dtype=torch.float64, device=dev)
         _C.check(L.tsrl_reduce_partials(_C.ptr(partials), nblk, 4 + A, _C.ptr(sums), s),
                  "tsrl_reduce_partials")
-        dp.all_reduce_(sums)
+        dp.all_reduce_(sums, kind="loss_sums")
         terms = torch.empty(4, dtype=torch.float32, device=dev)
         grad_ls = torch.empty(A, dtype=torch.float32, device=dev)
         _C.check(L.tsrl_ppo_gauss_finalize(_C.ptr(sums), A, _C.ptr(log_std), params,
@@ -116,7 +117,7 @@ class _CatPPOLoss(torch.autograd.Function):
             adv_sums = torch.empty(2, dtype=torch.float64, device=dev)
             _C.check(L.tsrl_reduce_partials(_C.ptr(pa), nblk, 2, _C.ptr(adv_sums), s),
                      "tsrl_reduce_partials")
-            dp.all_reduce_(adv_sums)
+            dp.all_reduce_(adv_sums, kind="adv_moments")
         grad_x = torch.empty_like(x)
         grad_value = torch.empty_like(value)
         partials = torch.empty(nblk * 4, dtype=torch.float64, device=dev)
@@ -127,7 +128,7 @@ class _CatPPOLoss(torch.autograd.Function):
         sums = torch.empty(4, dtype=torch.float64, device=dev)
         _C.check(L.tsrl_reduce_partials(_C.ptr(partials), nblk, 4, _C.ptr(sums), s),
                  "tsrl_reduce_partials")
-        dp.all_reduce_(sums)
+        dp.all_reduce_(sums, kind="loss_sums")
         terms = torch.empty(4, dtype=torch.float32, device=dev)
         _C.check(L.tsrl_ppo_cat_finalize(_C.ptr(sums), params, _C.ptr(terms), s),
                  "tsrl_ppo_cat_finalize")
@@ -381,7 +382,8 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
                 h = zlib.crc32(np.ascontiguousarray(st[1]).tobytes() +
                                int(st[2]).to_bytes(4, "little"))
                 hs = self.dp.all_gather_cat(torch.tensor([h, n], dtype=torch.int64,
-                                                         device=dev)).view(W, 2)
+                                                         device=dev),
+                                                kind="perm_check").view(W, 2)
                 if not bool((hs == hs[0]).all()):
                     raise RuntimeError(
                         "dp_permutation='global' needs the same global np.random state and "
@@ -514,6 +516,7 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
             self._mlp.bind_grads()
             torch.cuda.synchronize()
             graph = torch.cuda.CUDAGraph()
+            LOG.capture_begin()
             try:
                 with torch.cuda.graph(graph):
                     mom = None
@@ -537,7 +540,7 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
                 torch.cuda.synchronize()
                 return None
             st = dict(key=key, graph=graph, static=static, perm=sperm, terms=sterms,
-                      bounds=sbounds)
+                      bounds=sbounds, tally=LOG.capture_end())
             self._learn_graph = st
             first = False  # static arrays already hold this update's data
         if first:
@@ -545,6 +548,7 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
                 d.copy_(a)
         st["perm"].copy_(perm)
         st["graph"].replay()
+        LOG.replayed(st["tally"])
         return st["terms"].clone()
 
     def _learn_cat(self, batch: Batch, batch_size: int, repeat: int
@@ -617,7 +621,7 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
         if fa is not None:
             fa.zero_grad()  # autograd accumulates into the flat bucket in place
             loss.backward()
-            self.dp.all_reduce_(fa.flat_grad)
+            self.dp.all_reduce_(fa.flat_grad, kind="grad")
             fa.clip_adam(self._grad_norm, scale_grads=last)
             return t
         self.optim.zero_grad()
@@ -646,6 +650,7 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
             sterms = torch.empty(len(chunks), 4, dtype=torch.float32, device=dev)
             torch.cuda.synchronize()
             graph = torch.cuda.CUDAGraph()
+            LOG.capture_begin()
             try:
                 with torch.cuda.graph(graph):
                     for i, (s, e, b_glob) in enumerate(chunks):
@@ -659,13 +664,14 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
                 torch.cuda.synchronize()
                 return None
             st = self._learn_graph = dict(key=key, graph=graph, static=static, perm=sperm,
-                                          terms=sterms)
+                                          terms=sterms, tally=LOG.capture_end())
             first = False
         if first:
             for d, a in zip(st["static"], arrays):
                 d.copy_(a)
         st["perm"].copy_(perm)
         st["graph"].replay()
+        LOG.replayed(st["tally"])
         return st["terms"].clone()
 
     def _learn_generic(self, batch: Batch, batch_size: int, repeat: int
@@ -686,7 +692,7 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
                         a64 = adv.detach().double()
                         m = torch.stack([a64.new_tensor(float(a64.numel())), a64.sum(),
                                          (a64 * a64).sum()])
-                        self.dp.all_reduce_(m)
+                        self.dp.all_reduce_(m, kind="adv_moments")
                         cnt, s1, s2 = m[0], m[1], m[2]
                         mean = (s1 / cnt).to(adv.dtype)
                         std = ((s2 - s1 * s1 / cnt) / (cnt - 1)).clamp_(min=0).sqrt_() \
@@ -724,7 +730,7 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
                 terms4 = torch.stack([loss.detach(), clip_loss.detach(), vf_loss.detach(),
                                       ent_loss.detach()]).float()
                 if self.dp.active:  # equal per-rank shares: global mean = mean over ranks
-                    self.dp.all_reduce_(terms4)
+                    self.dp.all_reduce_(terms4, kind="loss_sums")
                     terms4 /= self.dp.world
                 losses.append(terms4[0])
                 clip_losses.append(terms4[1])

@@ -133,7 +133,7 @@ class DeviceRunningMeanStd:
                 buf[2 * self.dim] = mask[:k].sum()
             else:
                 buf[2 * self.dim] = float(k)
-            self.dp.all_reduce_(buf)
+            self.dp.all_reduce_(buf, kind="obs_rms")
             partials, nblk, mask = buf[:2 * self.dim].reshape(1, self.dim, 2), 1, None
             batch_count = buf[2 * self.dim:]
             k = max(k, 1)
@@ -163,7 +163,7 @@ class DeviceRunningMeanStd:
             _C.check(L.tsrl_rms_sum_partials2(_C.ptr(partials_step), _C.ptr(partials_reset),
                                               _C.ptr(blk_done), nblk, D, k, _C.ptr(pl), st),
                      "tsrl_rms_sum_partials2")
-            self.dp.all_reduce_(pl)
+            self.dp.all_reduce_(pl, kind="obs_rms")
             partials_step, partials_reset, blk_done = pl[:2 * D], pl[2 * D:4 * D], pl[4 * D:]
             k_dev, nblk = pl[4 * D + 1:], 1
         _C.check(L.tsrl_rms_merge2(
@@ -189,7 +189,7 @@ class DeviceRunningMeanStd:
         collect step) over the data-parallel ranks, then apply both updates (merge2)."""
         self.ensure_snapshot()
         pl, D = self.payload(), self.dim
-        self.dp.all_reduce_(pl)
+        self.dp.all_reduce_(pl, kind="obs_rms")
         _C.check(_C.lib().tsrl_rms_merge2(
             _C.ptr(pl[:2 * D]), _C.ptr(pl[2 * D:4 * D]), _C.ptr(pl[4 * D:]), 1, D, k,
             _C.ptr(self.mean_t), _C.ptr(self.var_t), _C.ptr(self.count_t),

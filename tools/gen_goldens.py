@@ -414,7 +414,7 @@ def gen_ppo_discrete():
 class SynthGymEnv(gym.Env):
     """One env of oracle.synth_env, exposed through the reference's gym surface."""
 
-    def __init__(self, e, obs_dim, act_dim, ep_len, seed=0):
+    def __init__(self, e, obs_dim, act_dim, ep_len, seed=0):  # seed: the env stream
         self.observation_space = gym.spaces.Box(-np.inf, np.inf, (obs_dim,), np.float32)
         self.action_space = gym.spaces.Box(-1.0, 1.0, (act_dim,), np.float32)
         self.e, self.obs_dim, self.ep_len, self.seed_ = e, obs_dim, ep_len, seed
@@ -540,6 +540,24 @@ def gen_collector_fused():
         out["c1_rms_mean"], out["c1_rms_var"], out["c1_rms_count"] = \
             np.asarray(rms.mean), np.asarray(rms.var), np.array(rms.count)
         out["c1_data_obs"] = np.asarray(c.data.obs)
+        # the update's first half on this rollout: sample(0) -> process_fn (critic V(s) and
+        # V(s'), GAE with rew_norm, ret_rms, logp_old; a2c.py:83-117, ppo.py:87-97).  Its
+        # policy forward samples actions (pg.py forward), so the torch RNG state is restored
+        # afterwards and the second collect below is the one recorded before this step.
+        rng = torch.get_rng_state()
+        batch, idx = buf.sample(0)
+        out["c1_indices"] = idx
+        batch = policy.process_fn(batch, buf, idx)
+        torch.set_rng_state(rng)
+        for k in ("v_s", "returns", "adv", "logp_old"):
+            out["pf_" + k] = batch[k].detach().numpy()
+        with torch.no_grad():
+            vn = [policy.critic(mb.obs_next).flatten()
+                  for mb in batch.split(policy._batch, shuffle=False, merge_last=True)]
+        out["pf_v_s_next"] = torch.cat(vn).numpy()
+        out["pf_ret_rms_mean"] = np.asarray(policy.ret_rms.mean)
+        out["pf_ret_rms_var"] = np.asarray(policy.ret_rms.var)
+        out["pf_ret_rms_count"] = np.asarray(policy.ret_rms.count)
         c.reset_buffer(keep_statistics=True)
         res2 = c.collect(n_step=E * T // 2)
         out.update(_stats_arrays("c2_", res2))
@@ -548,6 +566,99 @@ def gen_collector_fused():
         out["c2_rms_mean"], out["c2_rms_var"], out["c2_rms_count"] = \
             np.asarray(rms.mean), np.asarray(rms.var), np.array(rms.count)
         _save(f"collector_{tag}.npz", **out)
+
+
+# --------------------------------------------------------------------------------------
+# 7c. The reference OnpolicyTrainer driving Collector / VectorReplayBuffer / PPOPolicy on the
+#     synthetic env (trainer/base.py:396-439 train_step, 487-507 _update_on_entire_buffer,
+#     552-563 OnpolicyTrainer.policy_update_fn, 242-286 reset + test_episode, 306-359 the
+#     epoch loop; trainer/utils.py:11-33 test_episode, 36-95 gather_info).  Records every
+#     collect result of the train and test collectors (the synthetic env's rewards and
+#     episode boundaries do not depend on the actions, so they are comparable across action
+#     streams), the epoch statistics and gather_info's counters.
+# --------------------------------------------------------------------------------------
+def gen_trainer():
+    from tianshou.trainer import OnpolicyTrainer
+    E, ET, D, A, L = 8, 4, 8, 3, 7
+    cfg = dict(E=E, ET=ET, D=D, A=A, L=L, step_per_collect=E * 16, step_per_epoch=E * 32,
+               max_epoch=2, repeat=2, batch_size=64, episode_per_test=6)
+    log = {"train": [], "test": []}
+
+    class RecCollector(Collector):
+        tag = None
+
+        def collect(self, *a, **kw):
+            res = super().collect(*a, **kw)
+            log[self.tag].append(dict(
+                kw={k: v for k, v in kw.items() if k in ("n_step", "n_episode")},
+                n_ep=int(res["n/ep"]), n_st=int(res["n/st"]),
+                rews=np.asarray(res["rews"], np.float64).tolist(),
+                lens=np.asarray(res["lens"]).astype(int).tolist(),
+                idxs=np.asarray(res["idxs"]).astype(int).tolist(),
+                rew=float(res["rew"]), rew_std=float(res["rew_std"]),
+                len=float(res["len"]), len_std=float(res["len_std"]),
+                collect_step=self.collect_step, collect_episode=self.collect_episode))
+            return res
+
+    train_envs = VectorEnvNormObs(DummyVectorEnv(
+        [lambda e=e: SynthGymEnv(e, D, A, L) for e in range(E)]))
+    test_envs = VectorEnvNormObs(DummyVectorEnv(
+        [lambda e=e: SynthGymEnv(e, D, A, L, seed=9) for e in range(ET)]),
+        update_obs_rms=False)
+    test_envs.set_obs_rms(train_envs.get_obs_rms())
+    policy = _make_policy(D, A, seed=6, reward_normalization=True, ent_coef=0.0)
+    torch.manual_seed(2)
+    np.random.seed(2)
+    tc = RecCollector(policy, train_envs, VectorReplayBuffer(E * 16, E))
+    tc.tag = "train"
+    vc = RecCollector(policy, test_envs)
+    vc.tag = "test"
+    losses = []
+    orig_update = policy.update
+
+    def update(*a, **kw):
+        out = orig_update(*a, **kw)
+        losses.append({k: [type(x).__name__ for x in v] if isinstance(v, list)
+                       else type(v).__name__ for k, v in out.items()})
+        log.setdefault("update_kw", []).append(
+            {k: (v if isinstance(v, (int, float)) else type(v).__name__)
+             for k, v in kw.items()})
+        return out
+
+    policy.update = update
+    trainer = OnpolicyTrainer(policy, train_collector=tc, test_collector=vc,
+                              max_epoch=cfg["max_epoch"],
+                              step_per_epoch=cfg["step_per_epoch"],
+                              repeat_per_collect=cfg["repeat"],
+                              episode_per_test=cfg["episode_per_test"],
+                              batch_size=cfg["batch_size"],
+                              step_per_collect=cfg["step_per_collect"],
+                              show_progress=False, verbose=False)
+    epochs = []
+    for epoch, stat, info in trainer:
+        epochs.append(dict(epoch=epoch, env_step=int(stat["env_step"]),
+                           gradient_step=int(stat["gradient_step"]),
+                           n_ep=int(stat["n/ep"]), n_st=int(stat["n/st"]),
+                           rew=float(stat["rew"]), len=int(stat["len"]),
+                           test_reward=float(stat["test_reward"]),
+                           best_reward=float(stat["best_reward"]),
+                           best_epoch=int(stat["best_epoch"]),
+                           loss_keys=sorted(k for k in stat if k.startswith("loss")),
+                           train_step=int(info["train_step"]),
+                           train_episode=int(info["train_episode"]),
+                           test_step=int(info["test_step"]),
+                           test_episode=int(info["test_episode"])))
+    out = dict(cfg=cfg, log=log, epochs=epochs, learn_types=losses,
+               final=dict(train_collect_step=tc.collect_step,
+                          train_collect_episode=tc.collect_episode,
+                          test_collect_step=vc.collect_step,
+                          test_collect_episode=vc.collect_episode,
+                          gradient_step=trainer.gradient_step, env_step=trainer.env_step,
+                          rms_count=float(train_envs.get_obs_rms().count)))
+    path = os.path.join(OUT, "trainer.json")
+    with open(path, "w") as f:
+        json.dump(out, f, indent=1)
+    print("wrote", path)
 
 
 # --------------------------------------------------------------------------------------
@@ -1036,12 +1147,12 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["returns", "gae", "buffer", "split", "rms", "ppo", "collector",
                              "collector_fused",
                              "stack", "ppo_discrete", "npg", "replay", "cartpole", "sched",
-                             "persist"]
+                             "persist", "trainer"]
     table = dict(returns=gen_returns_known, gae=gen_gae_random, buffer=gen_buffer_traces,
                  split=gen_split, rms=gen_rms, ppo=gen_ppo, collector=gen_collector,
                  collector_fused=gen_collector_fused,
                  stack=gen_stack, ppo_discrete=gen_ppo_discrete, npg=gen_npg, replay=gen_replay,
                  cartpole=gen_cartpole, sched=gen_sched,
-                 persist=gen_persist)
+                 persist=gen_persist, trainer=gen_trainer)
     for w in which:
         table[w]()
