@@ -64,6 +64,8 @@ def _run(dev, fused, E, D, A, L, T, graph_steps, collects=2, bound="clip", det=F
     (100, 376, 17, 7, 12, 4),      # partial 16-row tile, 7 workgroups
     (600, 376, 17, 9, 10, 0),      # 3 groups (last partial), eager steps only
     (4096, 376, 17, 30, 20, 16),   # the headline shape: 256 workgroups, 16 groups
+    (512, 17, 6, 25, 24, 8),       # config 2's width (D % 4 != 0: scalar row paths)
+    (77, 5, 2, 6, 14, 4),          # D = 5, partial tile
 ])
 def test_fused_step_matches_four_launch_step(dev, E, D, A, L, T, G):
     a, ra = _run(dev, True, E, D, A, L, T, G)
@@ -102,3 +104,33 @@ def test_fused_step_rejects_mismatched_pending_add(dev):
     c.add.k = 8
     rc = _C.lib().tsrl_collect_box_step(c, _C.stream_ptr(dev))
     assert rc != 0
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_collect_longer_than_ring_keeps_every_episode(dev, fused):
+    """An n_step collect of more steps than the buffer holds per env (the ring laps rows this
+    collect wrote): the returned episode statistics are still every finished episode's, in
+    (step, env) order -- the same rews / lens as a collect into a buffer that never wraps
+    (collector.py:330-342 reads ep_rew / ep_len from buffer.add at every step)."""
+    from tianshou_amd.data import Collector, VectorReplayBuffer
+    from tianshou_amd.env import Box, SyntheticVectorEnv, VectorEnvNormObs
+    from tianshou_amd.policy import PPOPolicy
+    from tianshou_amd.utils.models import fixed_std_normal, get_actor_critic, init_and_get_optim
+    E, D, A, L, T = 16, 8, 3, 3, 37
+    out = []
+    for per_env in (4, T):
+        torch.manual_seed(0)
+        actor, critic = get_actor_critic((D,), (64, 64), (A,), dev)
+        optim = init_and_get_optim(actor.to(dev), critic.to(dev), 3e-4)
+        pol = PPOPolicy(actor, critic, optim, fixed_std_normal,
+                        action_space=Box(-1.0, 1.0, (A,))).to(dev)
+        env = VectorEnvNormObs(SyntheticVectorEnv(E, (D,), A, ep_len=L, seed=2, device=dev))
+        c = Collector(pol, env, VectorReplayBuffer(E * per_env, E, device=dev))
+        c.use_fused_step = fused
+        c.graph_steps = 4
+        res = c.collect(n_step=E * T)
+        out.append(res)
+    a, b = out
+    assert a["n/st"] == b["n/st"] == E * T
+    assert a["n/ep"] == b["n/ep"] > 0
+    assert np.array_equal(a["rews"], b["rews"]) and np.array_equal(a["lens"], b["lens"])

@@ -271,7 +271,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
     const int arw = t >> 5, aln = t & 31;
     const int nq = D >> 2;
     const int act_n = (int)(ad.act_row_bytes >> 2);
-    const bool fast = merge && ad.k > 0 && !ad.ids && ad.obs_next_src && ad.obs_next_dst &&
+    const bool fast = merge && ad.k > 0 && !ad.ids && (D & 3) == 0 && ad.obs_next_src && ad.obs_next_dst &&
                       ad.norm_mean && ad.reset_mean && ad.reset_src && ad.reset_mask &&
                       !ad.obs_src && !ad.obs_next_src_raw && ad.act_src && ad.act_dst &&
                       (ad.act_row_bytes & 3) == 0 && act_n <= 32 &&
@@ -445,7 +445,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         }
         if (a.add.rel_next && blockIdx.x == 0 && t == 0)
             *a.add.rel_next = (urel + 1) % a.add.ring_size;
-    } else {
+    } else if ((D & 3) == 0) {
         for (int i = t; i < nrows * nq; i += NT) {
             const int rw = i / nq, q = i - rw * nq;
             const float4 x = reinterpret_cast<const float4*>(a.cur + (r0 + rw) * D)[q];
@@ -453,6 +453,12 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
             sX[(4 * q + 1) * XP + rw] = x.y;
             sX[(4 * q + 2) * XP + rw] = x.z;
             sX[(4 * q + 3) * XP + rw] = x.w;
+        }
+    } else {
+        // rows of D % 4 != 0 columns (e.g. config 2's D = 17): not 16-byte aligned
+        for (int i = t; i < nrows * D; i += NT) {
+            const int rw = i / D, c = i - rw * D;
+            sX[c * XP + rw] = a.cur[(r0 + rw) * D + c];
         }
     }
     TSTAMP(1)
@@ -798,8 +804,8 @@ extern "C" int64_t tsrl_collect_workspace_bytes(int64_t k, int64_t dim) {
 extern "C" int tsrl_collect_box_step(const tsrl_collect_args* a, void* stream) {
     TSRL_CHECK_ARG(a != nullptr, "tsrl_collect_box_step: null args");
     const int64_t k = a->k, D = a->dim;
-    TSRL_CHECK_ARG(k > 0 && D > 0 && D % 4 == 0 && D <= KMAX,
-                   "tsrl_collect_box_step: need k > 0 and 0 < dim <= %d, dim %% 4 == 0", KMAX);
+    TSRL_CHECK_ARG(k > 0 && D > 0 && D <= KMAX,
+                   "tsrl_collect_box_step: need k > 0 and 0 < dim <= %d", KMAX);
     TSRL_CHECK_ARG(a->act_dim > 0 && a->act_dim <= AMAX && a->bound_method >= 0 &&
                        a->bound_method <= 2,
                    "tsrl_collect_box_step: 0 < act_dim <= %d, bound_method 0..2", AMAX);
@@ -810,8 +816,9 @@ extern "C" int tsrl_collect_box_step(const tsrl_collect_args* a, void* stream) {
                        a->rew && a->term && a->trunc && a->done && a->workspace && a->mean &&
                        a->var && a->count && (a->no_moments || (a->snap_mean && a->snap_var)),
                    "tsrl_collect_box_step: null pointer");
-    // w1p / workspace are this library's layouts; cur, w2 and w3 are read with 16-byte loads
-    // at 4-byte alignment (parameters may be views into a flat parameter buffer)
+    // w1p / workspace are this library's layouts; w2 and w3 (and cur when dim % 4 == 0) are
+    // read with 16-byte loads at 4-byte alignment (parameters may be views into a flat
+    // parameter buffer); rows of dim % 4 != 0 take the scalar paths (add_row's generic loop)
     TSRL_CHECK_ARG(aligned16(a->w1p) && aligned16(a->workspace) &&
                        ((reinterpret_cast<uintptr_t>(a->cur) | reinterpret_cast<uintptr_t>(a->w2) |
                          reinterpret_cast<uintptr_t>(a->w3)) & 3u) == 0,

@@ -117,6 +117,9 @@ __global__ __launch_bounds__(ANW * 64) void gauss_act_kernel(
     const float* xrow = obs + (live ? row : 0) * ldx;
     const float4* wp0 = reinterpret_cast<const float4*>(w1p) + l;
     const float4* wp1 = reinterpret_cast<const float4*>(w1p) + G * 64 + l;
+    // rows of D % 4 != 0 columns (or a pitch that is not a multiple of 4) are read as four
+    // scalars per group, each bounded by D
+    const bool vec = (D & 3) == 0 && (ldx & 3) == 0;
     // batches of 6 groups: all loads of a batch are in flight before its first MFMA
     constexpr int GB = 6;
     for (int64_t gb = g0; gb < g1; gb += GB) {
@@ -127,7 +130,14 @@ __global__ __launch_bounds__(ANW * 64) void gauss_act_kernel(
             const bool gin = g < g1;
             const int64_t k = h * S + 4 * (gin ? g : g0);
             const bool xin = gin && live && k < D;
-            xv[j] = *reinterpret_cast<const float4*>(xrow + (xin ? k : 0));
+            if (vec) {
+                xv[j] = *reinterpret_cast<const float4*>(xrow + (xin ? k : 0));
+            } else {
+                xv[j].x = xrow[xin ? k : 0];
+                xv[j].y = xin && k + 1 < D ? xrow[k + 1] : 0.0f;
+                xv[j].z = xin && k + 2 < D ? xrow[k + 2] : 0.0f;
+                xv[j].w = xin && k + 3 < D ? xrow[k + 3] : 0.0f;
+            }
             a0[j] = wp0[(gin ? g : g0) * 64];
             a1[j] = wp1[(gin ? g : g0) * 64];
             if (!xin) xv[j] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -283,15 +293,15 @@ extern "C" int tsrl_gauss_policy_act(const float* obs, int64_t ldx, int64_t n, i
                                      const float* log_std, int64_t act_dim, const float* eps,
                                      int bound_method, const float* low, const float* high,
                                      float* act, float* act_remap, void* stream) {
-    TSRL_CHECK_ARG(n >= 0 && D > 0 && D % 4 == 0 && ldx >= D && ldx % 4 == 0 && act_dim > 0 &&
-                       act_dim <= AMAX && bound_method >= 0 && bound_method <= 2,
-                   "tsrl_gauss_policy_act: bad sizes (D, ldx multiples of 4; 0 < act_dim <= %d)",
-                   AMAX);
+    TSRL_CHECK_ARG(n >= 0 && D > 0 && ldx >= D && act_dim > 0 && act_dim <= AMAX &&
+                       bound_method >= 0 && bound_method <= 2,
+                   "tsrl_gauss_policy_act: bad sizes (ldx >= D; 0 < act_dim <= %d)", AMAX);
     if (n == 0) return 0;
     TSRL_CHECK_ARG(obs && w1packed && b1 && w2 && b2 && w3 && b3 && log_std && act && act_remap,
                    "tsrl_gauss_policy_act: null pointer");
-    TSRL_CHECK_ARG(aligned16(obs) && aligned16(w1packed),
-                   "tsrl_gauss_policy_act: obs / packed weights must be 16-byte aligned");
+    TSRL_CHECK_ARG((aligned16(obs) || D % 4 || ldx % 4) && aligned16(w1packed),
+                   "tsrl_gauss_policy_act: obs (rows read as float4) / packed weights must be "
+                   "16-byte aligned");
     TSRL_CHECK_ARG((low == nullptr) == (high == nullptr), "tsrl_gauss_policy_act: low/high");
     ActParams p{(int)act_dim, bound_method, low != nullptr, eps != nullptr, 0ull};
     hipLaunchKernelGGL(gauss_act_kernel, dim3((unsigned)((n + 31) / 32)), dim3(ANW * 64), 0,
@@ -308,15 +318,16 @@ extern "C" int tsrl_gauss_policy_act_rng(const float* obs, int64_t ldx, int64_t 
                                          const int64_t* rng_ctr, int64_t* rng_next,
                                          int bound_method, const float* low, const float* high,
                                          float* act, float* act_remap, void* stream) {
-    TSRL_CHECK_ARG(n >= 0 && D > 0 && D % 4 == 0 && ldx >= D && ldx % 4 == 0 && act_dim > 0 &&
-                       act_dim <= AMAX && bound_method >= 0 && bound_method <= 2,
+    TSRL_CHECK_ARG(n >= 0 && D > 0 && ldx >= D && act_dim > 0 && act_dim <= AMAX &&
+                       bound_method >= 0 && bound_method <= 2,
                    "tsrl_gauss_policy_act_rng: bad sizes");
     if (n == 0) return 0;
     TSRL_CHECK_ARG(obs && w1packed && b1 && w2 && b2 && w3 && b3 && log_std && act && act_remap &&
                        rng_ctr && rng_next && rng_ctr != rng_next,
                    "tsrl_gauss_policy_act_rng: null pointer");
-    TSRL_CHECK_ARG(aligned16(obs) && aligned16(w1packed),
-                   "tsrl_gauss_policy_act_rng: obs / packed weights must be 16-byte aligned");
+    TSRL_CHECK_ARG((aligned16(obs) || D % 4 || ldx % 4) && aligned16(w1packed),
+                   "tsrl_gauss_policy_act_rng: obs (rows read as float4) / packed weights must "
+                   "be 16-byte aligned");
     TSRL_CHECK_ARG((low == nullptr) == (high == nullptr), "tsrl_gauss_policy_act_rng: low/high");
     ActParams p{(int)act_dim, bound_method, low != nullptr, 1, sm64(seed)};
     hipLaunchKernelGGL(gauss_act_kernel, dim3((unsigned)((n + 31) / 32)), dim3(ANW * 64), 0,

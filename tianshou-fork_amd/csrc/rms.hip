@@ -328,262 +328,50 @@ extern "C" int tsrl_rms_norm_rows(const float* x, const uint8_t* mask, int64_t k
 // (statistics.py:103-114).
 //
 // The two k-long dependent f32 add chains per column cannot be re-associated, so the kernel
-// is built around them: a workgroup owns XC = 8 columns and holds a whole span of up to 4096
-// rows of them in LDS ([column][row], 131 KB), loaded by all 8 waves with every load in
-// flight at once; lanes 0-7 of wave 0 then run the mean chains reading 4 rows per ds_read_b128
-// (32 rows of reads in flight ahead of the adds); the other waves replace the span by
+// is built around them (rms_exact.h): a workgroup owns 8 columns and holds a whole span of up
+// to 4096 rows of them in LDS ([column][row], 131 KB), loaded by all 8 waves with every load
+// in flight at once; lanes 0-7 of wave 0 run the mean chains reading 4 rows per ds_read_b128
+// (32 rows of reads in flight ahead of the adds); all waves then replace the span by
 // (x - mean)^2 in place (the var chain's independent sub / mul, off the chain wave); wave 0
-// runs the var chains.  Per row and pass the chain wave issues 1.25 instructions, so a
-// 4096-row update is ~2 x 4096 x 5 cycles of chain plus one load latency.  Round 3's kernel
-// (64 columns per workgroup, 128-row blocks staged one ahead with two barriers per block) paid
-// a global-load latency per block: ~290 us per 4096 x 376 step vs ~20 here.  Spans past 4096
-// rows (k > 4096: data-parallel global batches, large host collects) are streamed twice.
+// runs the var chains.  The reset rows' update (the second RunningMeanStd.update of a
+// Collector step: VectorEnvNormObs.reset of the finished envs, venv_wrappers.py:87-91) needs
+// only the state after the first for its merge, so its two chains run on wave 1 at the same
+// time as wave 0's (when its rows fit the 512-row side span).  Per row and pass the chain
+// wave issues 1.25 instructions, so a 4096-row update is ~2 x 4096 x 5 cycles of chain plus
+// one load latency.  Round 3's kernel (64 columns per workgroup, 128-row blocks staged one
+// ahead with two barriers per block) paid a global-load latency per block: ~290 us per
+// 4096 x 376 step.  Spans past 4096 rows (k > 4096: data-parallel global batches, large host
+// collects) are streamed twice.
 // ---------------------------------------------------------------------------------------
+#include "rms_exact.h"
+
 namespace tsrl {
 namespace {
 
-struct ExactRows {
-    const float* x;       // [k, dim]
-    const uint8_t* mask;  // rows taken (NULL: all), in row order
-    int64_t k;
-};
-
-constexpr int XC = 8;        // columns per workgroup
-constexpr int XT = 512;      // threads (8 waves)
-constexpr int XSPAN = 4096;  // rows resident per span
-constexpr int XP = XSPAN + 4;  // LDS pitch of a column (floats): 4-bank skew between columns
-
-struct ExactSmem {
-    float col[XC][XP];
-    int list[XSPAN];
-    float bm[XC];
-    int nsel;
-    int wcnt[XT / 64];
-};
-
-// Rows [s0, s0 + span) selected by the mask -> sm.list (row order), sm.nsel.
-__device__ void exact_list(const ExactRows& b, int64_t s0, int span, ExactSmem& sm) {
-    const int t = threadIdx.x, w = t >> 6, l = t & 63;
-    int base = 0;
-    for (int c0 = 0; c0 < span; c0 += XT) {
-        const int r = c0 + t;
-        const bool sel = r < span && b.mask[s0 + r];
-        const uint64_t bal = __ballot(sel);
-        const int before = __popcll(bal & ((1ull << l) - 1));
-        if (l == 0) sm.wcnt[w] = __popcll(bal);
-        __syncthreads();
-        int off = base;
-        for (int u = 0; u < w; ++u) off += sm.wcnt[u];
-        if (sel) sm.list[off + before] = r;
-        int tot = 0;
-        for (int u = 0; u < XT / 64; ++u) tot += sm.wcnt[u];
-        base += tot;
-        __syncthreads();
-    }
-    if (t == 0) sm.nsel = base;
-    __syncthreads();
-}
-
-// Load the n selected rows of span s0 (identity when unmasked) into sm.col[c][0, n) for the
-// workgroup's columns [c0, c0 + XC).  Wave w takes column half h = w & 1 and rows
-// (w >> 1) * 64 + lane + 256 j: 64 consecutive rows per store group (conflict-free LDS
-// stores), all of a thread's loads issued before its first store.
-__device__ void exact_load(const ExactRows& b, int64_t dim, int64_t c0, int64_t s0, int n,
-                           bool listed, bool vec4, ExactSmem& sm) {
-    const int t = threadIdx.x, w = t >> 6, l = t & 63;
-    const int h = w & 1;
-    const int rb = (w >> 1) * 64 + l;
-    constexpr int J = XSPAN / 256;  // 16 rows per thread
-    if (vec4) {
-        float4 v[J];
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-            const int e = rb + 256 * j;
-            v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (e < n) {
-                const int64_t r = s0 + (listed ? sm.list[e] : e);
-                v[j] = *reinterpret_cast<const float4*>(b.x + r * dim + c0 + 4 * h);
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < J; ++j) {
-            const int e = rb + 256 * j;
-            if (e < n) {
-                sm.col[4 * h + 0][e] = v[j].x;
-                sm.col[4 * h + 1][e] = v[j].y;
-                sm.col[4 * h + 2][e] = v[j].z;
-                sm.col[4 * h + 3][e] = v[j].w;
-            }
-        }
-    } else {
-        // any dim / alignment: 4 scalar loads per row and half (columns past dim read 0)
-#pragma unroll 4
-        for (int j = 0; j < J; ++j) {
-            const int e = rb + 256 * j;
-            if (e >= n) break;
-            const int64_t r = s0 + (listed ? sm.list[e] : e);
-            float v[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int64_t c = c0 + 4 * h + q;
-                v[q] = c < dim ? b.x[r * dim + c] : 0.0f;
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) sm.col[4 * h + q][e] = v[q];
-        }
-    }
-}
-
-// acc = (((acc + v0) + v1) + ... + v_{n-1}) in f32 over column lane's LDS run (wave 0 lanes
-// < XC): ds_read_b128 of 4 rows into two ping-pong register blocks of 32 rows, the reads of one
-// block issued before the 32 adds of the other (no register copies, one wait per block).
-__device__ __forceinline__ void exact_ld(const float* p, float4 (&v)[8]) {
-#pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(p + 4 * u);
-}
-__device__ __forceinline__ float exact_add(float acc, const float4 (&v)[8]) {
-#pragma clang fp contract(off)
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-        acc = acc + v[u].x;
-        acc = acc + v[u].y;
-        acc = acc + v[u].z;
-        acc = acc + v[u].w;
-    }
-    return acc;
-}
-__device__ __forceinline__ float exact_chain(const float* cp, int n, float acc) {
-#pragma clang fp contract(off)
-    int e = 0;
-    if (n >= 64) {
-        float4 A[8], B[8];
-        exact_ld(cp, A);
-        // the scheduling barriers pin each block's reads ahead of the other block's adds
-        // (without them the loop is rotated so that every block's reads are waited for
-        // right after their issue)
-        for (; e + 96 <= n; e += 64) {  // A holds rows [e, e + 32)
-            exact_ld(cp + e + 32, B);
-            __builtin_amdgcn_sched_barrier(0);
-            acc = exact_add(acc, A);
-            exact_ld(cp + e + 64, A);
-            __builtin_amdgcn_sched_barrier(0);
-            acc = exact_add(acc, B);
-        }
-        if (e + 64 <= n) {
-            exact_ld(cp + e + 32, B);
-            __builtin_amdgcn_sched_barrier(0);
-            acc = exact_add(acc, A);
-            acc = exact_add(acc, B);
-            e += 64;
-        } else {
-            acc = exact_add(acc, A);
-            e += 32;
-        }
-    }
-    for (; e < n; ++e) acc = acc + cp[e];
-    return acc;
-}
-
-__device__ void exact_update(const ExactRows& b, int64_t dim, int64_t c0, double cnt_old,
-                             float& mean, float& var, double& cnt_new, ExactSmem& sm) {
-#pragma clang fp contract(off)
-    const int t = threadIdx.x;
-    const bool chain = t < XC;
-    const bool vec4 = (dim & 3) == 0 && (reinterpret_cast<uintptr_t>(b.x) & 15) == 0 &&
-                      c0 + XC <= dim;
-    const bool listed = b.mask != nullptr;
-    // pass 1: S = sequential sum of the selected rows, span by span
-    float S = 0.0f;
-    int64_t cnt = 0;
-    int n = 0;
-    const int nspan = (int)((b.k + XSPAN - 1) / XSPAN);
-    for (int sp = 0; sp < nspan; ++sp) {
-        const int64_t s0 = (int64_t)sp * XSPAN;
-        const int span = (int)min((int64_t)XSPAN, b.k - s0);
-        if (listed) {
-            exact_list(b, s0, span, sm);
-            n = sm.nsel;
-        } else {
-            n = span;
-        }
-        exact_load(b, dim, c0, s0, n, listed, vec4, sm);
-        __syncthreads();
-        if (chain) S = exact_chain(&sm.col[t][0], n, S);
-        cnt += n;
-        if (sp + 1 < nspan) __syncthreads();  // the next span overwrites the columns
-    }
-    cnt_new = cnt_old;
-    if (cnt == 0) {
-        __syncthreads();
-        return;  // the reference updates only with rows (Collector resets none)
-    }
-    const float kf = (float)cnt;
-    if (chain) sm.bm[t] = S / kf;
-    __syncthreads();
-    // pass 2: Q = sequential sum of (x - bm)^2; the resident span (the last one loaded) is
-    // turned into its squares in place by every thread, earlier spans are reloaded first
-    float Q = 0.0f;
-    for (int sp = 0; sp < nspan; ++sp) {
-        const int64_t s0 = (int64_t)sp * XSPAN;
-        const int span = (int)min((int64_t)XSPAN, b.k - s0);
-        if (nspan > 1) {
-            if (listed) {
-                exact_list(b, s0, span, sm);
-                n = sm.nsel;
-            } else {
-                n = span;
-            }
-            exact_load(b, dim, c0, s0, n, listed, vec4, sm);
-            __syncthreads();
-        }
-        for (int i = t; i < XC * n; i += XT) {
-            const int c = i / n, e = i - c * n;
-            const float dv = sm.col[c][e] - sm.bm[c];
-            sm.col[c][e] = dv * dv;
-        }
-        __syncthreads();
-        if (chain) Q = exact_chain(&sm.col[t][0], n, Q);
-        __syncthreads();
-    }
-    const float bm = chain ? sm.bm[t] : 0.0f;
-    const float bv = Q / kf;
-    const double tot = cnt_old + (double)cnt;
-    const float cf = (float)cnt_old, tf = (float)tot;
-    const float delta = bm - mean;
-    const float new_mean = mean + (delta * kf) / tf;
-    const float m_a = var * cf;
-    const float m_b = bv * kf;
-    const float m_2 = (m_a + m_b) + (((delta * delta) * cf) * kf) / tf;
-    mean = new_mean;
-    var = m_2 / tf;
-    cnt_new = tot;
-}
+using exact::XC;
+using exact::XT;
+constexpr int XSPAN = 4096, XSPAN2 = 512;
 
 // First update with b1's rows, the state after it to snap_* (when given), then b2's rows
 // (when b2.x is given).  Every workgroup reads the old count first; the last to finish
 // (agent-scope ticket, re-armed) publishes the new one.  Workgroup b owns columns
 // [8 b, 8 b + 8).
-__global__ __launch_bounds__(XT) void rms_exact_kernel(ExactRows b1, ExactRows b2, int64_t dim,
-                                                      float* mean, float* var, double* count,
-                                                      float* snap_mean, float* snap_var,
-                                                      unsigned int* ticket) {
-    __shared__ ExactSmem sm;
+__global__ __launch_bounds__(XT) void rms_exact_kernel(exact::Rows b1, exact::Rows b2,
+                                                      int64_t dim, float* mean, float* var,
+                                                      double* count, float* snap_mean,
+                                                      float* snap_var, unsigned int* ticket) {
+    __shared__ exact::Smem<XSPAN, XSPAN2> sm;
     const int t = threadIdx.x;
     const int64_t c0 = (int64_t)blockIdx.x * XC;
     const int64_t d = c0 + t;
     const bool own = t < XC && d < dim;
     const double cold = *count;
     float m = own ? mean[d] : 0.0f, v = own ? var[d] : 1.0f;
-    double c1, c2;
-    exact_update(b1, dim, c0, cold, m, v, c1, sm);
+    float sm_ = 0.0f, sv_ = 0.0f;
+    double c2 = exact::two_updates<XSPAN, XSPAN2>(b1, b2, dim, c0, cold, m, v, sm_, sv_, sm);
     if (own && snap_mean) {
-        snap_mean[d] = m;
-        snap_var[d] = v;
-    }
-    c2 = c1;
-    if (b2.x) {
-        __syncthreads();
-        exact_update(b2, dim, c0, c1, m, v, c2, sm);
+        snap_mean[d] = sm_;
+        snap_var[d] = sv_;
     }
     if (own) {
         mean[d] = m;
@@ -610,11 +398,12 @@ extern "C" int tsrl_rms_exact_update(const float* x, const uint8_t* mask, int64_
     TSRL_CHECK_ARG(x && mean && var && count && ticket && dim > 0 && k >= 0 && k2 >= 0 &&
                        (snap_mean == nullptr) == (snap_var == nullptr),
                    "tsrl_rms_exact_update: bad arguments");
-    const ExactRows b1{x, mask, k};
-    const ExactRows b2{x2, mask2, x2 ? k2 : 0};
-    const unsigned grid = (unsigned)((dim + XC - 1) / XC);
-    hipLaunchKernelGGL(rms_exact_kernel, dim3(grid), dim3(XT), 0, as_stream(stream), b1, b2,
-                       dim, mean, var, count, snap_mean, snap_var, ticket);
+    const tsrl::exact::Rows b1{x, mask, k};
+    const tsrl::exact::Rows b2{x2, mask2, x2 ? k2 : 0};
+    const unsigned grid = (unsigned)((dim + tsrl::exact::XC - 1) / tsrl::exact::XC);
+    hipLaunchKernelGGL(tsrl::rms_exact_kernel, dim3(grid), dim3(tsrl::exact::XT), 0,
+                       as_stream(stream), b1, b2, dim, mean, var, count, snap_mean, snap_var,
+                       ticket);
     TSRL_LAUNCH_CHECK("tsrl_rms_exact_update");
     return 0;
 }

@@ -22,6 +22,7 @@ from tianshou_amd import _C
 from tianshou_amd.data.batch import Batch
 from tianshou_amd.data.buffer import ReplayBuffer, VectorReplayBuffer
 from tianshou_amd.dist import LOG
+from tianshou_amd.utils.capture import graph_capture
 from tianshou_amd.env.synthetic import DeviceVectorEnv
 from tianshou_amd.env.wrappers import VectorEnvNormObs
 
@@ -270,7 +271,7 @@ class Collector:
                 not norm.update_obs_rms:
             return False
         D = b.obs_numel
-        if D % 4 or D > 512 or self._act_spec()[1] != torch.float32:
+        if D > 512 or self._act_spec()[1] != torch.float32:
             return False
         # the exact int64 obs_rms moments (csrc/collect.hip D): a row adds <= 2^46 to a
         # column's sum of squares, so the rows summed into one totals slot -- every rank's
@@ -469,7 +470,7 @@ class Collector:
                 g = torch.cuda.CUDAGraph()
                 torch.cuda.synchronize()
                 LOG.capture_begin()
-                with torch.cuda.graph(g):
+                with graph_capture(g):
                     for i in range(G):
                         self._device_step(self._scratch["cur"], self.env_num, None, False,
                                           no_grad, dict(rel_dev=sc[i % 2, 0:1],
@@ -504,17 +505,25 @@ class Collector:
         cur = s["cur"] if kk == N else s["cur"][:kk]
         step_count = episode_count = 0
         written = []          # per step: uniform ring position (int) or the ptr array
-        ep_rows_host = []     # n_episode mode: finished rows in step order
+        ep_stats = []         # (rew, len, idx) arrays of finished episodes, in step order
         eager_steps = 0
+        S = buf._ring.size    # rows per sub-buffer: a collect of more steps wraps the ring
         while True:
+            if n_step is not None and len(written) >= S:
+                # the next step overwrites a row this collect wrote: read the finished
+                # episodes' statistics of the steps so far before the ring laps them
+                ep_stats.append(self._episode_stats(written))
+                written = []
             if (n_step is not None and self.graph_steps and not random and kk == N
                     and kk == buf.buffer_num and buf._ring.uniform_rel() is not None
                     and eager_steps > 0 and not self._noise_active()):
-                n_left = -(-(n_step - step_count) // N)
+                n_left = min(-(-(n_step - step_count) // N), S - len(written))
                 done_steps = self._replay_steps(no_grad, n_left, written)
                 step_count += done_steps * N
                 if step_count >= n_step:
                     break
+                if len(written) >= S:
+                    continue
             ids_np = None if ready is None else ready
             uni = buf._ring.uniform_rel() if ids_np is None and kk == buf.buffer_num else None
             if ids_np is None and kk != buf.buffer_num:
@@ -535,7 +544,11 @@ class Collector:
                 if done_np.any():
                     env_ind_local = np.flatnonzero(done_np)
                     episode_count += len(env_ind_local)
-                    ep_rows_host.append(np.asarray(ptr)[env_ind_local])
+                    # read now: a later step of this collect may overwrite these rows (the
+                    # trainer's test collector holds one row per env, trainer/utils.py:11-33)
+                    rows_t = torch.as_tensor(np.asarray(ptr)[env_ind_local], device=dev)
+                    ep_stats.append(tuple(buf._dev[k][rows_t].cpu().numpy() for k in
+                                          ("stat_rew", "stat_len", "stat_idx")))
                     surplus = kk - (n_episode - episode_count)
                     if surplus > 0:
                         mask = np.ones(kk, dtype=bool)
@@ -550,27 +563,34 @@ class Collector:
             elif step_count >= n_step:
                 break
         self._flush()
-        # one read-back of the episode statistics, in the reference's (step, env) order
-        d = buf._dev
-        if n_episode:
-            rows = np.concatenate(ep_rows_host) if ep_rows_host else np.zeros(0, np.int64)
-            rows_t = torch.as_tensor(rows, device=dev)
+        if not n_episode and written:
+            ep_stats.append(self._episode_stats(written))
+        # the episode statistics in the reference's (step, env) order
+        if ep_stats:
+            rews, lens, idxs = (np.concatenate([e[i] for e in ep_stats]) for i in range(3))
         else:
-            if all(isinstance(w, int) for w in written):
-                rel = torch.as_tensor(np.asarray(written, np.int64), device=dev)
-                rows_t = (rel[:, None] + d["offset"][None, :]).reshape(-1)
-            else:
-                rows_t = torch.as_tensor(np.concatenate(
-                    [np.asarray(w).reshape(-1) if not isinstance(w, int) else w + buf._offset
-                     for w in written]), device=dev)
-            rows_t = rows_t[buf._meta.done[rows_t]]
-        rews = d["stat_rew"][rows_t].cpu().numpy()
-        lens = d["stat_len"][rows_t].cpu().numpy()
-        idxs = d["stat_idx"][rows_t].cpu().numpy()
+            rews, lens, idxs = np.zeros(0), np.zeros(0, np.int64), np.zeros(0, np.int64)
         if not n_episode:
             episode_count = len(rews)
         self.data.obs = s["cur"]
         return step_count, episode_count, rews, lens, idxs
+
+    def _episode_stats(self, written):
+        """One read-back of the statistics of the episodes that finished in the steps of
+        ``written`` (uniform ring positions or ptr arrays, in step order; none of their rows
+        overwritten since): (rew, len, start index) in the reference's (step, env) order."""
+        self._flush()
+        buf = self.buffer
+        d, dev = buf._dev, buf.device
+        if all(isinstance(w, int) for w in written):
+            rel = torch.as_tensor(np.asarray(written, np.int64), device=dev)
+            rows_t = (rel[:, None] + d["offset"][None, :]).reshape(-1)
+        else:
+            rows_t = torch.as_tensor(np.concatenate(
+                [np.asarray(w).reshape(-1) if not isinstance(w, int) else w + buf._offset
+                 for w in written]), device=dev)
+        rows_t = rows_t[buf._meta.done[rows_t]]
+        return tuple(d[k][rows_t].cpu().numpy() for k in ("stat_rew", "stat_len", "stat_idx"))
 
     def _collect_generic(self, n_step, n_episode, random, render, no_grad, gym_reset_kwargs):
         """The reference loop (collector.py:250-361) for host envs; buffer still on device."""

@@ -186,7 +186,8 @@ def probe_collectives(dp: DataParallel, reps: int = 30) -> Dict[str, dict]:
         graph_us = None
         try:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            from tianshou_amd.utils.capture import graph_capture
+            with graph_capture(g):
                 for _ in range(reps):
                     dist.all_reduce(t, group=dp.group)
             g.replay()

@@ -25,7 +25,7 @@ def match_actor(actor) -> Optional[dict]:
         return None
     l1 = getattr(actor.preprocess, "model", None)
     D = getattr(getattr(l1, "model", [None])[0], "in_features", None) if l1 is not None else None
-    if not isinstance(D, int) or D % 4 != 0:
+    if not isinstance(D, int):
         return None
     tr = _trunk(actor.preprocess, D)
     mu = _seq(actor.mu)

@@ -20,6 +20,7 @@ from torch import nn
 from tianshou_amd import _C
 from tianshou_amd.data.batch import Batch, gather_rows, split_indices
 from tianshou_amd.dist import LOG
+from tianshou_amd.utils.capture import graph_capture
 from tianshou_amd.policy.a2c import A2CPolicy
 from tianshou_amd.policy.flat_adam import FlatAdam
 from tianshou_amd.policy.fused_eval import FusedEvalMixin, cat_logp, cat_mode  # noqa: F401
@@ -518,7 +519,7 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
             graph = torch.cuda.CUDAGraph()
             LOG.capture_begin()
             try:
-                with torch.cuda.graph(graph):
+                with graph_capture(graph):
                     mom = None
                     if self._norm_adv:
                         mom = self._mlp.epoch_adv_moments(static[2], sperm, sbounds, max_seg,
@@ -652,7 +653,7 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
             graph = torch.cuda.CUDAGraph()
             LOG.capture_begin()
             try:
-                with torch.cuda.graph(graph):
+                with graph_capture(graph):
                     for i, (s, e, b_glob) in enumerate(chunks):
                         t = self._cat_minibatch(fa, obs, sperm[s:e], b_glob, static,
                                                 last=(i == len(chunks) - 1))

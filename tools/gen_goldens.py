@@ -519,10 +519,11 @@ def gen_collector():
 
 def gen_collector_fused():
     """The same Collector + VectorEnvNormObs path at observation widths that take the build's
-    one-launch fused collect step (tsrl_collect_box_step needs D % 4 == 0): D = 8 and the
-    headline's D = 376, 16 envs x 24 steps, both done kinds (even envs terminate, odd ones
-    truncate), two n_step collects with reset_buffer(keep_statistics=True) between them."""
-    for D, A, L, tag in ((8, 3, 7, "d8"), (376, 17, 9, "d376")):
+    one-launch fused collect step: D = 8, config 2's D = 17 (rows not a multiple of 4 floats)
+    and the headline's D = 376, 16 envs x 24 steps, both done kinds (even envs terminate, odd
+    ones truncate), two n_step collects with reset_buffer(keep_statistics=True) between them,
+    and the process_fn of the first rollout."""
+    for D, A, L, tag in ((8, 3, 7, "d8"), (17, 6, 7, "d17"), (376, 17, 9, "d376")):
         E, T = 16, 24
         out = dict(E=np.array(E), D=np.array(D), A=np.array(A), L=np.array(L), T=np.array(T))
         venv = VectorEnvNormObs(DummyVectorEnv(
