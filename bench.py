@@ -75,6 +75,11 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=None,
                     help="T' of the bounded CPU-baseline sample (envs x T')")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--act-coef", type=float, default=0.0,
+                    help="diagnostic: the action-coupled synthetic env (obs = box + c * action, "
+                         "not 2^-23-quantised): the fused collect step's general path (env "
+                         "after the actor, f64 obs_rms moments); measures what the synthetic "
+                         "env's two shortcuts buy")
     ap.add_argument("--exact-obs-rms", action="store_true",
                     help="VectorEnvNormObs with the reference's f32 obs_rms arithmetic bit for "
                          "bit (sequential f32 column sums; opt-in, measures its cost)")
@@ -284,7 +289,8 @@ def main():
         coll, policy, buf = build_cartpole(args, dev, rank)
     else:
         env = VectorEnvNormObs(SyntheticVectorEnv(E, (D,), A, ep_len=args.ep_len, seed=rank,
-                                                  device=dev), exact_obs_rms=args.exact_obs_rms)
+                                                  device=dev, act_coef=args.act_coef),
+                               exact_obs_rms=args.exact_obs_rms)
         actor, critic = get_actor_critic((D,), (64, 64), (A,), dev)
         # to the device before the optimiser: fused + capturable Adam
         actor, critic = actor.to(dev), critic.to(dev)
@@ -416,7 +422,8 @@ def main():
                        "rccl_world_size": world if distributed else None,
                        "learn_graph": args.graph_learn,
                        "obs_rms": "exact f32 (reference arithmetic)" if args.exact_obs_rms
-                       else "f64 moments",
+                       else ("f64 moments (atomic), action-coupled env" if args.act_coef
+                             else "exact int64 moments (quantised synthetic obs), f64 merge"),
                        "learn_graph_capture_failed": bool(getattr(policy, "_graph_failed",
                                                                   False)),
                        "collect_s": phase["collect"] / args.steps,

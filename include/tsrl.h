@@ -93,6 +93,20 @@ int tsrl_synth_box_step_reset(int64_t k, int64_t dim, uint64_t seed, int64_t ep_
                               double* rew_out, uint8_t* term_out, uint8_t* trunc_out,
                               uint8_t* done_out, double* partials_step,
                               double* partials_reset, double* blk_done, void* stream);
+/* The action-coupled env (SyntheticVectorEnv(act_coef=c), synth.h coupled_val): the step rows
+ * read act[k, act_dim] (the remapped actions): obs = f32(box + f32(c * act[r][d mod act_dim]));
+ * reset rows are unchanged.  act NULL = the plain calls above. */
+int tsrl_synth_box_step_act(const int64_t* ids, int64_t k, int64_t dim, uint64_t seed,
+                            int64_t ep_len, int64_t* ep_j, int64_t* ep_t, float* obs_out,
+                            double* rew_out, uint8_t* term_out, uint8_t* trunc_out,
+                            double* col_partials, const float* act, int64_t act_dim,
+                            float act_coef, void* stream);
+int tsrl_synth_box_step_reset_act(int64_t k, int64_t dim, uint64_t seed, int64_t ep_len,
+                                  int64_t* ep_j, int64_t* ep_t, float* obs_out,
+                                  float* reset_out, double* rew_out, uint8_t* term_out,
+                                  uint8_t* trunc_out, uint8_t* done_out, double* partials_step,
+                                  double* partials_reset, double* blk_done, const float* act,
+                                  int64_t act_dim, float act_coef, void* stream);
 int tsrl_synth_box_reset(const int64_t* ids, const uint8_t* mask, int64_t k, int64_t dim,
                          uint64_t seed, int64_t ep_len, int64_t* ep_j, int64_t* ep_t,
                          float* obs_out, double* col_partials, void* stream);
@@ -273,6 +287,10 @@ typedef struct tsrl_collect_args {
     int64_t no_moments;      /* exact obs_rms: no moments (see above); 0: the deferred merge */
     int64_t rms_step;        /* index of this launch in its chain of deferred steps (0: the
                                 first after tsrl_collect_rms_finalize or a fresh workspace) */
+    float act_coef;          /* 0: the quantised synthetic env (action-independent; int64
+                                totals); c != 0: the action-coupled env (synth.h coupled_val:
+                                env phase after the actor, f64 totals; the act_dim action
+                                columns feed obs column d mod act_dim) */
 } tsrl_collect_args;
 int64_t tsrl_collect_pack_floats(int64_t dim);
 int tsrl_collect_pack_w1(const float* W, int64_t dim, float* packed, void* stream);
@@ -533,6 +551,17 @@ int tsrl_ppo_tail(const float* h1frag, int64_t n, const int64_t* idx,
                   const double* adv_sums, tsrl_ppo_params p, float* dz1,
                   const tsrl_tail_grads* grads, double* sums, void* workspace,
                   int64_t ws_bytes, void* stream);
+/* tsrl_ppo_tail_fin: tsrl_ppo_tail followed, inside its reduction launch, by the loss
+ * finalisation of tsrl_ppo_gauss_finalize on the reduced sums (losses[4] = loss, clip, vf,
+ * entropy; grad_log_std[act_dim]): the single-process minibatch (no all-reduce of the sums
+ * between the two), one launch fewer per minibatch. */
+int tsrl_ppo_tail_fin(const float* h1frag, int64_t n, const int64_t* idx,
+                      const tsrl_tail_weights* w, int64_t act_dim, const float* act,
+                      const float* logp_old, const float* adv, const float* ret, const float* v_s,
+                      const double* adv_sums, tsrl_ppo_params p, float* dz1,
+                      const tsrl_tail_grads* grads, double* sums, void* workspace,
+                      int64_t ws_bytes, const float* log_std, float* losses,
+                      float* grad_log_std, void* stream);
 /* tsrl_ppo_eval: forward only (process_fn): value_out[n] = critic(obs) and, when logp_out is
  * given, logp_out[n] = log N(act | mu(obs), exp(log_std)) summed over the action dims, from
  * the fragment-layout layer-1 activations of tsrl_mlp_l1_fwd (critic only: the actor tiles
@@ -605,8 +634,8 @@ int tsrl_segtree_prefix_idx(const double* tree, int64_t bound, const void* value
  * flat f32 parameter / gradient / moment buffers of n elements: partials (f64,
  * tsrl_clip_adam_partials(n) entries) receive slice norms, norm_out[0] = gradient norm,
  * norm_out[1] = clip coefficient (max_norm <= 0: no clipping, partials / norm_out may be
- * NULL); step[0..nstep) (device f32 step counters, all equal) is advanced by one.  ticket:
- * one device uint32, zero-initialised, kept zero.
+ * NULL); step[0..nstep) (device f32 step counters, all equal) is
+ * advanced by one.  ticket: two device uint32, zero-initialised, kept zero.
  * lr_dev (nullable device f32): the learning rate read at run time instead of `lr`, so a
  * captured learn graph follows an lr_scheduler (BasePolicy.update, base.py:312-313).
  * scale_grads: leave the gradient scaled by the clip coefficient in place (what p.grad holds

@@ -14,7 +14,9 @@ Spec (made concrete here; identical on CPU and HIP):
 * rew         = ``(sm(k ^ 0xD1B54A32D192ED03) >> 40) * 2**-24``  (exact in f32 and f64).
 * Episode length L.  ``reset`` of env e: j += 1 (j starts at -1), t = (e % L if j == 0 else 0),
   returns obs(e, j, t).  ``step``: t += 1, returns obs(e, j, t), rew(e, j, t),
-  terminated = (t >= L) and e even, truncated = (t >= L) and e odd.  Actions are ignored.
+  terminated = (t >= L) and e even, truncated = (t >= L) and e odd.  Actions are ignored,
+  except by the action-coupled variant (``act_coef`` c != 0, Box only): a step's obs[d] is
+  ``f32(box_obs[d] + f32(c * a[d % A]))`` for the env's (remapped) f32 action row a.
 
 The reference drives this through its own ``DummyVectorEnv``/``Collector``
 (``tianshou/env/venvs.py:300-381``, ``tianshou/data/collector.py:258-361``) when
@@ -81,10 +83,12 @@ def reward(k):
 class SynthVecEnvNP:
     """Vectorised NumPy version (all envs in one object), used as the CPU port."""
 
-    def __init__(self, num_envs, obs_shape, act_dim, ep_len, seed=0, u8=False, frame_stack=1):
+    def __init__(self, num_envs, obs_shape, act_dim, ep_len, seed=0, u8=False, frame_stack=1,
+                 act_coef=0.0):
         self.num_envs, self.obs_shape, self.act_dim = num_envs, tuple(obs_shape), act_dim
         self.ep_len, self.seed, self.u8 = ep_len, seed, u8
         self.frame_stack = frame_stack
+        self.act_coef = np.float32(act_coef)
         self.j = np.full(num_envs, -1, np.int64)
         self.t = np.zeros(num_envs, np.int64)
 
@@ -103,11 +107,16 @@ class SynthVecEnvNP:
         self.t[ids] = np.where(self.j[ids] == 0, ids % self.ep_len, 0)
         return self._obs(ids)
 
-    def step(self, ids=None):
+    def step(self, ids=None, action=None):
         ids = np.arange(self.num_envs) if ids is None else np.asarray(ids, np.int64)
         self.t[ids] += 1
         k = key(self.seed, ids, self.j[ids], self.t[ids])
         obs = self._obs(ids)
+        if self.act_coef != 0:
+            a = np.asarray(action, np.float32).reshape(len(ids), self.act_dim)
+            D = obs.shape[-1]
+            ca = (self.act_coef * a[:, np.arange(D) % self.act_dim]).astype(np.float32)
+            obs = (obs + ca).astype(np.float32)
         rew = reward(k)
         done = self.t[ids] >= self.ep_len
         term = done & (ids % 2 == 0)

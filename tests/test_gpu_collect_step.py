@@ -19,7 +19,8 @@ def dev():
     return torch.device("cuda", 0)
 
 
-def _run(dev, fused, E, D, A, L, T, graph_steps, collects=2, bound="clip", det=False):
+def _run(dev, fused, E, D, A, L, T, graph_steps, collects=2, bound="clip", det=False,
+         act_coef=0.0):
     from tianshou_amd.data import Collector, VectorReplayBuffer
     from tianshou_amd.env import Box, SyntheticVectorEnv, VectorEnvNormObs
     from tianshou_amd.policy import PPOPolicy
@@ -35,7 +36,8 @@ def _run(dev, fused, E, D, A, L, T, graph_steps, collects=2, bound="clip", det=F
                     deterministic_eval=det).to(dev)
     if det:
         pol.eval()
-    env = VectorEnvNormObs(SyntheticVectorEnv(E, (D,), A, ep_len=L, seed=5, device=dev))
+    env = VectorEnvNormObs(SyntheticVectorEnv(E, (D,), A, ep_len=L, seed=5, device=dev,
+                                              act_coef=act_coef))
     buf = VectorReplayBuffer(E * T * collects, E, device=dev)
     c = Collector(pol, env, buf)
     c.use_fused_step = fused
@@ -83,6 +85,37 @@ def test_fused_step_matches_four_launch_step(dev, E, D, A, L, T, G):
     np.testing.assert_allclose(a["rms"][1].numpy(), b["rms"][1].numpy(), rtol=1e-6, atol=1e-7)
     for k in ("obs", "obs_next", "cur"):
         np.testing.assert_allclose(a[k].numpy(), b[k].numpy(), rtol=1e-6, atol=1e-6, err_msg=k)
+    np.testing.assert_allclose(a["act"].numpy(), b["act"].numpy(), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("E,D,A,L,T,G", [
+    (64, 24, 5, 13, 40, 8),
+    (100, 376, 17, 7, 12, 4),
+    (512, 17, 6, 25, 24, 8),
+    (4096, 376, 17, 30, 20, 16),
+])
+def test_fused_step_action_coupled_env(dev, E, D, A, L, T, G):
+    """The general fused step: an env whose transition reads the action (SyntheticVectorEnv
+    act_coef: obs = box + 0.05 * a[d mod A], not 2^-23-quantised) runs its env phase AFTER the
+    actor in the same launch and sums obs_rms moments in f64 (atomic f64 adds) -- against the
+    four-launch step (torch-free fused act -> coupled step+reset kernel -> f64 partials merge ->
+    add) with the same noise stream.  Rewards / flags / episode statistics bit-identical;
+    actions differ by the actors' f32 summation order (rtol 1e-5) and feed the observations,
+    so obs / statistics agree at rtol 1e-5."""
+    a, ra = _run(dev, True, E, D, A, L, T, G, act_coef=0.05)
+    b, rb = _run(dev, False, E, D, A, L, T, G, act_coef=0.05)
+    for k in ("rew", "terminated", "truncated", "done", "env_id"):
+        assert torch.equal(a[k], b[k]), k
+    for x, y in zip(a["stats"], b["stats"]):
+        assert torch.equal(x, y)
+    for x, y in zip(ra, rb):
+        assert x["n/ep"] == y["n/ep"] and np.array_equal(x["lens"], y["lens"])
+        assert np.array_equal(x["rews"], y["rews"])
+    assert a["rms"][2] == b["rms"][2]
+    np.testing.assert_allclose(a["rms"][0].numpy(), b["rms"][0].numpy(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(a["rms"][1].numpy(), b["rms"][1].numpy(), rtol=1e-5, atol=1e-6)
+    for k in ("obs", "obs_next", "cur"):
+        np.testing.assert_allclose(a[k].numpy(), b[k].numpy(), rtol=1e-5, atol=1e-5, err_msg=k)
     np.testing.assert_allclose(a["act"].numpy(), b["act"].numpy(), rtol=1e-5, atol=1e-5)
 
 

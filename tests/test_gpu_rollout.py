@@ -83,6 +83,42 @@ def test_synth_env_matches_oracle(dev):
     assert np.array_equal(envu.step(None)[0].cpu().numpy(), ou.step()[0])
 
 
+def test_coupled_synth_env_matches_oracle(dev):
+    """The action-coupled env (SyntheticVectorEnv(act_coef=c)): step rows read the actions,
+    obs = f32(box + f32(c * a[d mod A])) (synth.h coupled_val), through both device env
+    kernels (step with ids, step + auto-reset) = the NumPy oracle, bit for bit."""
+    from tianshou_amd.env import SyntheticVectorEnv
+    E, D, A, L, c = 37, 29, 3, 9, 0.05
+    for fused_reset in (False, True):
+        env = SyntheticVectorEnv(E, (D,), A, ep_len=L, seed=5, device=dev, act_coef=c)
+        o = synth_env.SynthVecEnvNP(E, (D,), A, L, seed=5, act_coef=c)
+        env.reset()
+        o.reset()
+        g = torch.Generator(device=dev).manual_seed(1)
+        for t in range(20):
+            act = torch.rand(E, A, device=dev, generator=g) * 2 - 1
+            if fused_reset:
+                nxt = torch.empty(E, D, device=dev)
+                rst = torch.empty(E, D, device=dev)
+                rew = torch.empty(E, dtype=torch.float64, device=dev)
+                term, trunc, done = (torch.empty(E, dtype=torch.bool, device=dev)
+                                     for _ in range(3))
+                env._step_reset_raw(E, nxt, rst, rew, term, trunc, done, action=act)
+            else:
+                nxt, rew, term, trunc, _ = env.step(act)
+            n2, r2, t2, u2 = o.step(action=act.cpu().numpy())
+            assert np.array_equal(nxt.cpu().numpy(), n2)
+            assert np.array_equal(rew.cpu().numpy(), r2)
+            dn = np.flatnonzero(t2 | u2)
+            if len(dn):
+                o_r = o.reset(dn)
+                if fused_reset:
+                    assert np.array_equal(rst.cpu().numpy()[dn], o_r)
+                else:
+                    r_obs, _ = env.reset(dn)
+                    assert np.array_equal(r_obs.cpu().numpy(), o_r)
+
+
 def test_rms_kernels_vs_reference(golden_dir, dev):
     from tianshou_amd.utils.statistics import DeviceRunningMeanStd
     z = np.load(os.path.join(golden_dir, "rms.npz"))

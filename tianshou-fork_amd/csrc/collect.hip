@@ -63,11 +63,15 @@ constexpr int HP = 16;         // h1 / h2 tiles [feature][row]
 constexpr int WP = 68;         // W2 / W3 rows (4i + k banks: conflict-free A fragments)
 // diagnostic builds only (tools/collect_step_bench.py): return after phase 1 (add), 2 (actor)
 // or 3 (env); 0 = the whole step
-#ifndef COLLECT_ATOMIC_LATE
-#define COLLECT_ATOMIC_LATE 0  // 1: the obs_rms atomics after the actor (measured slower)
-#endif
+// (round 3 measured a variant issuing the obs_rms atomics after the actor: slower, removed)
 #ifndef COLLECT_STOP
 #define COLLECT_STOP 0
+#endif
+#ifndef COLLECT_NO_RAW
+#define COLLECT_NO_RAW 0  // diagnostic builds only: skip the raw env-row stores (wrong rows)
+#endif
+#ifndef COLLECT_NO_TOTALS
+#define COLLECT_NO_TOTALS 0  // diagnostic builds only: skip the obs_rms atomics (wrong stats)
 #endif
 // diagnostic builds only: per-workgroup s_memrealtime stamps (100 MHz) after each phase,
 // stored behind the workspace (tools/collect_step_bench.py --trace)
@@ -175,16 +179,16 @@ __device__ __forceinline__ void atomic_add_i64(long long* p, long long v) {
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// rms.hip rms_merge2_kernel's two RunningMeanStd updates for one column from exact integer
-// moments: (m0, v0, count) -> snapshot after the k step rows -> state after the nd reset rows.
-__device__ __forceinline__ void merge_column(double m0, double v0, double old_count, double k,
-                                             long long s1i, long long q1i, double nd,
-                                             long long s2i, long long q2i, float& snap_m,
-                                             float& snap_v, float& fin_m, float& fin_v) {
+// rms.hip rms_merge2_kernel's two RunningMeanStd updates for one column from the f64 sums of
+// the step rows (S1, Q1) and of the reset rows (S2, Q2): (m0, v0, count) -> snapshot after the
+// k step rows -> state after the nd reset rows.
+__device__ __forceinline__ void merge_column_f(double m0, double v0, double old_count, double k,
+                                               double S1, double Q1, double nd, double S2,
+                                               double Q2, float& snap_m, float& snap_v,
+                                               float& fin_m, float& fin_v) {
 #pragma clang fp contract(off)
     const double tot1 = old_count + k, tot2 = tot1 + nd;
     if (k > 0.0) {
-        const double S1 = (double)s1i * 0x1p-23, Q1 = (double)q1i * 0x1p-46;
         const double bm = S1 / k;
         double bv = Q1 / k - bm * bm;
         bv = bv < 0.0 ? 0.0 : bv;
@@ -197,7 +201,6 @@ __device__ __forceinline__ void merge_column(double m0, double v0, double old_co
     snap_m = (float)m0;
     snap_v = (float)v0;
     if (nd > 0.0) {
-        const double S2 = (double)s2i * 0x1p-23, Q2 = (double)q2i * 0x1p-46;
         const double bm = S2 / nd;
         double bv = Q2 / nd - bm * bm;
         bv = bv < 0.0 ? 0.0 : bv;
@@ -211,9 +214,30 @@ __device__ __forceinline__ void merge_column(double m0, double v0, double old_co
     fin_v = (float)v0;
 }
 
+// The same from exact integer moments of the quantised synthetic env (x = m 2^-23: the sums
+// scale exactly into f64).
+__device__ __forceinline__ void merge_column(double m0, double v0, double old_count, double k,
+                                             long long s1i, long long q1i, double nd,
+                                             long long s2i, long long q2i, float& snap_m,
+                                             float& snap_v, float& fin_m, float& fin_v) {
+#pragma clang fp contract(off)
+    merge_column_f(m0, v0, old_count, k, (double)s1i * 0x1p-23, (double)q1i * 0x1p-46, nd,
+                   (double)s2i * 0x1p-23, (double)q2i * 0x1p-46, snap_m, snap_v, fin_m, fin_v);
+}
+
+// A totals-slot entry: int64 for the quantised env, f64 (sums and counts) for the
+// action-coupled env (CPL)
+template <bool CPL>
+__device__ __forceinline__ double slot_f(const long long* p, int i) {
+    return CPL ? reinterpret_cast<const double*>(p)[i] : (double)p[i];
+}
+
 // SQC = kpad(dim) / 128: the 128-column groups of an observation row (a compile-time bound, so
-// the layer-1 weight fragments and the prefetched rows take only the registers dim needs)
-template <int SQC>
+// the layer-1 weight fragments and the prefetched rows take only the registers dim needs).
+// CPL: the action-coupled env (a.act_coef != 0, synth.h coupled_val): the env phase runs
+// AFTER the actor on this launch's actions, and the obs_rms moments are f64 sums (atomic f64
+// adds: the values are not 2^-23-quantised), the counts f64 too (one all-reducible f64 slot).
+template <int SQC, bool CPL>
 __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_args a, Ws ws) {
 #pragma clang fp contract(off)
     __shared__ float sX[KMAX * XP];
@@ -223,6 +247,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
     __shared__ float sb1[H], sb2[H], sb3[AMAX], ssig[AMAX], slo[AMAX], shi[AMAX];
     __shared__ float seps[R][AMAX + 1];
     __shared__ RowState rs[R], rr[R];
+    __shared__ float sAr[CPL ? R : 1][AMAX + 1];  // CPL: this workgroup's remapped actions
     __shared__ int s_nd;
     __shared__ int64_t s_row[R];
     // deferred obs_rms merge: the statistics after the previous step's step rows (obs_next
@@ -300,14 +325,14 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
     }
     TSTAMP2(0)
     float mm0 = 0.f, mv0 = 0.f;
-    long long ms1 = 0, mq1 = 0, ms2 = 0, mq2 = 0;
+    long long ms1 = 0, mq1 = 0, ms2 = 0, mq2 = 0;  // raw slot words (int64 or f64 bits)
     double mcount = 0.0, mnd = 0.0, mk = 0.0;
     if (merge) {
         const RmsState* sin = ws.st[par];
         const long long* tp = ws.tot[tprev];
         mcount = sin->count;
-        mnd = (double)tp[4 * D];
-        mk = (double)tp[4 * D + 1];
+        mnd = slot_f<CPL>(tp, 4 * D);
+        mk = slot_f<CPL>(tp, 4 * D + 1);
         if (t < D) {  // D <= KMAX = NT: one column per thread
             mm0 = sin->mean[t];
             mv0 = sin->var[t];
@@ -332,9 +357,16 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         // the step rows behind the totals (counted in the slot: k, or the sum of every
         // rank's k when the slot was all-reduced)
         const double kp = mk;
-        if (t < D)
-            merge_column((double)mm0, (double)mv0, mcount, kp, ms1, mq1, mnd, ms2, mq2,
-                         sSnapM[t], sSnapV[t], sFinM[t], sFinV[t]);
+        if (t < D) {
+            if (CPL)
+                merge_column_f((double)mm0, (double)mv0, mcount, kp, __longlong_as_double(ms1),
+                               __longlong_as_double(mq1), mnd, __longlong_as_double(ms2),
+                               __longlong_as_double(mq2), sSnapM[t], sSnapV[t], sFinM[t],
+                               sFinV[t]);
+            else
+                merge_column((double)mm0, (double)mv0, mcount, kp, ms1, mq1, mnd, ms2, mq2,
+                             sSnapM[t], sSnapV[t], sFinM[t], sFinV[t]);
+        }
         TSTAMP2(3)
         LDS_SYNC();
         TSTAMP2(4)
@@ -536,93 +568,132 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         row_store1(&a.obs_dst[s_row[rw] * D + c], sX[c * XP + rw]);
     }
     // ---- C. env step + auto-reset of these rows (env.hip box_step_reset_kernel) -------------
-    // The synthetic env's transition does not read the action, so the step runs before the
-    // actor: its obs_rms atomics drain while the actor computes.  Phase A of this launch has
-    // consumed the previous step's env rows of this workgroup (the __syncthreads above).
-    if (t == 0) s_nd = 0;
-    LDS_SYNC();
-    if (t < R) {
-        const int64_t r = r0 + t;
-        RowState st = {0ull, 0}, sr = {0ull, 0};
-        if (t < nrows) {
-            const int64_t e = r;
-            int64_t j = ej;
-            int64_t tt = et + 1;
-            st.key = env_key(a.env_seed, (uint64_t)e, j, tt);
-            st.active = 1;
-            const uint64_t h = sm64(st.key ^ REW_SALT);
-            a.rew[r] = (double)(h >> 40) * 0x1p-24;
-            const bool dn = tt >= a.ep_len;
-            a.term[r] = (uint8_t)(dn && (e % 2 == 0));
-            a.trunc[r] = (uint8_t)(dn && (e % 2 == 1));
-            a.done[r] = (uint8_t)dn;
-            if (dn) {
-                j += 1;
-                tt = (j == 0) ? (e % a.ep_len) : 0;
-                a.ep_j[e] = j;
-                sr.key = env_key(a.env_seed, (uint64_t)e, j, tt);
-                sr.active = 1;
-                atomicAdd(&s_nd, 1);
+    // The quantised synthetic env's transition does not read the action, so its step runs
+    // before the actor: its obs_rms atomics drain while the actor computes.  The
+    // action-coupled env (CPL) steps after the actor, on the actions in sAr.  Phase A of
+    // this launch has consumed the previous step's env rows of this workgroup (the barrier
+    // above).
+    auto env_phase = [&]() {
+        if (t == 0) s_nd = 0;
+        LDS_SYNC();
+        if (t < R) {
+            const int64_t r = r0 + t;
+            RowState st = {0ull, 0}, sr = {0ull, 0};
+            if (t < nrows) {
+                const int64_t e = r;
+                int64_t j = ej;
+                int64_t tt = et + 1;
+                st.key = env_key(a.env_seed, (uint64_t)e, j, tt);
+                st.active = 1;
+                const uint64_t h = sm64(st.key ^ REW_SALT);
+                a.rew[r] = (double)(h >> 40) * 0x1p-24;
+                const bool dn = tt >= a.ep_len;
+                a.term[r] = (uint8_t)(dn && (e % 2 == 0));
+                a.trunc[r] = (uint8_t)(dn && (e % 2 == 1));
+                a.done[r] = (uint8_t)dn;
+                if (dn) {
+                    j += 1;
+                    tt = (j == 0) ? (e % a.ep_len) : 0;
+                    a.ep_j[e] = j;
+                    sr.key = env_key(a.env_seed, (uint64_t)e, j, tt);
+                    sr.active = 1;
+                    atomicAdd(&s_nd, 1);
+                }
+                a.ep_t[e] = tt;
             }
-            a.ep_t[e] = tt;
+            rs[t] = st;
+            rr[t] = sr;
         }
-        rs[t] = st;
-        rr[t] = sr;
-    }
-    LDS_SYNC();
-    const int nd = s_nd;
-    long long* tc = ws.tot[tcur];
-    // this thread's column (D <= KMAX = NT): its exact integer moments, added to the totals
-    // slot by atomics after the actor (their issue would otherwise delay it)
-    long long cs1 = 0, cq1 = 0, cs2 = 0, cq2 = 0;
-    if (t < D) {
-        const int d = t;
-        for (int r = 0; r < nrows; ++r) {
-            const int m = box_m(rs[r].key, d);
-#if COLLECT_ROW_STORE == 4
-            row_store1(&a.raw[(r0 + r) * D + d], (float)m * 0x1p-23f);
-#elif !COLLECT_NO_RAW
-            a.raw[(r0 + r) * D + d] = (float)m * 0x1p-23f;  // == box_val(key, d), exactly
-#endif
-            cs1 += m;
-            cq1 += (long long)m * m;
-        }
-        if (nd > 0)
-            for (int r = 0; r < nrows; ++r) {
-                if (!rr[r].active) continue;
-                const int m = box_m(rr[r].key, d);
-#if COLLECT_ROW_STORE == 4
-                row_store1(&a.reset_raw[(r0 + r) * D + d], (float)m * 0x1p-23f);
-#else
-                a.reset_raw[(r0 + r) * D + d] = (float)m * 0x1p-23f;
-#endif
-                cs2 += m;
-                cq2 += (long long)m * m;
+        LDS_SYNC();
+        const int nd = s_nd;
+        long long* tc = ws.tot[tcur];
+        if (CPL) {
+            // the coupled env: f64 column moments of the step rows (their values read the
+            // actions) and of the reset rows, atomic f64 adds into the f64 slot
+            double fs1 = 0.0, fq1 = 0.0, fs2 = 0.0, fq2 = 0.0;
+            if (t < D) {
+                const int d = t, ad = d % A;
+                for (int r = 0; r < nrows; ++r) {
+                    const float x = synth::coupled_val(rs[r].key, d, sAr[r][ad], a.act_coef);
+                    a.raw[(r0 + r) * D + d] = x;
+                    fs1 += (double)x;
+                    fq1 += (double)x * (double)x;
+                }
+                if (nd > 0)
+                    for (int r = 0; r < nrows; ++r) {
+                        if (!rr[r].active) continue;
+                        const float x = box_val(rr[r].key, d);
+                        a.reset_raw[(r0 + r) * D + d] = x;
+                        fs2 += (double)x;
+                        fq2 += (double)x * (double)x;
+                    }
             }
-    }
-    auto add_totals = [&]() {
+            if (defer) {
+                double* tcd = reinterpret_cast<double*>(tc);
+                auto fadd = [](double* p, double v) {
+                    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                };
+                if (t < D) {
+                    fadd(tcd + t, fs1);
+                    fadd(tcd + D + t, fq1);
+                    if (nd > 0) {
+                        fadd(tcd + 2 * D + t, fs2);
+                        fadd(tcd + 3 * D + t, fq2);
+                    }
+                }
+                if (t == 0) {
+                    if (nd > 0) fadd(tcd + 4 * D, (double)nd);
+                    fadd(tcd + 4 * D + 1, (double)nrows);
+                }
+            }
+            return;
+        }
+        // this thread's column (D <= KMAX = NT): its exact integer moments, added to the totals
+        // slot by atomics
+        long long cs1 = 0, cq1 = 0, cs2 = 0, cq2 = 0;
         if (t < D) {
-            atomic_add_i64(tc + t, cs1);
-            atomic_add_i64(tc + D + t, cq1);
-            if (nd > 0) {
-                atomic_add_i64(tc + 2 * D + t, cs2);
-                atomic_add_i64(tc + 3 * D + t, cq2);
+            const int d = t;
+            for (int r = 0; r < nrows; ++r) {
+                const int m = box_m(rs[r].key, d);
+#if COLLECT_ROW_STORE == 4
+                row_store1(&a.raw[(r0 + r) * D + d], (float)m * 0x1p-23f);
+#elif !COLLECT_NO_RAW
+                a.raw[(r0 + r) * D + d] = (float)m * 0x1p-23f;  // == box_val(key, d), exactly
+#endif
+                cs1 += m;
+                cq1 += (long long)m * m;
+            }
+            if (nd > 0)
+                for (int r = 0; r < nrows; ++r) {
+                    if (!rr[r].active) continue;
+                    const int m = box_m(rr[r].key, d);
+#if COLLECT_ROW_STORE == 4
+                    row_store1(&a.reset_raw[(r0 + r) * D + d], (float)m * 0x1p-23f);
+#else
+                    a.reset_raw[(r0 + r) * D + d] = (float)m * 0x1p-23f;
+#endif
+                    cs2 += m;
+                    cq2 += (long long)m * m;
+                }
+        }
+#if !COLLECT_NO_TOTALS
+        if (defer) {
+            if (t < D) {
+                atomic_add_i64(tc + t, cs1);
+                atomic_add_i64(tc + D + t, cq1);
+                if (nd > 0) {
+                    atomic_add_i64(tc + 2 * D + t, cs2);
+                    atomic_add_i64(tc + 3 * D + t, cq2);
+                }
+            }
+            if (t == 0) {
+                if (nd > 0) atomic_add_i64(tc + 4 * D, nd);
+                atomic_add_i64(tc + 4 * D + 1, nrows);
             }
         }
-        if (t == 0) {
-            if (nd > 0) atomic_add_i64(tc + 4 * D, nd);
-            atomic_add_i64(tc + 4 * D + 1, nrows);
-        }
+#endif
     };
-#ifndef COLLECT_NO_RAW
-#define COLLECT_NO_RAW 0  // diagnostic builds only: skip the raw env-row stores (wrong rows)
-#endif
-#ifndef COLLECT_NO_TOTALS
-#define COLLECT_NO_TOTALS 0  // diagnostic builds only: skip the obs_rms atomics (wrong stats)
-#endif
-#if !COLLECT_ATOMIC_LATE && !COLLECT_NO_TOTALS
-    if (defer) add_totals();
-#endif
+    if (!CPL) env_phase();
     TSTAMP(2)
 #if COLLECT_STOP == 1
     return;
@@ -723,16 +794,18 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
                 y = lo + (hi - lo) * (y + 1.0f) / 2.0f;
             }
             a.act_remap[row * A + a_] = y;
+            if (CPL) sAr[rw][a_] = y;
         }
+    }
+    if (CPL) {
+        LDS_SYNC();  // sAr complete
+        env_phase();
     }
 
 #if COLLECT_STOP == 2
     return;
 #endif
     TSTAMP(3)
-#if COLLECT_ATOMIC_LATE
-    if (defer) add_totals();
-#endif
 }
 
 // tsrl_collect_rms_finalize: the last deferred step's totals merged into the caller's state
@@ -744,12 +817,20 @@ __global__ __launch_bounds__(NT) void rms_finalize_kernel(tsrl_collect_args a, W
     const int step = a.rms_step;  // the chain's last launch
     const RmsState* sin = ws.st[(step + 1) & 1];  // the state the last launch published
     long long* tp = ws.tot[step % 3];
-    const double old_count = sin->count, nd = (double)tp[4 * D];
-    const double kp = (double)tp[4 * D + 1];
+    const bool cpl = a.act_coef != 0.0f;  // the action-coupled env's f64 slot
+    const double old_count = sin->count;
+    const double nd = cpl ? slot_f<true>(tp, 4 * D) : slot_f<false>(tp, 4 * D);
+    const double kp = cpl ? slot_f<true>(tp, 4 * D + 1) : slot_f<false>(tp, 4 * D + 1);
     for (int d = t; d < D; d += NT) {
         float sm, sv, fm, fv;
-        merge_column((double)sin->mean[d], (double)sin->var[d], old_count, kp, tp[d],
-                     tp[D + d], nd, tp[2 * D + d], tp[3 * D + d], sm, sv, fm, fv);
+        if (cpl)
+            merge_column_f((double)sin->mean[d], (double)sin->var[d], old_count, kp,
+                           __longlong_as_double(tp[d]), __longlong_as_double(tp[D + d]), nd,
+                           __longlong_as_double(tp[2 * D + d]),
+                           __longlong_as_double(tp[3 * D + d]), sm, sv, fm, fv);
+        else
+            merge_column((double)sin->mean[d], (double)sin->var[d], old_count, kp, tp[d],
+                         tp[D + d], nd, tp[2 * D + d], tp[3 * D + d], sm, sv, fm, fv);
         a.snap_mean[d] = sm;
         a.snap_var[d] = sv;
         a.mean[d] = fm;
@@ -846,30 +927,32 @@ extern "C" int tsrl_collect_box_step(const tsrl_collect_args* a, void* stream) {
                                     "launch that produced it stored them)");
     }
     // one row adds <= 2^46 to a column's int64 sum of m^2: exact for <= 2^17 rows per slot (the
-    // data-parallel caller also checks world * k)
-    TSRL_CHECK_ARG(k <= (int64_t)1 << 17, "tsrl_collect_box_step: k <= 2^17 (exact int64 moments)");
+    // data-parallel caller also checks world * k); the coupled env's f64 slot has no such bound
+    TSRL_CHECK_ARG(a->act_coef != 0.0f || k <= (int64_t)1 << 17,
+                   "tsrl_collect_box_step: k <= 2^17 (exact int64 moments)");
     const Ws ws = make_ws(a);
     tsrl_collect_args p = *a;
     p.act_seed = sm64(a->act_seed);
     p.env_seed = sm64(a->env_seed);
+#define TSRL_COLLECT_LAUNCH(SQ, CP)                                                         \
+    hipLaunchKernelGGL((collect_box_step_kernel<SQ, CP>), dim3((unsigned)ws.nblk), dim3(NT), 0,  \
+                       as_stream(stream), p, ws)
+    const bool cpl = a->act_coef != 0.0f;
     switch (kpad(D) / 128) {
         case 1:
-            hipLaunchKernelGGL(collect_box_step_kernel<1>, dim3((unsigned)ws.nblk), dim3(NT), 0,
-                               as_stream(stream), p, ws);
+            if (cpl) TSRL_COLLECT_LAUNCH(1, true); else TSRL_COLLECT_LAUNCH(1, false);
             break;
         case 2:
-            hipLaunchKernelGGL(collect_box_step_kernel<2>, dim3((unsigned)ws.nblk), dim3(NT), 0,
-                               as_stream(stream), p, ws);
+            if (cpl) TSRL_COLLECT_LAUNCH(2, true); else TSRL_COLLECT_LAUNCH(2, false);
             break;
         case 3:
-            hipLaunchKernelGGL(collect_box_step_kernel<3>, dim3((unsigned)ws.nblk), dim3(NT), 0,
-                               as_stream(stream), p, ws);
+            if (cpl) TSRL_COLLECT_LAUNCH(3, true); else TSRL_COLLECT_LAUNCH(3, false);
             break;
         default:
-            hipLaunchKernelGGL(collect_box_step_kernel<4>, dim3((unsigned)ws.nblk), dim3(NT), 0,
-                               as_stream(stream), p, ws);
+            if (cpl) TSRL_COLLECT_LAUNCH(4, true); else TSRL_COLLECT_LAUNCH(4, false);
             break;
     }
+#undef TSRL_COLLECT_LAUNCH
     TSRL_LAUNCH_CHECK("tsrl_collect_box_step");
     return 0;
 }

@@ -18,15 +18,20 @@ using synth::RowState;
 constexpr int TPB = 256;
 constexpr int ROWS = 16;  // env rows per workgroup
 
-// Rows [r0, r0+ROWS): obs rows + column partials over active rows.
+// Rows [r0, r0+ROWS): obs rows + column partials over active rows.  act (nullable): the
+// rows' [k, act_dim] actions of the action-coupled env (synth.h coupled_val).
 __device__ void box_rows(const RowState* rs, int64_t r0, int64_t k, int64_t dim, float* obs,
-                         double* partials) {
+                         double* partials, const float* act = nullptr, int64_t act_dim = 1,
+                         float act_coef = 0.0f) {
     const int nrows = (int)min((int64_t)ROWS, k - r0);
     for (int64_t d = threadIdx.x; d < dim; d += blockDim.x) {
         double s = 0.0, ss = 0.0;
+        const int64_t ad = d % act_dim;
         for (int r = 0; r < nrows; ++r) {
             if (!rs[r].active) continue;
-            const float x = box_val(rs[r].key, d);
+            const float x = act ? synth::coupled_val(rs[r].key, d, act[(r0 + r) * act_dim + ad],
+                                                     act_coef)
+                                : box_val(rs[r].key, d);
             obs[(r0 + r) * dim + d] = x;
             s += (double)x;
             ss += (double)x * (double)x;
@@ -44,7 +49,8 @@ __global__ __launch_bounds__(TPB) void box_step_kernel(const int64_t* ids, int64
                                                        int64_t ep_len, int64_t* ep_j,
                                                        int64_t* ep_t, float* obs, double* rew,
                                                        uint8_t* term, uint8_t* trunc,
-                                                       double* partials) {
+                                                       double* partials, const float* act,
+                                                       int64_t act_dim, float act_coef) {
     __shared__ RowState rs[ROWS];
     const int64_t r0 = (int64_t)blockIdx.x * ROWS;
     if (threadIdx.x < ROWS) {
@@ -66,7 +72,7 @@ __global__ __launch_bounds__(TPB) void box_step_kernel(const int64_t* ids, int64
         rs[threadIdx.x] = st;
     }
     __syncthreads();
-    box_rows(rs, r0, k, dim, obs, partials);
+    box_rows(rs, r0, k, dim, obs, partials, act, act_dim, act_coef);
 }
 
 __global__ __launch_bounds__(TPB) void box_reset_kernel(const int64_t* ids, const uint8_t* mask,
@@ -101,7 +107,8 @@ __global__ __launch_bounds__(TPB) void box_reset_kernel(const int64_t* ids, cons
 __global__ __launch_bounds__(1024) void box_step_reset_kernel(
     int64_t k, int64_t dim, uint64_t s_seed, int64_t ep_len, int64_t* ep_j, int64_t* ep_t,
     float* obs, float* reset_obs, double* rew, uint8_t* term, uint8_t* trunc, uint8_t* done,
-    double* p_step, double* p_reset, double* blk_done) {
+    double* p_step, double* p_reset, double* blk_done, const float* act, int64_t act_dim,
+    float act_coef) {
     __shared__ RowState rs[ROWS], rr[ROWS];
     __shared__ int nd;
     const int64_t r0 = (int64_t)blockIdx.x * ROWS;
@@ -136,7 +143,7 @@ __global__ __launch_bounds__(1024) void box_step_reset_kernel(
         rr[threadIdx.x] = sr;
     }
     __syncthreads();
-    box_rows(rs, r0, k, dim, obs, p_step);
+    box_rows(rs, r0, k, dim, obs, p_step, act, act_dim, act_coef);
     if (nd > 0) {
         box_rows(rr, r0, k, dim, reset_obs, p_reset);
     } else if (p_reset) {
@@ -267,28 +274,42 @@ using namespace tsrl;
 
 extern "C" int64_t tsrl_env_num_partials(int64_t k) { return (k + ROWS - 1) / ROWS; }
 
-extern "C" int tsrl_synth_box_step(const int64_t* ids, int64_t k, int64_t dim, uint64_t seed,
-                                   int64_t ep_len, int64_t* ep_j, int64_t* ep_t, float* obs_out,
-                                   double* rew_out, uint8_t* term_out, uint8_t* trunc_out,
-                                   double* col_partials, void* stream) {
-    TSRL_CHECK_ARG(k >= 0 && dim > 0 && ep_len > 0, "tsrl_synth_box_step: bad sizes");
+extern "C" int tsrl_synth_box_step_act(const int64_t* ids, int64_t k, int64_t dim,
+                                       uint64_t seed, int64_t ep_len, int64_t* ep_j,
+                                       int64_t* ep_t, float* obs_out, double* rew_out,
+                                       uint8_t* term_out, uint8_t* trunc_out,
+                                       double* col_partials, const float* act, int64_t act_dim,
+                                       float act_coef, void* stream) {
+    TSRL_CHECK_ARG(k >= 0 && dim > 0 && ep_len > 0 && (!act || act_dim > 0),
+                   "tsrl_synth_box_step: bad sizes");
     if (k == 0) return 0;
     TSRL_CHECK_ARG(ep_j && ep_t && obs_out && rew_out && term_out && trunc_out,
                    "tsrl_synth_box_step: null pointer");
     hipLaunchKernelGGL(box_step_kernel, dim3(blocks_for(k)), dim3(TPB), 0, as_stream(stream),
                        ids, k, dim, sm64(seed), ep_len, ep_j, ep_t, obs_out, rew_out, term_out,
-                       trunc_out, col_partials);
+                       trunc_out, col_partials, act, act ? act_dim : 1, act_coef);
     TSRL_LAUNCH_CHECK("tsrl_synth_box_step");
     return 0;
 }
 
-extern "C" int tsrl_synth_box_step_reset(int64_t k, int64_t dim, uint64_t seed, int64_t ep_len,
-                                         int64_t* ep_j, int64_t* ep_t, float* obs_out,
-                                         float* reset_out, double* rew_out, uint8_t* term_out,
-                                         uint8_t* trunc_out, uint8_t* done_out,
-                                         double* partials_step, double* partials_reset,
-                                         double* blk_done, void* stream) {
-    TSRL_CHECK_ARG(k >= 0 && dim > 0 && ep_len > 0, "tsrl_synth_box_step_reset: bad sizes");
+extern "C" int tsrl_synth_box_step(const int64_t* ids, int64_t k, int64_t dim, uint64_t seed,
+                                   int64_t ep_len, int64_t* ep_j, int64_t* ep_t, float* obs_out,
+                                   double* rew_out, uint8_t* term_out, uint8_t* trunc_out,
+                                   double* col_partials, void* stream) {
+    return tsrl_synth_box_step_act(ids, k, dim, seed, ep_len, ep_j, ep_t, obs_out, rew_out,
+                                   term_out, trunc_out, col_partials, nullptr, 1, 0.0f, stream);
+}
+
+extern "C" int tsrl_synth_box_step_reset_act(int64_t k, int64_t dim, uint64_t seed,
+                                             int64_t ep_len, int64_t* ep_j, int64_t* ep_t,
+                                             float* obs_out, float* reset_out, double* rew_out,
+                                             uint8_t* term_out, uint8_t* trunc_out,
+                                             uint8_t* done_out, double* partials_step,
+                                             double* partials_reset, double* blk_done,
+                                             const float* act, int64_t act_dim, float act_coef,
+                                             void* stream) {
+    TSRL_CHECK_ARG(k >= 0 && dim > 0 && ep_len > 0 && (!act || act_dim > 0),
+                   "tsrl_synth_box_step_reset: bad sizes");
     if (k == 0) return 0;
     TSRL_CHECK_ARG(ep_j && ep_t && obs_out && reset_out && rew_out && term_out && trunc_out &&
                        done_out,
@@ -302,9 +323,20 @@ extern "C" int tsrl_synth_box_step_reset(int64_t k, int64_t dim, uint64_t seed, 
     hipLaunchKernelGGL(box_step_reset_kernel, dim3(blocks_for(k)), dim3(tpb), 0,
                        as_stream(stream), k, dim, sm64(seed), ep_len, ep_j, ep_t, obs_out,
                        reset_out, rew_out, term_out, trunc_out, done_out, partials_step,
-                       partials_reset, blk_done);
+                       partials_reset, blk_done, act, act ? act_dim : 1, act_coef);
     TSRL_LAUNCH_CHECK("tsrl_synth_box_step_reset");
     return 0;
+}
+
+extern "C" int tsrl_synth_box_step_reset(int64_t k, int64_t dim, uint64_t seed, int64_t ep_len,
+                                         int64_t* ep_j, int64_t* ep_t, float* obs_out,
+                                         float* reset_out, double* rew_out, uint8_t* term_out,
+                                         uint8_t* trunc_out, uint8_t* done_out,
+                                         double* partials_step, double* partials_reset,
+                                         double* blk_done, void* stream) {
+    return tsrl_synth_box_step_reset_act(k, dim, seed, ep_len, ep_j, ep_t, obs_out, reset_out,
+                                         rew_out, term_out, trunc_out, done_out, partials_step,
+                                         partials_reset, blk_done, nullptr, 1, 0.0f, stream);
 }
 
 extern "C" int tsrl_synth_box_reset(const int64_t* ids, const uint8_t* mask, int64_t k,

@@ -1122,10 +1122,21 @@ __device__ __forceinline__ T slab_sum(const T* __restrict__ base, int64_t stride
     return ((sh[o] + sh[64 + o]) + sh[128 + o]) + sh[192 + o];
 }
 
+// Optional loss finalisation folded into the loss-sum block (tsrl_ppo_tail_fin): the work of
+// ppo.hip's gauss_finalize_kernel (loss terms, the log-std gradient) on the sums this block
+// just reduced, so the single-process minibatch needs no separate launch for it.
+struct TailFin {
+    const float* log_std;
+    float* losses;        // NULL: no finalisation
+    float* grad_log_std;
+    float vf_coef, ent_coef;
+    double inv_b;
+};
+
 __global__ __launch_bounds__(256) void tail_reduce_kernel(const float* __restrict__ slab_f,
                                                           const double* __restrict__ slab_d,
                                                           int nslab, int A, TailGrads g,
-                                                          double* __restrict__ sums) {
+                                                          double* __restrict__ sums, TailFin fin) {
     __shared__ float shf[256];
     __shared__ double shd[256];
     const int nfb = (SL_F + 63) / 64;
@@ -1145,6 +1156,26 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(const float* __restric
         const int k0 = threadIdx.x & 63;
         const double s = slab_sum(slab_d, SL_D, nslab, k0, k0 < SL_D, shd);
         if (threadIdx.x < 64 && k0 < 4 + A) sums[k0] = s;
+        if (fin.losses) {
+            __shared__ double fs[64];
+            if (threadIdx.x < 64) fs[k0] = s;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                float ent = 0.0f;
+                for (int a = 0; a < A; ++a) {
+                    const float sig = expf(fin.log_std[a]);
+                    ent += 1.4189385332046727f + logf(sig);  // f32(0.5 + 0.5 log 2 pi) + log(scale)
+                }
+                const float clip = (float)(fs[0] * fin.inv_b);
+                const float vf = (float)(fs[1] * fin.inv_b);
+                fin.losses[0] = clip + fin.vf_coef * vf - fin.ent_coef * ent;
+                fin.losses[1] = clip;
+                fin.losses[2] = vf;
+                fin.losses[3] = ent;
+            }
+            for (int a = threadIdx.x; a < A; a += blockDim.x)
+                fin.grad_log_std[a] = (float)(fs[4 + a] - (double)fin.ent_coef);
+        }
     }
 }
 
@@ -1462,12 +1493,12 @@ extern "C" int64_t tsrl_ppo_tail_workspace_bytes(int64_t n) {
            (TAIL_TRACE ? 256 + 2 * (int64_t)g * TAIL_NW * TAIL_TRACE_TILES * TAIL_NSTAMP * 8 : 0);
 }
 
-extern "C" int tsrl_ppo_tail(const float* h1frag, int64_t n, const int64_t* idx,
-                             const tsrl_tail_weights* wt, int64_t act_dim, const float* act,
-                             const float* logp_old, const float* adv, const float* ret,
-                             const float* v_s, const double* adv_sums, tsrl_ppo_params prm,
-                             float* dz1, const tsrl_tail_grads* grads, double* sums,
-                             void* workspace, int64_t ws_bytes, void* stream) {
+static int ppo_tail_impl(const float* h1frag, int64_t n, const int64_t* idx,
+                         const tsrl_tail_weights* wt, int64_t act_dim, const float* act,
+                         const float* logp_old, const float* adv, const float* ret,
+                         const float* v_s, const double* adv_sums, tsrl_ppo_params prm,
+                         float* dz1, const tsrl_tail_grads* grads, double* sums,
+                         void* workspace, int64_t ws_bytes, TailFin fin, void* stream) {
     TSRL_CHECK_ARG(n > 0 && act_dim > 0 && act_dim <= AMAX,
                    "tsrl_ppo_tail: need n > 0 and 0 < act_dim <= %d", AMAX);
     TSRL_CHECK_ARG(h1frag && wt && grads && act && logp_old && adv && ret && dz1 && sums &&
@@ -1495,9 +1526,34 @@ extern "C" int tsrl_ppo_tail(const float* h1frag, int64_t n, const int64_t* idx,
     TailGrads gg{grads->w2a, grads->b2a, grads->w2c, grads->b2c, grads->w3a, grads->b3a,
                  grads->w3c, grads->b3c};
     hipLaunchKernelGGL(tail_reduce_kernel, dim3((SL_F + 63) / 64 + 1), dim3(256), 0,
-                       as_stream(stream), slab_f, slab_d, g, (int)act_dim, gg, sums);
+                       as_stream(stream), slab_f, slab_d, g, (int)act_dim, gg, sums, fin);
     TSRL_LAUNCH_CHECK("tsrl_ppo_tail(reduce)");
     return 0;
+}
+
+extern "C" int tsrl_ppo_tail(const float* h1frag, int64_t n, const int64_t* idx,
+                             const tsrl_tail_weights* wt, int64_t act_dim, const float* act,
+                             const float* logp_old, const float* adv, const float* ret,
+                             const float* v_s, const double* adv_sums, tsrl_ppo_params prm,
+                             float* dz1, const tsrl_tail_grads* grads, double* sums,
+                             void* workspace, int64_t ws_bytes, void* stream) {
+    const TailFin fin{nullptr, nullptr, nullptr, 0.f, 0.f, 0.0};
+    return ppo_tail_impl(h1frag, n, idx, wt, act_dim, act, logp_old, adv, ret, v_s, adv_sums, prm,
+                         dz1, grads, sums, workspace, ws_bytes, fin, stream);
+}
+
+extern "C" int tsrl_ppo_tail_fin(const float* h1frag, int64_t n, const int64_t* idx,
+                                 const tsrl_tail_weights* wt, int64_t act_dim, const float* act,
+                                 const float* logp_old, const float* adv, const float* ret,
+                                 const float* v_s, const double* adv_sums, tsrl_ppo_params prm,
+                                 float* dz1, const tsrl_tail_grads* grads, double* sums,
+                                 void* workspace, int64_t ws_bytes, const float* log_std,
+                                 float* losses, float* grad_log_std, void* stream) {
+    TSRL_CHECK_ARG(log_std && losses && grad_log_std, "tsrl_ppo_tail_fin: null pointer");
+    const TailFin fin{log_std, losses, grad_log_std, (float)prm.vf_coef, (float)prm.ent_coef,
+                      1.0 / prm.b_global};
+    return ppo_tail_impl(h1frag, n, idx, wt, act_dim, act, logp_old, adv, ret, v_s, adv_sums, prm,
+                         dz1, grads, sums, workspace, ws_bytes, fin, stream);
 }
 
 extern "C" int64_t tsrl_mlp_dw_workspace_bytes(int64_t n, int64_t D) {

@@ -3,8 +3,9 @@
 // MLP keeps every parameter, gradient and Adam moment of the actor-critic in flat buffers
 // (policy/fused_mlp.py bind_adam), so torch's per-tensor foreach norm, scale and fused Adam
 // kernels (~50-60 us per minibatch, launch- and latency-bound on 57 763 parameters) become
-// three short launches: per-slice squared norms, Adam over 2048-element slices, and the
-// in-place gradient scaling.
+// one launch over 2048-element slices (each workgroup's squared slice norm, an in-kernel
+// hand-off of the slice norms, Adam) plus, on the last minibatch only, the in-place gradient
+// scaling.
 //
 //   norm  = ||g||_2 (f64 sum of squares), coef = max_norm / (norm + 1e-6) clamped at 1,
 //   g    *= coef                                   (clip_grad_norm_, torch/nn/utils/clip_grad.py)
@@ -52,7 +53,9 @@ __device__ __forceinline__ void split_store(const SplitOut& so, int64_t i, float
     o[2 * so.plane] = (__bf16)(r1 - (float)a1);
 }
 
-// Sum of squares of each 2048-element gradient slice (f64), one workgroup per slice.
+// Sum of squares of each 2048-element gradient slice (f64), one workgroup per slice, in the
+// order clip_adam_kernel's in-kernel form uses: the separate launch for grids too large to be
+// resident at once (more than 256 slices, 2^19 parameters).
 __global__ __launch_bounds__(OTPB) void norm_partials_kernel(const float* __restrict__ g,
                                                              int64_t n, double* partials) {
     __shared__ double red[OTPB / kWave];
@@ -75,18 +78,24 @@ __global__ __launch_bounds__(OTPB) void norm_partials_kernel(const float* __rest
     }
 }
 
-// Each workgroup updates its own 2048-element slice with the clip coefficient of the
-// partial norms; the last workgroup to finish (agent-scope ticket, as rms.hip) advances the
-// device step counter.
+// Each workgroup updates its own 2048-element slice with the clip coefficient of the slice
+// norms.  Clipping: every workgroup first publishes its slice's f64 sum of squares (per thread
+// the 8 elements in order, a wave reduction, the 4 waves in order) and arrives at ticket[1]
+// (agent-scope release); it then waits until all have arrived (acquire; at most 29
+// workgroups for the 57 763-parameter nets, all resident together) and folds the slice sums
+// in the same fixed order in every workgroup.  This replaces round 3's separate
+// norm_partials launch (5.5 us + a dependent boundary per minibatch) with a hand-off of one
+// memory round trip.  The last workgroup to finish (ticket[0]) advances the device step
+// counter and re-arms both tickets.
 __global__ __launch_bounds__(OTPB) void clip_adam_kernel(float* __restrict__ p,
                                                          float* __restrict__ g,
                                                          float* __restrict__ m,
                                                          float* __restrict__ v, int64_t n,
                                                          float* __restrict__ step, int64_t nstep,
-                                                         AdamArgs a, const double* __restrict__ partials,
+                                                         AdamArgs a, double* __restrict__ partials,
                                                          float* __restrict__ norm_out,
                                                          unsigned int* ticket, const float* __restrict__ lr_dev,
-                                                         SplitOut so) {
+                                                         SplitOut so, int fused_norm) {
     __shared__ float s_scale;
     const int t = threadIdx.x;
     const bool clip = a.max_norm > 0.0f;
@@ -105,12 +114,42 @@ __global__ __launch_bounds__(OTPB) void clip_adam_kernel(float* __restrict__ p,
         vr[q] = in ? v[i] : 0.0f;
         pr[q] = in ? p[i] : 0.0f;
     }
+    if (clip && fused_norm) {
+        __shared__ double red[OTPB / kWave];
+        double ss = 0.0;
+#pragma unroll
+        for (int q = 0; q < EPT; ++q) {
+            const double x = (double)gr[q];
+            ss += x * x;
+        }
+        ss = wave_sum(ss);
+        if ((t & (kWave - 1)) == 0) red[t / kWave] = ss;
+        __syncthreads();
+        if (t == 0) {
+            double tot = 0.0;
+            for (int w = 0; w < OTPB / kWave; ++w) tot += red[w];
+            __hip_atomic_store(&partials[blockIdx.x], tot, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&ticket[1], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            // bounded wait: every workgroup of this small grid is resident (the arrivals
+            // never depend on a workgroup that waits); the bound only turns an impossible
+            // hang into a wrong coefficient
+            for (uint32_t spin = 0; spin < (1u << 24); ++spin) {
+                if (__hip_atomic_load(&ticket[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >=
+                    gridDim.x)
+                    break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+    }
     if (clip) {
-        // the per-slice sums of squares of norm_partials_kernel, folded by wave 0 in the same
-        // fixed order in every workgroup (so every workgroup gets the identical coefficient)
+        __syncthreads();
+        // the slice sums folded by wave 0 in the same fixed order in every workgroup (so every
+        // workgroup gets the identical coefficient)
         if (t < kWave) {
             double ss = 0.0;
-            for (int64_t b = t; b < gridDim.x; b += kWave) ss += partials[b];
+            for (int64_t b = t; b < gridDim.x; b += kWave)
+                ss += __hip_atomic_load(&partials[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             ss = wave_sum(ss);
             if (t == 0) {
                 const float norm = (float)sqrt(ss);
@@ -155,6 +194,8 @@ __global__ __launch_bounds__(OTPB) void clip_adam_kernel(float* __restrict__ p,
                                                          __HIP_MEMORY_SCOPE_AGENT);
         if (done == gridDim.x - 1) {  // every workgroup has read step[0] and the gradients
             for (int64_t i = 0; i < nstep; ++i) step[i] = st;
+            // every workgroup has also passed the slice-norm wait (it precedes its ticket add)
+            __hip_atomic_store(&ticket[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
@@ -188,7 +229,10 @@ extern "C" int tsrl_clip_adam(float* param, float* grad, float* exp_avg, float* 
     const int64_t grid = (n + OCHUNK - 1) / OCHUNK;
     TSRL_CHECK_ARG(max_norm <= 0.0f || (norm_out && partials),
                    "tsrl_clip_adam: clipping needs partials and norm_out[2]");
-    if (max_norm > 0.0f) {
+    // the in-kernel slice-norm hand-off needs every workgroup resident at once: up to one
+    // slice per CU; larger parameter sets take the separate norm launch
+    const int fused_norm = grid <= 256;
+    if (max_norm > 0.0f && !fused_norm) {
         hipLaunchKernelGGL(norm_partials_kernel, dim3((unsigned)grid), dim3(OTPB), 0,
                            as_stream(stream), grad, n, partials);
         TSRL_LAUNCH_CHECK("tsrl_clip_adam (norm)");
@@ -205,7 +249,7 @@ extern "C" int tsrl_clip_adam(float* param, float* grad, float* exp_avg, float* 
     }
     hipLaunchKernelGGL(clip_adam_kernel, dim3((unsigned)grid), dim3(OTPB), 0,
                        as_stream(stream), param, grad, exp_avg, exp_avg_sq, n, step, nstep, a,
-                       partials, norm_out, ticket, lr_dev, so);
+                       partials, norm_out, ticket, lr_dev, so, fused_norm);
     TSRL_LAUNCH_CHECK("tsrl_clip_adam");
     if (max_norm > 0.0f && scale_grads) {
         const unsigned g2 = (unsigned)std::min<int64_t>((n + OTPB - 1) / OTPB, 1024);

@@ -19,6 +19,17 @@ __device__ __forceinline__ float box_val(uint64_t k, int64_t d) {
     return (float)(h >> 40) * 0x1p-23f - 1.0f;
 }
 
+// The action-coupled variant (SyntheticVectorEnv(act_coef=c), SURVEY.md §8d's env made to
+// read its action like a MuJoCo env does): a step's observation value is
+// f32(box_val + f32(c * a[d mod A])) with a the env's (remapped) action row; reset
+// observations are box_val.  Its values are no longer multiples of 2^-23, so obs_rms moments
+// of this env are general f64 sums.
+__device__ __forceinline__ float coupled_val(uint64_t k, int64_t d, float a, float c) {
+#pragma clang fp contract(off)
+    const float ca = c * a;
+    return box_val(k, d) + ca;
+}
+
 struct RowState {
     uint64_t key;
     int active;

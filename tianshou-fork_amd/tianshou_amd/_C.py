@@ -52,7 +52,7 @@ class CollectArgs(ctypes.Structure):
         ("env_seed", _u64), ("ep_len", _i64), ("ep_j", _p), ("ep_t", _p),
         ("raw", _p), ("reset_raw", _p), ("rew", _p), ("term", _p), ("trunc", _p), ("done", _p),
         ("workspace", _p), ("mean", _p), ("var", _p), ("snap_mean", _p), ("snap_var", _p),
-        ("count", _p), ("no_moments", _i64), ("rms_step", _i64),
+        ("count", _p), ("no_moments", _i64), ("rms_step", _i64), ("act_coef", ctypes.c_float),
     ]
 
 
@@ -95,6 +95,11 @@ _SIGS = {
                             ctypes.c_int),
     "tsrl_synth_box_step_reset": ([_i64, _i64, _u64, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p,
                                    _p, _p, _p], ctypes.c_int),
+    "tsrl_synth_box_step_act": ([_p, _i64, _i64, _u64, _i64, _p, _p, _p, _p, _p, _p, _p, _p,
+                                 _i64, ctypes.c_float, _p], ctypes.c_int),
+    "tsrl_synth_box_step_reset_act": ([_i64, _i64, _u64, _i64, _p, _p, _p, _p, _p, _p, _p, _p,
+                                       _p, _p, _p, _p, _i64, ctypes.c_float, _p],
+                                      ctypes.c_int),
     "tsrl_rms_merge2": ([_p, _p, _p, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p],
                         ctypes.c_int),
     "tsrl_synth_box_reset": ([_p, _p, _i64, _i64, _u64, _i64, _p, _p, _p, _p, _p], ctypes.c_int),
@@ -171,6 +176,9 @@ _SIGS = {
     "tsrl_ppo_tail": ([_p, _i64, _p, ctypes.POINTER(TailWeights), _i64, _p, _p, _p, _p, _p, _p,
                        PPOParams, _p, ctypes.POINTER(TailGrads), _p, _p, _i64, _p],
                       ctypes.c_int),
+    "tsrl_ppo_tail_fin": ([_p, _i64, _p, ctypes.POINTER(TailWeights), _i64, _p, _p, _p, _p, _p,
+                           _p, PPOParams, _p, ctypes.POINTER(TailGrads), _p, _p, _i64, _p, _p,
+                           _p, _p], ctypes.c_int),
     "tsrl_ppo_eval": ([_p, _i64, ctypes.POINTER(TailWeights), _i64, _p, _p, _p, _p],
                       ctypes.c_int),
     "tsrl_mlp_dw_workspace_bytes": ([_i64, _i64], _i64),

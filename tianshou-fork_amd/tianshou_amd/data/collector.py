@@ -278,7 +278,9 @@ class Collector:
         # after the data-parallel all-reduce -- must stay <= 2^17
         rms = norm.obs_rms
         world = rms.dp.world if (rms.dp is not None and rms.dp.active) else 1
-        if kk * world > 1 << 17:
+        if kk * world > 1 << 17 and b.act_coef == 0.0:
+            return False
+        if b.act_coef != 0.0 and self._act_spec()[0] != (b.act_dim,):
             return False
         buf = self.buffer
         buf._alloc_storage(b.obs_shape, b.obs_torch_dtype, *self._act_spec())
@@ -313,6 +315,7 @@ class Collector:
         assert self.policy.fused_collect_fill(c, (sc[p, 1:2], sc[1 - p, 1:2]))
         c.act, c.act_remap = _C.ptr(s["act"]), _C.ptr(s["act_remap"])
         c.env_seed, c.ep_len = b.seed_, b.ep_len
+        c.act_coef = b.act_coef  # != 0: the action-coupled env (env after the actor, f64 moments)
         c.ep_j, c.ep_t = _C.ptr(b.ep_j), _C.ptr(b.ep_t)
         c.raw, c.reset_raw = _C.ptr(s["raw"]), _C.ptr(s["reset_raw"])
         c.rew, c.term, c.trunc, c.done = (_C.ptr(s[x]) for x in ("rew", "term", "trunc", "done"))
@@ -333,7 +336,8 @@ class Collector:
             # (the slot carries its own step-row count, so unequal env shards merge right)
             off = int(_C.lib().tsrl_collect_totals_offset(self._rms_step))
             n = 4 * b.obs_numel + 2
-            rms.dp.all_reduce_(ws[off:off + 8 * n].view(torch.int64), kind="obs_rms")
+            rms.dp.all_reduce_(ws[off:off + 8 * n].view(torch.float64 if b.act_coef
+                                                        else torch.int64), kind="obs_rms")
         # deferred merge: the next launch (or _flush's tsrl_collect_rms_finalize) merges this
         # step's obs_rms moments
         self._rms_chain = None if rms.exact else c
@@ -395,7 +399,7 @@ class Collector:
             blk = s["blk_done"]
             b._step_reset_raw(kk, raw, s["reset_raw"][:kk], rew, term, trunc, done,
                               s["part"] if upd else None, s["part2"] if upd else None,
-                              blk if upd else None)
+                              blk if upd else None, action=action_remap)
             rms = norm_obj.obs_rms if norm_obj is not None else None
             if upd and rms.exact:
                 rms.exact_update(raw, None, s["reset_raw"][:kk], done, snapshot=True)

@@ -46,14 +46,20 @@ class DeviceVectorEnv:
 
 class SyntheticVectorEnv(DeviceVectorEnv):
     """Box(obs_dim) f32 or u8 (e.g. 4x84x84) observations, Box(act_dim) or Discrete actions;
-    episode length ``ep_len``; even envs terminate, odd envs truncate; actions are ignored."""
+    episode length ``ep_len``; even envs terminate, odd envs truncate; actions are ignored
+    unless ``act_coef`` is set."""
 
     def __init__(self, num_envs: int, obs_shape, act_dim: int = 1, ep_len: int = 1000,
                  seed: int = 0, device=None, obs_dtype=np.float32, discrete: bool = False,
-                 frame_stack: int = 1):
+                 frame_stack: int = 1, act_coef: float = 0.0):
         """``frame_stack`` S > 1 (u8 only): obs_shape = (S, *frame) holds the last S frames
         like gymnasium's FrameStack wrapper (the Atari setup of
-        examples/atari/atari_wrapper.py), so a save_only_last_obs buffer rebuilds it."""
+        examples/atari/atari_wrapper.py), so a save_only_last_obs buffer rebuilds it.
+        ``act_coef`` c != 0 (Box f32 obs and actions only): the env reads its action, as a
+        MuJoCo env does -- a step's observation is f32(box + f32(c * a[d mod act_dim])) of
+        the remapped action a (csrc/synth.h coupled_val).  Its observations are then not
+        2^-23-quantised and its transition depends on the action, so the fused collect step
+        runs the env after the actor and sums obs_rms moments in f64."""
         self.env_num = int(num_envs)
         self.obs_shape = tuple(np.atleast_1d(obs_shape).tolist())
         self.obs_numel = int(np.prod(self.obs_shape))
@@ -73,6 +79,20 @@ class SyntheticVectorEnv(DeviceVectorEnv):
         self.ep_t = torch.zeros(self.env_num, dtype=torch.int64, device=self.device)
         self.obs_torch_dtype = torch.uint8 if self.u8 else torch.float32
         self.nblk = int(_C.lib().tsrl_env_num_partials(self.env_num))
+        self.act_coef = float(act_coef)
+        self.act_dim = int(act_dim)
+        assert self.act_coef == 0.0 or (not self.u8 and not discrete), \
+            "act_coef needs Box observations and Box actions"
+
+    def _act_arg(self, action, k: int):
+        """(pointer, act_dim) of the f32 [k, act_dim] action rows the coupled env reads."""
+        if self.act_coef == 0.0:
+            return None, 1
+        assert action is not None, "the action-coupled env needs the step's actions"
+        a = torch.as_tensor(action, device=self.device, dtype=torch.float32)
+        a = a.reshape(k, self.act_dim).contiguous()
+        self._act_keep = a  # alive until the launch is enqueued (and graph replays)
+        return _C.ptr(a), self.act_dim
 
     # -- fused hooks ---------------------------------------------------------------------------
     def nblk_for(self, k: int) -> int:
@@ -98,24 +118,28 @@ class SyntheticVectorEnv(DeviceVectorEnv):
                                           _C.ptr(obs_out), _C.ptr(rew_out), _C.ptr(term_out),
                                           _C.ptr(trunc_out), s), "tsrl_synth_u8_step")
         else:
-            _C.check(L.tsrl_synth_box_step(_C.ptr(ids), k, self.obs_numel, self.seed_,
-                                           self.ep_len, _C.ptr(self.ep_j), _C.ptr(self.ep_t),
-                                           _C.ptr(obs_out), _C.ptr(rew_out), _C.ptr(term_out),
-                                           _C.ptr(trunc_out), _C.ptr(partials), s),
-                     "tsrl_synth_box_step")
+            ap, ad = self._act_arg(action, k)
+            _C.check(L.tsrl_synth_box_step_act(_C.ptr(ids), k, self.obs_numel, self.seed_,
+                                               self.ep_len, _C.ptr(self.ep_j), _C.ptr(self.ep_t),
+                                               _C.ptr(obs_out), _C.ptr(rew_out), _C.ptr(term_out),
+                                               _C.ptr(trunc_out), _C.ptr(partials), ap, ad,
+                                               self.act_coef, s), "tsrl_synth_box_step")
 
     @property
     def supports_step_reset(self) -> bool:
         return not self.u8
 
     def _step_reset_raw(self, k: int, obs_out, reset_out, rew_out, term_out, trunc_out,
-                        done_out, partials=None, partials_reset=None, blk_done=None) -> None:
+                        done_out, partials=None, partials_reset=None, blk_done=None,
+                        action=None) -> None:
         """Step all k envs and reset the finished ones in one launch (f32 obs only)."""
-        _C.check(_C.lib().tsrl_synth_box_step_reset(
+        ap, ad = self._act_arg(action, k)
+        _C.check(_C.lib().tsrl_synth_box_step_reset_act(
             k, self.obs_numel, self.seed_, self.ep_len, _C.ptr(self.ep_j), _C.ptr(self.ep_t),
             _C.ptr(obs_out), _C.ptr(reset_out), _C.ptr(rew_out), _C.ptr(term_out),
             _C.ptr(trunc_out), _C.ptr(done_out), _C.ptr(partials), _C.ptr(partials_reset),
-            _C.ptr(blk_done), _C.stream_ptr(self.device)), "tsrl_synth_box_step_reset")
+            _C.ptr(blk_done), ap, ad, self.act_coef, _C.stream_ptr(self.device)),
+            "tsrl_synth_box_step_reset")
 
     def _reset_raw(self, ids: Optional[torch.Tensor], mask: Optional[torch.Tensor], k: int,
                    obs_out, partials=None) -> None:

@@ -181,7 +181,7 @@ class FlatAdam:
             o += k
         self._adam = dict(optim=optim, p=flat_p, m=flat_m, v=flat_v, steps=steps, pviews=pviews,
                           mviews=mviews, vviews=vviews,
-                          ticket=torch.zeros(1, dtype=torch.int32, device=dev),
+                          ticket=torch.zeros(2, dtype=torch.int32, device=dev),
                           partials=torch.zeros(
                               max(int(_C.lib().tsrl_clip_adam_partials(n)), 1),
                               dtype=torch.float64, device=dev),

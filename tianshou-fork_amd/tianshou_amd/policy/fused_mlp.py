@@ -264,17 +264,25 @@ class FusedActorCritic(FlatAdam):
         sums = self._buf("sums", 4 + A, torch.float64)[:4 + A]
         wsb = int(lib.tsrl_ppo_tail_workspace_bytes(b))
         ws = self._buf("tail_ws", wsb, torch.uint8)
-        _C.check(lib.tsrl_ppo_tail(
-            _C.ptr(h1), b, ip, self._tail_w, A, _C.ptr(act), _C.ptr(logp_old), _C.ptr(adv),
-            _C.ptr(ret), _C.ptr(v_s), _C.ptr(adv_sums) if adv_sums is not None else None,
-            params, _C.ptr(dz1), self._tail_grads, _C.ptr(sums), _C.ptr(ws), wsb, s),
-            "tsrl_ppo_tail")
+        args = (_C.ptr(h1), b, ip, self._tail_w, A, _C.ptr(act), _C.ptr(logp_old), _C.ptr(adv),
+                _C.ptr(ret), _C.ptr(v_s), _C.ptr(adv_sums) if adv_sums is not None else None,
+                params, _C.ptr(dz1), self._tail_grads, _C.ptr(sums), _C.ptr(ws), wsb)
+        terms = None
+        if dp.active:
+            _C.check(lib.tsrl_ppo_tail(*args, s), "tsrl_ppo_tail")
+        else:
+            # single process: the loss finalisation rides the tail's reduction launch
+            terms = torch.empty(4, dtype=torch.float32, device=dev)
+            _C.check(lib.tsrl_ppo_tail_fin(*args, _C.ptr(L["sigma"]), _C.ptr(terms),
+                                           _C.ptr(L["sigma"].grad), s), "tsrl_ppo_tail_fin")
         wsb2 = int(lib.tsrl_mlp_dw_workspace_bytes(b, D))
         ws2 = self._buf("dw_ws", wsb2, torch.uint8)
         _C.check(lib.tsrl_mlp_dw(
             _C.ptr(dz1), _C.ptr(obs), ldx, ip, b, D, _C.ptr(L["w1a"].weight.grad),
             _C.ptr(L["w1a"].bias.grad), _C.ptr(L["w1c"].weight.grad),
             _C.ptr(L["w1c"].bias.grad), _C.ptr(ws2), wsb2, s), "tsrl_mlp_dw")
+        if terms is not None:
+            return terms
         return self._reduce_finalize(sums, params, dp)
 
     def _empty_minibatch(self, params, dp, adv_sums) -> torch.Tensor:
