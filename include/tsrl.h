@@ -236,6 +236,11 @@ typedef struct tsrl_add_args {
      * source then points at frame stack-1 of row 0 and the pitch is the whole row. */
     int64_t obs_src_pitch;
     int64_t obs_next_src_pitch;
+    /* destination row pitch of obs_dst / obs_next_dst / obs_next_dst_raw in bytes (0: the row
+     * size): the storage of wide f32 observations is padded to a 128-byte multiple
+     * (VectorReplayBuffer, e.g. 376 -> 384 floats) so the learn kernels' row gathers start on
+     * a cache line; the pad columns stay zero. */
+    int64_t obs_dst_pitch;
 } tsrl_add_args;
 int tsrl_buffer_add(const tsrl_add_args* a, void* stream);
 
@@ -287,6 +292,7 @@ typedef struct tsrl_collect_args {
     int64_t no_moments;      /* exact obs_rms: no moments (see above); 0: the deferred merge */
     int64_t rms_step;        /* index of this launch in its chain of deferred steps (0: the
                                 first after tsrl_collect_rms_finalize or a fresh workspace) */
+    int64_t obs_pitch;       /* obs_dst row pitch in floats (0: dim) */
     float act_coef;          /* 0: the quantised synthetic env (action-independent; int64
                                 totals); c != 0: the action-coupled env (synth.h coupled_val:
                                 env phase after the actor, f64 totals; the act_dim action
@@ -419,6 +425,9 @@ int tsrl_shuffle_apply(const uint32_t* draws, int64_t n, int64_t* out, void* wor
  * buffer/base.py:360-389). */
 int tsrl_gather_rows(const void* src, int64_t row_bytes, const int64_t* idx, int64_t k,
                      void* dst, void* stream);
+/* The same from a source whose rows are src_pitch bytes apart (a padded buffer storage). */
+int tsrl_gather_rows_pitched(const void* src, int64_t src_pitch, int64_t row_bytes,
+                             const int64_t* idx, int64_t k, void* dst, void* stream);
 
 /* out[c] = sum_r x[r][c] for a row-major f32 [rows, cols] matrix: the bias gradients
  * (db = sum over the minibatch of dY) and the reduction of the split-K partial products of

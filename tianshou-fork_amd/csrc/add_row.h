@@ -36,15 +36,16 @@ __device__ __forceinline__ void add_row_copies(const tsrl_add_args& a, int64_t r
                                                int64_t ptr, int nl) {
     const int64_t obs_pitch = a.obs_src_pitch ? a.obs_src_pitch : a.obs_row_bytes;
     const int64_t next_pitch = a.obs_next_src_pitch ? a.obs_next_src_pitch : a.obs_row_bytes;
+    const int64_t dst_pitch = a.obs_dst_pitch ? a.obs_dst_pitch : a.obs_row_bytes;
     if (a.obs_src && a.obs_dst)
         copy_row((const char*)a.obs_src + r * obs_pitch,
-                 (char*)a.obs_dst + ptr * a.obs_row_bytes, a.obs_row_bytes, lane, nl);
+                 (char*)a.obs_dst + ptr * dst_pitch, a.obs_row_bytes, lane, nl);
     if (a.act_src && a.act_dst)
         copy_row((const char*)a.act_src + r * a.act_row_bytes,
                  (char*)a.act_dst + ptr * a.act_row_bytes, a.act_row_bytes, lane, nl);
     if (a.obs_next_src_raw && a.obs_next_dst_raw)
         copy_row((const char*)a.obs_next_src_raw + r * next_pitch,
-                 (char*)a.obs_next_dst_raw + ptr * a.obs_row_bytes, a.obs_row_bytes, lane, nl);
+                 (char*)a.obs_next_dst_raw + ptr * dst_pitch, a.obs_row_bytes, lane, nl);
 }
 
 // The lane-0 part of add_row: flags, env id and the episode bookkeeping of row r, split
@@ -116,7 +117,8 @@ __device__ __forceinline__ void add_row(const tsrl_add_args& a, int64_t r, int l
     add_row_copies(a, r, lane, ptr, nl);
     if (a.obs_next_src && (a.obs_next_dst || a.cur_obs)) {
         const float* src = a.obs_next_src + r * a.obs_dim;
-        float* dst = a.obs_next_dst ? a.obs_next_dst + ptr * a.obs_dim : nullptr;
+        const int64_t dpitch = a.obs_dst_pitch ? a.obs_dst_pitch / 4 : a.obs_dim;
+        float* dst = a.obs_next_dst ? a.obs_next_dst + ptr * dpitch : nullptr;
         float* cur = a.cur_obs ? a.cur_obs + r * a.obs_dim : nullptr;
         const bool nrm = a.norm_mean != nullptr;
         const bool rst = a.reset_mask && a.reset_mask[r];

@@ -24,14 +24,15 @@ __global__ __launch_bounds__(TPB) void buffer_add_kernel(tsrl_add_args a) {
     if (a.rel_next && blockIdx.x == 0 && threadIdx.x == 0) *a.rel_next = (urel + 1) % a.ring_size;
 }
 
-__global__ __launch_bounds__(TPB) void gather_rows_kernel(const char* src, int64_t row_bytes,
+__global__ __launch_bounds__(TPB) void gather_rows_kernel(const char* src, int64_t src_pitch,
+                                                          int64_t row_bytes,
                                                           const int64_t* idx, int64_t k,
                                                           char* dst) {
     const int lane = threadIdx.x & (kWave - 1);
     const int64_t nw = (int64_t)gridDim.x * ROWS_PER_BLOCK;
     for (int64_t r = (int64_t)blockIdx.x * ROWS_PER_BLOCK + threadIdx.x / kWave; r < k;
          r += nw) {
-        copy_row(src + idx[r] * row_bytes, dst + r * row_bytes, row_bytes, lane);
+        copy_row(src + idx[r] * src_pitch, dst + r * row_bytes, row_bytes, lane);
     }
 }
 
@@ -173,14 +174,20 @@ extern "C" int tsrl_buffer_add(const tsrl_add_args* a, void* stream) {
     return 0;
 }
 
-extern "C" int tsrl_gather_rows(const void* src, int64_t row_bytes, const int64_t* idx,
-                                int64_t k, void* dst, void* stream) {
-    TSRL_CHECK_ARG(k >= 0 && row_bytes > 0, "tsrl_gather_rows: bad sizes");
+extern "C" int tsrl_gather_rows_pitched(const void* src, int64_t src_pitch, int64_t row_bytes,
+                                        const int64_t* idx, int64_t k, void* dst, void* stream) {
+    TSRL_CHECK_ARG(k >= 0 && row_bytes > 0 && src_pitch >= row_bytes,
+                   "tsrl_gather_rows: bad sizes");
     if (k == 0) return 0;
     TSRL_CHECK_ARG(src && idx && dst, "tsrl_gather_rows: null pointer");
     const int64_t grid = std::min<int64_t>((k + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK, 16384);
     hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)grid), dim3(TPB), 0, as_stream(stream),
-                       (const char*)src, row_bytes, idx, k, (char*)dst);
+                       (const char*)src, src_pitch, row_bytes, idx, k, (char*)dst);
     TSRL_LAUNCH_CHECK("tsrl_gather_rows");
     return 0;
+}
+
+extern "C" int tsrl_gather_rows(const void* src, int64_t row_bytes, const int64_t* idx,
+                                int64_t k, void* dst, void* stream) {
+    return tsrl_gather_rows_pitched(src, row_bytes, row_bytes, idx, k, dst, stream);
 }

@@ -439,7 +439,8 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
             // rows, the live obs of a reset env with those after the reset rows (add_row)
             if (arow) {
                 const int64_t aptr = ad.ptr ? aptr_ld : aptr_ld + urel;
-                float4* dst = reinterpret_cast<float4*>(ad.obs_next_dst + aptr * D);
+                float4* dst = reinterpret_cast<float4*>(
+                    ad.obs_next_dst + aptr * (ad.obs_dst_pitch ? ad.obs_dst_pitch / 4 : D));
                 const float eps = ad.norm_eps, clip = ad.norm_clip;
 #pragma unroll
                 for (int j = 0; j < AQ; ++j) {
@@ -563,9 +564,10 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         s_row[t] = a.obs_offset[r0 + t] + urel;
     }
     LDS_SYNC();
+    const int64_t opitch = a.obs_pitch ? a.obs_pitch : D;
     for (int i = t; i < nrows * D; i += NT) {
         const int rw = i / D, c = i - rw * D;
-        row_store1(&a.obs_dst[s_row[rw] * D + c], sX[c * XP + rw]);
+        row_store1(&a.obs_dst[s_row[rw] * opitch + c], sX[c * XP + rw]);
     }
     // ---- C. env step + auto-reset of these rows (env.hip box_step_reset_kernel) -------------
     // The quantised synthetic env's transition does not read the action, so its step runs
@@ -892,6 +894,9 @@ extern "C" int tsrl_collect_box_step(const tsrl_collect_args* a, void* stream) {
                    "tsrl_collect_box_step: 0 < act_dim <= %d, bound_method 0..2", AMAX);
     TSRL_CHECK_ARG(a->obs_dst && a->obs_offset && (a->obs_rel_dev || a->obs_uniform_rel >= 0),
                    "tsrl_collect_box_step: obs_dst / obs_offset / this step's ring position");
+    TSRL_CHECK_ARG(a->obs_pitch == 0 || a->obs_pitch >= D, "tsrl_collect_box_step: obs_pitch < dim");
+    TSRL_CHECK_ARG(a->add.k == 0 || a->add.obs_dst_pitch % 16 == 0,
+                   "tsrl_collect_box_step: add.obs_dst_pitch must keep rows 16-byte aligned");
     TSRL_CHECK_ARG(a->cur && a->w1p && a->b1 && a->w2 && a->b2 && a->w3 && a->b3 && a->log_std &&
                        a->act && a->act_remap && a->ep_j && a->ep_t && a->raw && a->reset_raw &&
                        a->rew && a->term && a->trunc && a->done && a->workspace && a->mean &&

@@ -379,7 +379,7 @@ __device__ __forceinline__ void glds16(const void* src, uint32_t lds) {
 template <bool TANH>
 __global__ __launch_bounds__(RNW * 64, 1) void l1_ring_kernel(
     const float* __restrict__ X, int64_t ldx, const int64_t* __restrict__ idx, int64_t n,
-    int64_t ntiles, int Kp, const __bf16* __restrict__ wsp, const float* __restrict__ ba,
+    int64_t ntiles, int Kp, int dq, const __bf16* __restrict__ wsp, const float* __restrict__ ba,
     const float* __restrict__ bc, float* __restrict__ out, int64_t frag_tiles) {
     __shared__ __attribute__((aligned(16))) char sm[RLDS];
     const int t = threadIdx.x;
@@ -447,8 +447,9 @@ __global__ __launch_bounds__(RNW * 64, 1) void l1_ring_kernel(
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             int k = px_kc * KC + xoff[i];
-            // past the row (last chunk only): a finite value that meets zero weights
-            if (last) k = k < ldx ? k : 0;
+            // past the row's data (last chunk only; dq = roundup(D, 4)): column 0, a finite
+            // value that meets zero weights -- a padded row pitch (ldx > dq) is never read
+            if (last) k = k < dq ? k : 0;
             glds16(xb[i] + k, st + (uint32_t)(i * 8 * XROWB));
         }
         px_s = px_s == RXS - 1 ? 0 : px_s + 1;
@@ -686,11 +687,13 @@ extern "C" int tsrl_mlp_l1_fwd_x6(const float* X, int64_t ldx, const int64_t* id
         if (act_tanh)
             hipLaunchKernelGGL(l1_ring_kernel<true>, dim3(grid), dim3(RNW * 64), 0,
                                as_stream(stream), X, ldx, idx, n, ntiles, (int)kpad32(D),
-                               reinterpret_cast<const __bf16*>(wsplit), ba, bc, out, frag_tiles);
+                               (int)((D + 3) / 4 * 4), reinterpret_cast<const __bf16*>(wsplit),
+                               ba, bc, out, frag_tiles);
         else
             hipLaunchKernelGGL(l1_ring_kernel<false>, dim3(grid), dim3(RNW * 64), 0,
                                as_stream(stream), X, ldx, idx, n, ntiles, (int)kpad32(D),
-                               reinterpret_cast<const __bf16*>(wsplit), ba, bc, out, frag_tiles);
+                               (int)((D + 3) / 4 * 4), reinterpret_cast<const __bf16*>(wsplit),
+                               ba, bc, out, frag_tiles);
         TSRL_LAUNCH_CHECK("tsrl_mlp_l1_fwd_x6(ring)");
         return 0;
     }

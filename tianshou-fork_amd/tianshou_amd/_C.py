@@ -37,6 +37,7 @@ class AddArgs(ctypes.Structure):
         ("stat_rew", _p), ("stat_len", _p), ("stat_idx", _p),
         ("reset_src", _p), ("reset_mask", _p), ("reset_mean", _p), ("reset_var", _p),
         ("rel_next", _p), ("obs_src_pitch", _i64), ("obs_next_src_pitch", _i64),
+        ("obs_dst_pitch", _i64),
     ]
 
 
@@ -52,7 +53,8 @@ class CollectArgs(ctypes.Structure):
         ("env_seed", _u64), ("ep_len", _i64), ("ep_j", _p), ("ep_t", _p),
         ("raw", _p), ("reset_raw", _p), ("rew", _p), ("term", _p), ("trunc", _p), ("done", _p),
         ("workspace", _p), ("mean", _p), ("var", _p), ("snap_mean", _p), ("snap_var", _p),
-        ("count", _p), ("no_moments", _i64), ("rms_step", _i64), ("act_coef", ctypes.c_float),
+        ("count", _p), ("no_moments", _i64), ("rms_step", _i64), ("obs_pitch", _i64),
+        ("act_coef", ctypes.c_float),
     ]
 
 
@@ -121,6 +123,7 @@ _SIGS = {
     "tsrl_collect_rms_finalize": ([ctypes.POINTER(CollectArgs), _p], ctypes.c_int),
     "tsrl_collect_totals_offset": ([_i64], _i64),
     "tsrl_gather_rows": ([_p, _i64, _p, _i64, _p, _p], ctypes.c_int),
+    "tsrl_gather_rows_pitched": ([_p, _i64, _i64, _p, _i64, _p, _p], ctypes.c_int),
     "tsrl_np_shuffle_draws": ([_p, _p, _i64, _p], ctypes.c_int),
     "tsrl_shuffle_apply_workspace_bytes": ([_i64], _i64),
     "tsrl_shuffle_apply": ([_p, _i64, _p, _p, _i64, _p], ctypes.c_int),
@@ -239,3 +242,16 @@ def ptr(t, dtype=None):
     if not t.is_contiguous():
         raise ValueError("libtsrl kernels need contiguous tensors")
     return t.data_ptr()
+
+
+def ptr_rows(t):
+    """Device pointer of a HIP tensor whose ROWS are contiguous, the rows possibly further
+    apart than their length (a padded storage view [n, d] of [n, pitch]; the caller passes
+    the pitch, ``t.stride(0)``, to the kernel)."""
+    if t is None:
+        return None
+    if t.dim() >= 2 and t[0].is_contiguous() and t.stride(0) >= t[0].numel():
+        if t.device.type != "cuda":
+            raise TsrlError(f"libtsrl kernels need HIP device tensors; got a tensor on {t.device}")
+        return t.data_ptr()
+    return ptr(t)

@@ -27,6 +27,13 @@ def gather_rows(t: torch.Tensor, index) -> torch.Tensor:
     if k == 0:
         return out
     row_bytes = t.element_size() * (t[0].numel() if t.dim() > 1 else 1)
+    if t.dim() >= 2 and t[0].is_contiguous() and t.stride(0) > t[0].numel():
+        # rows of a padded storage (VectorReplayBuffer pads wide f32 observation rows to a
+        # 128-byte multiple): gathered in place, no copy of the storage
+        _C.check(_C.lib().tsrl_gather_rows_pitched(
+            _C.ptr(t), t.stride(0) * t.element_size(), row_bytes, _C.ptr(index), k,
+            _C.ptr(out), _C.stream_ptr()), "tsrl_gather_rows")
+        return out
     src = t if t.is_contiguous() else t.contiguous()
     _C.check(_C.lib().tsrl_gather_rows(_C.ptr(src), row_bytes, _C.ptr(index), k, _C.ptr(out),
                                        _C.stream_ptr()), "tsrl_gather_rows")

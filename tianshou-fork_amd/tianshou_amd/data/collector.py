@@ -309,7 +309,8 @@ class Collector:
         c.k, c.dim, c.cur = kk, b.obs_numel, _C.ptr(cur)
         # this step's stored obs rows come from the launch itself (the live obs never
         # round-trips through HBM between fused steps); the adds then copy no obs
-        c.obs_dst, c.obs_offset = _C.ptr(buf._meta.obs), _C.ptr(buf._dev["offset"])
+        c.obs_dst, c.obs_offset = _C.ptr_rows(buf._meta.obs), _C.ptr(buf._dev["offset"])
+        c.obs_pitch = buf._meta.obs.stride(0)  # padded storage rows (buffer.py obs_storage)
         c.obs_rel_dev = _C.ptr(add_kw.get("rel_dev"))
         c.obs_uniform_rel = int(add_kw.get("uniform_rel", 0))
         assert self.policy.fused_collect_fill(c, (sc[p, 1:2], sc[1 - p, 1:2]))

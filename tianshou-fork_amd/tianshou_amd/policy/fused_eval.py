@@ -103,8 +103,12 @@ class FusedEvalMixin:
             return self._eval_values_shared(batch, obs, obs_next, buffer, indices)
         if self._mlp is None or not obs.is_cuda or obs.dtype != torch.float32 or obs.dim() != 2:
             return super()._eval_values(batch, obs, obs_next, buffer, indices)
-        obs = obs.contiguous()
-        obs_next = obs_next.contiguous()
+        # rows must be contiguous, not the whole tensor: the buffer's padded storage views
+        # (128-byte row pitch) are read in place (a .contiguous() here copied 12.6 GB)
+        if obs.stride(-1) != 1 or obs.stride(0) < obs.shape[1]:
+            obs = obs.contiguous()
+        if obs_next.stride(-1) != 1 or obs_next.stride(0) < obs_next.shape[1]:
+            obs_next = obs_next.contiguous()
         n = obs.shape[0]
         act = torch.as_tensor(batch.act, device=obs.device).to(torch.float32).reshape(n, -1)
         v_s, logp = self._mlp.evaluate(obs, act.contiguous())

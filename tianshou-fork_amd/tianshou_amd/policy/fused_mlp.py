@@ -154,9 +154,15 @@ class FusedActorCritic(FlatAdam):
                  "tsrl_mlp_split_w")
 
     def rows(self, obs: torch.Tensor, key: str = "xpad") -> torch.Tensor:
-        """The observation rows as the kernels read them: obs itself when D % 4 == 0, else a
-        zero-padded [n, roundup(D, 4)] copy in a persistent buffer (stable address: the
-        captured learn graph reads it)."""
+        """The observation rows as the kernels read them (row pitch = ``stride(0)``, the
+        kernels' ldx): obs itself when its rows are contiguous, 16-byte aligned and at least
+        roundup(D, 4) floats apart -- a padded VectorReplayBuffer storage view included (no
+        copy; the kernels read no column past roundup(D, 4)) -- else a zero-padded
+        [n, roundup(D, 4)] copy in a persistent buffer (stable address: the captured learn
+        graph reads it)."""
+        if (obs.dim() == 2 and obs.stride(1) == 1 and obs.stride(0) >= self.Dp and
+                obs.stride(0) % 4 == 0 and obs.data_ptr() % 16 == 0 and obs.shape[0] > 0):
+            return obs
         if self.Dp == self.D:
             return obs.contiguous()
         n = obs.shape[0]
@@ -179,7 +185,7 @@ class FusedActorCritic(FlatAdam):
         D, A = self.D, self.A
         assert obs.dim() == 2 and obs.shape[1] == D
         obs = self.rows(obs, "xpad_eval")
-        ldx = obs.shape[1]
+        ldx = obs.stride(0)
         n = obs.shape[0] if idx is None else idx.numel()
         values = torch.empty(n, dtype=torch.float32, device=dev)
         logp = torch.empty(n, dtype=torch.float32, device=dev) if act is not None else None
@@ -243,8 +249,8 @@ class FusedActorCritic(FlatAdam):
         dev = obs.device
         s = _C.stream_ptr(dev)
         D, A = self.D, self.A
-        assert obs.dim() == 2 and obs.shape[1] == self.Dp and obs.is_contiguous()
-        ldx = self.Dp
+        assert obs.dim() == 2 and obs.stride(1) == 1 and obs.stride(0) >= self.Dp
+        ldx = obs.stride(0)
         assert act.shape[-1] == A and act.is_contiguous()
         ip = _C.ptr(idx) if idx is not None else None
         if b == 0:
@@ -259,7 +265,7 @@ class FusedActorCritic(FlatAdam):
                      "tsrl_reduce_partials")
             dp.all_reduce_(adv_sums, kind="adv_moments")
         h1 = self._buf("h1", int(lib.tsrl_mlp_frag_floats(b)))
-        self._l1_fwd(_C.ptr(obs), ldx, ip, b, _C.ptr(h1), 1, split=split_w)
+        self._l1_fwd(_C.ptr_rows(obs), ldx, ip, b, _C.ptr(h1), 1, split=split_w)
         dz1 = self._buf("dz1", b * 2 * 64)
         sums = self._buf("sums", 4 + A, torch.float64)[:4 + A]
         wsb = int(lib.tsrl_ppo_tail_workspace_bytes(b))
@@ -278,7 +284,7 @@ class FusedActorCritic(FlatAdam):
         wsb2 = int(lib.tsrl_mlp_dw_workspace_bytes(b, D))
         ws2 = self._buf("dw_ws", wsb2, torch.uint8)
         _C.check(lib.tsrl_mlp_dw(
-            _C.ptr(dz1), _C.ptr(obs), ldx, ip, b, D, _C.ptr(L["w1a"].weight.grad),
+            _C.ptr(dz1), _C.ptr_rows(obs), ldx, ip, b, D, _C.ptr(L["w1a"].weight.grad),
             _C.ptr(L["w1a"].bias.grad), _C.ptr(L["w1c"].weight.grad),
             _C.ptr(L["w1c"].bias.grad), _C.ptr(ws2), wsb2, s), "tsrl_mlp_dw")
         if terms is not None:
