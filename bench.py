@@ -80,6 +80,9 @@ def parse():
                          "not 2^-23-quantised): the fused collect step's general path (env "
                          "after the actor, f64 obs_rms moments); measures what the synthetic "
                          "env's two shortcuts buy")
+    ap.add_argument("--obs-pad", choices=["on", "off"], default="on",
+                    help="diagnostic: off stores the 376-float observation rows unpadded "
+                         "(VectorReplayBuffer.PAD_MIN; default: 128-byte row pitch)")
     ap.add_argument("--exact-obs-rms", action="store_true",
                     help="VectorEnvNormObs with the reference's f32 obs_rms arithmetic bit for "
                          "bit (sequential f32 column sums; opt-in, measures its cost)")
@@ -274,6 +277,8 @@ def main():
     from tianshou_amd.data import Collector, VectorReplayBuffer
     from tianshou_amd.env import SyntheticVectorEnv, VectorEnvNormObs
     from tianshou_amd.policy import PPOPolicy, base as pbase
+    if args.obs_pad == "off":
+        VectorReplayBuffer.PAD_MIN = 1 << 30
     from tianshou_amd.utils.models import fixed_std_normal, get_actor_critic, init_and_get_optim
 
     torch.manual_seed(0)  # identical network init on every rank (the policy also

@@ -64,8 +64,8 @@ def main():
     p.eps_clip, p.dual_clip, p.vf_coef, p.ent_coef, p.adv_eps = 0.2, 0.0, 0.25, 0.0, 1e-8
     p.b_global, p.value_clip, p.norm_adv = float(B), 0, 1
     dp = DataParallel()
-    fm.minibatch(obs[:, :D].contiguous() if ld != D else obs, idx, B, act, logp_old, adv, ret,
-                 v_s, p, dp)
+    obs_v = obs[:, :D]  # the padded-storage view when ld > D (rows read in place)
+    fm.minibatch(obs_v, idx, B, act, logp_old, adv, ret, v_s, p, dp)
     torch.cuda.synchronize()
     L = _C.lib()
     s = _C.stream_ptr(dev)
@@ -113,13 +113,13 @@ def main():
                                _C.ptr(ws2), ws2.numel(), s))
 
     def whole():
-        fm.minibatch(obs, idx, B, act, logp_old, adv, ret, v_s, p, dp)
+        fm.minibatch(obs_v, idx, B, act, logp_old, adv, ret, v_s, p, dp)
 
     EV = min(N, 1 << 21)
     flop_eval = 2.0 * EV * (D * 128 + 64 * 64 * 2 + 64 * (A + 1))
 
     def evaluate():  # process_fn: V(s) + logp_old of one 2M-row chunk (l1 + eval tail)
-        fm.evaluate(obs[:EV], act[:EV])
+        fm.evaluate(obs_v[:EV], act[:EV])
 
     if a.tail_trace:
         tail_trace_report(tail, ws, B, a.tail_trace)
@@ -131,7 +131,7 @@ def main():
                            ("eval(2M rows)", evaluate, flop_eval)):
         if a.only and not name.startswith(a.only):
             continue
-        if ld != D and name in ("l1_fwd", "l1_x6_staged(rows)", "minibatch"):
+        if ld != D and name in ("l1_fwd", "l1_x6_staged(rows)"):
             continue
         fn()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
