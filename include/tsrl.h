@@ -571,6 +571,17 @@ int tsrl_ppo_tail_fin(const float* h1frag, int64_t n, const int64_t* idx,
                       const tsrl_tail_grads* grads, double* sums, void* workspace,
                       int64_t ws_bytes, const float* log_std, float* losses,
                       float* grad_log_std, void* stream);
+/* tsrl_ppo_tail_stage: the same work in two stages so the caller can run the reduction on a
+ * second stream beside tsrl_mlp_dw (both only read what the tail kernels wrote):
+ * stages & 1 = the actor and critic tail kernels, stages & 2 = the reduction (with the loss
+ * finalisation when log_std/losses/grad_log_std are given — all three or none), 3 = both. */
+int tsrl_ppo_tail_stage(const float* h1frag, int64_t n, const int64_t* idx,
+                        const tsrl_tail_weights* w, int64_t act_dim, const float* act,
+                        const float* logp_old, const float* adv, const float* ret,
+                        const float* v_s, const double* adv_sums, tsrl_ppo_params p, float* dz1,
+                        const tsrl_tail_grads* grads, double* sums, void* workspace,
+                        int64_t ws_bytes, const float* log_std, float* losses,
+                        float* grad_log_std, int stages, void* stream);
 /* tsrl_ppo_eval: forward only (process_fn): value_out[n] = critic(obs) and, when logp_out is
  * given, logp_out[n] = log N(act | mu(obs), exp(log_std)) summed over the action dims, from
  * the fragment-layout layer-1 activations of tsrl_mlp_l1_fwd (critic only: the actor tiles

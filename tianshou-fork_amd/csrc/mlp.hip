@@ -1498,7 +1498,9 @@ static int ppo_tail_impl(const float* h1frag, int64_t n, const int64_t* idx,
                          const float* logp_old, const float* adv, const float* ret,
                          const float* v_s, const double* adv_sums, tsrl_ppo_params prm,
                          float* dz1, const tsrl_tail_grads* grads, double* sums,
-                         void* workspace, int64_t ws_bytes, TailFin fin, void* stream) {
+                         void* workspace, int64_t ws_bytes, TailFin fin, int stages,
+                         void* stream) {
+    TSRL_CHECK_ARG(stages >= 1 && stages <= 3, "tsrl_ppo_tail: stages must be 1, 2 or 3");
     TSRL_CHECK_ARG(n > 0 && act_dim > 0 && act_dim <= AMAX,
                    "tsrl_ppo_tail: need n > 0 and 0 < act_dim <= %d", AMAX);
     TSRL_CHECK_ARG(h1frag && wt && grads && act && logp_old && adv && ret && dz1 && sums &&
@@ -1517,12 +1519,17 @@ static int ppo_tail_impl(const float* h1frag, int64_t n, const int64_t* idx,
     TailWeights w{wt->w2a, wt->b2a, wt->w2c, wt->b2c, wt->w3a, wt->b3a, wt->w3c, wt->b3c,
                   wt->log_std};
     const TailParams tp = make_tail_params(prm, (int)act_dim);
-    hipLaunchKernelGGL(ppo_tail_kernel<0>, dim3(g), dim3(TAIL_TPB), 0, as_stream(stream), h1frag,
-                       n, idx, w, act, logp_old, adv, ret, v_s, adv_sums, tp, dz1, slab_f, slab_d);
-    TSRL_LAUNCH_CHECK("tsrl_ppo_tail(actor)");
-    hipLaunchKernelGGL(ppo_tail_kernel<1>, dim3(g), dim3(TAIL_TPB), 0, as_stream(stream), h1frag,
-                       n, idx, w, act, logp_old, adv, ret, v_s, adv_sums, tp, dz1, slab_f, slab_d);
-    TSRL_LAUNCH_CHECK("tsrl_ppo_tail");
+    if (stages & 1) {
+        hipLaunchKernelGGL(ppo_tail_kernel<0>, dim3(g), dim3(TAIL_TPB), 0, as_stream(stream),
+                           h1frag, n, idx, w, act, logp_old, adv, ret, v_s, adv_sums, tp, dz1,
+                           slab_f, slab_d);
+        TSRL_LAUNCH_CHECK("tsrl_ppo_tail(actor)");
+        hipLaunchKernelGGL(ppo_tail_kernel<1>, dim3(g), dim3(TAIL_TPB), 0, as_stream(stream),
+                           h1frag, n, idx, w, act, logp_old, adv, ret, v_s, adv_sums, tp, dz1,
+                           slab_f, slab_d);
+        TSRL_LAUNCH_CHECK("tsrl_ppo_tail");
+    }
+    if (!(stages & 2)) return 0;
     TailGrads gg{grads->w2a, grads->b2a, grads->w2c, grads->b2c, grads->w3a, grads->b3a,
                  grads->w3c, grads->b3c};
     hipLaunchKernelGGL(tail_reduce_kernel, dim3((SL_F + 63) / 64 + 1), dim3(256), 0,
@@ -1539,7 +1546,7 @@ extern "C" int tsrl_ppo_tail(const float* h1frag, int64_t n, const int64_t* idx,
                              void* workspace, int64_t ws_bytes, void* stream) {
     const TailFin fin{nullptr, nullptr, nullptr, 0.f, 0.f, 0.0};
     return ppo_tail_impl(h1frag, n, idx, wt, act_dim, act, logp_old, adv, ret, v_s, adv_sums, prm,
-                         dz1, grads, sums, workspace, ws_bytes, fin, stream);
+                         dz1, grads, sums, workspace, ws_bytes, fin, 3, stream);
 }
 
 extern "C" int tsrl_ppo_tail_fin(const float* h1frag, int64_t n, const int64_t* idx,
@@ -1553,7 +1560,22 @@ extern "C" int tsrl_ppo_tail_fin(const float* h1frag, int64_t n, const int64_t* 
     const TailFin fin{log_std, losses, grad_log_std, (float)prm.vf_coef, (float)prm.ent_coef,
                       1.0 / prm.b_global};
     return ppo_tail_impl(h1frag, n, idx, wt, act_dim, act, logp_old, adv, ret, v_s, adv_sums, prm,
-                         dz1, grads, sums, workspace, ws_bytes, fin, stream);
+                         dz1, grads, sums, workspace, ws_bytes, fin, 3, stream);
+}
+
+extern "C" int tsrl_ppo_tail_stage(const float* h1frag, int64_t n, const int64_t* idx,
+                                   const tsrl_tail_weights* wt, int64_t act_dim, const float* act,
+                                   const float* logp_old, const float* adv, const float* ret,
+                                   const float* v_s, const double* adv_sums, tsrl_ppo_params prm,
+                                   float* dz1, const tsrl_tail_grads* grads, double* sums,
+                                   void* workspace, int64_t ws_bytes, const float* log_std,
+                                   float* losses, float* grad_log_std, int stages, void* stream) {
+    TSRL_CHECK_ARG((log_std && losses && grad_log_std) || (!log_std && !losses && !grad_log_std),
+                   "tsrl_ppo_tail_stage: log_std/losses/grad_log_std all set or all null");
+    const TailFin fin{log_std, losses, grad_log_std, (float)prm.vf_coef, (float)prm.ent_coef,
+                      1.0 / prm.b_global};
+    return ppo_tail_impl(h1frag, n, idx, wt, act_dim, act, logp_old, adv, ret, v_s, adv_sums, prm,
+                         dz1, grads, sums, workspace, ws_bytes, fin, stages, stream);
 }
 
 extern "C" int64_t tsrl_mlp_dw_workspace_bytes(int64_t n, int64_t D) {

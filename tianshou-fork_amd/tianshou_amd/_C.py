@@ -182,6 +182,9 @@ _SIGS = {
     "tsrl_ppo_tail_fin": ([_p, _i64, _p, ctypes.POINTER(TailWeights), _i64, _p, _p, _p, _p, _p,
                            _p, PPOParams, _p, ctypes.POINTER(TailGrads), _p, _p, _i64, _p, _p,
                            _p, _p], ctypes.c_int),
+    "tsrl_ppo_tail_stage": ([_p, _i64, _p, ctypes.POINTER(TailWeights), _i64, _p, _p, _p, _p,
+                             _p, _p, PPOParams, _p, ctypes.POINTER(TailGrads), _p, _p, _i64, _p,
+                             _p, _p, ctypes.c_int, _p], ctypes.c_int),
     "tsrl_ppo_eval": ([_p, _i64, ctypes.POINTER(TailWeights), _i64, _p, _p, _p, _p],
                       ctypes.c_int),
     "tsrl_mlp_dw_workspace_bytes": ([_i64, _i64], _i64),

@@ -14,6 +14,7 @@ data-parallel all-reduce is a single call and torch's (fused) Adam and ``clip_gr
 consume them unchanged (ppo.py:143-151).  Every gradient element is overwritten each
 minibatch, which is what ``optim.zero_grad()`` + ``loss.backward()`` amount to.
 """
+import os
 from typing import Dict, Optional
 
 import torch
@@ -27,6 +28,9 @@ MAX_ACT = 32
 # first-layer forward on the bf16 matrix cores with the exact 3-way operand split
 # (tsrl_mlp_l1_fwd_x6, f32-level error); False: the f32-input MFMA kernel (tsrl_mlp_l1_fwd)
 L1_X6 = True
+# the tail's reduction launch runs on a second stream beside tsrl_mlp_dw (TSRL_TAIL_OVERLAP=0:
+# one stream)
+TAIL_OVERLAP = os.environ.get("TSRL_TAIL_OVERLAP", "1") != "0"
 
 
 def _seq(mlp) -> Optional[list]:
@@ -273,23 +277,41 @@ class FusedActorCritic(FlatAdam):
         args = (_C.ptr(h1), b, ip, self._tail_w, A, _C.ptr(act), _C.ptr(logp_old), _C.ptr(adv),
                 _C.ptr(ret), _C.ptr(v_s), _C.ptr(adv_sums) if adv_sums is not None else None,
                 params, _C.ptr(dz1), self._tail_grads, _C.ptr(sums), _C.ptr(ws), wsb)
-        terms = None
-        if dp.active:
-            _C.check(lib.tsrl_ppo_tail(*args, s), "tsrl_ppo_tail")
+        # single process: the loss finalisation rides the tail's reduction launch
+        terms = None if dp.active else torch.empty(4, dtype=torch.float32, device=dev)
+        fin = (None, None, None) if terms is None else (
+            _C.ptr(L["sigma"]), _C.ptr(terms), _C.ptr(L["sigma"].grad))
+        side = self._side_stream(dev)
+        if side is None:
+            _C.check(lib.tsrl_ppo_tail_stage(*args, *fin, 3, s), "tsrl_ppo_tail_stage")
         else:
-            # single process: the loss finalisation rides the tail's reduction launch
-            terms = torch.empty(4, dtype=torch.float32, device=dev)
-            _C.check(lib.tsrl_ppo_tail_fin(*args, _C.ptr(L["sigma"]), _C.ptr(terms),
-                                           _C.ptr(L["sigma"].grad), s), "tsrl_ppo_tail_fin")
+            # the tail's reduction only reads the tail kernels' slabs and dw only their dz1:
+            # the reduction runs on a second stream beside the first-layer weight gradients
+            _C.check(lib.tsrl_ppo_tail_stage(*args, *fin, 1, s), "tsrl_ppo_tail_stage")
+            cur = torch.cuda.current_stream(dev)
+            side.wait_stream(cur)
+            _C.check(lib.tsrl_ppo_tail_stage(*args, *fin, 2, side.cuda_stream),
+                     "tsrl_ppo_tail_stage")
         wsb2 = int(lib.tsrl_mlp_dw_workspace_bytes(b, D))
         ws2 = self._buf("dw_ws", wsb2, torch.uint8)
         _C.check(lib.tsrl_mlp_dw(
             _C.ptr(dz1), _C.ptr_rows(obs), ldx, ip, b, D, _C.ptr(L["w1a"].weight.grad),
             _C.ptr(L["w1a"].bias.grad), _C.ptr(L["w1c"].weight.grad),
             _C.ptr(L["w1c"].bias.grad), _C.ptr(ws2), wsb2, s), "tsrl_mlp_dw")
+        if side is not None:
+            cur.wait_stream(side)
         if terms is not None:
             return terms
         return self._reduce_finalize(sums, params, dp)
+
+    def _side_stream(self, dev) -> Optional[torch.cuda.Stream]:
+        """The second stream of the tail/dw overlap (None when TSRL_TAIL_OVERLAP=0)."""
+        if not TAIL_OVERLAP:
+            return None
+        st = getattr(self, "_side", None)
+        if st is None or st.device != dev:
+            st = self._side = torch.cuda.Stream(device=dev)
+        return st
 
     def _empty_minibatch(self, params, dp, adv_sums) -> torch.Tensor:
         sums = self._buf("sums", 4 + self.A, torch.float64)[:4 + self.A]
