@@ -1303,6 +1303,9 @@ __global__ __launch_bounds__(256, 2) void dw_kernel(
 #ifndef DWX6_OCC
 #define DWX6_OCC 2
 #endif
+#ifndef DWX6_FULL
+#define DWX6_FULL 1
+#endif
 __global__ __launch_bounds__(256, DWX6_OCC) void dw_x6_kernel(
     const float* __restrict__ dz, const float* __restrict__ X, int64_t ldx,
     const int64_t* __restrict__ idx, int64_t n, int D, int64_t rows_per_split, int ncolpad,
@@ -1328,6 +1331,7 @@ __global__ __launch_bounds__(256, DWX6_OCC) void dw_x6_kernel(
     const float ones = k == D ? 1.0f : 0.0f;  // db1 through a ones column at k == D
     const bool kin = k < D;
     const float* xcol = X + (kin ? k : 0);
+    const uint64_t ldx32 = (uint32_t)ldx;
     float zr[16], xr[16];
 #define DWX6_LOAD(rb)                                                                       \
     {                                                                                       \
@@ -1337,6 +1341,23 @@ __global__ __launch_bounds__(256, DWX6_OCC) void dw_x6_kernel(
             const int64_t ri = idx ? idx[rr] : rr;                                          \
             zr[q] = dz[rr * HC + fc];                                                       \
             xr[q] = xcol[ri * ldx];                                                         \
+        }                                                                                   \
+    }
+    /* a whole chunk of gathered rows (rb + DW_KB <= r1): no clamps, so the 8 contiguous  */ \
+    /* row indices of a group come in one scalar load and the dZ1 rows sit at immediate   */ \
+    /* offsets of one base; the X row offset is a 32 x 32 -> 64-bit product of the row    */ \
+    /* index (< 2^32, tsrl.h) and the pitch: 4 SALU per row instead of ~12 with the clamp  */ \
+#define DWX6_LOAD_FULL(rb)                                                                  \
+    {                                                                                       \
+        _Pragma("unroll") for (int g_ = 0; g_ < 2; ++g_) {                                  \
+            const int64_t rg0_ = (rb) + 8 * (rg + 2 * g_);                                  \
+            const float* zb_ = dz + rg0_ * HC + fc;                                         \
+            const int64_t* ib_ = idx + rg0_;                                                \
+            _Pragma("unroll") for (int j_ = 0; j_ < 8; ++j_) {                              \
+                zr[8 * g_ + j_] = zb_[j_ * HC];                                             \
+                const uint64_t ri_ = (uint32_t)ib_[j_];                                     \
+                xr[8 * g_ + j_] = xcol[ri_ * ldx32];                                        \
+            }                                                                               \
         }                                                                                   \
     }
     /* masks applied at the LDS store, not next to the loads (a select on a loaded value */ \
@@ -1376,7 +1397,13 @@ __global__ __launch_bounds__(256, DWX6_OCC) void dw_x6_kernel(
     }
     __syncthreads();
     for (int64_t ch = 0; ch < nchunk; ++ch) {
-        if (ch + 1 < nchunk) DWX6_LOAD(r0 + (ch + 1) * DW_KB)
+        if (ch + 1 < nchunk) {
+            const int64_t rb = r0 + (ch + 1) * DW_KB;
+            if (DWX6_FULL && idx && rb + DW_KB <= r1)
+                DWX6_LOAD_FULL(rb)
+            else
+                DWX6_LOAD(rb)
+        }
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             bf16x8 b[NPL];
@@ -1400,6 +1427,7 @@ __global__ __launch_bounds__(256, DWX6_OCC) void dw_x6_kernel(
         }
     }
 #undef DWX6_LOAD
+#undef DWX6_LOAD_FULL
 #undef DWX6_STORE
     float* o = part + (int64_t)split * HC * ncolpad;
 #pragma unroll
@@ -1589,7 +1617,7 @@ extern "C" int tsrl_mlp_dw(const float* dz1, const float* X, int64_t ldx, const 
                            void* workspace, int64_t ws_bytes, void* stream) {
     TSRL_CHECK_ARG(n > 0 && D > 0 && ldx >= D, "tsrl_mlp_dw: bad sizes");
     TSRL_CHECK_ARG(dz1 && X && gWa && gba && gWc && gbc && workspace, "tsrl_mlp_dw: null pointer");
-    TSRL_CHECK_ARG(aligned16(dz1) && aligned16(X) && ldx % 4 == 0 && ldx >= (D + 3) / 4 * 4,
+    TSRL_CHECK_ARG(aligned16(dz1) && aligned16(X) && ldx % 4 == 0 && ldx >= (D + 3) / 4 * 4 && ldx < (int64_t(1) << 32),
                    "tsrl_mlp_dw: dz1/X must be 16-byte aligned, ldx a multiple of 4 and >= "
                    "roundup(D, 4) (columns D.. of the padding read as data-free)");
     TSRL_CHECK_ARG(ws_bytes >= tsrl_mlp_dw_workspace_bytes(n, D), "tsrl_mlp_dw: workspace too small");
