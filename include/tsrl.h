@@ -525,7 +525,9 @@ int tsrl_cat_gumbel_argmax(const float* logits, const float* u, int64_t n, int64
  * tsrl_ppo_tail: layers 2-3 of both nets, the PPO loss of tsrl_ppo_gauss_fwd_bwd and the
  *   backward to dZ1 [n, 128] (row-major), writing the layer-2/3 parameter gradients of the
  *   mean loss and the loss sums [4 + A] (layout of tsrl_ppo_gauss_finalize's input).
- * tsrl_mlp_dw: first-layer gradients dW = dZ1^T X[idx], db = column sums of dZ1.
+ * tsrl_mlp_dw: first-layer gradients dW = dZ1^T X[idx], db = column sums of dZ1.  Row
+ *   indices idx[] and the pitch ldx must be < 2^32 (the row offsets are 32 x 32-bit
+ *   products; ldx is checked).
  * ------------------------------------------------------------------------------- */
 typedef struct tsrl_tail_weights {
     const float *w2a, *b2a;   /* actor layer 2 [64,64], [64] */

@@ -288,6 +288,42 @@ def test_fused_minibatch_matches_autograd(dev, D, A, B, kw):
         assert e_fused <= max(4 * e_torch, 2e-6), (k, e_fused, e_torch)
 
 
+@pytest.mark.parametrize("B", [262144 + 45, 1000])
+def test_tail_reduction_on_side_stream_is_bitwise_single_stream(dev, monkeypatch, B):
+    """The tail's reduction on a second stream beside dW1 (TSRL_TAIL_OVERLAP, the default)
+    gives the same bits as the one-stream sequence: same kernels, only the stream differs."""
+    from tianshou_amd import _C
+    from tianshou_amd.dist import DataParallel
+    from tianshou_amd.policy import fused_mlp
+    from tianshou_amd.utils.net import ActorCritic
+    D, A = 376, 17
+    actor, critic = _nets(D, A, dev, 7)
+    layers = fused_mlp.match(actor, critic)
+    fm = fused_mlp.FusedActorCritic(layers, ActorCritic(actor, critic).parameters())
+    g = torch.Generator().manual_seed(3)
+    n = B + 300
+    obs = torch.randn(n, D, generator=g).to(dev)
+    act = torch.randn(n, A, generator=g).to(dev)
+    adv = torch.randn(n, generator=g).to(dev)
+    ret = torch.randn(n, generator=g).to(dev)
+    v_s = torch.randn(n, generator=g).to(dev)
+    logp_old = (0.3 * torch.randn(n, generator=g) - 24.0).to(dev)  # ratio near 1
+    idx = torch.randperm(n, generator=g)[:B].to(dev)
+    p = _C.PPOParams()
+    p.eps_clip, p.dual_clip, p.vf_coef, p.ent_coef, p.adv_eps = 0.2, 3.0, 0.25, 0.01, 1e-8
+    p.b_global, p.value_clip, p.norm_adv = float(B), 1, 1
+    params = list(ActorCritic(actor, critic).parameters())
+    out = []
+    for overlap in (True, False):
+        monkeypatch.setattr(fused_mlp, "TAIL_OVERLAP", overlap)
+        terms = fm.minibatch(obs, idx, B, act, logp_old, adv, ret, v_s, p, DataParallel())
+        torch.cuda.synchronize()
+        out.append((terms.cpu().clone(), [q.grad.detach().cpu().clone() for q in params]))
+    assert torch.equal(out[0][0], out[1][0])
+    for a, b in zip(out[0][1], out[1][1]):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("value_clip", [False, True])
 def test_learn_fused_mlp_vs_layers(dev, value_clip):
     from tianshou_amd.data import Batch

@@ -256,6 +256,7 @@ class FusedActorCritic(FlatAdam):
         assert obs.dim() == 2 and obs.stride(1) == 1 and obs.stride(0) >= self.Dp
         ldx = obs.stride(0)
         assert act.shape[-1] == A and act.is_contiguous()
+        assert obs.shape[0] < 2 ** 32, "tsrl_mlp_dw: row indices must be < 2^32"
         ip = _C.ptr(idx) if idx is not None else None
         if b == 0:
             return self._empty_minibatch(params, dp, adv_sums)
