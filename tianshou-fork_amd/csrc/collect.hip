@@ -99,6 +99,11 @@ constexpr int WP = 68;         // W2 / W3 rows (4i + k banks: conflict-free A fr
 #ifndef COLLECT_ROW_STORE
 #define COLLECT_ROW_STORE 3
 #endif
+// 1: this step's stored obs rows leave LDS one column per thread over the 16 rows; 0: the
+// round-3 flat loop over row * D + column (an integer division by D per element)
+#ifndef COLLECT_OBS_COLS
+#define COLLECT_OBS_COLS 1
+#endif
 __device__ __forceinline__ void row_store4(float4* p, float4 x) {
 #if COLLECT_ROW_STORE >= 3
     typedef float f4v __attribute__((ext_vector_type(4)));
@@ -249,7 +254,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
     __shared__ RowState rs[R], rr[R];
     __shared__ float sAr[CPL ? R : 1][AMAX + 1];  // CPL: this workgroup's remapped actions
     __shared__ int s_nd;
-    __shared__ int64_t s_row[R];
+    __shared__ float* s_row[R];  // this step's stored obs row of each env (obs_dst + pitch)
     // deferred obs_rms merge: the statistics after the previous step's step rows (obs_next
     // normalisation) and after its reset rows (reset rows, state)
     __shared__ __attribute__((aligned(16))) float sSnapM[KMAX], sSnapV[KMAX], sFinM[KMAX],
@@ -561,14 +566,20 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         } else {
             urel = a.obs_rel_dev ? *a.obs_rel_dev : a.obs_uniform_rel;
         }
-        s_row[t] = a.obs_offset[r0 + t] + urel;
+        const int64_t opitch = a.obs_pitch ? a.obs_pitch : D;
+        s_row[t] = a.obs_dst + (a.obs_offset[r0 + t] + urel) * opitch;
     }
     LDS_SYNC();
-    const int64_t opitch = a.obs_pitch ? a.obs_pitch : D;
+#if COLLECT_OBS_COLS
+    // one column per thread (D <= NT), the rows in turn: no index division, coalesced rows
+    if (t < D)
+        for (int rw = 0; rw < nrows; ++rw) row_store1(s_row[rw] + t, sX[t * XP + rw]);
+#else
     for (int i = t; i < nrows * D; i += NT) {
         const int rw = i / D, c = i - rw * D;
-        row_store1(&a.obs_dst[s_row[rw] * opitch + c], sX[c * XP + rw]);
+        row_store1(s_row[rw] + c, sX[c * XP + rw]);
     }
+#endif
     // ---- C. env step + auto-reset of these rows (env.hip box_step_reset_kernel) -------------
     // The quantised synthetic env's transition does not read the action, so its step runs
     // before the actor: its obs_rms atomics drain while the actor computes.  The
