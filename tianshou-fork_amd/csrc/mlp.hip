@@ -1362,12 +1362,12 @@ __global__ __launch_bounds__(256, DWX6_OCC) void dw_x6_kernel(
     }
     /* masks applied at the LDS store, not next to the loads (a select on a loaded value */ \
     /* there would make the wave wait for the data before the chunk's MFMAs)           */ \
-#define DWX6_STORE(rb)                                                                      \
+#define DWX6_STORE(rb, FULL)                                                                \
     {                                                                                       \
         _Pragma("unroll") for (int g = 0; g < 2; ++g) {                                     \
             bf16x8 zp[NPL], xp[NPL];                                                        \
             _Pragma("unroll") for (int j = 0; j < 8; ++j) {                                 \
-                const bool lv = (rb) + 8 * (rg + 2 * g) + j < r1;                           \
+                const bool lv = (FULL) || (rb) + 8 * (rg + 2 * g) + j < r1;                 \
                 const float zv = lv ? zr[8 * g + j] : 0.0f;                                 \
                 const float xv = lv ? (kin ? xr[8 * g + j] : ones) : 0.0f;                  \
                 __bf16 a0, a1, a2;                                                          \
@@ -1393,7 +1393,7 @@ __global__ __launch_bounds__(256, DWX6_OCC) void dw_x6_kernel(
     const int64_t nchunk = r1 > r0 ? (r1 - r0 + DW_KB - 1) / DW_KB : 0;
     if (nchunk > 0) {
         DWX6_LOAD(r0)
-        DWX6_STORE(r0)
+        DWX6_STORE(r0, false)
     }
     __syncthreads();
     for (int64_t ch = 0; ch < nchunk; ++ch) {
@@ -1422,7 +1422,11 @@ __global__ __launch_bounds__(256, DWX6_OCC) void dw_x6_kernel(
         }
         if (ch + 1 < nchunk) {
             __syncthreads();
-            DWX6_STORE(r0 + (ch + 1) * DW_KB)
+            const int64_t rb = r0 + (ch + 1) * DW_KB;
+            if (DWX6_FULL && rb + DW_KB <= r1)
+                DWX6_STORE(rb, true)  // no row masks in a whole chunk
+            else
+                DWX6_STORE(rb, false)
             __syncthreads();
         }
     }
