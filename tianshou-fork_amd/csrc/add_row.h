@@ -30,6 +30,12 @@ __device__ __forceinline__ float norm1(float x, float m, float v, float eps, flo
     if (clip > 0.0f) y = fminf(fmaxf(y, -clip), clip);
     return y;
 }
+// norm1 with s = sqrt(v + eps) computed once per column by the caller (same bits)
+__device__ __forceinline__ float norm1s(float x, float m, float s, float clip) {
+    float y = (x - m) / s;
+    if (clip > 0.0f) y = fminf(fmaxf(y, -clip), clip);
+    return y;
+}
 
 // The payload copies of add_row (obs, act, raw obs_next rows) by nl lanes.
 __device__ __forceinline__ void add_row_copies(const tsrl_add_args& a, int64_t r, int lane,

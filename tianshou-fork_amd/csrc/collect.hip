@@ -259,6 +259,9 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
     // normalisation) and after its reset rows (reset rows, state)
     __shared__ __attribute__((aligned(16))) float sSnapM[KMAX], sSnapV[KMAX], sFinM[KMAX],
         sFinV[KMAX];
+    // sqrt(var + eps) of both statistics, once per column (the add divides by them: the
+    // correctly rounded square root is ~20 VALU, per element before)
+    __shared__ __attribute__((aligned(16))) float sSnapS[KMAX], sFinS[KMAX];
     const int t = threadIdx.x;
     const int w = t >> 6, l = t & 63;
     const int64_t k = a.k;
@@ -371,6 +374,8 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
             else
                 merge_column((double)mm0, (double)mv0, mcount, kp, ms1, mq1, mnd, ms2, mq2,
                              sSnapM[t], sSnapV[t], sFinM[t], sFinV[t]);
+            sSnapS[t] = __builtin_sqrtf(sSnapV[t] + ad.norm_eps);
+            sFinS[t] = __builtin_sqrtf(sFinV[t] + ad.norm_eps);
         }
         TSTAMP2(3)
         LDS_SYNC();
@@ -446,27 +451,27 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
                 const int64_t aptr = ad.ptr ? aptr_ld : aptr_ld + urel;
                 float4* dst = reinterpret_cast<float4*>(
                     ad.obs_next_dst + aptr * (ad.obs_dst_pitch ? ad.obs_dst_pitch / 4 : D));
-                const float eps = ad.norm_eps, clip = ad.norm_clip;
+                const float clip = ad.norm_clip;
 #pragma unroll
                 for (int j = 0; j < AQ; ++j) {
                     const int q = aln + 32 * j;
                     if (q >= nq) break;
                     const float4 m = *reinterpret_cast<const float4*>(&sSnapM[4 * q]);
-                    const float4 v = *reinterpret_cast<const float4*>(&sSnapV[4 * q]);
+                    const float4 v = *reinterpret_cast<const float4*>(&sSnapS[4 * q]);
                     float4 x = axs[j];
-                    x.x = norm1(x.x, m.x, v.x, eps, clip);
-                    x.y = norm1(x.y, m.y, v.y, eps, clip);
-                    x.z = norm1(x.z, m.z, v.z, eps, clip);
-                    x.w = norm1(x.w, m.w, v.w, eps, clip);
+                    x.x = norm1s(x.x, m.x, v.x, clip);
+                    x.y = norm1s(x.y, m.y, v.y, clip);
+                    x.z = norm1s(x.z, m.z, v.z, clip);
+                    x.w = norm1s(x.w, m.w, v.w, clip);
                     row_store4(&dst[q], x);
                     if (amask) {
                         const float4 mr = *reinterpret_cast<const float4*>(&sFinM[4 * q]);
-                        const float4 vr = *reinterpret_cast<const float4*>(&sFinV[4 * q]);
+                        const float4 vr = *reinterpret_cast<const float4*>(&sFinS[4 * q]);
                         x = axr[j];
-                        x.x = norm1(x.x, mr.x, vr.x, eps, clip);
-                        x.y = norm1(x.y, mr.y, vr.y, eps, clip);
-                        x.z = norm1(x.z, mr.z, vr.z, eps, clip);
-                        x.w = norm1(x.w, mr.w, vr.w, eps, clip);
+                        x.x = norm1s(x.x, mr.x, vr.x, clip);
+                        x.y = norm1s(x.y, mr.y, vr.y, clip);
+                        x.z = norm1s(x.z, mr.z, vr.z, clip);
+                        x.w = norm1s(x.w, mr.w, vr.w, clip);
                     }
                     float* lx = sX + arw;
                     lx[(4 * q) * XP] = x.x;
