@@ -114,9 +114,14 @@ __device__ __forceinline__ void add_row_tail(const tsrl_add_args& a, int64_t r, 
 // Row r of one add (urel = the uniform ring position of this step) by nl lanes (lane < nl).
 // lx (nullable): the new live obs row is also written to lx[col * lxp] (the fused collect step
 // keeps it in LDS for the next policy step); cur_hbm = false then skips its HBM copy.
+// STD: norm_var / reset_var hold sqrt(var + eps) per column already (norm1s; same bits).
+template <bool STD = false>
 __device__ __forceinline__ void add_row(const tsrl_add_args& a, int64_t r, int lane,
                                         int64_t urel, float* lx = nullptr, int lxp = 0,
                                         int nl = kWave, bool cur_hbm = true) {
+    auto nrm1 = [&](float x, float m, float v) {
+        return STD ? norm1s(x, m, v, a.norm_clip) : norm1(x, m, v, a.norm_eps, a.norm_clip);
+    };
     const int64_t b = a.ids ? a.ids[r] : r;
     const int64_t ptr = a.ptr ? a.ptr[r] : a.offset[b] + urel;
 
@@ -171,20 +176,20 @@ __device__ __forceinline__ void add_row(const tsrl_add_args& a, int64_t r, int l
                     if (q >= nq) break;
                     float4 x = xs[j];
                     if (nrm) {
-                        x.x = norm1(x.x, ms[j].x, vs[j].x, a.norm_eps, a.norm_clip);
-                        x.y = norm1(x.y, ms[j].y, vs[j].y, a.norm_eps, a.norm_clip);
-                        x.z = norm1(x.z, ms[j].z, vs[j].z, a.norm_eps, a.norm_clip);
-                        x.w = norm1(x.w, ms[j].w, vs[j].w, a.norm_eps, a.norm_clip);
+                        x.x = nrm1(x.x, ms[j].x, vs[j].x);
+                        x.y = nrm1(x.y, ms[j].y, vs[j].y);
+                        x.z = nrm1(x.z, ms[j].z, vs[j].z);
+                        x.w = nrm1(x.w, ms[j].w, vs[j].w);
                     }
                     if (dst) reinterpret_cast<float4*>(dst)[q] = x;
                     if (cur) {
                         if (rst) {
                             x = xr[j];
                             if (rnrm) {
-                                x.x = norm1(x.x, mr[j].x, vr[j].x, a.norm_eps, a.norm_clip);
-                                x.y = norm1(x.y, mr[j].y, vr[j].y, a.norm_eps, a.norm_clip);
-                                x.z = norm1(x.z, mr[j].z, vr[j].z, a.norm_eps, a.norm_clip);
-                                x.w = norm1(x.w, mr[j].w, vr[j].w, a.norm_eps, a.norm_clip);
+                                x.x = nrm1(x.x, mr[j].x, vr[j].x);
+                                x.y = nrm1(x.y, mr[j].y, vr[j].y);
+                                x.z = nrm1(x.z, mr[j].z, vr[j].z);
+                                x.w = nrm1(x.w, mr[j].w, vr[j].w);
                             }
                         }
                         if (cur_hbm) reinterpret_cast<float4*>(cur)[q] = x;
@@ -200,13 +205,13 @@ __device__ __forceinline__ void add_row(const tsrl_add_args& a, int64_t r, int l
         } else
         for (int64_t d = lane; d < a.obs_dim; d += nl) {
             float x = src[d];
-            if (nrm) x = norm1(x, a.norm_mean[d], a.norm_var[d], a.norm_eps, a.norm_clip);
+            if (nrm) x = nrm1(x, a.norm_mean[d], a.norm_var[d]);
             if (dst) dst[d] = x;
             if (cur) {
                 if (rst) {
                     x = a.reset_src[r * a.obs_dim + d];
                     if (a.reset_mean)
-                        x = norm1(x, a.reset_mean[d], a.reset_var[d], a.norm_eps, a.norm_clip);
+                        x = nrm1(x, a.reset_mean[d], a.reset_var[d]);
                 }
                 if (cur_hbm) cur[d] = x;
                 if (lx) lx[d * lxp] = x;

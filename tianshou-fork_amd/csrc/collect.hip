@@ -391,13 +391,14 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
             long long* tz = ws.tot[tnext];
             for (int i = t; i < 4 * D + 2; i += NT) tz[i] = 0;
         }
+        // the add reads the statistics from LDS, with sqrt(var + eps) per column (add_row<true>)
         if (ad.norm_mean) {
             ad.norm_mean = sSnapM;
-            ad.norm_var = sSnapV;
+            ad.norm_var = sSnapS;
         }
         if (ad.reset_mean) {
             ad.reset_mean = sFinM;
-            ad.reset_var = sFinV;
+            ad.reset_var = sFinS;
         }
     } else if (defer && blockIdx.x == 0) {
         // first step of a chain: the caller's state seeds the state slot (slot 1 of the
@@ -408,6 +409,29 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
             so->var[d] = a.var[d];
         }
         if (t == 0) so->count = *a.count;
+    }
+    if (!merge && ad.k > 0 && (ad.norm_mean || ad.reset_mean)) {
+        // statistics of a launch without the deferred merge (exact obs_rms, a chain's first
+        // step): staged into LDS with sqrt(var + eps) per column, as the merge leaves them
+        for (int d = t; d < D; d += NT) {
+            if (ad.norm_mean) {
+                sSnapM[d] = ad.norm_mean[d];
+                sSnapS[d] = __builtin_sqrtf(ad.norm_var[d] + ad.norm_eps);
+            }
+            if (ad.reset_mean) {
+                sFinM[d] = ad.reset_mean[d];
+                sFinS[d] = __builtin_sqrtf(ad.reset_var[d] + ad.norm_eps);
+            }
+        }
+        LDS_SYNC();
+        if (ad.norm_mean) {
+            ad.norm_mean = sSnapM;
+            ad.norm_var = sSnapS;
+        }
+        if (ad.reset_mean) {
+            ad.reset_mean = sFinM;
+            ad.reset_var = sFinS;
+        }
     }
 
     // actor weights: issued after every load the add and the merge wait for (vmcnt retires
@@ -484,7 +508,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
             }
         } else {
             // 32 lanes per row: all 16 rows' loads in flight at once
-            if (arw < nrows) add_row(ad, r0 + arw, aln, urel, sX + arw, XP, 32, false);
+            if (arw < nrows) add_row<true>(ad, r0 + arw, aln, urel, sX + arw, XP, 32, false);
         }
         if (a.add.rel_next && blockIdx.x == 0 && t == 0)
             *a.add.rel_next = (urel + 1) % a.add.ring_size;
