@@ -99,6 +99,12 @@ constexpr int WP = 68;         // W2 / W3 rows (4i + k banks: conflict-free A fr
 #ifndef COLLECT_ROW_STORE
 #define COLLECT_ROW_STORE 3
 #endif
+// 1: the env rows' counter keys, reward and flags are computed at the top of the launch by
+// the last R threads (wave 7: no merge column for D <= NT - R) while the merge's loads are in
+// flight, and the env phase only stores them; 0: computed inside the env phase by wave 0.
+#ifndef COLLECT_EARLY_KEYS
+#define COLLECT_EARLY_KEYS 1
+#endif
 // 1: this step's stored obs rows leave LDS one column per thread over the 16 rows; 0: the
 // round-3 flat loop over row * D + column (an integer division by D per element)
 #ifndef COLLECT_OBS_COLS
@@ -254,6 +260,11 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
     __shared__ RowState rs[R], rr[R];
     __shared__ float sAr[CPL ? R : 1][AMAX + 1];  // CPL: this workgroup's remapped actions
     __shared__ int s_nd;
+    // COLLECT_EARLY_KEYS: the rows' reward, flags (term | trunc << 1 | done << 2) and new
+    // episode counters, stored to HBM by the env phase
+    __shared__ double s_rew[R];
+    __shared__ int s_flg[R];
+    __shared__ int64_t s_jn[R], s_tn[R];
     __shared__ float* s_row[R];  // this step's stored obs row of each env (obs_dst + pitch)
     // deferred obs_rms merge: the statistics after the previous step's step rows (obs_next
     // normalisation) and after its reset rows (reset rows, state)
@@ -310,6 +321,15 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
                       (ad.act_row_bytes & 3) == 0 && act_n <= 32 &&
                       aligned16(ad.obs_next_src) && aligned16(ad.obs_next_dst) &&
                       aligned16(ad.reset_src);
+    // COLLECT_EARLY_KEYS: the episode counters of the key rows, loaded before anything else
+    constexpr int KT0 = NT - R;
+    const int ki = t - KT0;
+    const bool krow = COLLECT_EARLY_KEYS && ki >= 0 && ki < nrows;
+    int64_t kj = 0, kt = 0;
+    if (krow) {
+        kj = a.ep_j[r0 + ki];
+        kt = a.ep_t[r0 + ki];
+    }
     const int64_t ar = r0 + arw;
     const bool arow = fast && arw < nrows;
     float4 axs[AQ], axr[AQ];
@@ -361,6 +381,38 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         }
     }
     TSTAMP2(2)
+#if COLLECT_EARLY_KEYS
+    if (ki >= 0) {
+        // this step's counter keys (env.hip box_step_reset_kernel): every read the env phase
+        // needs from them goes to LDS; the HBM stores wait for the env phase (the pending add
+        // still reads the previous step's flags and counters of these rows)
+        RowState st = {0ull, 0}, sr = {0ull, 0};
+        bool dn = false;
+        if (krow) {
+            const int64_t e = r0 + ki;
+            int64_t j = kj;
+            int64_t tt = kt + 1;
+            st.key = env_key(a.env_seed, (uint64_t)e, j, tt);
+            st.active = 1;
+            const uint64_t h = sm64(st.key ^ REW_SALT);
+            s_rew[ki] = (double)(h >> 40) * 0x1p-24;
+            dn = tt >= a.ep_len;
+            s_flg[ki] = (dn && (e % 2 == 0) ? 1 : 0) | (dn && (e % 2 == 1) ? 2 : 0) | (dn ? 4 : 0);
+            if (dn) {
+                j += 1;
+                tt = (j == 0) ? (e % a.ep_len) : 0;
+                sr.key = env_key(a.env_seed, (uint64_t)e, j, tt);
+                sr.active = 1;
+            }
+            s_jn[ki] = j;
+            s_tn[ki] = tt;
+        }
+        rs[ki] = st;
+        rr[ki] = sr;
+        const uint64_t dm = __ballot(dn);
+        if (ki == 0) s_nd = __popcll(dm);
+    }
+#endif
     if (merge) {
         // the step rows behind the totals (counted in the slot: k, or the sum of every
         // rank's k when the slot was all-reduced)
@@ -529,12 +581,14 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         }
     }
     TSTAMP(1)
+#if !COLLECT_EARLY_KEYS
     // the env rows' episode counters: loaded now, used by the env step
     int64_t ej = 0, et = 0;
     if (t < nrows) {
         ej = a.ep_j[r0 + t];
         et = a.ep_t[r0 + t];
     }
+#endif
     // zero padding: columns [D, Kp) and rows past the last env of a partial tile
     for (int i = t; i < (Kp - D) * R; i += NT) sX[(D + i / R) * XP + (i % R)] = 0.0f;
     if (nrows < R)
@@ -616,6 +670,19 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
     // this launch has consumed the previous step's env rows of this workgroup (the barrier
     // above).
     auto env_phase = [&]() {
+#if COLLECT_EARLY_KEYS
+        if (t < nrows) {
+            // keys, reward and flags came from the top of the launch (LDS)
+            const int64_t r = r0 + t;
+            const int f = s_flg[t];
+            a.rew[r] = s_rew[t];
+            a.term[r] = (uint8_t)(f & 1);
+            a.trunc[r] = (uint8_t)((f >> 1) & 1);
+            a.done[r] = (uint8_t)((f >> 2) & 1);
+            if (f & 4) a.ep_j[r] = s_jn[t];
+            a.ep_t[r] = s_tn[t];
+        }
+#else
         if (t == 0) s_nd = 0;
         LDS_SYNC();
         if (t < R) {
@@ -647,6 +714,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
             rr[t] = sr;
         }
         LDS_SYNC();
+#endif
         const int nd = s_nd;
         long long* tc = ws.tot[tcur];
         if (CPL) {
