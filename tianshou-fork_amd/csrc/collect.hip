@@ -325,10 +325,11 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
     constexpr int KT0 = NT - R;
     const int ki = t - KT0;
     const bool krow = COLLECT_EARLY_KEYS && ki >= 0 && ki < nrows;
-    int64_t kj = 0, kt = 0;
+    int64_t kj = 0, kt = 0, koff = 0;
     if (krow) {
         kj = a.ep_j[r0 + ki];
         kt = a.ep_t[r0 + ki];
+        koff = a.obs_offset[r0 + ki];
     }
     const int64_t ar = r0 + arw;
     const bool arow = fast && arw < nrows;
@@ -411,6 +412,15 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         rr[ki] = sr;
         const uint64_t dm = __ballot(dn);
         if (ki == 0) s_nd = __popcll(dm);
+        if (krow) {
+            // this step's stored obs row of the env (see the store loop after the add); with a
+            // pending add, block 0 advances the device cursor concurrently, so the position
+            // is the add's own (urel) plus one, the ring's uniform next
+            const int64_t uo = a.add.k > 0
+                                   ? (urel + 1) % a.add.ring_size
+                                   : (a.obs_rel_dev ? *a.obs_rel_dev : a.obs_uniform_rel);
+            s_row[ki] = a.obs_dst + (koff + uo) * (a.obs_pitch ? a.obs_pitch : D);
+        }
     }
 #endif
     if (merge) {
@@ -638,7 +648,9 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
     LDS_SYNC();
     // this step's stored obs rows (ReplayBuffer obs of step i = the live obs the actor sees):
     // written here from LDS, so the add of step i (next launch / flush) copies nothing and the
-    // live obs never round-trips through HBM between fused steps
+    // live obs never round-trips through HBM between fused steps (COLLECT_EARLY_KEYS: their
+    // row pointers came from the top of the launch)
+#if !COLLECT_EARLY_KEYS
     if (t < nrows) {
         // with a pending add this launch's block 0 advances the device cursor concurrently,
         // so the position is the add's own plus one (the ring's uniform next)
@@ -653,6 +665,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         s_row[t] = a.obs_dst + (a.obs_offset[r0 + t] + urel) * opitch;
     }
     LDS_SYNC();
+#endif
 #if COLLECT_OBS_COLS
     // one column per thread (D <= NT), the rows in turn: no index division, coalesced rows
     if (t < D)
