@@ -103,12 +103,18 @@ constexpr int WP = 68;         // W2 / W3 rows (4i + k banks: conflict-free A fr
 // the last R threads (wave 7: no merge column for D <= NT - R) while the merge's loads are in
 // flight, and the env phase only stores them; 0: computed inside the env phase by wave 0.
 #ifndef COLLECT_EARLY_KEYS
-#define COLLECT_EARLY_KEYS 1
+#define COLLECT_EARLY_KEYS 0
+#endif
+// 1: sqrt(var + eps) of both statistics computed once per column and staged in LDS, the add
+// divides by it (same bits as norm1); 0: norm1 per element (a correctly rounded square root
+// per normalised value)
+#ifndef COLLECT_NORM_STD
+#define COLLECT_NORM_STD 0
 #endif
 // 1: this step's stored obs rows leave LDS one column per thread over the 16 rows; 0: the
 // round-3 flat loop over row * D + column (an integer division by D per element)
 #ifndef COLLECT_OBS_COLS
-#define COLLECT_OBS_COLS 1
+#define COLLECT_OBS_COLS 0
 #endif
 __device__ __forceinline__ void row_store4(float4* p, float4 x) {
 #if COLLECT_ROW_STORE >= 3
@@ -260,11 +266,13 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
     __shared__ RowState rs[R], rr[R];
     __shared__ float sAr[CPL ? R : 1][AMAX + 1];  // CPL: this workgroup's remapped actions
     __shared__ int s_nd;
-    // COLLECT_EARLY_KEYS: the rows' reward, flags (term | trunc << 1 | done << 2) and new
-    // episode counters, stored to HBM by the env phase
+#if COLLECT_EARLY_KEYS
+    // the rows' reward, flags (term | trunc << 1 | done << 2) and new episode counters,
+    // stored to HBM by the env phase
     __shared__ double s_rew[R];
     __shared__ int s_flg[R];
     __shared__ int64_t s_jn[R], s_tn[R];
+#endif
     __shared__ float* s_row[R];  // this step's stored obs row of each env (obs_dst + pitch)
     // deferred obs_rms merge: the statistics after the previous step's step rows (obs_next
     // normalisation) and after its reset rows (reset rows, state)
@@ -272,7 +280,8 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         sFinV[KMAX];
     // sqrt(var + eps) of both statistics, once per column (the add divides by them: the
     // correctly rounded square root is ~20 VALU, per element before)
-    __shared__ __attribute__((aligned(16))) float sSnapS[KMAX], sFinS[KMAX];
+    __shared__ __attribute__((aligned(16))) float sSnapS[COLLECT_NORM_STD ? KMAX : 4],
+        sFinS[COLLECT_NORM_STD ? KMAX : 4];
     const int t = threadIdx.x;
     const int w = t >> 6, l = t & 63;
     const int64_t k = a.k;
@@ -321,16 +330,18 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
                       (ad.act_row_bytes & 3) == 0 && act_n <= 32 &&
                       aligned16(ad.obs_next_src) && aligned16(ad.obs_next_dst) &&
                       aligned16(ad.reset_src);
-    // COLLECT_EARLY_KEYS: the episode counters of the key rows, loaded before anything else
+#if COLLECT_EARLY_KEYS
+    // the episode counters of the key rows, loaded before anything else
     constexpr int KT0 = NT - R;
     const int ki = t - KT0;
-    const bool krow = COLLECT_EARLY_KEYS && ki >= 0 && ki < nrows;
+    const bool krow = ki >= 0 && ki < nrows;
     int64_t kj = 0, kt = 0, koff = 0;
     if (krow) {
         kj = a.ep_j[r0 + ki];
         kt = a.ep_t[r0 + ki];
         koff = a.obs_offset[r0 + ki];
     }
+#endif
     const int64_t ar = r0 + arw;
     const bool arow = fast && arw < nrows;
     float4 axs[AQ], axr[AQ];
@@ -436,8 +447,10 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
             else
                 merge_column((double)mm0, (double)mv0, mcount, kp, ms1, mq1, mnd, ms2, mq2,
                              sSnapM[t], sSnapV[t], sFinM[t], sFinV[t]);
+#if COLLECT_NORM_STD
             sSnapS[t] = __builtin_sqrtf(sSnapV[t] + ad.norm_eps);
             sFinS[t] = __builtin_sqrtf(sFinV[t] + ad.norm_eps);
+#endif
         }
         TSTAMP2(3)
         LDS_SYNC();
@@ -453,14 +466,15 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
             long long* tz = ws.tot[tnext];
             for (int i = t; i < 4 * D + 2; i += NT) tz[i] = 0;
         }
-        // the add reads the statistics from LDS, with sqrt(var + eps) per column (add_row<true>)
+        // the add reads the statistics from LDS (COLLECT_NORM_STD: with sqrt(var + eps) per
+        // column, add_row<true>)
         if (ad.norm_mean) {
             ad.norm_mean = sSnapM;
-            ad.norm_var = sSnapS;
+            ad.norm_var = COLLECT_NORM_STD ? sSnapS : sSnapV;
         }
         if (ad.reset_mean) {
             ad.reset_mean = sFinM;
-            ad.reset_var = sFinS;
+            ad.reset_var = COLLECT_NORM_STD ? sFinS : sFinV;
         }
     } else if (defer && blockIdx.x == 0) {
         // first step of a chain: the caller's state seeds the state slot (slot 1 of the
@@ -472,7 +486,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         }
         if (t == 0) so->count = *a.count;
     }
-    if (!merge && ad.k > 0 && (ad.norm_mean || ad.reset_mean)) {
+    if (COLLECT_NORM_STD && !merge && ad.k > 0 && (ad.norm_mean || ad.reset_mean)) {
         // statistics of a launch without the deferred merge (exact obs_rms, a chain's first
         // step): staged into LDS with sqrt(var + eps) per column, as the merge leaves them
         for (int d = t; d < D; d += NT) {
@@ -542,23 +556,33 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
                 for (int j = 0; j < AQ; ++j) {
                     const int q = aln + 32 * j;
                     if (q >= nq) break;
+#if COLLECT_NORM_STD
+#define NRM(x_, m_, s_) norm1s(x_, m_, s_, clip)
+                    const float* const sv = sSnapS;
+                    const float* const fv = sFinS;
+#else
+#define NRM(x_, m_, v_) norm1(x_, m_, v_, ad.norm_eps, clip)
+                    const float* const sv = sSnapV;
+                    const float* const fv = sFinV;
+#endif
                     const float4 m = *reinterpret_cast<const float4*>(&sSnapM[4 * q]);
-                    const float4 v = *reinterpret_cast<const float4*>(&sSnapS[4 * q]);
+                    const float4 v = *reinterpret_cast<const float4*>(&sv[4 * q]);
                     float4 x = axs[j];
-                    x.x = norm1s(x.x, m.x, v.x, clip);
-                    x.y = norm1s(x.y, m.y, v.y, clip);
-                    x.z = norm1s(x.z, m.z, v.z, clip);
-                    x.w = norm1s(x.w, m.w, v.w, clip);
+                    x.x = NRM(x.x, m.x, v.x);
+                    x.y = NRM(x.y, m.y, v.y);
+                    x.z = NRM(x.z, m.z, v.z);
+                    x.w = NRM(x.w, m.w, v.w);
                     row_store4(&dst[q], x);
                     if (amask) {
                         const float4 mr = *reinterpret_cast<const float4*>(&sFinM[4 * q]);
-                        const float4 vr = *reinterpret_cast<const float4*>(&sFinS[4 * q]);
+                        const float4 vr = *reinterpret_cast<const float4*>(&fv[4 * q]);
                         x = axr[j];
-                        x.x = norm1s(x.x, mr.x, vr.x, clip);
-                        x.y = norm1s(x.y, mr.y, vr.y, clip);
-                        x.z = norm1s(x.z, mr.z, vr.z, clip);
-                        x.w = norm1s(x.w, mr.w, vr.w, clip);
+                        x.x = NRM(x.x, mr.x, vr.x);
+                        x.y = NRM(x.y, mr.y, vr.y);
+                        x.z = NRM(x.z, mr.z, vr.z);
+                        x.w = NRM(x.w, mr.w, vr.w);
                     }
+#undef NRM
                     float* lx = sX + arw;
                     lx[(4 * q) * XP] = x.x;
                     lx[(4 * q + 1) * XP] = x.y;
@@ -570,7 +594,8 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
             }
         } else {
             // 32 lanes per row: all 16 rows' loads in flight at once
-            if (arw < nrows) add_row<true>(ad, r0 + arw, aln, urel, sX + arw, XP, 32, false);
+            if (arw < nrows)
+                add_row<COLLECT_NORM_STD != 0>(ad, r0 + arw, aln, urel, sX + arw, XP, 32, false);
         }
         if (a.add.rel_next && blockIdx.x == 0 && t == 0)
             *a.add.rel_next = (urel + 1) % a.add.ring_size;

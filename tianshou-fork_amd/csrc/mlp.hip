@@ -1304,7 +1304,7 @@ __global__ __launch_bounds__(256, 2) void dw_kernel(
 #define DWX6_OCC 2
 #endif
 #ifndef DWX6_FULL
-#define DWX6_FULL 1
+#define DWX6_FULL 0
 #endif
 __global__ __launch_bounds__(256, DWX6_OCC) void dw_x6_kernel(
     const float* __restrict__ dz, const float* __restrict__ X, int64_t ldx,
