@@ -318,8 +318,10 @@ def test_tail_reduction_on_side_stream_is_bitwise_single_stream(dev, monkeypatch
         monkeypatch.setattr(fused_mlp, "TAIL_OVERLAP", overlap)
         terms = fm.minibatch(obs, idx, B, act, logp_old, adv, ret, v_s, p, DataParallel())
         torch.cuda.synchronize()
-        out.append((terms.cpu().clone(), [q.grad.detach().cpu().clone() for q in params]))
+        out.append((terms.cpu().clone(),
+                    [q.grad.detach().cpu().clone() for q in params if q.grad is not None]))
     assert torch.equal(out[0][0], out[1][0])
+    assert len(out[0][1]) == len(out[1][1]) >= 13  # both nets' Linear weights/biases + log-std
     for a, b in zip(out[0][1], out[1][1]):
         assert torch.equal(a, b)
 
