@@ -1,7 +1,8 @@
 """Data-parallel host logic on CPU with world_size-2 and -4 gloo groups (no GPU): gradient
 all-reduce (sum and average), all_gather_cat order, and the scaling convention the fused PPO
 loss relies on -- per-rank sums divided by the GLOBAL minibatch size, then summed across
-ranks -- reproduces the single-process full-batch gradient."""
+ranks -- reproduces the single-process full-batch gradient; the bench's N > 1 self-report
+pieces (CollectiveLog call counts and payloads, the replica hash's MAX == MIN check)."""
 import os
 import socket
 
@@ -29,7 +30,8 @@ def _worker(rank, world, port, out):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from tianshou_amd.dist import DataParallel
+    from tianshou_amd.dist import LOG, DataParallel, param_hash
+    LOG.reset()
     dp = DataParallel()
     assert dp.active and dp.world == world and dp.rank == rank
     # all_gather_cat keeps rank order
@@ -60,7 +62,21 @@ def _worker(rank, world, port, out):
     rep = torch.nn.Sequential(torch.nn.Linear(7, 16), torch.nn.Tanh(), torch.nn.Linear(16, 3))
     dp.broadcast_params_(rep.parameters())
     flat = torch.cat([q.detach().reshape(-1) for q in rep.parameters()])
-    out[rank] = (grads_sum, grads_avg, sums, flat)
+    # replica-consistency hash (bench.py's MAX == MIN check): equal replicas, equal hashes;
+    # one flipped bit moves it
+    h = param_hash(rep.parameters())
+    hmax, hmin = h.clone(), h.clone()
+    dist.all_reduce(hmax, op=dist.ReduceOp.MAX)
+    dist.all_reduce(hmin, op=dist.ReduceOp.MIN)
+    bent = [q.detach().clone() for q in rep.parameters()]
+    bent[1].view(-1).view(torch.int32)[3] ^= 1
+    moved = int(param_hash(bent)) != int(h)
+    # the collective log: logical calls by kind and the last payload of each kind
+    log = (dict(LOG.calls), dict(LOG.payload))
+    LOG.replayed({"obs_rms": 3})
+    LOG.replayed(None)
+    replayed = LOG.calls["obs_rms"]
+    out[rank] = (grads_sum, grads_avg, sums, flat, (int(hmax), int(hmin), moved, log, replayed))
     dist.destroy_process_group()
 
 
@@ -79,9 +95,16 @@ def test_data_parallel_gloo_ranks(world):
     torch.manual_seed(100)
     rep0 = torch.nn.Sequential(torch.nn.Linear(7, 16), torch.nn.Tanh(), torch.nn.Linear(16, 3))
     want = torch.cat([q.detach().reshape(-1) for q in rep0.parameters()])
+    n_grad = sum(q.numel() for q in net.parameters())
     for r in range(world):
-        gs, ga, sums, flat = out[r]
+        gs, ga, sums, flat, (hmax, hmin, moved, (calls, payload), replayed) = out[r]
         assert torch.equal(flat, want)
+        assert hmax == hmin and moved
+        assert calls == {"other": 2, "grad": 2, "param_broadcast": 1}
+        assert payload["grad"] == ("all_reduce", n_grad, "float32", 4 * n_grad)
+        assert payload["param_broadcast"] == ("broadcast", n_grad, "float32", 4 * n_grad)
+        assert payload["other"] == ("all_reduce", 2, "float64", 16)
+        assert replayed == 3
         for a, b in zip(gs, full):
             np.testing.assert_allclose(a.numpy(), b.numpy(), rtol=1e-5, atol=1e-7)
         for a, b in zip(ga, full):  # equal shards: mean of means == global mean
