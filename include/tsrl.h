@@ -326,6 +326,9 @@ int tsrl_ring_advance(int64_t* rel_dev, int64_t ring_size, void* stream);
  *   save_only_last_obs frame store of the Atari setup, examples/atari/atari_ppo.py:183-189,
  *   or whole stored rows); chain_out [k][stack_num] (nullable) receives the row indices so
  *   that other keys (info, policy) can be stacked alike; dst may be NULL (chain only).
+ * tsrl_stack_gather_pitched: the same with source rows src_pitch bytes apart (a padded
+ *   storage: wide f32 observation rows kept 128-byte aligned, see tsrl_gather_rows_pitched);
+ *   the output frames are packed (frame_bytes apart).
  * ------------------------------------------------------------------------------- */
 int tsrl_ring_step_index(const int64_t* idx, int64_t k, const uint8_t* done,
                          const int64_t* last_index, const int64_t* lengths, int64_t size,
@@ -334,6 +337,11 @@ int tsrl_stack_gather(const void* src, int64_t frame_bytes, const int64_t* idx, 
                       int64_t stack_num, const uint8_t* done, const int64_t* last_index,
                       const int64_t* lengths, int64_t size, int64_t num, void* dst,
                       int64_t* chain_out, void* stream);
+int tsrl_stack_gather_pitched(const void* src, int64_t src_pitch, int64_t frame_bytes,
+                              const int64_t* idx, int64_t k, int64_t stack_num,
+                              const uint8_t* done, const int64_t* last_index,
+                              const int64_t* lengths, int64_t size, int64_t num, void* dst,
+                              int64_t* chain_out, void* stream);
 
 /* Frame-stack input of the Atari trunk: dst[r][p][ch] = lut[src[r][ch][p]] for n rows of c
  * planes of hw bytes -- the uint8 [n, c, h, w] observations as the channels_last (NHWC) f32

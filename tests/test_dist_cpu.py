@@ -68,9 +68,11 @@ def _worker(rank, world, port, out):
     hmax, hmin = h.clone(), h.clone()
     dist.all_reduce(hmax, op=dist.ReduceOp.MAX)
     dist.all_reduce(hmin, op=dist.ReduceOp.MIN)
-    bent = [q.detach().clone() for q in rep.parameters()]
-    bent[1].view(-1).view(torch.int32)[3] ^= 1
-    moved = int(param_hash(bent)) != int(h)
+    moved = True
+    for bit in (0, 31):  # the lowest mantissa bit and the sign bit
+        bent = [q.detach().clone() for q in rep.parameters()]
+        bent[1].view(-1).view(torch.int32)[3] ^= (1 << bit) if bit < 31 else -(1 << 31)
+        moved = moved and int(param_hash(bent)) != int(h)
     # the collective log: logical calls by kind and the last payload of each kind
     log = (dict(LOG.calls), dict(LOG.payload))
     LOG.replayed({"obs_rms": 3})

@@ -97,6 +97,7 @@ __global__ __launch_bounds__(OTPB) void clip_adam_kernel(float* __restrict__ p,
                                                          unsigned int* ticket, const float* __restrict__ lr_dev,
                                                          SplitOut so, int fused_norm) {
     __shared__ float s_scale;
+    __shared__ int s_late;  // the slice-norm hand-off timed out
     const int t = threadIdx.x;
     const bool clip = a.max_norm > 0.0f;
     const float st = step[0] + 1.0f;
@@ -114,6 +115,7 @@ __global__ __launch_bounds__(OTPB) void clip_adam_kernel(float* __restrict__ p,
         vr[q] = in ? v[i] : 0.0f;
         pr[q] = in ? p[i] : 0.0f;
     }
+    if (t == 0) s_late = 0;
     if (clip && fused_norm) {
         __shared__ double red[OTPB / kWave];
         double ss = 0.0;
@@ -131,15 +133,21 @@ __global__ __launch_bounds__(OTPB) void clip_adam_kernel(float* __restrict__ p,
             __hip_atomic_store(&partials[blockIdx.x], tot, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_fetch_add(&ticket[1], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            // bounded wait: every workgroup of this small grid is resident (the arrivals
-            // never depend on a workgroup that waits); the bound only turns an impossible
-            // hang into a wrong coefficient
+            // bounded wait: every workgroup of this small grid (<= the host's resident-slot
+            // count) is resident, so the arrivals never depend on a workgroup that waits; if
+            // the bound still runs out (e.g. another process holding the CUs), the norm is
+            // poisoned with NaN below -- a loud NaN step (and norm_out NaN) instead of a
+            // silently wrong clip coefficient from missing partials
+            int late = 1;
             for (uint32_t spin = 0; spin < (1u << 24); ++spin) {
                 if (__hip_atomic_load(&ticket[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >=
-                    gridDim.x)
+                    gridDim.x) {
+                    late = 0;
                     break;
+                }
                 __builtin_amdgcn_s_sleep(1);
             }
+            s_late = late;
         }
     }
     if (clip) {
@@ -152,7 +160,7 @@ __global__ __launch_bounds__(OTPB) void clip_adam_kernel(float* __restrict__ p,
                 ss += __hip_atomic_load(&partials[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             ss = wave_sum(ss);
             if (t == 0) {
-                const float norm = (float)sqrt(ss);
+                const float norm = s_late ? __builtin_nanf("") : (float)sqrt(ss);
                 // torch.clamp(coef, max=1.0): a NaN norm (a NaN or infinite gradient element)
                 // gives a NaN coefficient that reaches every gradient, as in clip_grad_norm_
                 // (fminf would return 1.0 and leave the finite gradients unclipped)
@@ -230,8 +238,17 @@ extern "C" int tsrl_clip_adam(float* param, float* grad, float* exp_avg, float* 
     TSRL_CHECK_ARG(max_norm <= 0.0f || (norm_out && partials),
                    "tsrl_clip_adam: clipping needs partials and norm_out[2]");
     // the in-kernel slice-norm hand-off needs every workgroup resident at once: up to one
-    // slice per CU; larger parameter sets take the separate norm launch
-    const int fused_norm = grid <= 256;
+    // slice per CU of this device (hipDeviceAttributeMultiprocessorCount, 256 on MI355X);
+    // larger parameter sets take the separate norm launch
+    static int n_cu = 0;
+    if (n_cu == 0) {
+        int dev = 0, cu = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cu = 1;
+        n_cu = cu > 0 ? cu : 1;
+    }
+    const int fused_norm = grid <= n_cu;
     if (max_norm > 0.0f && !fused_norm) {
         hipLaunchKernelGGL(norm_partials_kernel, dim3((unsigned)grid), dim3(OTPB), 0,
                            as_stream(stream), grad, n, partials);

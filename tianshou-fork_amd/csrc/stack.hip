@@ -44,6 +44,7 @@ __device__ __forceinline__ void copy_frame(const char* s, char* d, int64_t bytes
 
 // Output row r, frame s: wave (r * S + s) over the flattened grid.
 __global__ __launch_bounds__(TPB) void stack_gather_kernel(Ring g, const char* src,
+                                                           int64_t src_pitch,
                                                            int64_t frame_bytes,
                                                            const int64_t* idx, int64_t k,
                                                            int S, char* dst, int64_t* chain) {
@@ -55,7 +56,7 @@ __global__ __launch_bounds__(TPB) void stack_gather_kernel(Ring g, const char* s
     // base.py:344-350: the newest frame is val[index] (index as given), older ones step prev
     int64_t i = pmod(idx[r], g.maxsize);
     for (int q = S - 1; q > s; --q) i = ring_prev(g, i);
-    if (dst) copy_frame(src + i * frame_bytes, dst + wv * frame_bytes, frame_bytes, lane);
+    if (dst) copy_frame(src + i * src_pitch, dst + wv * frame_bytes, frame_bytes, lane);
     if (chain && lane == 0) chain[wv] = i;
 }
 
@@ -148,12 +149,14 @@ extern "C" int tsrl_ring_step_index(const int64_t* idx, int64_t k, const uint8_t
     return 0;
 }
 
-extern "C" int tsrl_stack_gather(const void* src, int64_t frame_bytes, const int64_t* idx,
-                                 int64_t k, int64_t stack_num, const uint8_t* done,
-                                 const int64_t* last_index, const int64_t* lengths,
-                                 int64_t size, int64_t num, void* dst, int64_t* chain_out,
-                                 void* stream) {
-    TSRL_CHECK_ARG(k >= 0 && stack_num >= 1 && stack_num <= 1024 && frame_bytes >= 0,
+extern "C" int tsrl_stack_gather_pitched(const void* src, int64_t src_pitch,
+                                         int64_t frame_bytes, const int64_t* idx, int64_t k,
+                                         int64_t stack_num, const uint8_t* done,
+                                         const int64_t* last_index, const int64_t* lengths,
+                                         int64_t size, int64_t num, void* dst,
+                                         int64_t* chain_out, void* stream) {
+    TSRL_CHECK_ARG(k >= 0 && stack_num >= 1 && stack_num <= 1024 && frame_bytes >= 0 &&
+                       src_pitch >= frame_bytes,
                    "tsrl_stack_gather: bad sizes");
     if (k == 0) return 0;
     if (int rc = check_ring(done, last_index, lengths, size, num, "tsrl_stack_gather"))
@@ -165,8 +168,18 @@ extern "C" int tsrl_stack_gather(const void* src, int64_t frame_bytes, const int
     const int64_t grid = (waves + WPB - 1) / WPB;
     TSRL_CHECK_ARG(grid < (1ll << 31), "tsrl_stack_gather: too many rows");
     hipLaunchKernelGGL(stack_gather_kernel, dim3((unsigned)grid), dim3(TPB), 0,
-                       as_stream(stream), g, reinterpret_cast<const char*>(src), frame_bytes,
-                       idx, k, (int)stack_num, reinterpret_cast<char*>(dst), chain_out);
+                       as_stream(stream), g, reinterpret_cast<const char*>(src), src_pitch,
+                       frame_bytes, idx, k, (int)stack_num, reinterpret_cast<char*>(dst),
+                       chain_out);
     TSRL_LAUNCH_CHECK("tsrl_stack_gather");
     return 0;
+}
+
+extern "C" int tsrl_stack_gather(const void* src, int64_t frame_bytes, const int64_t* idx,
+                                 int64_t k, int64_t stack_num, const uint8_t* done,
+                                 const int64_t* last_index, const int64_t* lengths,
+                                 int64_t size, int64_t num, void* dst, int64_t* chain_out,
+                                 void* stream) {
+    return tsrl_stack_gather_pitched(src, frame_bytes, frame_bytes, idx, k, stack_num, done,
+                                     last_index, lengths, size, num, dst, chain_out, stream);
 }

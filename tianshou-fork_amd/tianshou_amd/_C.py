@@ -129,6 +129,8 @@ _SIGS = {
     "tsrl_shuffle_apply": ([_p, _i64, _p, _p, _i64, _p], ctypes.c_int),
     "tsrl_ring_step_index": ([_p, _i64, _p, _p, _p, _i64, _i64, ctypes.c_int, _p, _p],
                              ctypes.c_int),
+    "tsrl_stack_gather_pitched": ([_p, _i64, _i64, _p, _i64, _i64, _p, _p, _p, _i64, _i64, _p,
+                                   _p, _p], ctypes.c_int),
     "tsrl_stack_gather": ([_p, _i64, _p, _i64, _i64, _p, _p, _p, _i64, _i64, _p, _p, _p],
                           ctypes.c_int),
     "tsrl_frames_to_f32_nhwc": ([_p, _i64, _i64, _i64, _p, _p, _p], ctypes.c_int),

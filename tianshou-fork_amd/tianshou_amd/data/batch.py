@@ -31,7 +31,7 @@ def gather_rows(t: torch.Tensor, index) -> torch.Tensor:
         # rows of a padded storage (VectorReplayBuffer pads wide f32 observation rows to a
         # 128-byte multiple): gathered in place, no copy of the storage
         _C.check(_C.lib().tsrl_gather_rows_pitched(
-            _C.ptr(t), t.stride(0) * t.element_size(), row_bytes, _C.ptr(index), k,
+            _C.ptr_rows(t), t.stride(0) * t.element_size(), row_bytes, _C.ptr(index), k,
             _C.ptr(out), _C.stream_ptr()), "tsrl_gather_rows")
         return out
     src = t if t.is_contiguous() else t.contiguous()

@@ -589,8 +589,11 @@ class VectorReplayBuffer:
             return out, chain
         done, last, lengths = self._ring_dev()
         row_bytes = val.element_size() * int(np.prod(val.shape[1:]))
-        _C.check(_C.lib().tsrl_stack_gather(
-            _C.ptr(val), row_bytes, _C.ptr(it), k, stack_num, _C.ptr(done), _C.ptr(last),
+        # padded storage (wide f32 rows 128-byte aligned, obs_storage): rows stride(0) apart
+        pitch = val.stride(0) * val.element_size() if val.dim() >= 2 else row_bytes
+        _C.check(_C.lib().tsrl_stack_gather_pitched(
+            _C.ptr_rows(val), pitch, row_bytes, _C.ptr(it), k, stack_num, _C.ptr(done),
+            _C.ptr(last),
             _C.ptr(lengths), self._ring.size, self.buffer_num, _C.ptr(out), _C.ptr(chain),
             _C.stream_ptr(self.device)), "tsrl_stack_gather")
         return out, chain

@@ -151,10 +151,12 @@ def param_hash(params: Iterable[torch.Tensor]) -> torch.Tensor:
     compares its all-reduced MAX and MIN)."""
     h = None
     for i, p in enumerate(params):
+        # every one of the 32 bits (the sign too) as a value in [0, 2^32); times a weight
+        # < 2^31 it stays below 2^63
         bits = p.detach().reshape(-1).contiguous().view(torch.int32).to(torch.int64)
         w = torch.arange(bits.numel(), device=bits.device, dtype=torch.int64) * 2654435761 \
             + (i + 1) * 97
-        v = ((bits & 0x7FFFFFFF) * (w % 2147483647 + 1)).remainder(2305843009213693951).sum()
+        v = ((bits & 0xFFFFFFFF) * (w % 2147483647 + 1)).remainder(2305843009213693951).sum()
         h = v if h is None else (h * 31 + v).remainder(2305843009213693951)
     return h
 
