@@ -49,6 +49,13 @@ def rank_runs(tmp_path_factory):
     dirs["c4"] = d
     procs += [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "dist_c4_worker.py"),
                                 str(r), "2", port, str(d)], env=env) for r in range(2)]
+    # unequal env shards (48 + 80 envs), fused collect step, global split (dist_unequal_worker)
+    port = str(_free_port())
+    d = tmp_path_factory.mktemp("uneq")
+    dirs["uneq"] = d
+    procs += [subprocess.Popen([sys.executable,
+                                os.path.join(ROOT, "tests", "dist_unequal_worker.py"),
+                                str(r), "2", port, str(d)], env=env) for r in range(2)]
     rcs = [p.wait(timeout=600) for p in procs]
     assert rcs == [0] * len(procs), rcs
     return dirs
@@ -137,6 +144,50 @@ def test_config4_shape_dp_update(rank_runs):
     r = torch.load(rank_runs["c4"] / "c4.pt", weights_only=True)
     assert r["rms_count"] >= 2 * 512 * 2049  # both shards' reset + step rows (+ auto-resets)
     assert r["loss"].shape == r["loss_ref"].shape == (4, 32)
+    np.testing.assert_allclose(r["loss"].numpy(), r["loss_ref"].numpy(), rtol=1e-4, atol=1e-6)
+    for k, v in r["sd"].items():
+        # one Adam step moves a weight by up to lr = 3e-4: atol = lr / 3
+        np.testing.assert_allclose(v.numpy(), r["sd_ref"][k].numpy(), rtol=1e-4, atol=1e-4,
+                                   err_msg=k)
+
+
+def test_unequal_env_shards(rank_runs):
+    """Data parallelism over unequal env shards (48 and 80 envs, D = 376, the fused collect
+    step; dist_unequal_worker.py): every rank holds the obs_rms of ONE VectorEnvNormObs over
+    all 128 envs (count exact, mean / var vs a host RunningMeanStd over the NumPy env at the
+    device recipe's tolerance), and one update with the global-batch split equals the single
+    process over the union (venv_wrappers.py:93-99, batch.py:896-912)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import dist_unequal_worker as w
+    r = torch.load(rank_runs["uneq"] / "uneq.pt", weights_only=True)
+    assert torch.equal(r["rms_mean"], r["rms_mean1"]) and torch.equal(r["rms_var"], r["rms_var1"])
+    from oracle.synth_env import SynthVecEnvNP
+    envs = [SynthVecEnvNP(E, (w.D,), w.A, w.L, seed=k) for k, E in enumerate(w.SHARDS)]
+    mean, var, count = np.zeros(w.D), np.ones(w.D), 0.0
+
+    def upd(x):
+        nonlocal mean, var, count
+        if len(x) == 0:
+            return
+        x = x.astype(np.float64)
+        bm, bv, bc = x.mean(0), x.var(0), float(len(x))
+        delta = bm - mean
+        tot = count + bc
+        mean, var = mean + delta * bc / tot, \
+            (var * count + bv * bc + delta ** 2 * count * bc / tot) / tot
+        count = tot
+
+    upd(np.concatenate([e.reset() for e in envs]))
+    for _ in range(w.T):
+        outs = [e.step() for e in envs]
+        upd(np.concatenate([o[0] for o in outs]))
+        resets = [e.reset(np.flatnonzero(o[2] | o[3])) for e, o in zip(envs, outs)
+                  if (o[2] | o[3]).any()]
+        upd(np.concatenate(resets) if resets else np.zeros((0, w.D), np.float32))
+    assert int(r["rms_count"]) == int(count)
+    np.testing.assert_allclose(r["rms_mean"].numpy(), mean, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(r["rms_var"].numpy(), var, rtol=1e-5, atol=1e-6)
+    assert r["loss"].shape == r["loss_ref"].shape == (4, sum(w.SHARDS) * w.T // (2 * w.BS))
     np.testing.assert_allclose(r["loss"].numpy(), r["loss_ref"].numpy(), rtol=1e-4, atol=1e-6)
     for k, v in r["sd"].items():
         # one Adam step moves a weight by up to lr = 3e-4: atol = lr / 3

@@ -209,3 +209,45 @@ def test_frame_stack_oracle(golden_dir, name, stack_num, last_only, ign_next, av
         assert np.array_equal(ref.avail_indices(ix, stack_num), z[p + "sample0"])
     else:
         assert np.array_equal(ix.sample_indices0(), z[p + "sample0"])
+
+
+def test_rms_production_rows(golden_dir):
+    """RunningMeanStd at the headline's row count: two updates on [4096, 376] batches of the
+    synthetic env's raw rows (regenerated from the env keys) give the reference's f32
+    mean / var bit for bit (tools/gen_goldens.py gen_rms_wide; statistics.py:99-114)."""
+    z = _load(golden_dir, "rms_wide.npz")
+    E, D = int(z["E"]), int(z["D"])
+    r = ref.RMS()
+    for i in range(2):
+        k = synth_env.key(0, np.arange(E), np.zeros(E, np.int64), np.full(E, int(z[f"t{i}"])))
+        r.update(synth_env.box_obs(k, D))
+        assert np.array_equal(np.asarray(r.mean), z[f"mean{i}"])
+        assert np.array_equal(np.asarray(r.var), z[f"var{i}"])
+        assert r.count == int(z[f"count{i}"])
+
+
+def test_synth_env_obs_rms_production_rows(golden_dir):
+    """The reference Collector + VectorEnvNormObs at 4096 envs x D = 376 (gen_collector_wide):
+    the NumPy env + RMS restatement reproduces obs_rms after the initial reset and after every
+    one of the 8 vector steps bit for bit, and the stored rewards."""
+    z = _load(golden_dir, "collector_wide.npz")
+    E, D, L, T = (int(z[k]) for k in ("E", "D", "L", "T"))
+    env = synth_env.SynthVecEnvNP(E, (D,), int(z["A"]), L)
+    rms = ref.RMS()
+
+    def check(t):
+        assert np.array_equal(np.asarray(rms.mean, np.float32), z[f"rms{t}_mean"]), t
+        assert np.array_equal(np.asarray(rms.var, np.float32), z[f"rms{t}_var"]), t
+        assert rms.count == int(z[f"rms{t}_count"]), t
+
+    rms.update(env.reset())
+    check(0)
+    rew = np.zeros((E, T))
+    for t in range(T):
+        nxt, rew[:, t], term, trunc = env.step()
+        rms.update(nxt)
+        done = np.flatnonzero(term | trunc)
+        if len(done):
+            rms.update(env.reset(done))
+        check(t + 1)
+    assert np.array_equal(rew.reshape(-1), z["c1_rew"])

@@ -61,18 +61,6 @@ constexpr int KMAX = 512;      // observation columns handled (padded to 128)
 constexpr int XP = 17;         // LDS pitch of the live-obs tile sX[col][row]
 constexpr int HP = 16;         // h1 / h2 tiles [feature][row]
 constexpr int WP = 68;         // W2 / W3 rows (4i + k banks: conflict-free A fragments)
-// diagnostic builds only (tools/collect_step_bench.py): return after phase 1 (add), 2 (actor)
-// or 3 (env); 0 = the whole step
-// (round 3 measured a variant issuing the obs_rms atomics after the actor: slower, removed)
-#ifndef COLLECT_STOP
-#define COLLECT_STOP 0
-#endif
-#ifndef COLLECT_NO_RAW
-#define COLLECT_NO_RAW 0  // diagnostic builds only: skip the raw env-row stores (wrong rows)
-#endif
-#ifndef COLLECT_NO_TOTALS
-#define COLLECT_NO_TOTALS 0  // diagnostic builds only: skip the obs_rms atomics (wrong stats)
-#endif
 // diagnostic builds only: per-workgroup s_memrealtime stamps (100 MHz) after each phase,
 // stored behind the workspace (tools/collect_step_bench.py --trace)
 #ifndef COLLECT_TRACE
@@ -89,48 +77,30 @@ constexpr int WP = 68;         // W2 / W3 rows (4i + k banks: conflict-free A fr
 #define TSTAMP2(i)
 #endif
 
-// Store form of the replay rows this step writes (obs and obs_next: 12.6 MB per 4096 x 376
-// step, not read again by this collect).  3 (default): write-through `sc1` vector stores
-// (inline asm, s_nop 1 after each so the data VGPRs are read before reuse), which leave no
-// dirty lines for the end-of-kernel write-back: 23.97-24.04 vs 25.66-25.87 us per step with
-// plain stores, two A/B rounds in one call (tools/collect_ab.sh).  4: also the raw env rows
-// (re-read by the next launch): 24.13-24.21.  0: plain.  Measured earlier and dropped: 1 =
-// non-temporal stores (26.2 vs 25.6), 2 = relaxed agent-scope 8-byte atomic stores (28.9).
-#ifndef COLLECT_ROW_STORE
-#define COLLECT_ROW_STORE 3
-#endif
-// 1: the env rows' counter keys, reward and flags are computed at the top of the launch by
-// the last R threads (wave 7: no merge column for D <= NT - R) while the merge's loads are in
-// flight, and the env phase only stores them; 0: computed inside the env phase by wave 0.
-#ifndef COLLECT_EARLY_KEYS
-#define COLLECT_EARLY_KEYS 0
-#endif
-// 1: sqrt(var + eps) of both statistics computed once per column and staged in LDS, the add
-// divides by it (same bits as norm1); 0: norm1 per element (a correctly rounded square root
-// per normalised value)
-#ifndef COLLECT_NORM_STD
-#define COLLECT_NORM_STD 0
-#endif
-// 1: this step's stored obs rows leave LDS one column per thread over the 16 rows; 0: the
-// round-3 flat loop over row * D + column (an integer division by D per element)
-#ifndef COLLECT_OBS_COLS
-#define COLLECT_OBS_COLS 0
-#endif
+// The replay rows this step writes (obs and obs_next: 12.6 MB per 4096 x 376 step, not read
+// again by this collect) leave as write-through `sc1` vector stores (inline asm, s_nop 1
+// after each so the data VGPRs are read before reuse): no dirty lines for the end-of-kernel
+// write-back, 23.97-24.04 vs 25.66-25.87 us per step with plain stores, two A/B rounds in one
+// call (tools/collect_ab.sh, round 3).  Measured and dropped: the raw env rows (re-read by
+// the next launch) write-through as well (24.13-24.21), non-temporal stores (26.2 vs 25.6),
+// relaxed agent-scope 8-byte atomic stores (28.9).
+// Round 5 A/B of the round-4 variants (tools/r05_ab.sh, profiles/r05_variant_ab.log), all
+// three now the only form: 24.0-24.2 -> 21.5 us per step together (each alone: 24.1 / 23.6 /
+// 23.4) --
+//  * the env rows' counter keys, reward and flags are computed at the top of the launch by
+//    the last R threads (wave 7: no merge column for D <= NT - R) while the merge's loads are
+//    in flight, and the env phase only stores them;
+//  * sqrt(var + eps) of both statistics is computed once per column and staged in LDS, and
+//    the add divides by it (same bits as a correctly rounded square root per element);
+//  * this step's stored obs rows leave LDS one column per thread over the 16 rows (no integer
+//    division by D per element).
 __device__ __forceinline__ void row_store4(float4* p, float4 x) {
-#if COLLECT_ROW_STORE >= 3
     typedef float f4v __attribute__((ext_vector_type(4)));
     const f4v v = {x.x, x.y, x.z, x.w};
     asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
-#else
-    *p = x;
-#endif
 }
 __device__ __forceinline__ void row_store1(float* p, float x) {
-#if COLLECT_ROW_STORE >= 3
     asm volatile("global_store_dword %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(x) : "memory");
-#else
-    *p = x;
-#endif
 }
 
 // Workgroup barrier that orders LDS only: outstanding global loads and stores stay in flight
@@ -266,13 +236,11 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
     __shared__ RowState rs[R], rr[R];
     __shared__ float sAr[CPL ? R : 1][AMAX + 1];  // CPL: this workgroup's remapped actions
     __shared__ int s_nd;
-#if COLLECT_EARLY_KEYS
     // the rows' reward, flags (term | trunc << 1 | done << 2) and new episode counters,
     // stored to HBM by the env phase
     __shared__ double s_rew[R];
     __shared__ int s_flg[R];
     __shared__ int64_t s_jn[R], s_tn[R];
-#endif
     __shared__ float* s_row[R];  // this step's stored obs row of each env (obs_dst + pitch)
     // deferred obs_rms merge: the statistics after the previous step's step rows (obs_next
     // normalisation) and after its reset rows (reset rows, state)
@@ -280,8 +248,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         sFinV[KMAX];
     // sqrt(var + eps) of both statistics, once per column (the add divides by them: the
     // correctly rounded square root is ~20 VALU, per element before)
-    __shared__ __attribute__((aligned(16))) float sSnapS[COLLECT_NORM_STD ? KMAX : 4],
-        sFinS[COLLECT_NORM_STD ? KMAX : 4];
+    __shared__ __attribute__((aligned(16))) float sSnapS[KMAX], sFinS[KMAX];
     const int t = threadIdx.x;
     const int w = t >> 6, l = t & 63;
     const int64_t k = a.k;
@@ -293,9 +260,6 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
     const int64_t rng_step = a.rng_ctr ? *a.rng_ctr : 0;
     // this step's ring position of the pending add (first load: nothing waits behind it)
     const int64_t urel = a.add.k > 0 ? (a.add.rel_dev ? *a.add.rel_dev : a.add.uniform_rel) : 0;
-#if COLLECT_STOP == 9
-    if (t >= 0) return;  // launch overhead only
-#endif
 #if COLLECT_TRACE
     if (t == 0) {
         unsigned xcc, hwid;
@@ -330,7 +294,6 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
                       (ad.act_row_bytes & 3) == 0 && act_n <= 32 &&
                       aligned16(ad.obs_next_src) && aligned16(ad.obs_next_dst) &&
                       aligned16(ad.reset_src);
-#if COLLECT_EARLY_KEYS
     // the episode counters of the key rows, loaded before anything else
     constexpr int KT0 = NT - R;
     const int ki = t - KT0;
@@ -341,7 +304,6 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         kt = a.ep_t[r0 + ki];
         koff = a.obs_offset[r0 + ki];
     }
-#endif
     const int64_t ar = r0 + arw;
     const bool arow = fast && arw < nrows;
     float4 axs[AQ], axr[AQ];
@@ -393,7 +355,6 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         }
     }
     TSTAMP2(2)
-#if COLLECT_EARLY_KEYS
     if (ki >= 0) {
         // this step's counter keys (env.hip box_step_reset_kernel): every read the env phase
         // needs from them goes to LDS; the HBM stores wait for the env phase (the pending add
@@ -433,7 +394,6 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
             s_row[ki] = a.obs_dst + (koff + uo) * (a.obs_pitch ? a.obs_pitch : D);
         }
     }
-#endif
     if (merge) {
         // the step rows behind the totals (counted in the slot: k, or the sum of every
         // rank's k when the slot was all-reduced)
@@ -447,10 +407,8 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
             else
                 merge_column((double)mm0, (double)mv0, mcount, kp, ms1, mq1, mnd, ms2, mq2,
                              sSnapM[t], sSnapV[t], sFinM[t], sFinV[t]);
-#if COLLECT_NORM_STD
             sSnapS[t] = __builtin_sqrtf(sSnapV[t] + ad.norm_eps);
             sFinS[t] = __builtin_sqrtf(sFinV[t] + ad.norm_eps);
-#endif
         }
         TSTAMP2(3)
         LDS_SYNC();
@@ -466,15 +424,15 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
             long long* tz = ws.tot[tnext];
             for (int i = t; i < 4 * D + 2; i += NT) tz[i] = 0;
         }
-        // the add reads the statistics from LDS (COLLECT_NORM_STD: with sqrt(var + eps) per
-        // column, add_row<true>)
+        // the add reads the statistics from LDS, with sqrt(var + eps) per column
+        // (add_row<true>)
         if (ad.norm_mean) {
             ad.norm_mean = sSnapM;
-            ad.norm_var = COLLECT_NORM_STD ? sSnapS : sSnapV;
+            ad.norm_var = sSnapS;
         }
         if (ad.reset_mean) {
             ad.reset_mean = sFinM;
-            ad.reset_var = COLLECT_NORM_STD ? sFinS : sFinV;
+            ad.reset_var = sFinS;
         }
     } else if (defer && blockIdx.x == 0) {
         // first step of a chain: the caller's state seeds the state slot (slot 1 of the
@@ -486,7 +444,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         }
         if (t == 0) so->count = *a.count;
     }
-    if (COLLECT_NORM_STD && !merge && ad.k > 0 && (ad.norm_mean || ad.reset_mean)) {
+    if (!merge && ad.k > 0 && (ad.norm_mean || ad.reset_mean)) {
         // statistics of a launch without the deferred merge (exact obs_rms, a chain's first
         // step): staged into LDS with sqrt(var + eps) per column, as the merge leaves them
         for (int d = t; d < D; d += NT) {
@@ -556,15 +514,9 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
                 for (int j = 0; j < AQ; ++j) {
                     const int q = aln + 32 * j;
                     if (q >= nq) break;
-#if COLLECT_NORM_STD
 #define NRM(x_, m_, s_) norm1s(x_, m_, s_, clip)
                     const float* const sv = sSnapS;
                     const float* const fv = sFinS;
-#else
-#define NRM(x_, m_, v_) norm1(x_, m_, v_, ad.norm_eps, clip)
-                    const float* const sv = sSnapV;
-                    const float* const fv = sFinV;
-#endif
                     const float4 m = *reinterpret_cast<const float4*>(&sSnapM[4 * q]);
                     const float4 v = *reinterpret_cast<const float4*>(&sv[4 * q]);
                     float4 x = axs[j];
@@ -595,7 +547,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         } else {
             // 32 lanes per row: all 16 rows' loads in flight at once
             if (arw < nrows)
-                add_row<COLLECT_NORM_STD != 0>(ad, r0 + arw, aln, urel, sX + arw, XP, 32, false);
+                add_row<true>(ad, r0 + arw, aln, urel, sX + arw, XP, 32, false);
         }
         if (a.add.rel_next && blockIdx.x == 0 && t == 0)
             *a.add.rel_next = (urel + 1) % a.add.ring_size;
@@ -616,14 +568,6 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         }
     }
     TSTAMP(1)
-#if !COLLECT_EARLY_KEYS
-    // the env rows' episode counters: loaded now, used by the env step
-    int64_t ej = 0, et = 0;
-    if (t < nrows) {
-        ej = a.ep_j[r0 + t];
-        et = a.ep_t[r0 + t];
-    }
-#endif
     // zero padding: columns [D, Kp) and rows past the last env of a partial tile
     for (int i = t; i < (Kp - D) * R; i += NT) sX[(D + i / R) * XP + (i % R)] = 0.0f;
     if (nrows < R)
@@ -673,34 +617,11 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
     LDS_SYNC();
     // this step's stored obs rows (ReplayBuffer obs of step i = the live obs the actor sees):
     // written here from LDS, so the add of step i (next launch / flush) copies nothing and the
-    // live obs never round-trips through HBM between fused steps (COLLECT_EARLY_KEYS: their
-    // row pointers came from the top of the launch)
-#if !COLLECT_EARLY_KEYS
-    if (t < nrows) {
-        // with a pending add this launch's block 0 advances the device cursor concurrently,
-        // so the position is the add's own plus one (the ring's uniform next)
-        int64_t urel;
-        if (a.add.k > 0) {
-            const int64_t up = a.add.rel_dev ? *a.add.rel_dev : a.add.uniform_rel;
-            urel = (up + 1) % a.add.ring_size;
-        } else {
-            urel = a.obs_rel_dev ? *a.obs_rel_dev : a.obs_uniform_rel;
-        }
-        const int64_t opitch = a.obs_pitch ? a.obs_pitch : D;
-        s_row[t] = a.obs_dst + (a.obs_offset[r0 + t] + urel) * opitch;
-    }
-    LDS_SYNC();
-#endif
-#if COLLECT_OBS_COLS
+    // live obs never round-trips through HBM between fused steps (their row pointers came
+    // from the top of the launch)
     // one column per thread (D <= NT), the rows in turn: no index division, coalesced rows
     if (t < D)
         for (int rw = 0; rw < nrows; ++rw) row_store1(s_row[rw] + t, sX[t * XP + rw]);
-#else
-    for (int i = t; i < nrows * D; i += NT) {
-        const int rw = i / D, c = i - rw * D;
-        row_store1(s_row[rw] + c, sX[c * XP + rw]);
-    }
-#endif
     // ---- C. env step + auto-reset of these rows (env.hip box_step_reset_kernel) -------------
     // The quantised synthetic env's transition does not read the action, so its step runs
     // before the actor: its obs_rms atomics drain while the actor computes.  The
@@ -708,7 +629,6 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
     // this launch has consumed the previous step's env rows of this workgroup (the barrier
     // above).
     auto env_phase = [&]() {
-#if COLLECT_EARLY_KEYS
         if (t < nrows) {
             // keys, reward and flags came from the top of the launch (LDS)
             const int64_t r = r0 + t;
@@ -720,39 +640,6 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
             if (f & 4) a.ep_j[r] = s_jn[t];
             a.ep_t[r] = s_tn[t];
         }
-#else
-        if (t == 0) s_nd = 0;
-        LDS_SYNC();
-        if (t < R) {
-            const int64_t r = r0 + t;
-            RowState st = {0ull, 0}, sr = {0ull, 0};
-            if (t < nrows) {
-                const int64_t e = r;
-                int64_t j = ej;
-                int64_t tt = et + 1;
-                st.key = env_key(a.env_seed, (uint64_t)e, j, tt);
-                st.active = 1;
-                const uint64_t h = sm64(st.key ^ REW_SALT);
-                a.rew[r] = (double)(h >> 40) * 0x1p-24;
-                const bool dn = tt >= a.ep_len;
-                a.term[r] = (uint8_t)(dn && (e % 2 == 0));
-                a.trunc[r] = (uint8_t)(dn && (e % 2 == 1));
-                a.done[r] = (uint8_t)dn;
-                if (dn) {
-                    j += 1;
-                    tt = (j == 0) ? (e % a.ep_len) : 0;
-                    a.ep_j[e] = j;
-                    sr.key = env_key(a.env_seed, (uint64_t)e, j, tt);
-                    sr.active = 1;
-                    atomicAdd(&s_nd, 1);
-                }
-                a.ep_t[e] = tt;
-            }
-            rs[t] = st;
-            rr[t] = sr;
-        }
-        LDS_SYNC();
-#endif
         const int nd = s_nd;
         long long* tc = ws.tot[tcur];
         if (CPL) {
@@ -803,11 +690,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
             const int d = t;
             for (int r = 0; r < nrows; ++r) {
                 const int m = box_m(rs[r].key, d);
-#if COLLECT_ROW_STORE == 4
-                row_store1(&a.raw[(r0 + r) * D + d], (float)m * 0x1p-23f);
-#elif !COLLECT_NO_RAW
                 a.raw[(r0 + r) * D + d] = (float)m * 0x1p-23f;  // == box_val(key, d), exactly
-#endif
                 cs1 += m;
                 cq1 += (long long)m * m;
             }
@@ -815,16 +698,11 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
                 for (int r = 0; r < nrows; ++r) {
                     if (!rr[r].active) continue;
                     const int m = box_m(rr[r].key, d);
-#if COLLECT_ROW_STORE == 4
-                    row_store1(&a.reset_raw[(r0 + r) * D + d], (float)m * 0x1p-23f);
-#else
                     a.reset_raw[(r0 + r) * D + d] = (float)m * 0x1p-23f;
-#endif
                     cs2 += m;
                     cq2 += (long long)m * m;
                 }
         }
-#if !COLLECT_NO_TOTALS
         if (defer) {
             if (t < D) {
                 atomic_add_i64(tc + t, cs1);
@@ -839,13 +717,9 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
                 atomic_add_i64(tc + 4 * D + 1, nrows);
             }
         }
-#endif
     };
     if (!CPL) env_phase();
     TSTAMP(2)
-#if COLLECT_STOP == 1
-    return;
-#endif
 
     // ---- B. actor: layer 1 (wave w: k in [w KW, (w+1) KW), all 64 features) -----------------
     {
@@ -950,9 +824,6 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         env_phase();
     }
 
-#if COLLECT_STOP == 2
-    return;
-#endif
     TSTAMP(3)
 }
 

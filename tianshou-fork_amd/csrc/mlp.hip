@@ -4,15 +4,15 @@
 // critic = Linear(D,64)-Tanh-Linear(64,64)-Tanh-Linear(64,1)      (Critic)
 // with the state-independent log-std of fixed_std_normal.
 //
-// Three kernels per minibatch, all on v_mfma_f32_32x32x2_f32 (exact f32 fma chains, the
-// f32 matrix rate of gfx950):
-//   l1_fwd_kernel : H1^T = tanh(W1cat . X[idx]^T + b1) for both nets at once (W1cat = the
+// Kernels of a minibatch (the production path runs the bf16x6 forms: exact three-way bf16
+// splits of every f32 operand, x6.h; l1_fwd_kernel is the f32-input MFMA reference form):
+//   l1_fwd_kernel / l1_ring_kernel (mlp_x6.hip): H1^T = tanh(W1cat . X[idx]^T + b1) for both nets at once (W1cat = the
 //                   two first-layer weights stacked, 128 features).  Minibatch rows are read
 //                   through the permutation index (no gathered copy of the observations).
 //   ppo_tail_kernel: layers 2-3 of both nets, the clipped-surrogate/value loss and its
 //                   backward down to dZ1, plus the weight gradients of layers 2-3, per wave
 //                   of 32 minibatch rows, without leaving registers/LDS.
-//   dw_kernel     : dW1cat = dZ1^T . X[idx] (+ db1 through a ones column), split over the
+//   dw_x6_kernel  : dW1cat = dZ1^T . X[idx] (+ db1 through a ones column), split over the
 //                   minibatch rows; dw_reduce_kernel folds the split partials.
 //
 // Orientation: every activation lives "feature-major" in the MFMA C layout, minibatch rows
@@ -179,46 +179,26 @@ struct TailParams {
     double inv_b64;
 };
 
-#ifndef TAIL_VARIANT
-#define TAIL_VARIANT 0  // diagnostic builds only: 1 = no layer-2/3 weight-gradient MFMAs
-#endif
 // per-workgroup slab of weight-gradient partial sums (floats) and loss partial sums (doubles)
 constexpr int SL_W2A = 0, SL_B2A = SL_W2A + H * H, SL_W2C = SL_B2A + H, SL_B2C = SL_W2C + H * H,
               SL_W3A = SL_B2C + H, SL_B3A = SL_W3A + AMAX * H, SL_W3C = SL_B3A + AMAX,
               SL_B3C = SL_W3C + H, SL_F = SL_B3C + 4;
 constexpr int SL_D = 4 + AMAX;  // clip, vf, count, 0, d/dlog_std[AMAX]
-// Waves per workgroup (one workgroup per CU).  Measured round 3 (tools/mlp_kernel_bench.py
+// Four waves per workgroup, one workgroup per CU.  Measured round 3 (tools/mlp_kernel_bench.py
 // --only tail, both nets + reduce, 262144 rows; per-phase s_memtime stamps with TAIL_TRACE):
 // round 2's kernel 234 us (actor tile 29.7k cycles: head + loss 9.5k of them, 89
-// ds_bpermute per tile); bf16x6 weight gradients 226; + deferred column sums and H1 kept
-// live 210-213 (actor tile 24.4k: head + loss 7.7k, ~1.5k instructions issued one after the
-// other by the only wave of the SIMD).  Two waves per SIMD do not pay: 8 waves each with its
-// own accumulators spill (256 VGPRs) 220-222 us; a lockstep form in which the 8 waves of a
-// round share the weight-gradient MFMAs through LDS (2 accumulator tiles per wave, 8
-// workgroup barriers per round) still spills 20 VGPRs and ran 226-229 us.
-#ifndef TAIL_WAVES
-#define TAIL_WAVES 4
-#endif
-// Column sums over the minibatch rows (db2, db3, dlog_std, the critic's dW3) accumulated per
-// lane across the wave's tiles and reduced across lanes once at the end (1: default), instead
-// of a 16-shuffle reduce-scatter per tile and sum (ds_bpermute chains: 89 per tile in the
-// actor, where they were most of the 9.5k-cycle head + loss phase).
-#ifndef TAIL_DEFER
-#define TAIL_DEFER (TAIL_WAVES == 4)
-#endif
-// keep H1 in registers through the tile (1) or re-read it from L2 for dZ1 (0: fewer VGPRs)
-#ifndef TAIL_KEEP_H1
-#define TAIL_KEEP_H1 (TAIL_WAVES == 4)
-#endif
-// next tile's inputs prefetched into registers during the current tile (needed at one wave
-// per SIMD; at two the partner wave covers the loads and the registers are better spent)
-#ifndef TAIL_PF
-#define TAIL_PF (TAIL_WAVES == 4)
-#endif
-// layer-2/3 weight gradients as bf16x6 products (f32 MFMA, 1/16 of the bf16 rate, before)
-#ifndef TAIL_WG_X6
-#define TAIL_WG_X6 1
-#endif
+// ds_bpermute per tile); bf16x6 weight gradients (f32 MFMA at 1/16 of the bf16 rate before)
+// 226; + deferred column sums and H1 kept live 210-213 (actor tile 24.4k: head + loss 7.7k,
+// ~1.5k instructions issued one after the other by the only wave of the SIMD).  Two waves
+// per SIMD did not pay in that form: 8 waves each with its own accumulators spill (256 VGPRs)
+// 220-222 us; a lockstep form in which the 8 waves of a round share the weight-gradient MFMAs
+// through LDS (2 accumulator tiles per wave, 8 workgroup barriers per round) still spills 20
+// VGPRs and ran 226-229 us.  What the kernel keeps from those measurements: the column sums
+// over the minibatch rows (db2, db3, dlog_std, the critic's dW3) accumulate per lane across
+// the wave's tiles and are reduced across lanes once at the end (a 16-shuffle reduce-scatter
+// per tile and sum before: 89 ds_bpermute chains per actor tile); H1 stays in registers
+// through the tile; the next tile's inputs are prefetched into registers during the current
+// one (one wave per SIMD: nothing else hides the loads).
 // diagnostic builds only (tools/mlp_kernel_bench.py --tail-trace): s_memtime stamps per wave
 // and tile at the phase boundaries, stored behind the workspace slabs
 #ifndef TAIL_TRACE
@@ -226,7 +206,7 @@ constexpr int SL_D = 4 + AMAX;  // clip, vf, count, 0, d/dlog_std[AMAX]
 #endif
 constexpr int TAIL_NSTAMP = 8;
 constexpr int TAIL_TRACE_TILES = 8;  // first tiles of each wave
-constexpr int TAIL_NW = TAIL_WAVES;
+constexpr int TAIL_NW = 4;
 constexpr int TAIL_TPB = 64 * TAIL_NW;
 
 struct TailWeights {
@@ -269,7 +249,7 @@ __device__ __forceinline__ int rs_reg(int l) {
 // half-tile transpose scratch: [64 features][16 rows]; stride 20 floats (80 B) keeps the
 // 8-row float4 reads of the bf16x6 weight gradients 16-byte aligned and spreads the 16 lanes
 // of a read phase over all 16 bank groups (5 is odd)
-constexpr int SH = TAIL_WG_X6 ? 20 : 18;
+constexpr int SH = 20;
 constexpr int T_B2 = 0, T_B3 = T_B2 + H, T_W3C = T_B3 + AMAX, T_VAR = T_W3C + H,
               T_LS = T_VAR + AMAX, T_IV = T_LS + AMAX, T_IV2 = T_IV + AMAX,
               T_SCR = T_IV2 + AMAX, T_END = T_SCR + TAIL_NW * 2 * H * SH;
@@ -338,33 +318,10 @@ __device__ __forceinline__ void split_frag(const float (&v)[16], int s, bf16x8 (
     }
 }
 
-// Accumulate D += A^T-in-LDS . B^T-in-LDS over 16 minibatch rows: the two operands were
-// written feature-major ([feature][row], stride SH) from the C layout; tiles ot x ft.
-template <int NOT, int NFT>
-__device__ __forceinline__ void acc_wgrad(f32x16 (&g)[NOT][NFT], const float* S1, const float* S2,
-                                          int c, int h) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        float2 a2[NOT], b2[NFT];
-#pragma unroll
-        for (int i = 0; i < NOT; ++i)
-            a2[i] = *reinterpret_cast<const float2*>(&S1[(32 * i + c) * SH + 4 * s + 2 * h]);
-#pragma unroll
-        for (int i = 0; i < NFT; ++i)
-            b2[i] = *reinterpret_cast<const float2*>(&S2[(32 * i + c) * SH + 4 * s + 2 * h]);
-#pragma unroll
-        for (int ot = 0; ot < NOT; ++ot)
-#pragma unroll
-            for (int ft = 0; ft < NFT; ++ft) {
-                g[ot][ft] = mfma(a2[ot].x, b2[ft].x, g[ot][ft]);
-                g[ot][ft] = mfma(a2[ot].y, b2[ft].y, g[ot][ft]);
-            }
-    }
-}
-
-// bf16x6 form of acc_wgrad: one 16-deep k-step of v_mfma_f32_32x32x16_bf16 covers the 16
+// Accumulate D += A^T-in-LDS . B^T-in-LDS over 16 minibatch rows, bf16x6: one 16-deep k-step of v_mfma_f32_32x32x16_bf16 covers the 16
 // rows; lane (c, h) reads rows 8h..8h+7 of feature c of each tile (two float4 reads) and
-// splits them into the three planes in registers.  The C layout of g is acc_wgrad's.
+// splits them into the three planes in registers.  Both operands were written feature-major
+// ([feature][row], stride SH) from the C layout; tiles ot x ft.
 template <int NOT, int NFT>
 __device__ __forceinline__ void acc_wgrad_x6(f32x16 (&g)[NOT][NFT], const float* S1,
                                              const float* S2, int c, int h) {
@@ -391,16 +348,6 @@ __device__ __forceinline__ void acc_wgrad_x6(f32x16 (&g)[NOT][NFT], const float*
 #pragma unroll
         for (int ft = 0; ft < NFT; ++ft) g[ot][ft] = mfma6(a, b[ft], g[ot][ft]);
     }
-}
-
-template <int NOT, int NFT>
-__device__ __forceinline__ void acc_wgrad_any(f32x16 (&g)[NOT][NFT], const float* S1,
-                                              const float* S2, int c, int h) {
-#if TAIL_WG_X6
-    acc_wgrad_x6<NOT, NFT>(g, S1, S2, c, h);
-#else
-    acc_wgrad<NOT, NFT>(g, S1, S2, c, h);
-#endif
 }
 
 // Write a C-layout activation (NT32 tiles of 32 features) rows [16*half, 16*half+16) into
@@ -506,7 +453,6 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
     float gb2[2] = {0.f, 0.f}, gw3c[2] = {0.f, 0.f};
     float gb3 = 0.f;
     double dls_acc = 0.0, loss_acc = 0.0, cnt_acc = 0.0;
-#if TAIL_DEFER
     // per-lane partial column sums (lane = row c, register r = feature rho(r) + 4h)
     float gb2_l[2][16], gw3c_l[2][16], gb3_l[16], dls_l[16], gv_l = 0.f;
 #pragma unroll
@@ -514,7 +460,6 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
         gb2_l[0][r] = gb2_l[1][r] = gw3c_l[0][r] = gw3c_l[1][r] = 0.f;
         gb3_l[r] = dls_l[r] = 0.f;
     }
-#endif
 
     const int64_t ntiles = (n + 31) / 32;
     const int64_t gw = (int64_t)blockIdx.x * TAIL_NW + w, nw = (int64_t)gridDim.x * TAIL_NW;
@@ -561,21 +506,13 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
             nx1 = p.value_clip ? v_s[j32_] : 0.0f;                                          \
         }                                                                                   \
     }
-#if TAIL_PF
     int64_t j_next = row_index(gw);
     TAIL_PREFETCH(gw, j_next)
     j_next = row_index(gw + nw);
-#endif
     for (int64_t bt = gw; bt < ntiles; bt += nw) {
         const int64_t brow = bt * 32 + c;
         const bool live = brow < n;
         TAIL_STAMP(0)
-#if !TAIL_PF
-        {
-            const int64_t jc = row_index(bt);
-            TAIL_PREFETCH(bt, jc)
-        }
-#endif
         // ---- this tile's inputs (prefetched), then the next tile's loads --------------------
         float h1[2][16], av[16];
 #pragma unroll
@@ -585,13 +522,11 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
 #pragma unroll
         for (int r = 0; r < 16; ++r) av[r] = nav[r];
         const float x0 = nx0, x1 = nx1;
-#if TAIL_PF
         {
             const int64_t jn = j_next;
             TAIL_PREFETCH(bt + nw, jn)
             j_next = row_index(bt + 2 * nw);
         }
-#endif
         // ---- layer 2 -----------------------------------------------------------------------
         TAIL_STAMP(1)
         float h2[2][16];
@@ -690,16 +625,11 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
                 dmu[0][r] = g_logp * diff[r] * iv;
                 dls[r] = (a < A && live) ? g_logp * (diff[r] * diff[r] * iv - 1.0f) : 0.0f;
             }
-#if TAIL_DEFER
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 dls_l[r] += dls[r];
                 gb3_l[r] += dmu[0][r];
             }
-#else
-            dls_acc += (double)rs_sum16(dls, l);
-            gb3 += rs_sum16(dmu[0], l);
-#endif
             __builtin_amdgcn_sched_barrier(0);
             // dW3a = dMu^T . H2a over the 32 rows, two half passes
             TAIL_STAMP(3)
@@ -710,9 +640,7 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
                 put_half<1>(S1, dmu, c, h, half);
                 put_half<2>(S2, h2, c, h, half);
                 wave_sync_lds();
-#if TAIL_VARIANT != 1
-                acc_wgrad_any<1, 2>(gW3, S1, S2, c, h);
-#endif
+                acc_wgrad_x6<1, 2>(gW3, S1, S2, c, h);
             }
             // dZ2 = (W3a^T dMu) * (1 - H2^2)
             TAIL_STAMP(4)
@@ -774,25 +702,11 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
                 if (h == 0) loss_acc += (double)vf;
             }
             {
-#if TAIL_DEFER
 #pragma unroll
                 for (int it = 0; it < 2; ++it)
 #pragma unroll
                     for (int r = 0; r < 16; ++r) gw3c_l[it][r] += gv * h2[it][r];
                 gv_l += h == 0 ? gv : 0.0f;
-#else
-                float gvh[16];
-#pragma unroll
-                for (int it = 0; it < 2; ++it) {
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) gvh[r] = gv * h2[it][r];
-                    gw3c[it] += rs_sum16(gvh, l);
-                }
-                float gsum = h == 0 ? gv : 0.0f;
-#pragma unroll
-                for (int off = 32; off > 0; off >>= 1) gsum += __shfl_xor(gsum, off, 64);
-                gb3 += gsum;
-#endif
             }
 #pragma unroll
             for (int ft = 0; ft < 2; ++ft)
@@ -803,27 +717,6 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
         }
         // ---- dZ1 = (W2^T dZ2) * (1 - H1^2) -> HBM (row-major [n][128]) -------------------
         TAIL_STAMP(5)
-#if !TAIL_KEEP_H1
-        {
-            // re-read this tile's H1 (L2-hot) instead of keeping it live through the loss and
-            // head phases: an opaque zero offset stops the compiler from reusing the first load
-            int zoff;
-            asm volatile("s_mov_b32 %0, 0" : "=s"(zoff));
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const float4* src = reinterpret_cast<const float4*>(
-                    h1f + ((bt * NT + 2 * net + i) * 64 + l) * 16 + zoff);
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const float4 v = src[q];
-                    h1[i][4 * q] = v.x;
-                    h1[i][4 * q + 1] = v.y;
-                    h1[i][4 * q + 2] = v.z;
-                    h1[i][4 * q + 3] = v.w;
-                }
-            }
-        }
-#endif
         f32x16 dd0 = zero16(), dd1 = zero16();
 #pragma unroll
         for (int kc = 0; kc < 2; ++kc)
@@ -855,12 +748,8 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
         TAIL_STAMP(6)
 #pragma unroll
         for (int ot = 0; ot < 2; ++ot) {
-#if TAIL_DEFER
 #pragma unroll
             for (int r = 0; r < 16; ++r) gb2_l[ot][r] += dz2[ot][r];
-#else
-            gb2[ot] += rs_sum16(dz2[ot], l);
-#endif
         }
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
@@ -869,9 +758,7 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
             put_half<2>(S1, dz2, c, h, half);
             put_half<2>(S2, h1, c, h, half);
             wave_sync_lds();
-#if TAIL_VARIANT != 1
-            acc_wgrad_any<2, 2>(gW2, S1, S2, c, h);
-#endif
+            acc_wgrad_x6<2, 2>(gW2, S1, S2, c, h);
         }
         TAIL_STAMP(7)
 #if TAIL_TRACE
@@ -879,7 +766,6 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
 #endif
     }
 #undef TAIL_PREFETCH
-#if TAIL_DEFER
     // the deferred column sums: one reduce-scatter each (rs_sum16's lane ownership)
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
@@ -895,7 +781,6 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
         for (int off = 32; off > 0; off >>= 1) gsum += __shfl_xor(gsum, off, 64);
         gb3 = gsum;
     }
-#endif
     // ---- fold the TAIL_NW waves (fixed order) into this workgroup's slab ---------------------
     __syncthreads();
     float* red = sm;  // T_END >= TAIL_NW * 32 * 64 floats
@@ -1187,107 +1072,8 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(const float* __restric
 constexpr int DW_COLS = 128;
 constexpr int DW_KB = 32;
 
-__global__ __launch_bounds__(256, 2) void dw_kernel(
-    const float* __restrict__ dz, const float* __restrict__ X, int64_t ldx,
-    const int64_t* __restrict__ idx, int64_t n, int D, int64_t rows_per_split,
-    int ncolpad, float* __restrict__ part) {
-    // Zs holds dZ1 rows with feature f = 32i + c at [c][i], so a lane's four A fragments
-    // (one per feature tile) are one 16-byte LDS read.
-    __shared__ __attribute__((aligned(16))) float Zs[2][DW_KB][HC];
-    __shared__ __attribute__((aligned(16))) float Xs[2][DW_KB][DW_COLS];
-    const int t = threadIdx.x;
-    const int w = t >> 6, l = t & 63, h = l >> 5, c = l & 31;
-    const int col0 = blockIdx.x * DW_COLS;
-    const int64_t r0 = (int64_t)blockIdx.y * rows_per_split;
-    const int64_t r1 = min(n, r0 + rows_per_split);
-    // staging: thread t moves float4 (t & 31) of rows (t >> 5) + 8q, q = 0..3.  The gather
-    // index of chunk ch+1 is loaded one chunk ahead (no dependent-load stall per chunk).
-    const int sc = 4 * (t & 31);
-    const int k = col0 + sc;
-    // the float4 at column k starts inside the row; its columns >= D are the caller's zero
-    // padding (ldx >= roundup(D, 4)) and are masked per element below
-    const bool kin = k < D;
-    float4 zr[4], xr[4];
-    int64_t rid[4];       // gather rows of the NEXT chunk to load (raw index values)
-    bool live_ld[4];      // row liveness of the chunk whose loads are in flight
-    auto load_idx = [&](int64_t rb) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int64_t r = min(rb + (t >> 5) + 8 * q, r1 - 1);
-            rid[q] = idx ? idx[r] : r;
-        }
-    };
-    // loads go straight to registers; masks are applied in store() after the MFMA phase
-    auto load = [&](int64_t rb) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int64_t r = rb + (t >> 5) + 8 * q;
-            live_ld[q] = r < r1;
-            const int64_t rr = min(r, r1 - 1);
-            zr[q] = *reinterpret_cast<const float4*>(dz + rr * HC + sc);
-            xr[q] = *reinterpret_cast<const float4*>(X + rid[q] * ldx + (kin ? k : 0));
-        }
-    };
-    auto store = [&](int buf) {
-        const int i = sc >> 5, c0 = sc & 31;
-        // ones column (db) at k == D; data columns k + e < D
-        const float o0 = k == D ? 1.f : 0.f, o1 = k + 1 == D ? 1.f : 0.f,
-                    o2 = k + 2 == D ? 1.f : 0.f, o3 = k + 3 == D ? 1.f : 0.f;
-        const bool d0 = k < D, d1 = k + 1 < D, d2 = k + 2 < D, d3 = k + 3 < D;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const bool lv = live_ld[q];
-            float* zd = &Zs[buf][(t >> 5) + 8 * q][0];
-            zd[(c0 + 0) * 4 + i] = lv ? zr[q].x : 0.f;
-            zd[(c0 + 1) * 4 + i] = lv ? zr[q].y : 0.f;
-            zd[(c0 + 2) * 4 + i] = lv ? zr[q].z : 0.f;
-            zd[(c0 + 3) * 4 + i] = lv ? zr[q].w : 0.f;
-            *reinterpret_cast<float4*>(&Xs[buf][(t >> 5) + 8 * q][sc]) =
-                make_float4(lv ? (d0 ? xr[q].x : o0) : 0.f, lv ? (d1 ? xr[q].y : o1) : 0.f,
-                            lv ? (d2 ? xr[q].z : o2) : 0.f, lv ? (d3 ? xr[q].w : o3) : 0.f);
-        }
-    };
-    f32x16 acc[NT];
-#pragma unroll
-    for (int i = 0; i < NT; ++i) acc[i] = zero16();
-    const int64_t nchunk = r1 > r0 ? (r1 - r0 + DW_KB - 1) / DW_KB : 0;
-    if (nchunk > 0) {
-        load_idx(r0);
-        load(r0);
-        store(0);
-        if (nchunk > 1) load_idx(r0 + DW_KB);
-    }
-    __syncthreads();
-    for (int64_t ch = 0; ch < nchunk; ++ch) {
-        const int buf = ch & 1;
-        if (ch + 1 < nchunk) {
-            load(r0 + (ch + 1) * DW_KB);
-            if (ch + 2 < nchunk) load_idx(r0 + (ch + 2) * DW_KB);
-        }
-#pragma unroll
-        for (int s = 0; s < DW_KB / 2; ++s) {
-            const float4 a4 = *reinterpret_cast<const float4*>(&Zs[buf][2 * s + h][4 * c]);
-            const float b = Xs[buf][2 * s + h][32 * w + c];
-            acc[0] = mfma(a4.x, b, acc[0]);
-            acc[1] = mfma(a4.y, b, acc[1]);
-            acc[2] = mfma(a4.z, b, acc[2]);
-            acc[3] = mfma(a4.w, b, acc[3]);
-        }
-        if (ch + 1 < nchunk) store(buf ^ 1);
-        __syncthreads();
-    }
-    // partial [split][f][colpad]
-    float* o = part + (int64_t)blockIdx.y * HC * ncolpad;
-#pragma unroll
-    for (int i = 0; i < NT; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-            o[(int64_t)(32 * i + rho(r) + 4 * h) * ncolpad + col0 + 32 * w + c] = acc[i][r];
-}
-
-// bf16x6 form of dw_kernel (x6.h): the same workgroup tiling and partial layout, rows staged
-// 32 at a time, but every staged element is split once, by the thread that loads it, into
-// three bf16 planes stored transposed ([feature or column][32 rows], x6::sw_off rows), so a
+// bf16x6 (x6.h): every staged element is split once, by the thread that loads it, into three
+// bf16 planes stored transposed ([feature or column][32 rows], x6::sw_off rows), so a
 // lane's MFMA fragment (8 consecutive minibatch rows of one feature / column) is one
 // ds_read_b128 per plane and the inner loop is 15 LDS reads + 24 bf16 MFMAs per 16 rows.
 // Staging: thread t owns feature / column (t & 127) and the 8-row groups {rg, rg + 2} of the
@@ -1300,11 +1086,13 @@ __global__ __launch_bounds__(256, 2) void dw_kernel(
 // CU covering all 384 columns, so each dZ1 element is loaded and split once instead of three
 // times -- 4 waves with 12 accumulator tiles each 311-317 us vs 264-267 for this kernel; 8
 // waves with 6 tiles each, MFMAs issued ahead of the next chunk's split 258-261 vs 246.
+// Round 5 (tools/r05_ab.sh, profiles/r05_variant_ab.log): chunks fully inside the row range
+// take their row indices eight at a time in one scalar load with 32-bit row offsets and are
+// staged without row masks (static count of the per-chunk loop 700 -> 460 instructions, SALU
+// 180 -> 42): dW1 + reduce 246.9 / 255.5 -> 237.0 / 235.8 us, minibatch 719 / 731 -> 695 /
+// 680 us, two A/B rounds in one call -- now the only form.
 #ifndef DWX6_OCC
 #define DWX6_OCC 2
-#endif
-#ifndef DWX6_FULL
-#define DWX6_FULL 0
 #endif
 __global__ __launch_bounds__(256, DWX6_OCC) void dw_x6_kernel(
     const float* __restrict__ dz, const float* __restrict__ X, int64_t ldx,
@@ -1399,7 +1187,7 @@ __global__ __launch_bounds__(256, DWX6_OCC) void dw_x6_kernel(
     for (int64_t ch = 0; ch < nchunk; ++ch) {
         if (ch + 1 < nchunk) {
             const int64_t rb = r0 + (ch + 1) * DW_KB;
-            if (DWX6_FULL && idx && rb + DW_KB <= r1)
+            if (idx && rb + DW_KB <= r1)
                 DWX6_LOAD_FULL(rb)
             else
                 DWX6_LOAD(rb)
@@ -1423,7 +1211,7 @@ __global__ __launch_bounds__(256, DWX6_OCC) void dw_x6_kernel(
         if (ch + 1 < nchunk) {
             __syncthreads();
             const int64_t rb = r0 + (ch + 1) * DW_KB;
-            if (DWX6_FULL && rb + DW_KB <= r1)
+            if (rb + DW_KB <= r1)
                 DWX6_STORE(rb, true)  // no row masks in a whole chunk
             else
                 DWX6_STORE(rb, false)
@@ -1630,15 +1418,8 @@ extern "C" int tsrl_mlp_dw(const float* dz1, const float* X, int64_t ldx, const 
     const int nsplit = dw_nsplit(n);
     const int64_t rps = ((n + nsplit - 1) / nsplit + DW_KB - 1) / DW_KB * DW_KB;
     float* part = reinterpret_cast<float*>(workspace);
-#ifndef DW_X6
-#define DW_X6 1
-#endif
-    if (DW_X6)
-        hipLaunchKernelGGL(dw_x6_kernel, dim3(ncolt * nsplit), dim3(256), 0, as_stream(stream),
-                           dz1, X, ldx, idx, n, (int)D, rps, ncolpad, ncolt, part);
-    else
-        hipLaunchKernelGGL(dw_kernel, dim3(ncolt, nsplit), dim3(256), 0, as_stream(stream), dz1,
-                           X, ldx, idx, n, (int)D, rps, ncolpad, part);
+    hipLaunchKernelGGL(dw_x6_kernel, dim3(ncolt * nsplit), dim3(256), 0, as_stream(stream),
+                       dz1, X, ldx, idx, n, (int)D, rps, ncolpad, ncolt, part);
     TSRL_LAUNCH_CHECK("tsrl_mlp_dw");
     const int64_t outs = (int64_t)HC * ncolpad;
     hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((outs + 63) / 64)), dim3(256), 0,

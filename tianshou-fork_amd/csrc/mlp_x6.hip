@@ -116,12 +116,6 @@ __global__ void split_w_kernel(const float* __restrict__ Wa, const float* __rest
 // in registers one chunk ahead and stored into the single-buffered LDS tiles after the
 // chunk's MFMAs.  X6_IL interleaves the six products of two feature tiles; X6_OCC is the
 // workgroups-per-CU bound (variants measured equal within 2 %, 2/1 kept).
-#ifndef X6_IL
-#define X6_IL 1
-#endif
-#ifndef X6_COAL
-#define X6_COAL 1
-#endif
 #ifndef X6_OCC
 #define X6_OCC 2
 #endif
@@ -137,7 +131,6 @@ __global__ __launch_bounds__(256, X6_OCC) void l1_fwd_x6_kernel(
     const int64_t row0 = (int64_t)blockIdx.x * XR;
     if (t < HC) sb[t] = t < H ? ba[t] : bc[t - H];
     const int srow = t >> 1, sq = 2 * (t & 1);
-#if X6_COAL
     // X staging: thread t loads float4 (t & 7) of rows (t >> 3) + 32 i, i = 0..3: each load
     // instruction reads 8 whole 128-byte row segments (8 consecutive lanes per row)
     const int xq = t & 7, xr0 = t >> 3;
@@ -149,11 +142,6 @@ __global__ __launch_bounds__(256, X6_OCC) void l1_fwd_x6_kernel(
         xl_[i] = g_ < n;
         xs_[i] = X + (xl_[i] ? (idx ? idx[g_] : g_) : 0) * ldx;
     }
-#else
-    const int64_t gr = row0 + srow;
-    const bool live = gr < n;
-    const float* xsrc = X + (live ? (idx ? idx[gr] : gr) : 0) * ldx;
-#endif
     const int64_t plane = (int64_t)HC * Kp;
     const __bf16* wsrc = wsp + (int64_t)srow * Kp + 8 * sq;
     const int nch = Kp / KC;
@@ -163,7 +151,6 @@ __global__ __launch_bounds__(256, X6_OCC) void l1_fwd_x6_kernel(
     // staging values are named scalars (no arrays or lambdas that end up in scratch).
     float4 x0, x1, x2, x3;
     uint4 w00, w01, w10, w11, w20, w21;
-#if X6_COAL
 #define X6_XLOAD(kc)                                                                        \
     {                                                                                       \
         const int k_ = (kc) * KC + 4 * xq;                                                  \
@@ -180,26 +167,6 @@ __global__ __launch_bounds__(256, X6_OCC) void l1_fwd_x6_kernel(
         *reinterpret_cast<float4*>(&Xs[swf_off(xr0 + 64, xq)]) = keep4(xl_[2] && k_ < D, x2);\
         *reinterpret_cast<float4*>(&Xs[swf_off(xr0 + 96, xq)]) = keep4(xl_[3] && k_ < D, x3);\
     }
-#else
-#define X6_XLOAD(kc)                                                                        \
-    {                                                                                       \
-        const int k_ = (kc) * KC + 8 * sq;                                                  \
-        const bool i0_ = live && k_ < D, i1_ = live && k_ + 4 < D;                          \
-        const bool i2_ = live && k_ + 8 < D, i3_ = live && k_ + 12 < D;                     \
-        x0 = *reinterpret_cast<const float4*>(xsrc + (i0_ ? k_ : 0));                       \
-        x1 = *reinterpret_cast<const float4*>(xsrc + (i1_ ? k_ + 4 : 0));                   \
-        x2 = *reinterpret_cast<const float4*>(xsrc + (i2_ ? k_ + 8 : 0));                   \
-        x3 = *reinterpret_cast<const float4*>(xsrc + (i3_ ? k_ + 12 : 0));                  \
-    }
-#define X6_XSTORE(kc)                                                                       \
-    {                                                                                       \
-        const int k_ = (kc) * KC + 8 * sq;                                                  \
-        *reinterpret_cast<float4*>(&Xs[xo0]) = keep4(live && k_ < D, x0);                   \
-        *reinterpret_cast<float4*>(&Xs[xo1]) = keep4(live && k_ + 4 < D, x1);               \
-        *reinterpret_cast<float4*>(&Xs[xo2]) = keep4(live && k_ + 8 < D, x2);               \
-        *reinterpret_cast<float4*>(&Xs[xo3]) = keep4(live && k_ + 12 < D, x3);              \
-    }
-#endif
 #define X6_LOAD(kc)                                                                         \
     {                                                                                       \
         X6_XLOAD(kc)                                                                        \
@@ -215,10 +182,6 @@ __global__ __launch_bounds__(256, X6_OCC) void l1_fwd_x6_kernel(
     }
     const int off0 = sw_off(srow, sq), off1 = sw_off(srow, sq + 1);
     // f32 X rows, 16-B chunk qc = 4 * (t & 1) + i of row srow
-#if !X6_COAL
-    const int xo0 = swf_off(srow, 2 * sq), xo1 = swf_off(srow, 2 * sq + 1);
-    const int xo2 = swf_off(srow, 2 * sq + 2), xo3 = swf_off(srow, 2 * sq + 3);
-#endif
 // The out-of-range float4s are zeroed here, at the LDS store, not right after their loads:
 // a select next to the load makes the wave wait for the data before the chunk's MFMAs (the
 // whole fetch latency exposed once per chunk).
@@ -255,7 +218,6 @@ __global__ __launch_bounds__(256, X6_OCC) void l1_fwd_x6_kernel(
                 split4(u, b[0], b[1], b[2], 0);
                 split4(v, b[0], b[1], b[2], 4);
             }
-#if X6_IL
             // two feature tiles at a time, their six products interleaved (two independent
             // accumulation chains in flight)
 #pragma unroll
@@ -279,17 +241,6 @@ __global__ __launch_bounds__(256, X6_OCC) void l1_fwd_x6_kernel(
                 X6_PAIR(2, 0)
 #undef X6_PAIR
             }
-#else
-#pragma unroll
-            for (int i = 0; i < NT; ++i) {
-                bf16x8 a[NPL];
-                const int aoff = sw_off(32 * i + c, 2 * s + h);
-#pragma unroll
-                for (int p = 0; p < NPL; ++p)
-                    a[p] = *reinterpret_cast<const bf16x8*>(&Ws[p][aoff]);
-                acc[i] = mfma6(a, b, acc[i]);
-            }
-#endif
         }
         if (kc + 1 < nch) {
             __syncthreads();
@@ -345,12 +296,6 @@ __global__ __launch_bounds__(256, X6_OCC) void l1_fwd_x6_kernel(
 // too, so the compiler inserts no drain of its own); the per-tile epilogue stores count in
 // vmcnt and are skipped by the count of the wait that follows them.
 // ---------------------------------------------------------------------------------------
-#ifndef RING_PREFETCH
-#define RING_PREFETCH 0  // 1: all of a chunk's LDS operands read ahead of its MFMAs
-#endif
-#ifndef RING_VARIANT
-#define RING_VARIANT 0  // diagnostic builds only: 1 = no LDS-DMA in the loop, 2 = no MFMAs
-#endif
 constexpr int RNW = 8;                   // waves per workgroup
 constexpr int RROWS = 32 * RNW;          // rows per tile
 constexpr int RTPW = 4;                  // tiles per workgroup (at most)
@@ -475,9 +420,6 @@ __global__ __launch_bounds__(RNW * 64, 1) void l1_ring_kernel(
         issue_x();
         if (C > 1) issue_x();
     }
-#if RING_VARIANT == 3
-    if (w >= 4) __builtin_amdgcn_s_setprio(1);  // static priority for the second-dispatched half
-#endif
     bool epi_prev = false;
     int cs_x = 0, cs_w = 0;  // ring slots of the chunk being computed
     for (int cc = 0, tl = 0, kc = 0; cc < C; ++cc) {
@@ -492,73 +434,12 @@ __global__ __launch_bounds__(RNW * 64, 1) void l1_ring_kernel(
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         __builtin_amdgcn_s_barrier();
-#if RING_VARIANT != 1
         if (nx) issue_w();
         if (cc + 2 < C) issue_x();
-#endif
         const char* Xs = sm + cs_x * RXSTAGE;
         const char* Ws = sm + RWOFF + cs_w * RWSTAGE;
         cs_x = cs_x == RXS - 1 ? 0 : cs_x + 1;
         cs_w ^= 1;
-#if RING_PREFETCH
-        // every LDS operand of the chunk (both k-steps: 2 x 2 f32 X pieces, 2 x 4 x 3 weight
-        // fragments) read up front, then the two k-steps' splits and MFMAs: the reads' latency
-        // is exposed once per chunk instead of before every MFMA group
-        {
-            typedef float f32x4v __attribute__((ext_vector_type(4)));
-            f32x4v xu[2], xv[2];
-            bf16x8 af[2][NT][NPL];
-            const int xr = 32 * w + c;
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                xu[s] = *reinterpret_cast<const f32x4v*>(&Xs[swf_off(xr, 4 * s + 2 * h)]);
-                xv[s] = *reinterpret_cast<const f32x4v*>(&Xs[swf_off(xr, 4 * s + 2 * h + 1)]);
-#pragma unroll
-                for (int i = 0; i < NT; ++i) {
-                    const int ao = sw_off(32 * i + c, 2 * s + h);
-#pragma unroll
-                    for (int p = 0; p < NPL; ++p)
-                        af[s][i][p] = *reinterpret_cast<const bf16x8*>(&Ws[p * HC * ROWB + ao]);
-                }
-            }
-            // pin the reads here (the IR passes otherwise sink each next to its MFMA, with a
-            // wait before every group): one wait per chunk
-            auto pin = [&](int s) {
-                asm volatile("" : "+v"(xu[s]), "+v"(xv[s]));
-#pragma unroll
-                for (int i = 0; i < NT; ++i)
-#pragma unroll
-                    for (int p = 0; p < NPL; ++p) asm volatile("" : "+v"(af[s][i][p]));
-            };
-#if RING_PREFETCH == 1
-            pin(0);
-            pin(1);
-#endif
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-#if RING_PREFETCH == 2
-                pin(s);  // k-step 1's reads still in flight during k-step 0's MFMAs
-#endif
-                bf16x8 b[NPL];
-                split4(make_float4(xu[s].x, xu[s].y, xu[s].z, xu[s].w), b[0], b[1], b[2], 0);
-                split4(make_float4(xv[s].x, xv[s].y, xv[s].z, xv[s].w), b[0], b[1], b[2], 4);
-#pragma unroll
-                for (int ip = 0; ip < NT; ip += 2) {
-#define RX6_PAIR(pa, pb)                                                                    \
-    acc[ip] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s][ip][pa], b[pb], acc[ip], 0, 0, 0); \
-    acc[ip + 1] =                                                                           \
-        __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s][ip + 1][pa], b[pb], acc[ip + 1], 0, 0, 0);
-                    RX6_PAIR(0, 0)
-                    RX6_PAIR(0, 1)
-                    RX6_PAIR(1, 0)
-                    RX6_PAIR(0, 2)
-                    RX6_PAIR(1, 1)
-                    RX6_PAIR(2, 0)
-#undef RX6_PAIR
-                }
-            }
-        }
-#else
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             bf16x8 b[NPL];
@@ -580,14 +461,9 @@ __global__ __launch_bounds__(RNW * 64, 1) void l1_ring_kernel(
                     a0[p] = *reinterpret_cast<const bf16x8*>(&Ws[p * HC * ROWB + ao0]);
                     a1[p] = *reinterpret_cast<const bf16x8*>(&Ws[p * HC * ROWB + ao1]);
                 }
-#if RING_VARIANT == 2
-#define RX6_PAIR(pa, pb)                                                                    \
-    asm volatile("" ::"v"(a0[pa]), "v"(a1[pa]), "v"(b[pb]));
-#else
 #define RX6_PAIR(pa, pb)                                                                    \
     acc[ip] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[pa], b[pb], acc[ip], 0, 0, 0);     \
     acc[ip + 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[pa], b[pb], acc[ip + 1], 0, 0, 0);
-#endif
                 RX6_PAIR(0, 0)
                 RX6_PAIR(0, 1)
                 RX6_PAIR(1, 0)
@@ -596,17 +472,7 @@ __global__ __launch_bounds__(RNW * 64, 1) void l1_ring_kernel(
                 RX6_PAIR(2, 0)
 #undef RX6_PAIR
             }
-#if RING_VARIANT == 4
-            // interleave: per MFMA one LDS read and three VALU of the neighbouring split
-#pragma unroll
-            for (int g = 0; g < 24; ++g) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-                __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // VALU
-            }
-#endif
         }
-#endif
         epi_prev = kc == nch - 1;
         if (epi_prev) {
             // bias + tanh -> fragment layout [row tile][feature tile][lane][16]

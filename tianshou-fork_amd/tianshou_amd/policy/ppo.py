@@ -166,6 +166,7 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
         self._np_perm = LegacyPermutation()
         self._plan_stream = None
         self._np_perm_used, self._np_perm_n = False, 0
+        self._dp_shards = (0, 0)  # (this rank's first global row, global rows) of learn()
         # data-parallel minibatch composition (see _minibatch_plan): "global" = the
         # reference's split of the global batch, "local" = every rank splits its own rows
         self.dp_permutation = "global"
@@ -330,10 +331,11 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
         Single process: Batch.split(batch_size, shuffle=True, merge_last=True) over one
         permutation (batch.py:896-912).  Data parallel, ``dp_permutation == "global"``: the
         reference's split of the GLOBAL batch -- every rank draws the same
-        np.random.permutation(world * n) (identical global RandomState on every rank; rank r
-        owns global rows [r*n, (r+1)*n), the env-major order of one VectorReplayBuffer over
-        all ranks' envs) with global minibatches of world * batch_size rows, and keeps its
-        own rows of each, in permutation order.  ``"local"``: each rank splits its own n rows
+        np.random.permutation(N) of the N = sum of every rank's n rows (identical global
+        RandomState on every rank; rank r owns global rows [n_0 + ... + n_{r-1}, ... + n_r),
+        the env-major order of one VectorReplayBuffer over all ranks' envs -- shards may be
+        unequal) with global minibatches of world * batch_size rows, and keeps its own rows
+        of each, in permutation order.  ``"local"``: each rank splits its own n rows
         (weak scaling: the sequential host draws stay O(n) per rank)."""
         return self._take_plan(self._issue_plan(n, dev, batch_size, allow_global, None), dev)
 
@@ -349,13 +351,14 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
         if self._plan_stream is None or self._plan_stream.device != dev:
             self._plan_stream = torch.cuda.Stream(dev)
         side = self._plan_stream
-        W = self.dp.world if self.dp.active else 1
-        pn = n * W if self._global_perm(n, dev, allow_global) else n
         issued = {}
 
         def plans(k):
             if k not in issued:
                 issued[k] = self._issue_plan(n, dev, batch_size, allow_global, side)
+            # the permutation size: the global row count (known after the first plan's
+            # shard-size exchange) or this rank's n
+            pn = self._np_perm_n if self._global_perm(n, dev, allow_global) else n
             if k + 1 < repeat and k + 1 not in issued and self._np_perm.next_ready(pn):
                 issued[k + 1] = self._issue_plan(n, dev, batch_size, allow_global, side)
             return self._take_plan(issued.pop(k), dev)
@@ -369,33 +372,38 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
     def _issue_plan(self, n: int, dev, batch_size: int, allow_global: bool, stream):
         """Enqueue one repeat's minibatch plan on ``stream`` (None: the current stream) and
         return it pending; _take_plan orders the current stream after it.  No host
-        synchronisation here: the data-parallel share selection is a compaction by prefix
-        sum whose size is known (every rank owns exactly n of the global rows), and the
-        per-minibatch share counts travel back to pinned host memory behind an event."""
+        synchronisation here (beyond the once-per-learn() check of the ranks' RandomStates,
+        which also exchanges the shard sizes): the data-parallel share selection is a
+        compaction by prefix sum whose size is known (this rank owns exactly n of the global
+        rows), and the per-minibatch share counts travel back to pinned host memory behind an
+        event."""
         W = self.dp.world if self.dp.active else 1
         ctx = torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
         cuda = dev.type == "cuda"
         if self._global_perm(n, dev, allow_global):
-            N, B = n * W, batch_size * W
-            gb = split_bounds(N, B, merge_last=True)
             if not self._np_perm_used:  # once per learn(): every rank holds the same stream
                 st = np.random.get_state()
                 h = zlib.crc32(np.ascontiguousarray(st[1]).tobytes() +
                                int(st[2]).to_bytes(4, "little"))
                 hs = self.dp.all_gather_cat(torch.tensor([h, n], dtype=torch.int64,
                                                          device=dev),
-                                                kind="perm_check").view(W, 2)
-                if not bool((hs == hs[0]).all()):
+                                                kind="perm_check").view(W, 2).cpu()
+                if not bool((hs[:, 0] == hs[0, 0]).all()):
                     raise RuntimeError(
-                        "dp_permutation='global' needs the same global np.random state and "
-                        "the same number of rows on every rank (seed np.random identically, "
-                        "or set dp_permutation='local')")
+                        "dp_permutation='global' needs the same global np.random state on "
+                        "every rank (seed np.random identically, or set "
+                        "dp_permutation='local')")
+                sizes = hs[:, 1].tolist()
+                assert sizes[self.dp.rank] == n
+                self._dp_shards = (sum(sizes[:self.dp.rank]), sum(sizes))
+            lo, N = self._dp_shards
+            B = batch_size * W
+            gb = split_bounds(N, B, merge_last=True)
             self._np_perm_used = True
             self._np_perm_n = N
             ends = torch.tensor([ge - 1 for _, ge in gb], dtype=torch.int64)
             with ctx:
                 perm_g = self._np_perm(N, dev)
-                lo = self.dp.rank * n
                 mine = (perm_g >= lo) & (perm_g < lo + n)
                 cs = torch.cumsum(mine, 0)
                 # this rank's rows in permutation order: row perm_g[p] - lo goes to slot

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Collect-step A/B at the headline shape: the in-tree library, then each variant named on the
 # command line (variants/libtsrl_<name>.so from tools/build_variant.sh, e.g. a
-# -DCOLLECT_ROW_STORE=1 build of collect.hip in round 3).
+# -D... build of collect.hip, e.g. the round-5 A/B of tools/r05_ab.sh).
 set -o pipefail
 for v in main "$@"; do
   if [ $v = main ]; then unset TSRL_LIB_PATH; else export TSRL_LIB_PATH=variants/libtsrl_$v.so; fi

@@ -2,8 +2,8 @@
 bench's actor): one-launch fused step (csrc/collect.hip) vs the four-launch step.
 
 python tools/collect_step_bench.py [--steps 256] [--envs 4096]
-TSRL_LIB_PATH=<variant .so> selects a diagnostic build (e.g. -DCOLLECT_STOP=n: the fused
-kernel returns after phase n), so phase costs can be read off by difference."""
+TSRL_LIB_PATH=<variant .so> selects a variant build (tools/build_variant.sh; e.g.
+-DCOLLECT_TRACE=1 with --trace: per-workgroup phase stamps of the fused kernel)."""
 import argparse
 import os
 import sys

@@ -569,6 +569,70 @@ def gen_collector_fused():
         _save(f"collector_{tag}.npz", **out)
 
 
+def gen_collector_wide():
+    """The headline's obs_rms arithmetic at the PRODUCTION row count:
+    4096 envs x D = 376 through the reference Collector + VectorEnvNormObs, so every
+    RunningMeanStd.update of a step sees 4096 rows (statistics.py:99-114 -- NumPy's
+    axis-0 f32 mean / var, venv_wrappers.py:93-99 -- applied per vector step, and to the
+    reset rows of the envs that finished), then sample(0) -> process_fn (a2c.py:83-117,
+    ppo.py:87-97).  T single-step collects (collect(n_step=E) is exactly one vector step
+    with every env ready), so obs_rms can be recorded after each one.  Stored: the statistic
+    after the Collector's initial reset and after every step, per-collect statistics, and
+    the process_fn outputs -- not the 49 MB of observations (the device test regenerates
+    its own rollout from the same env keys)."""
+    E, D, A, L, T = 4096, 376, 17, 9, 8
+    out = dict(E=np.array(E), D=np.array(D), A=np.array(A), L=np.array(L), T=np.array(T))
+    venv = VectorEnvNormObs(DummyVectorEnv(
+        [lambda e=e: SynthGymEnv(e, D, A, L) for e in range(E)]))
+    policy = _make_policy(D, A, seed=4, reward_normalization=True, ent_coef=0.0)
+    out.update(_sd_arrays("init_", policy))
+    buf = VectorReplayBuffer(E * T, E)
+    torch.manual_seed(1)
+    np.random.seed(1)
+    c = Collector(policy, venv, buf)
+
+    def rms_now(prefix):
+        rms = venv.get_obs_rms()
+        out[prefix + "mean"] = np.array(rms.mean, copy=True)
+        out[prefix + "var"] = np.array(rms.var, copy=True)
+        out[prefix + "count"] = np.array(rms.count)
+
+    rms_now("rms0_")
+    for t in range(T):
+        res = c.collect(n_step=E)
+        out.update(_stats_arrays(f"s{t}_", res))
+        rms_now(f"rms{t + 1}_")
+    batch, idx = buf.sample(0)
+    out["c1_indices"] = idx
+    out["c1_rew"] = np.array(buf._meta.rew, copy=True)
+    batch = policy.process_fn(batch, buf, idx)
+    for k in ("v_s", "returns", "adv"):
+        out["pf_" + k] = batch[k].detach().numpy()
+    out["pf_ret_rms_mean"] = np.asarray(policy.ret_rms.mean)
+    out["pf_ret_rms_var"] = np.asarray(policy.ret_rms.var)
+    out["pf_ret_rms_count"] = np.asarray(policy.ret_rms.count)
+    _save("collector_wide.npz", **out)
+
+
+def gen_rms_wide():
+    """One RunningMeanStd.update on a [4096, 376] batch of the synthetic env's raw rows, then
+    a second one (the merge), stats only: the batch is regenerated from the env keys
+    (oracle.synth_env, seed 0, env e, episode 0, step t) by the test."""
+    E, D = 4096, 376
+    rms = RunningMeanStd()
+    out = dict(E=np.array(E), D=np.array(D))
+    for i, t in enumerate((5, 6)):
+        k = synth_env.key(0, np.arange(E), np.zeros(E, np.int64), np.full(E, t))
+        x = synth_env.box_obs(k, D)
+        assert x.dtype == np.float32 and x.shape == (E, D)
+        rms.update(x)
+        out[f"t{i}"] = np.array(t)
+        out[f"mean{i}"] = np.array(rms.mean, copy=True)
+        out[f"var{i}"] = np.array(rms.var, copy=True)
+        out[f"count{i}"] = np.array(rms.count)
+    _save("rms_wide.npz", **out)
+
+
 # --------------------------------------------------------------------------------------
 # 7c. The reference OnpolicyTrainer driving Collector / VectorReplayBuffer / PPOPolicy on the
 #     synthetic env (trainer/base.py:396-439 train_step, 487-507 _update_on_entire_buffer,
@@ -1146,12 +1210,13 @@ def gen_cartpole():
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     which = sys.argv[1:] or ["returns", "gae", "buffer", "split", "rms", "ppo", "collector",
-                             "collector_fused",
+                             "collector_fused", "collector_wide", "rms_wide",
                              "stack", "ppo_discrete", "npg", "replay", "cartpole", "sched",
                              "persist", "trainer"]
     table = dict(returns=gen_returns_known, gae=gen_gae_random, buffer=gen_buffer_traces,
                  split=gen_split, rms=gen_rms, ppo=gen_ppo, collector=gen_collector,
-                 collector_fused=gen_collector_fused,
+                 collector_fused=gen_collector_fused, collector_wide=gen_collector_wide,
+                 rms_wide=gen_rms_wide,
                  stack=gen_stack, ppo_discrete=gen_ppo_discrete, npg=gen_npg, replay=gen_replay,
                  cartpole=gen_cartpole, sched=gen_sched,
                  persist=gen_persist, trainer=gen_trainer)

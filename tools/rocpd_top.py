@@ -1,7 +1,10 @@
 """Per-kernel totals from a rocprofv3 rocpd database (the sqlite *_results.db it writes):
 python tools/rocpd_top.py <db> [N] [--last-ms MS]  -> name, calls, total ms, mean us (top N by
 total); --last-ms keeps only the kernels that start in the last MS milliseconds of the trace
-(a steady-state window: e.g. the last timed iteration, after warm-up and MIOpen's find)."""
+(a steady-state window: e.g. the last timed iteration, after warm-up and MIOpen's find).
+Whatever the top-N cut, the kernels the bench line and DESIGN.md cite are always listed
+afterwards (ALWAYS: the GAE kernel of `roofline`, the fused collect step, the minibatch
+kernels), with min / max durations, so the roofline is reproducible from the summary alone."""
 import os
 import sqlite3
 import sys
@@ -29,3 +32,14 @@ for name, cnt, ms, us in c.execute(
         f"select name, count(*), sum(duration)/1e6, avg(duration)/1e3 from kernels {where} "
         "group by name order by sum(duration) desc limit ?", params + (n,)):
     print(f"{ms:10.2f} ms {cnt:7d} x {us:10.1f} us  {name[:140]}")
+ALWAYS = ("gae_rows_staged_kernel", "collect_box_step_kernel", "l1_ring_kernel",
+          "dw_x6_kernel", "dw_reduce_kernel", "ppo_tail_kernel", "tail_reduce_kernel",
+          "clip_adam_kernel", "rms_exact_kernel", "eval_tail_kernel")
+print("cited kernels (every launch in the window): total ms, calls, mean / min / max us")
+for pat in ALWAYS:
+    for name, cnt, ms, us, lo, hi in c.execute(
+            "select name, count(*), sum(duration)/1e6, avg(duration)/1e3, min(duration)/1e3, "
+            f"max(duration)/1e3 from kernels {where + (' and' if where else 'where')} "
+            "name like ? group by name order by name", params + (f"%{pat}%",)):
+        print(f"{ms:10.2f} ms {cnt:7d} x {us:10.2f} us (min {lo:.2f}, max {hi:.2f})  "
+              f"{name[:120]}")
