@@ -78,6 +78,10 @@ def _worker(rank, world, port, out):
     LOG.replayed({"obs_rms": 3})
     LOG.replayed(None)
     replayed = LOG.calls["obs_rms"]
+    # ragged all_gather_cat (unequal env shards' ret_rms partials): rank r sends r + 1 values
+    rg = dp.all_gather_cat(torch.arange(rank + 1, dtype=torch.float64) + 10 * rank,
+                           kind="ret_rms", ragged=True)
+    assert rg.tolist() == [10.0 * r + i for r in range(world) for i in range(r + 1)], rg
     out[rank] = (grads_sum, grads_avg, sums, flat, (int(hmax), int(hmin), moved, log, replayed))
     dist.destroy_process_group()
 

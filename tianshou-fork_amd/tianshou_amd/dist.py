@@ -83,13 +83,32 @@ class DataParallel:
             dist.all_reduce(t, group=self.group)
         return t
 
-    def all_gather_cat(self, t: torch.Tensor, kind: str = "other") -> torch.Tensor:
-        """Concatenate equally-shaped tensors of every rank in rank order."""
+    def all_gather_cat(self, t: torch.Tensor, kind: str = "other",
+                       ragged: bool = False) -> torch.Tensor:
+        """Concatenate the 1-D (or equally-shaped) tensors of every rank in rank order.
+        ``ragged``: the ranks' lengths may differ (e.g. per-workgroup partials of unequal env
+        shards): the lengths are exchanged first (one small all-gather, kind "shape", and a
+        host read), every rank's tensor is padded to the longest and the padding dropped."""
         if not self.active:
             return t
+        t = t.contiguous()
+        if ragged:
+            n = torch.tensor([t.numel()], dtype=torch.int64, device=t.device)
+            LOG.note("shape", n, "all_gather")
+            ns = [torch.empty_like(n) for _ in range(self.world)]
+            dist.all_gather(ns, n, group=self.group)
+            ns = [int(x) for x in torch.cat(ns).cpu()]
+            m = max(ns)
+            if m != t.numel() or len(set(ns)) > 1:
+                pad = torch.zeros(m, dtype=t.dtype, device=t.device)
+                pad[:t.numel()] = t.reshape(-1)
+                LOG.note(kind, pad, "all_gather")
+                out = [torch.empty_like(pad) for _ in range(self.world)]
+                dist.all_gather(out, pad, group=self.group)
+                return torch.cat([o[:k] for o, k in zip(out, ns)])
         LOG.note(kind, t, "all_gather")
         out = [torch.empty_like(t) for _ in range(self.world)]
-        dist.all_gather(out, t.contiguous(), group=self.group)
+        dist.all_gather(out, t, group=self.group)
         return torch.cat(out)
 
     def broadcast_params_(self, params: Iterable[torch.nn.Parameter], src: int = 0) -> None:

@@ -132,7 +132,9 @@ class A2CPolicy(PGPolicy):
             adv, ret, _, _ = gae_device(v_s, v_s_, rew, term, trunc, self._gamma, self._lambda,
                                         row_len, extra, scale, ret_partials=partials)
             if self.dp.active:  # every rank folds every rank's partials in rank order
-                partials = self.dp.all_gather_cat(partials[:nparts * 3], kind="ret_rms")
+                # (unequal env shards give unequal partial counts: ragged all-gather)
+                partials = self.dp.all_gather_cat(partials[:nparts * 3], kind="ret_rms",
+                                                  ragged=True)
                 nparts = partials.numel() // 3
             self.ret_rms.update_from_partials(partials, nparts)
         else:
