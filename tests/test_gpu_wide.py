@@ -30,9 +30,10 @@ def dev():
     return torch.device("cuda", 0)
 
 
-def _ratio(got, want, rtol=1e-5):
+def _ratio(got, want, rtol=1e-5, atol=1e-7):
+    """max |got - want| / (rtol |want| + atol): <= 1 passes assert_allclose(rtol, atol)."""
     got, want = np.asarray(got, np.float64), np.asarray(want, np.float64)
-    return float((np.abs(got - want) / (rtol * np.abs(want) + 1e-30)).max())
+    return float((np.abs(got - want) / (rtol * np.abs(want) + atol)).max())
 
 
 @pytest.mark.parametrize("exact", [False, True])
@@ -53,7 +54,7 @@ def test_rms_update_production_rows(golden_dir, dev, exact):
             assert np.array_equal(r.var, z[f"var{i}"]), i
         else:
             rm, rv = _ratio(r.mean, z[f"mean{i}"]), _ratio(r.var, z[f"var{i}"])
-            print(f"update {i}: default obs_rms vs reference, max err / rtol 1e-5: "
+            print(f"update {i}: default obs_rms vs reference, max err / (rtol 1e-5, atol 1e-7): "
                   f"mean {rm:.3g}, var {rv:.3g}")
             np.testing.assert_allclose(r.mean, z[f"mean{i}"], rtol=1e-5, atol=1e-7)
             np.testing.assert_allclose(r.var, z[f"var{i}"], rtol=1e-5)
@@ -91,7 +92,8 @@ def test_headline_width_production_rows_matches_reference(golden_dir, dev, exact
         _check_stats(z, f"s{t}_", res)
         check(t + 1)
     if not exact:
-        print(f"default obs_rms vs reference over {T + 1} states, max err / rtol 1e-5: "
+        print(f"default obs_rms vs reference over {T + 1} states, max err / (rtol 1e-5, atol "
+              f"1e-7): "
               f"mean {worst['mean']:.3g}, var {worst['var']:.3g}")
     assert np.array_equal(buf._meta.rew.cpu().numpy(), z["c1_rew"])
     batch, idx = buf.sample(0)
