@@ -858,6 +858,551 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
 }
 
 // ---------------------------------------------------------------------------------------
+// ppo_tail16_kernel: the same tail (layers 2-3, loss, backward to dZ1, layer-2/3 weight
+// gradients) on 16-row tiles at TWO waves per SIMD.  The 32-row kernel above runs one wave
+// per SIMD (505 / 384 VGPR+AGPR): its waves issue 54-56 % of their cycles and wait on their
+// own dependent MFMA -> tanh -> MFMA chains the rest (profiles/r03_learn_sq_pmc.txt), and a
+// quarter of its vector instructions move values between VGPRs and AGPRs.  Here a wave owns
+// 16 minibatch rows at a time: the chain products run on v_mfma_f32_16x16x32_bf16 (bf16x6,
+// 16 cycles each, the same matrix-core time per row), so the per-tile activations take half
+// the registers and the kernel fits 256 (8 waves per workgroup, one workgroup per CU, the
+// weight images shared by all 8).  The weight gradients still accumulate per wave on
+// v_mfma_f32_32x32x16_bf16 over the tile's 16 rows (acc_wgrad_x6, one K step).
+//
+// Layouts (lane l: row b = l & 15 of the tile, lane group g = l >> 4):
+//   H1: the 16 layer-1 features Fh1(g, r) = 32 (g >> 1) + rho(r) + 4 (g & 1), r = 0..15 --
+//       one 64-byte run of the layer-1 kernel's 32x32 fragment (tile 2 net + (g >> 1), lane
+//       (16 half + b) + 32 (g & 1)), so the load is four float4 reads;
+//   16x16 C tiles (layer 2, heads, dZ2, dZ1): lane (b, g) holds rows 4g + r, r = 0..3, of
+//       the tile's 16 features, column b;
+//   B operands come straight from those registers: K chunk kc of a 64-feature activation is
+//       register set 8 kc .. 8 kc + 7 (H1) or C tiles 2 kc, 2 kc + 1 (H2, dZ2), each lane
+//       group supplying its own 8 k; the weight images hold the matching permuted k.
+// Image of a [NTILE x 16 rows][NKC x 32 k] operand: plane p, tile, chunk kc, row i, group g
+// -> 16 bytes at ((p NTILE + tile) NKC + kc) 1024 + 64 i + 16 g, the 8 bf16 k = 8 g + j;
+// lane l reads the chunk at + 16 l: 64 lanes, 1 KB contiguous, no bank conflicts.
+// ---------------------------------------------------------------------------------------
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int T16_NW = 8;               // waves per workgroup (2 per SIMD)
+constexpr int T16_TPB = 64 * T16_NW;
+
+__device__ __forceinline__ int fh1(int g, int r) { return 32 * (g >> 1) + rho(r) + 4 * (g & 1); }
+// feature of register (tile t, r) of a 16x16 C tile held by lane group g
+__device__ __forceinline__ int fc16(int g, int t, int r) { return 16 * t + 4 * g + r; }
+// k slot j of chunk kc of a B operand built from C tiles 2 kc, 2 kc + 1
+__device__ __forceinline__ int fb16(int g, int kc, int j) { return fc16(g, 2 * kc + (j >> 2), j & 3); }
+
+__device__ __forceinline__ f32x4 zero4() {
+    f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    return z;
+}
+
+__device__ __forceinline__ f32x4 mfma6_16(const bf16x8 (&a)[NPL], const bf16x8 (&b)[NPL],
+                                          f32x4 acc) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], acc, 0, 0, 0);
+    return acc;
+}
+
+// Split an image: val(tile, kc, i, g, j) for tiles x nkc chunks; each thread writes whole
+// 16-byte chunks of the three planes.
+template <typename F>
+__device__ __forceinline__ void build_img16(char* img, int ntile, int nkc, F val) {
+    const int total = ntile * nkc * 64;
+    for (int q = threadIdx.x; q < total; q += T16_TPB) {
+        const int g = q & 3, i = (q >> 2) & 15, kc = (q >> 6) % nkc, tile = (q >> 6) / nkc;
+        bf16x8 p0, p1, p2;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            __bf16 a, b, c;
+            split1(val(tile, kc, i, g, j), a, b, c);
+            p0[j] = a;
+            p1[j] = b;
+            p2[j] = c;
+        }
+        const int off = (tile * nkc + kc) * 1024 + 64 * i + 16 * g;
+        const int pl = ntile * nkc * 1024;
+        *reinterpret_cast<bf16x8*>(img + off) = p0;
+        *reinterpret_cast<bf16x8*>(img + pl + off) = p1;
+        *reinterpret_cast<bf16x8*>(img + 2 * pl + off) = p2;
+    }
+}
+
+__device__ __forceinline__ void ld_img16(const char* img, int ntile, int nkc, int tile, int kc,
+                                         int l, bf16x8 (&a)[NPL]) {
+    const int pl = ntile * nkc * 1024, off = (tile * nkc + kc) * 1024 + 16 * l;
+#pragma unroll
+    for (int p = 0; p < NPL; ++p) a[p] = *reinterpret_cast<const bf16x8*>(img + p * pl + off);
+}
+
+// B operand: 8 values split into the three planes
+__device__ __forceinline__ void split8(const float (&v)[8], bf16x8 (&b)[NPL]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        __bf16 x0, x1, x2;
+        split1(v[j], x0, x1, x2);
+        b[0][j] = x0;
+        b[1][j] = x1;
+        b[2][j] = x2;
+    }
+}
+
+// Feature-major scratch [feature][16 rows] (stride SH) from 16 registers whose features are
+// feat(reg): lane (b, g) writes column b.
+template <int NV, typename F>
+__device__ __forceinline__ void put16(float* S, const float (&v)[NV], int b, F feat) {
+#pragma unroll
+    for (int r = 0; r < NV; ++r) S[feat(r) * SH + b] = v[r];
+}
+
+// Sum of the 16 row values of scratch row S[0 .. 16) (fixed order).
+__device__ __forceinline__ float rowsum16(const float* S) {
+    const float4* q = reinterpret_cast<const float4*>(S);
+    const float4 a = q[0], b = q[1], c = q[2], d = q[3];
+    return ((a.x + a.y) + (a.z + a.w)) + ((b.x + b.y) + (b.z + b.w)) +
+           (((c.x + c.y) + (c.z + c.w)) + ((d.x + d.y) + (d.z + d.w)));
+}
+
+constexpr int I16_W2 = 0;                          // W2: [4 out tiles][2 kc]
+constexpr int I16_W2T = I16_W2 + NPL * 8 * 1024;   // W2^T: [4 f tiles][2 kc]
+constexpr int I16_W3 = I16_W2T + NPL * 8 * 1024;   // W3: [2 a tiles][2 kc] (actor)
+constexpr int I16_W3T = I16_W3 + NPL * 4 * 1024;   // W3^T: [4 out tiles][1 kc] (actor)
+constexpr int I16_ACTOR = I16_W3T + NPL * 4 * 1024, I16_CRITIC = I16_W3;
+// per-wave scratch: S1, S2 [64 features][SH]; reused by the final folds
+constexpr int T16_SCR = T16_NW * 2 * H * SH;
+static_assert(T16_SCR >= T16_NW * 32 * H, "fold scratch");
+static_assert(T16_SCR >= T16_NW * 64 * 18, "vector fold scratch");
+constexpr int T16_V = 0, T16_B2 = 0, T16_B3 = T16_B2 + H, T16_W3C = T16_B3 + AMAX,
+              T16_LS = T16_W3C + H, T16_IV = T16_LS + AMAX, T16_IV2 = T16_IV + AMAX,
+              T16_VEND = T16_IV2 + AMAX;
+
+template <int NET>
+__global__ __launch_bounds__(T16_TPB, 1) void ppo_tail16_kernel(
+    const float* __restrict__ h1f, int64_t n, const int64_t* __restrict__ idx, TailWeights wt,
+    const float* __restrict__ act, const float* __restrict__ logp_old,
+    const float* __restrict__ adv, const float* __restrict__ ret, const float* __restrict__ v_s,
+    const double* __restrict__ adv_sums, TailParams p, float* __restrict__ dz1,
+    float* __restrict__ slab_f, double* __restrict__ slab_d) {
+    constexpr bool actor = NET == 0;
+    constexpr int net = NET;
+    __shared__ __attribute__((aligned(16))) char img[actor ? I16_ACTOR : I16_CRITIC];
+    __shared__ __attribute__((aligned(16))) float scr[T16_SCR];
+    __shared__ float sv[T16_VEND];
+    __shared__ double sred[T16_NW][SL_D];
+    const int t = threadIdx.x;
+    const int w = t >> 6, l = t & 63, b = l & 15, g = l >> 4;
+    const int A = p.A;
+    {
+        const float* w2 = actor ? wt.w2a : wt.w2c;
+        const float* b2 = actor ? wt.b2a : wt.b2c;
+        // layer 2: A = W2 [out 16 ot + i][k -> feature fh1(g, 8 kc + j)]
+        build_img16(img + I16_W2, 4, 2, [=](int ot, int kc, int i, int gg, int j) {
+            return w2[(16 * ot + i) * H + fh1(gg, 8 * kc + j)];
+        });
+        // dZ1: A = W2^T [f = fh1(i >> 2, 4 ft + (i & 3))][k -> out fb16(g, kc, j)]
+        build_img16(img + I16_W2T, 4, 2, [=](int ft, int kc, int i, int gg, int j) {
+            return w2[fb16(gg, kc, j) * H + fh1(i >> 2, 4 * ft + (i & 3))];
+        });
+        if (t < H) sv[T16_B2 + t] = b2[t];
+        if (actor) {
+            const float* w3 = wt.w3a;
+            // mu head: A = W3 [a = 16 at + i][k -> h2 feature fb16(g, kc, j)]
+            build_img16(img + I16_W3, 2, 2, [=](int at, int kc, int i, int gg, int j) {
+                const int a = 16 * at + i;
+                return a < A ? w3[a * H + fb16(gg, kc, j)] : 0.0f;
+            });
+            // dZ2: A = W3^T [out 16 ot + i][k -> a = fb16(g, 0, j)]
+            build_img16(img + I16_W3T, 4, 1, [=](int ot, int, int i, int gg, int j) {
+                const int a = fb16(gg, 0, j);
+                return a < A ? w3[a * H + 16 * ot + i] : 0.0f;
+            });
+            if (t < AMAX) {
+                sv[T16_B3 + t] = t < A ? wt.b3a[t] : 0.0f;
+                const float sig = t < A ? expf(wt.log_std[t]) : 1.0f;
+                sv[T16_LS + t] = logf(sig);
+                sv[T16_IV + t] = 1.0f / (sig * sig);
+                sv[T16_IV2 + t] = 1.0f / (2.0f * (sig * sig));
+            }
+        } else if (t < H) {
+            sv[T16_W3C + t] = wt.w3c[t];
+        }
+    }
+    __syncthreads();
+    float* S1 = scr + w * 2 * H * SH;
+    float* S2 = S1 + H * SH;
+    const float b3c = wt.b3c[0];
+    float mean_f = 0.0f, std_f = 1.0f;
+    if (actor && p.norm_adv) {
+        const double nn = 1.0 / p.inv_b64;
+        const double m = adv_sums[0] / nn;
+        const double var = (adv_sums[1] - adv_sums[0] * m) / (nn - 1.0);
+        mean_f = (float)m;
+        std_f = (float)sqrt(var > 0.0 ? var : 0.0);
+    }
+    // per-wave accumulators (32x32 C layout of acc_wgrad_x6) and per-lane column sums
+    f32x16 gW2[2][2], gW3[1][actor ? 2 : 1];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) gW2[i][j] = zero16();
+#pragma unroll
+    for (int i = 0; i < (actor ? 2 : 1); ++i) gW3[0][i] = zero16();
+    // column sums over the minibatch rows.  Each tile's are read off the feature-major
+    // scratch the weight gradients stage anyway (one row of 16 values per lane): colA = db2
+    // of feature l; colB (actor) = db3 of action l (l < 32) or d/dlog_std of action l - 32
+    // (staged in S1 rows 32..63, which dW3 does not read).  Critic: dW3c and db3c as
+    // per-lane partial sums (vl: 16 features of the lane's group, then gv).
+    float colA = 0.f, colB = 0.f;
+    constexpr int NV = actor ? 1 : 17;
+    float vl[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) vl[i] = 0.f;
+    double loss_acc = 0.0, cnt_acc = 0.0;
+    const int c32 = l & 31, h32 = l >> 5;  // lane coordinates of the 32x32 weight-gradient tiles
+
+    const int64_t ntiles = (n + 15) / 16;
+    const int64_t gw = (int64_t)blockIdx.x * T16_NW + w, nw = (int64_t)gridDim.x * T16_NW;
+    const uint32_t A_u = (uint32_t)A;
+    for (int64_t tt = gw; tt < ntiles; tt += nw) {
+        const int64_t row = tt * 16 + b;
+        const bool live = row < n;
+        const int64_t bt = tt >> 1;
+        const int half = (int)(tt & 1);
+        // ---- inputs ----------------------------------------------------------------------
+        float h1[16];
+        {
+            const float4* src = reinterpret_cast<const float4*>(
+                h1f + ((bt * NT + 2 * net + (g >> 1)) * 64 + 16 * half + b + 32 * (g & 1)) * 16);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 v = src[q];
+                h1[4 * q] = v.x;
+                h1[4 * q + 1] = v.y;
+                h1[4 * q + 2] = v.z;
+                h1[4 * q + 3] = v.w;
+            }
+        }
+        const uint32_t j32 = live ? (uint32_t)(idx ? idx[row] : row) : 0u;
+        float x0, x1;
+        float av[8];
+        if constexpr (actor) {
+            const uint32_t ab = j32 * A_u;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const uint32_t a = (uint32_t)fc16(g, r >> 2, r & 3);
+                av[r] = act[ab + (a < A_u ? a : 0u)];
+            }
+            x0 = logp_old[j32];
+            x1 = adv[j32];
+        } else {
+            x0 = ret[j32];
+            x1 = p.value_clip ? v_s[j32] : 0.0f;
+        }
+        // ---- layer 2 ---------------------------------------------------------------------
+        float h2[4][4];
+        {
+            f32x4 z[4] = {zero4(), zero4(), zero4(), zero4()};
+#pragma unroll
+            for (int kc = 0; kc < 2; ++kc) {
+                bf16x8 bb[NPL];
+                float v8[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v8[j] = h1[8 * kc + j];
+                split8(v8, bb);
+#pragma unroll
+                for (int ot = 0; ot < 4; ++ot) {
+                    bf16x8 aa[NPL];
+                    ld_img16(img + I16_W2, 4, 2, ot, kc, l, aa);
+                    z[ot] = mfma6_16(aa, bb, z[ot]);
+                }
+            }
+#pragma unroll
+            for (int ot = 0; ot < 4; ++ot)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    h2[ot][r] = tanh_nb(z[ot][r] + sv[T16_B2 + fc16(g, ot, r)]);
+        }
+        float dz2[4][4];
+        if constexpr (actor) {
+            // ---- mu head + clipped surrogate ---------------------------------------------
+            f32x4 mu[2] = {zero4(), zero4()};
+#pragma unroll
+            for (int kc = 0; kc < 2; ++kc) {
+                bf16x8 bb[NPL];
+                float v8[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v8[j] = h2[2 * kc + (j >> 2)][j & 3];
+                split8(v8, bb);
+#pragma unroll
+                for (int at = 0; at < 2; ++at) {
+                    bf16x8 aa[NPL];
+                    ld_img16(img + I16_W3, 2, 2, at, kc, l, aa);
+                    mu[at] = mfma6_16(aa, bb, mu[at]);
+                }
+            }
+            float diff[8];
+            float lp = 0.0f;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const int a = fc16(g, r >> 2, r & 3);
+                const bool in = a < A && live;
+                const float d = av[r] - (mu[r >> 2][r & 3] + sv[T16_B3 + a]);
+                const float term = -(d * d) * sv[T16_IV2 + a] - sv[T16_LS + a] - LOG_SQRT_2PI;
+                diff[r] = in ? d : 0.0f;
+                lp += in ? term : 0.0f;
+            }
+            const float lp2 = lp + __shfl_xor(lp, 16, 64);
+            const float logp = lp2 + __shfl_xor(lp2, 32, 64);
+            float g_logp = 0.0f;
+            if (live) {
+                float an = x1;
+                if (p.norm_adv) an = (an - mean_f) / (std_f + p.adv_eps);
+                const float ratio = expf(logp - x0);
+                const float surr1 = ratio * an;
+                const float rc = fminf(fmaxf(ratio, p.lo), p.hi);
+                const float surr2 = rc * an;
+                const float in_rng = (ratio >= p.lo && ratio <= p.hi) ? 1.0f : 0.0f;
+                float clip1, d1;
+                if (surr1 < surr2) {
+                    clip1 = surr1;
+                    d1 = an;
+                } else if (surr2 < surr1) {
+                    clip1 = surr2;
+                    d1 = in_rng * an;
+                } else {
+                    clip1 = surr1;
+                    d1 = 0.5f * an + 0.5f * in_rng * an;
+                }
+                float obj = clip1, dobj = d1;
+                if (p.use_dual && an < 0.0f) {
+                    const float tt2 = p.dual * an;
+                    if (clip1 > tt2) {
+                        obj = clip1;
+                    } else if (clip1 < tt2) {
+                        obj = tt2;
+                        dobj = 0.0f;
+                    } else {
+                        obj = clip1;
+                        dobj = 0.5f * d1;
+                    }
+                }
+                g_logp = (float)(-(double)dobj * (double)ratio * p.inv_b64);
+                if (g == 0) {
+                    loss_acc += -(double)obj;
+                    cnt_acc += 1.0;
+                }
+            }
+            float dmu[8], dls[8];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const int a = fc16(g, r >> 2, r & 3);
+                const float iv = sv[T16_IV + a];
+                dmu[r] = g_logp * diff[r] * iv;
+                dls[r] = (a < A && live) ? g_logp * (diff[r] * diff[r] * iv - 1.0f) : 0.0f;
+            }
+            // dW3 = dMu^T . H2 over the tile's 16 rows; db3 and d/dlog_std from the scratch
+            {
+                float h2f[16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) h2f[r] = h2[r >> 2][r & 3];
+                wave_sync_lds();
+                put16(S1, dmu, b, [=](int r) { return fc16(g, r >> 2, r & 3); });
+                put16(S1, dls, b, [=](int r) { return 32 + fc16(g, r >> 2, r & 3); });
+                put16(S2, h2f, b, [=](int r) { return fc16(g, r >> 2, r & 3); });
+                wave_sync_lds();
+                acc_wgrad_x6<1, 2>(gW3, S1, S2, c32, h32);
+                colB += rowsum16(S1 + l * SH);
+            }
+            // dZ2 = (W3^T dMu) * (1 - H2^2)
+            {
+                bf16x8 bb[NPL];
+                split8(dmu, bb);
+#pragma unroll
+                for (int ot = 0; ot < 4; ++ot) {
+                    bf16x8 aa[NPL];
+                    ld_img16(img + I16_W3T, 4, 1, ot, 0, l, aa);
+                    const f32x4 d = mfma6_16(aa, bb, zero4());
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) dz2[ot][r] = d[r] * (1.0f - h2[ot][r] * h2[ot][r]);
+                }
+            }
+        } else {
+            // ---- value head + value loss ---------------------------------------------------
+            float vpart = 0.0f;
+#pragma unroll
+            for (int ot = 0; ot < 4; ++ot)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) vpart += sv[T16_W3C + fc16(g, ot, r)] * h2[ot][r];
+            const float v2 = vpart + __shfl_xor(vpart, 16, 64);
+            const float value = v2 + __shfl_xor(v2, 32, 64) + b3c;
+            float gv = 0.0f;
+            if (live) {
+                const float rt = x0;
+                float dv, vf;
+                if (p.value_clip) {
+                    const float vs = x1;
+                    const float dlt = value - vs;
+                    const float dcl = fminf(fmaxf(dlt, -p.eps_clip), p.eps_clip);
+                    const float vcl = vs + dcl;
+                    const float e1 = rt - value, e2 = rt - vcl;
+                    const float vf1 = e1 * e1, vf2 = e2 * e2;
+                    const float g1 = -2.0f * e1;
+                    const float g2 = (dlt >= -p.eps_clip && dlt <= p.eps_clip) ? -2.0f * e2 : 0.0f;
+                    if (vf1 > vf2) {
+                        vf = vf1;
+                        dv = g1;
+                    } else if (vf2 > vf1) {
+                        vf = vf2;
+                        dv = g2;
+                    } else {
+                        vf = vf1;
+                        dv = 0.5f * g1 + 0.5f * g2;
+                    }
+                } else {
+                    const float e1 = rt - value;
+                    vf = e1 * e1;
+                    dv = -2.0f * e1;
+                }
+                gv = (float)((double)p.vf_coef * (double)dv * p.inv_b64);
+                if (g == 0) loss_acc += (double)vf;
+            }
+#pragma unroll
+            for (int ot = 0; ot < 4; ++ot)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    vl[4 * ot + r] += gv * h2[ot][r];
+                    dz2[ot][r] = gv * sv[T16_W3C + fc16(g, ot, r)] * (1.0f - h2[ot][r] * h2[ot][r]);
+                }
+            vl[NV - 1] += g == 0 ? gv : 0.0f;
+        }
+        // ---- dZ1 = (W2^T dZ2) * (1 - H1^2) -> HBM (row-major [n][128]) -------------------
+        {
+            f32x4 d1[4] = {zero4(), zero4(), zero4(), zero4()};
+#pragma unroll
+            for (int kc = 0; kc < 2; ++kc) {
+                bf16x8 bb[NPL];
+                float v8[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v8[j] = dz2[2 * kc + (j >> 2)][j & 3];
+                split8(v8, bb);
+#pragma unroll
+                for (int ft = 0; ft < 4; ++ft) {
+                    bf16x8 aa[NPL];
+                    ld_img16(img + I16_W2T, 4, 2, ft, kc, l, aa);
+                    d1[ft] = mfma6_16(aa, bb, d1[ft]);
+                }
+            }
+            if (live) {
+                // register 4 ft + r holds feature fh1(g, 4 ft + r): four runs of 4 features
+                float* o = dz1 + row * HC + 64 * net + 32 * (g >> 1) + 4 * (g & 1);
+#pragma unroll
+                for (int ft = 0; ft < 4; ++ft) {
+                    const float4 v = make_float4(
+                        d1[ft][0] * (1.0f - h1[4 * ft] * h1[4 * ft]),
+                        d1[ft][1] * (1.0f - h1[4 * ft + 1] * h1[4 * ft + 1]),
+                        d1[ft][2] * (1.0f - h1[4 * ft + 2] * h1[4 * ft + 2]),
+                        d1[ft][3] * (1.0f - h1[4 * ft + 3] * h1[4 * ft + 3]));
+                    *reinterpret_cast<float4*>(o + 8 * ft) = v;
+                }
+            }
+        }
+        // ---- db2, dW2 = dZ2^T . H1 over the tile's 16 rows ---------------------------------
+        {
+            float dzf[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) dzf[r] = dz2[r >> 2][r & 3];
+            wave_sync_lds();
+            put16(S1, dzf, b, [=](int r) { return fc16(g, r >> 2, r & 3); });
+            put16(S2, h1, b, [=](int r) { return fh1(g, r); });
+            wave_sync_lds();
+            acc_wgrad_x6<2, 2>(gW2, S1, S2, c32, h32);
+            colA += rowsum16(S1 + l * SH);
+        }
+    }
+    // ---- fold the T16_NW waves (fixed order) into this workgroup's slab -------------------
+    __syncthreads();
+    float* red = scr;
+    float* slab = slab_f + (int64_t)blockIdx.x * SL_F;
+    auto fold = [&](const f32x16 (&gg)[2], int o0, int base) {
+        // rows [o0, o0+32) of a [rows][64] matrix held as 32x32 C layout
+#pragma unroll
+        for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                red[w * 32 * H + (rho(r) + 4 * h32) * H + 32 * ft + c32] = gg[ft][r];
+        __syncthreads();
+        for (int i = t; i < 32 * H; i += T16_TPB) {
+            float v = red[i];
+#pragma unroll
+            for (int ww = 1; ww < T16_NW; ++ww) v += red[ww * 32 * H + i];
+            slab[base + o0 * H + i] = v;
+        }
+        __syncthreads();
+    };
+    const int base2 = actor ? SL_W2A : SL_W2C;
+    fold(gW2[0], 0, base2);
+    fold(gW2[1], 32, base2);
+    if constexpr (actor) fold(gW3[0], 0, SL_W3A);
+    // column sums: [wave][lane][NF] = colA, colB, then (critic) the per-lane partials vl
+    constexpr int NF = 2 + (actor ? 0 : NV);
+    red[(w * 64 + l) * NF] = colA;
+    red[(w * 64 + l) * NF + 1] = colB;
+    if constexpr (!actor) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) red[(w * 64 + l) * NF + 2 + i] = vl[i];
+    }
+    loss_acc = wave_sum(loss_acc);
+    cnt_acc = wave_sum(cnt_acc);
+    if (l == 0) {
+        sred[w][0] = loss_acc;
+        sred[w][1] = cnt_acc;
+    }
+    __syncthreads();
+    auto wsum = [&](int lane, int k) -> double {  // over the waves, fixed order
+        double v = 0.0;
+        for (int ww = 0; ww < T16_NW; ++ww) v += (double)red[(ww * 64 + lane) * NF + k];
+        return v;
+    };
+    // critic per-lane partials: feature o of lane group (o >> 2) & 3, register
+    // 4 (o >> 4) + (o & 3), over the group's 16 lanes (rows) and the waves
+    auto gsum = [&](int gg, int k) -> double {
+        double v = 0.0;
+        for (int ww = 0; ww < T16_NW; ++ww) {
+            float s = 0.f;
+            for (int bb = 0; bb < 16; ++bb) s += red[(ww * 64 + 16 * gg + bb) * NF + k];
+            v += (double)s;
+        }
+        return v;
+    };
+    double* sd = slab_d + (int64_t)blockIdx.x * SL_D;
+    if (t < H) {
+        slab[(actor ? SL_B2A : SL_B2C) + t] = (float)wsum(t, 0);
+        if (!actor) slab[SL_W3C + t] = (float)gsum((t >> 2) & 3, 2 + 4 * (t >> 4) + (t & 3));
+    } else if (actor && t < H + AMAX) {
+        slab[SL_B3A + t - H] = (float)wsum(t - H, 1);
+    } else if (actor && t < H + 2 * AMAX) {
+        sd[4 + t - H - AMAX] = wsum(t - H, 1);  // lanes 32..63: d/dlog_std
+    } else if (!actor && t == H) {
+        slab[SL_B3C] = (float)gsum(0, 2 + NV - 1);
+    } else if (t >= 3 * H && t < 3 * H + 2) {
+        double v = 0.0;
+#pragma unroll
+        for (int ww = 0; ww < T16_NW; ++ww) v += sred[ww][t - 3 * H];
+        if (actor) {
+            if (t == 3 * H) sd[0] = v;  // clip sum
+            else sd[2] = v;             // row count
+        } else if (t == 3 * H) {
+            sd[1] = v;                  // vf sum
+        }
+    }
+    if (actor && t == 3 * H + 2) sd[3] = 0.0;
+}
+
+// ---------------------------------------------------------------------------------------
 // Forward-only evaluation for PPOPolicy.process_fn: critic values V(s) (a2c.py:83-100) and,
 // with LOGP, the Gaussian log-prob of the stored actions (logp_old, ppo.py:95-96), from the
 // layer-1 activations of tsrl_mlp_l1_fwd.  One wave = 32 rows.
@@ -1266,10 +1811,16 @@ TailParams make_tail_params(const tsrl_ppo_params& q, int A) {
     return p;
 }
 
+// 1: the 16-row-tile tail at two waves per SIMD (ppo_tail16_kernel); 0: the 32-row kernel
+#ifndef TAIL16
+#define TAIL16 1
+#endif
+
 int tail_grid(int64_t n) {
     // workgroups per net (one launch per net), one resident per CU
-    const int64_t tiles = (n + 31) / 32;
-    const int64_t g = (tiles + TAIL_NW - 1) / TAIL_NW;
+    const int64_t tiles = TAIL16 ? (n + 15) / 16 : (n + 31) / 32;
+    const int64_t waves = TAIL16 ? T16_NW : TAIL_NW;
+    const int64_t g = (tiles + waves - 1) / waves;
     return (int)std::min<int64_t>(g, 256);
 }
 
@@ -1339,7 +1890,16 @@ static int ppo_tail_impl(const float* h1frag, int64_t n, const int64_t* idx,
     TailWeights w{wt->w2a, wt->b2a, wt->w2c, wt->b2c, wt->w3a, wt->b3a, wt->w3c, wt->b3c,
                   wt->log_std};
     const TailParams tp = make_tail_params(prm, (int)act_dim);
-    if (stages & 1) {
+    if ((stages & 1) && TAIL16) {
+        hipLaunchKernelGGL(ppo_tail16_kernel<0>, dim3(g), dim3(T16_TPB), 0, as_stream(stream),
+                           h1frag, n, idx, w, act, logp_old, adv, ret, v_s, adv_sums, tp, dz1,
+                           slab_f, slab_d);
+        TSRL_LAUNCH_CHECK("tsrl_ppo_tail(actor)");
+        hipLaunchKernelGGL(ppo_tail16_kernel<1>, dim3(g), dim3(T16_TPB), 0, as_stream(stream),
+                           h1frag, n, idx, w, act, logp_old, adv, ret, v_s, adv_sums, tp, dz1,
+                           slab_f, slab_d);
+        TSRL_LAUNCH_CHECK("tsrl_ppo_tail");
+    } else if (stages & 1) {
         hipLaunchKernelGGL(ppo_tail_kernel<0>, dim3(g), dim3(TAIL_TPB), 0, as_stream(stream),
                            h1frag, n, idx, w, act, logp_old, adv, ret, v_s, adv_sums, tp, dz1,
                            slab_f, slab_d);
