@@ -19,6 +19,19 @@ sys.path.insert(0, os.path.join(ROOT, "tianshou-fork_amd"))
 
 SHARDS, T, D, A, L, BS = (48, 80), 32, 376, 17, 9, 256
 KEYS = ("obs", "obs_next", "act", "rew", "terminated", "truncated", "done")
+PF = ("v_s", "returns", "adv", "logp_old")
+
+
+def _capture(policy):
+    """Keep a CPU copy of process_fn's outputs (diagnostics of the comparison)."""
+    cap, orig = {}, policy.process_fn
+
+    def pf(batch, buffer, indices):
+        out = orig(batch, buffer, indices)
+        cap.update({k: out[k].detach().reshape(-1).float().cpu() for k in PF})
+        return out
+    policy.process_fn = pf
+    return cap
 
 
 def main():
@@ -49,6 +62,7 @@ def main():
     assert coll._step_on, "the fused one-launch step did not run"
     rms = env.get_obs_rms()
     rms_state = (torch.as_tensor(rms.mean), torch.as_tensor(rms.var), float(rms.count))
+    cap = _capture(policy)
     np.random.seed(0)  # one global np.random stream: the reference split of the global batch
     res = policy.update(0, buf, batch_size=BS, repeat=1)
     sd = {k: v.detach().cpu() for k, v in policy.state_dict().items()}
@@ -58,6 +72,8 @@ def main():
             dist.send(t.to(torch.uint8) if t.dtype == torch.bool else t, 0)
         dist.send(rms_state[0], 0)
         dist.send(rms_state[1], 0)
+        for k in PF:
+            dist.send(cap[k], 0)
         dist.barrier()
         dist.destroy_process_group()
         return
@@ -73,6 +89,11 @@ def main():
     other = [torch.empty(D), torch.empty(D)]
     dist.recv(other[0], 1)
     dist.recv(other[1], 1)
+    pf = {k: [cap[k]] for k in PF}
+    for k in PF:
+        t = torch.empty(SHARDS[1] * T, dtype=cap[k].dtype)
+        dist.recv(t, 1)
+        pf[k].append(t)
     dist.barrier()
     dist.destroy_process_group()
     del coll, env
@@ -87,6 +108,7 @@ def main():
     ref = build(dev)
     ref.dp = DataParallel()
     ref.dp.enabled = False
+    cap_ref = _capture(ref)
     np.random.seed(0)
     res_ref = ref.update(0, union, batch_size=world * BS, repeat=1)
     sd_ref = {k: v.detach().cpu() for k, v in ref.state_dict().items()}
@@ -94,7 +116,8 @@ def main():
     torch.save(dict(loss=torch.tensor([res[k] for k in terms]),
                     loss_ref=torch.tensor([res_ref[k] for k in terms]),
                     sd=sd, sd_ref=sd_ref, rms_mean=rms_state[0], rms_var=rms_state[1],
-                    rms_count=rms_state[2], rms_mean1=other[0], rms_var1=other[1]),
+                    rms_count=rms_state[2], rms_mean1=other[0], rms_var1=other[1],
+                    pf={k: torch.cat(v) for k, v in pf.items()}, pf_ref=cap_ref),
                os.path.join(outdir, "uneq.pt"))
 
 

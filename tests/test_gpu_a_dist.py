@@ -189,6 +189,11 @@ def test_unequal_env_shards(rank_runs):
     np.testing.assert_allclose(r["rms_var"].numpy(), var, rtol=1e-5, atol=1e-6)
     assert r["loss"].shape == r["loss_ref"].shape == (4, sum(w.SHARDS) * w.T // (2 * w.BS))
     print("unequal shards: losses (dp, single)\n", r["loss"].numpy(), "\n", r["loss_ref"].numpy())
+    for k, v in r["pf"].items():
+        ref = r["pf_ref"][k]
+        err = (v - ref).abs().max().item()
+        print(f"process_fn {k}: max |dp - single| {err:.3g} (max |single| {ref.abs().max():.3g})")
+        np.testing.assert_allclose(v.numpy(), ref.numpy(), rtol=1e-4, atol=1e-5, err_msg=k)
     # per-minibatch loss terms of 512-row global minibatches (the tolerance of the 2/4-rank
     # test's 256 x world minibatches)
     np.testing.assert_allclose(r["loss"].numpy(), r["loss_ref"].numpy(), rtol=1e-4, atol=1e-5)

@@ -879,8 +879,8 @@ __global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
 //       register set 8 kc .. 8 kc + 7 (H1) or C tiles 2 kc, 2 kc + 1 (H2, dZ2), each lane
 //       group supplying its own 8 k; the weight images hold the matching permuted k.
 // Image of a [NTILE x 16 rows][NKC x 32 k] operand: plane p, tile, chunk kc, row i, group g
-// -> 16 bytes at ((p NTILE + tile) NKC + kc) 1024 + 64 i + 16 g, the 8 bf16 k = 8 g + j;
-// lane l reads the chunk at + 16 l: 64 lanes, 1 KB contiguous, no bank conflicts.
+// -> 16 bytes at ((p NTILE + tile) NKC + kc) 1024 + 16 (16 g + i), the 8 bf16 k = 8 g + j:
+// lane l = 16 g + i reads the chunk at + 16 l, 64 lanes, 1 KB contiguous, no bank conflicts.
 // ---------------------------------------------------------------------------------------
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int T16_NW = 8;               // waves per workgroup (2 per SIMD)
@@ -924,7 +924,7 @@ __device__ __forceinline__ void build_img16(char* img, int ntile, int nkc, F val
             p1[j] = b;
             p2[j] = c;
         }
-        const int off = (tile * nkc + kc) * 1024 + 64 * i + 16 * g;
+        const int off = (tile * nkc + kc) * 1024 + 16 * (16 * g + i);  // lane 16 g + i
         const int pl = ntile * nkc * 1024;
         *reinterpret_cast<bf16x8*>(img + off) = p0;
         *reinterpret_cast<bf16x8*>(img + pl + off) = p1;
