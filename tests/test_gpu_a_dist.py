@@ -193,6 +193,13 @@ def test_unequal_env_shards(rank_runs):
         ref = r["pf_ref"][k]
         err = (v - ref).abs().max().item()
         print(f"process_fn {k}: max |dp - single| {err:.3g} (max |single| {ref.abs().max():.3g})")
+        bad = np.flatnonzero(~np.isclose(v.numpy(), ref.numpy(), rtol=1e-4, atol=1e-5))
+        if len(bad):
+            n0 = w.SHARDS[0] * w.T
+            print(f"  mismatched rows: {int((bad < n0).sum())} of rank 0's {n0}, "
+                  f"{int((bad >= n0).sum())} of rank 1's; first {bad[:12].tolist()}, "
+                  f"step-in-env {(bad[:12] % w.T).tolist()}")
+            print("  dp    ", v.numpy()[bad[:8]], "\n  single", ref.numpy()[bad[:8]])
         np.testing.assert_allclose(v.numpy(), ref.numpy(), rtol=1e-4, atol=1e-5, err_msg=k)
     # per-minibatch loss terms of 512-row global minibatches (the tolerance of the 2/4-rank
     # test's 256 x world minibatches)

@@ -93,7 +93,8 @@ def test_gae_full_golden_fast_path(golden_dir, dev):
     assert _bitexact_frac(adv32.cpu().numpy(), z["full_adv"]) > 0.999
 
 
-@pytest.mark.parametrize("envs,steps", [(4096, 2048), (512, 128), (3, 5000), (7, 1000)])
+@pytest.mark.parametrize("envs,steps", [(4096, 2048), (512, 128), (3, 5000), (7, 1000),
+                                        (80, 32), (48, 32)])
 def test_gae_full_size_vs_c_oracle(dev, envs, steps):
     """BASELINE sizes (4096x2048 = 8.4M transitions) against the C oracle, both paths."""
     from tianshou_amd.policy.base import gae_device
@@ -185,7 +186,8 @@ def test_ret_rms_update(dev):
         assert rms.count == host.count
 
 
-@pytest.mark.parametrize("envs,steps", [(4096, 2048), (64, 4096), (256, 128), (96, 512)])
+@pytest.mark.parametrize("envs,steps", [(4096, 2048), (64, 4096), (256, 128), (96, 512),
+                                        (80, 32), (48, 32)])
 @pytest.mark.parametrize("scaled", [False, True])
 def test_gae_staged_rows_kernel(dev, envs, steps, scaled, monkeypatch):
     """The LDS-staged row kernel (f32 outputs only, rows a multiple of the 2048-transition

@@ -184,79 +184,20 @@ constexpr int SL_W2A = 0, SL_B2A = SL_W2A + H * H, SL_W2C = SL_B2A + H, SL_B2C =
               SL_W3A = SL_B2C + H, SL_B3A = SL_W3A + AMAX * H, SL_W3C = SL_B3A + AMAX,
               SL_B3C = SL_W3C + H, SL_F = SL_B3C + 4;
 constexpr int SL_D = 4 + AMAX;  // clip, vf, count, 0, d/dlog_std[AMAX]
-// Four waves per workgroup, one workgroup per CU.  Measured round 3 (tools/mlp_kernel_bench.py
-// --only tail, both nets + reduce, 262144 rows; per-phase s_memtime stamps with TAIL_TRACE):
-// round 2's kernel 234 us (actor tile 29.7k cycles: head + loss 9.5k of them, 89
-// ds_bpermute per tile); bf16x6 weight gradients (f32 MFMA at 1/16 of the bf16 rate before)
-// 226; + deferred column sums and H1 kept live 210-213 (actor tile 24.4k: head + loss 7.7k,
-// ~1.5k instructions issued one after the other by the only wave of the SIMD).  Two waves
-// per SIMD did not pay in that form: 8 waves each with its own accumulators spill (256 VGPRs)
-// 220-222 us; a lockstep form in which the 8 waves of a round share the weight-gradient MFMAs
-// through LDS (2 accumulator tiles per wave, 8 workgroup barriers per round) still spills 20
-// VGPRs and ran 226-229 us.  What the kernel keeps from those measurements: the column sums
-// over the minibatch rows (db2, db3, dlog_std, the critic's dW3) accumulate per lane across
-// the wave's tiles and are reduced across lanes once at the end (a 16-shuffle reduce-scatter
-// per tile and sum before: 89 ds_bpermute chains per actor tile); H1 stays in registers
-// through the tile; the next tile's inputs are prefetched into registers during the current
-// one (one wave per SIMD: nothing else hides the loads).
-// diagnostic builds only (tools/mlp_kernel_bench.py --tail-trace): s_memtime stamps per wave
-// and tile at the phase boundaries, stored behind the workspace slabs
-#ifndef TAIL_TRACE
-#define TAIL_TRACE 0
-#endif
-constexpr int TAIL_NSTAMP = 8;
-constexpr int TAIL_TRACE_TILES = 8;  // first tiles of each wave
-constexpr int TAIL_NW = 4;
-constexpr int TAIL_TPB = 64 * TAIL_NW;
-
 struct TailWeights {
     const float *w2a, *b2a, *w2c, *b2c, *w3a, *b3a, *w3c, *b3c, *log_std;
 };
 
-// Sum of v[16] (one 32-feature tile in C layout) over the 32 lanes of each half-wave.
-// Reduce-scatter: afterwards lane l holds the sum of register R(l) = 8*b4+4*b3+2*b2+b1 (the
-// lane's bits 4..1) for feature rho(R)+4h; lanes l and l^1 hold the same value.
-__device__ __forceinline__ float rs_sum16(const float (&v)[16], int l) {
-    float a8[8], a4[4], a2[2];
-    const bool b4 = l & 16, b3 = l & 8, b2 = l & 4, b1 = l & 2;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const float keep = b4 ? v[i + 8] : v[i], send = b4 ? v[i] : v[i + 8];
-        a8[i] = keep + __shfl_xor(send, 16, 64);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const float keep = b3 ? a8[i + 4] : a8[i], send = b3 ? a8[i] : a8[i + 4];
-        a4[i] = keep + __shfl_xor(send, 8, 64);
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const float keep = b2 ? a4[i + 2] : a4[i], send = b2 ? a4[i] : a4[i + 2];
-        a2[i] = keep + __shfl_xor(send, 4, 64);
-    }
-    const float keep = b1 ? a2[1] : a2[0], send = b1 ? a2[0] : a2[1];
-    float a1 = keep + __shfl_xor(send, 2, 64);
-    return a1 + __shfl_xor(a1, 1, 64);
-}
-__device__ __forceinline__ int rs_reg(int l) {
-    return 8 * ((l >> 4) & 1) + 4 * ((l >> 3) & 1) + 2 * ((l >> 2) & 1) + ((l >> 1) & 1);
-}
-
-// Workgroups with blockIdx.y == 0 run the actor half (layer 2, mu head, clipped surrogate,
-// backward), blockIdx.y == 1 the critic half (layer 2, value head, value loss, backward):
-// the loss gradient w.r.t. mu depends only on actor outputs and w.r.t. the value only on
-// critic outputs, so the halves are independent and each keeps half the live state.
-// half-tile transpose scratch: [64 features][16 rows]; stride 20 floats (80 B) keeps the
+// The actor (NET 0: layer 2, mu head, clipped surrogate, backward) and the critic (NET 1:
+// layer 2, value head, value loss, backward) run as two launches: the loss gradient w.r.t.
+// mu depends only on actor outputs and w.r.t. the value only on critic outputs.
+// Feature-major weight-gradient scratch [feature][16 rows]: stride 20 floats (80 B) keeps the
 // 8-row float4 reads of the bf16x6 weight gradients 16-byte aligned and spreads the 16 lanes
-// of a read phase over all 16 bank groups (5 is odd)
+// of a read phase over all 16 bank groups (5 is odd).
 constexpr int SH = 20;
-constexpr int T_B2 = 0, T_B3 = T_B2 + H, T_W3C = T_B3 + AMAX, T_VAR = T_W3C + H,
-              T_LS = T_VAR + AMAX, T_IV = T_LS + AMAX, T_IV2 = T_IV + AMAX,
-              T_SCR = T_IV2 + AMAX, T_END = T_SCR + TAIL_NW * 2 * H * SH;
-static_assert(T_END >= TAIL_NW * 32 * H, "fold scratch");
 
-// The chain products (layer 2, mu head, dZ2 = W3^T dMu, dZ1 = W2^T dZ2) run as bf16x6 (x6.h):
-// their activation operand is the C-layout tile itself -- registers 8s..8s+7 of a 32x32 tile
+// 32-row images (process_fn's eval_tail_kernel): the chain products (layer 2, mu head) run as
+// bf16x6 (x6.h): their activation operand is the C-layout tile itself -- registers 8s..8s+7 of a 32x32 tile
 // are the 8 k of k-step s on each lane half, element j of half h being feature
 // 16s + 8(j>>2) + 4h + (j&3) of the tile -- split in registers, and the weight operand is an
 // LDS image of the matrix, split once per workgroup into 3 bf16 planes whose rows hold the
@@ -266,7 +207,6 @@ constexpr int IMG_W2 = 0;                              // W2   [64 out][64 in]
 constexpr int IMG_W2T = IMG_W2 + NPL * 2 * H * 64;     // W2^T [64 in][64 out]
 constexpr int IMG_W3 = IMG_W2T + NPL * 2 * H * 64;     // W3   [32 act][64]      (actor)
 constexpr int IMG_W3T = IMG_W3 + NPL * 2 * AMAX * 64;  // W3^T [64][32 act]      (actor)
-constexpr int IMG_ACTOR = IMG_W3T + NPL * 1 * H * 64, IMG_CRITIC = IMG_W3;
 
 __device__ __forceinline__ int img_off(int p, int kc, int row, int q, int nkc, int rows) {
     return (p * nkc + kc) * rows * 64 + sw_off(row, q);
@@ -293,10 +233,6 @@ __device__ __forceinline__ void build_img_n(char* img, int rows, int nkc, F val)
     }
 }
 
-template <typename F>
-__device__ __forceinline__ void build_img(char* img, int rows, int nkc, F val) {
-    build_img_n<TAIL_TPB>(img, rows, nkc, val);
-}
 
 // The 3 planes of one operand fragment: row `row`, 32-k chunk kc, k-step s, lane half h.
 __device__ __forceinline__ void ld_img(const char* img, int nkc, int rows, int kc, int row,
@@ -350,524 +286,26 @@ __device__ __forceinline__ void acc_wgrad_x6(f32x16 (&g)[NOT][NFT], const float*
     }
 }
 
-// Write a C-layout activation (NT32 tiles of 32 features) rows [16*half, 16*half+16) into
-// feature-major scratch [feature][row - 16*half].
-template <int NT32>
-__device__ __forceinline__ void put_half(float* S, const float (&v)[NT32][16], int c, int h,
-                                         int half) {
-    if ((c >> 4) == half) {
-#pragma unroll
-        for (int it = 0; it < NT32; ++it)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) S[(32 * it + rho(r) + 4 * h) * SH + (c & 15)] = v[it][r];
-    }
-}
-
 __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// one workgroup per CU: the bf16x6 weight images (72 KB actor / 48 KB critic) + scratch
-template <int NET>
-__global__ __launch_bounds__(TAIL_TPB, 1) void ppo_tail_kernel(
-    const float* __restrict__ h1f, int64_t n, const int64_t* __restrict__ idx, TailWeights wt,
-    const float* __restrict__ act, const float* __restrict__ logp_old,
-    const float* __restrict__ adv, const float* __restrict__ ret, const float* __restrict__ v_s,
-    const double* __restrict__ adv_sums, TailParams p, float* __restrict__ dz1,
-    float* __restrict__ slab_f, double* __restrict__ slab_d) {
-#if TAIL_TRACE
-    uint64_t* trace = reinterpret_cast<uint64_t*>(
-        (reinterpret_cast<uintptr_t>(slab_d + (int64_t)gridDim.x * SL_D) + 255) & ~uintptr_t(255)) +
-        (int64_t)NET * gridDim.x * TAIL_NW * TAIL_TRACE_TILES * TAIL_NSTAMP;
-    int tr_tile = 0;
-#define TAIL_STAMP(i)                                                                       \
-    {                                                                                       \
-        __builtin_amdgcn_sched_barrier(0);                                                  \
-        const uint64_t ts_ = __builtin_amdgcn_s_memtime();                                  \
-        if (l == 0 && tr_tile < TAIL_TRACE_TILES)                                           \
-            trace[(((int64_t)blockIdx.x * TAIL_NW + w) * TAIL_TRACE_TILES + tr_tile) *      \
-                      TAIL_NSTAMP + (i)] = ts_;                                             \
-        __builtin_amdgcn_sched_barrier(0);                                                  \
-    }
-#else
-#define TAIL_STAMP(i)
-#endif
-    __shared__ __attribute__((aligned(16))) float sm[T_END];
-    __shared__ __attribute__((aligned(16))) char img[NET == 0 ? IMG_ACTOR : IMG_CRITIC];
-    __shared__ double sred[TAIL_NW][SL_D];
-    const int t = threadIdx.x;
-    const int w = t >> 6, l = t & 63, h = l >> 5, c = l & 31;
-    const int A = p.A;
-    constexpr bool actor = NET == 0;
-    constexpr int net = NET;
-    {
-        const float* w2 = actor ? wt.w2a : wt.w2c;
-        const float* b2 = actor ? wt.b2a : wt.b2c;
-        build_img(img + IMG_W2, H, 2, [=](int r, int k) { return w2[r * H + k]; });
-        build_img(img + IMG_W2T, H, 2, [=](int r, int k) { return w2[k * H + r]; });
-        if (t < H) sm[T_B2 + t] = b2[t];
-        if (actor) {
-            const float* w3 = wt.w3a;
-            build_img(img + IMG_W3, AMAX, 2,
-                      [=](int r, int k) { return r < A ? w3[r * H + k] : 0.0f; });
-            build_img(img + IMG_W3T, H, 1,
-                      [=](int r, int k) { return k < A ? w3[k * H + r] : 0.0f; });
-            if (t < AMAX) {
-                sm[T_B3 + t] = t < A ? wt.b3a[t] : 0.0f;
-                const float sig = t < A ? expf(wt.log_std[t]) : 1.0f;
-                sm[T_VAR + t] = sig * sig;
-                sm[T_LS + t] = logf(sig);
-                // reciprocals once per workgroup: the per-row terms multiply (a correctly
-                // rounded f32 division is ~10 VALU; the products differ from the divisions
-                // by at most one rounding)
-                sm[T_IV + t] = 1.0f / (sig * sig);
-                sm[T_IV2 + t] = 1.0f / (2.0f * (sig * sig));
-            }
-        } else if (t < H) {
-            sm[T_W3C + t] = wt.w3c[t];
-        }
-    }
-    __syncthreads();
-    float* S1 = sm + T_SCR + w * 2 * H * SH;
-    float* S2 = S1 + H * SH;
-    const float b3c = wt.b3c[0];
-    float mean_f = 0.0f, std_f = 1.0f;
-    if (actor && p.norm_adv) {
-        const double nn = 1.0 / p.inv_b64;
-        const double m = adv_sums[0] / nn;
-        const double var = (adv_sums[1] - adv_sums[0] * m) / (nn - 1.0);
-        mean_f = (float)m;
-        std_f = (float)sqrt(var > 0.0 ? var : 0.0);
-    }
-
-    // persistent per-wave accumulators
-    f32x16 gW2[2][2], gW3[1][actor ? 2 : 1];
-#pragma unroll
-    for (int i = 0; i < (actor ? 2 : 1); ++i) gW3[0][i] = zero16();
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) gW2[i][j] = zero16();
-    float gb2[2] = {0.f, 0.f}, gw3c[2] = {0.f, 0.f};
-    float gb3 = 0.f;
-    double dls_acc = 0.0, loss_acc = 0.0, cnt_acc = 0.0;
-    // per-lane partial column sums (lane = row c, register r = feature rho(r) + 4h)
-    float gb2_l[2][16], gw3c_l[2][16], gb3_l[16], dls_l[16], gv_l = 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        gb2_l[0][r] = gb2_l[1][r] = gw3c_l[0][r] = gw3c_l[1][r] = 0.f;
-        gb3_l[r] = dls_l[r] = 0.f;
-    }
-
-    const int64_t ntiles = (n + 31) / 32;
-    const int64_t gw = (int64_t)blockIdx.x * TAIL_NW + w, nw = (int64_t)gridDim.x * TAIL_NW;
-    // Software pipeline over this wave's tiles (one wave per SIMD: nothing else hides
-    // latency): while tile bt computes, the NEXT tile's H1 fragments and gathered per-row
-    // inputs are in flight, and the index of the tile after that.  Loads are branch-free:
-    // rows past n read row 0 / tile 0 and are discarded by `live`.  Two tiles of inputs in
-    // flight (a second register stage, 433 / 321 VGPR+AGPR) measured 1-2 % slower (round 2):
-    // past one tile ahead the dependent MFMA / tanh chain of the tile, not the loads, paces it.
-    float nh1[2][16], nav[16];
-    float nx0 = 0.f, nx1 = 0.f;  // actor: logp_old, adv; critic: ret, v_s
-    auto row_index = [&](int64_t bt_) -> int64_t {
-        const int64_t br_ = bt_ * 32 + c;
-        return (bt_ < ntiles && br_ < n) ? (idx ? idx[br_] : br_) : 0;
-    };
-    // per-row inputs addressed by 32-bit element offsets from the (uniform) base pointers:
-    // one VGPR per address instead of two (the 16 act gathers were spilling)
-    const uint32_t A_u = (uint32_t)A;
-#define TAIL_PREFETCH(BT, J)                                                                \
-    {                                                                                       \
-        const int64_t bts_ = (BT) < ntiles ? (BT) : 0;                                      \
-        _Pragma("unroll") for (int i_ = 0; i_ < 2; ++i_) {                                  \
-            const float4* src_ = reinterpret_cast<const float4*>(                           \
-                h1f + ((bts_ * NT + 2 * net + i_) * 64 + l) * 16);                          \
-            _Pragma("unroll") for (int q_ = 0; q_ < 4; ++q_) {                              \
-                const float4 v_ = src_[q_];                                                 \
-                nh1[i_][4 * q_] = v_.x;                                                     \
-                nh1[i_][4 * q_ + 1] = v_.y;                                                 \
-                nh1[i_][4 * q_ + 2] = v_.z;                                                 \
-                nh1[i_][4 * q_ + 3] = v_.w;                                                 \
-            }                                                                               \
-        }                                                                                   \
-        const uint32_t j32_ = (uint32_t)(J);                                                \
-        if constexpr (actor) {                                                              \
-            const uint32_t ab_ = j32_ * A_u;                                                \
-            _Pragma("unroll") for (int r_ = 0; r_ < 16; ++r_) {                             \
-                const uint32_t a_ = (uint32_t)(rho(r_) + 4 * h);                            \
-                nav[r_] = act[ab_ + (a_ < A_u ? a_ : 0u)];                                  \
-            }                                                                               \
-            nx0 = logp_old[j32_];                                                           \
-            nx1 = adv[j32_];                                                                \
-        } else {                                                                            \
-            nx0 = ret[j32_];                                                                \
-            nx1 = p.value_clip ? v_s[j32_] : 0.0f;                                          \
-        }                                                                                   \
-    }
-    int64_t j_next = row_index(gw);
-    TAIL_PREFETCH(gw, j_next)
-    j_next = row_index(gw + nw);
-    for (int64_t bt = gw; bt < ntiles; bt += nw) {
-        const int64_t brow = bt * 32 + c;
-        const bool live = brow < n;
-        TAIL_STAMP(0)
-        // ---- this tile's inputs (prefetched), then the next tile's loads --------------------
-        float h1[2][16], av[16];
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) h1[i][r] = nh1[i][r];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) av[r] = nav[r];
-        const float x0 = nx0, x1 = nx1;
-        {
-            const int64_t jn = j_next;
-            TAIL_PREFETCH(bt + nw, jn)
-            j_next = row_index(bt + 2 * nw);
-        }
-        // ---- layer 2 -----------------------------------------------------------------------
-        TAIL_STAMP(1)
-        float h2[2][16];
-        {
-            f32x16 z0 = zero16(), z1 = zero16();
-#pragma unroll
-            for (int kc = 0; kc < 2; ++kc)
-#pragma unroll
-                for (int s = 0; s < 2; ++s) {
-                    bf16x8 b[NPL], a[NPL];
-                    split_frag(h1[kc], s, b);
-                    ld_img(img + IMG_W2, 2, H, kc, c, s, h, a);
-                    z0 = mfma6(a, b, z0);
-                    ld_img(img + IMG_W2, 2, H, kc, 32 + c, s, h, a);
-                    z1 = mfma6(a, b, z1);
-                }
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                h2[0][r] = tanh_nb(z0[r] + sm[T_B2 + rho(r) + 4 * h]);
-                h2[1][r] = tanh_nb(z1[r] + sm[T_B2 + 32 + rho(r) + 4 * h]);
-            }
-        }
-        float dz2[2][16];
-        if constexpr (actor) {
-            // ---- mu head + clipped surrogate ----------------------------------------------
-            TAIL_STAMP(2)
-            f32x16 mu = zero16();
-#pragma unroll
-            for (int kc = 0; kc < 2; ++kc)
-#pragma unroll
-                for (int s = 0; s < 2; ++s) {
-                    bf16x8 b[NPL], a[NPL];
-                    split_frag(h2[kc], s, b);
-                    ld_img(img + IMG_W3, 2, AMAX, kc, c, s, h, a);
-                    mu = mfma6(a, b, mu);
-                }
-            float diff[16];
-            float lp = 0.0f;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                // branch-free (the LDS vectors are padded to AMAX): a branch per element
-                // made 16 dependent LDS round trips
-                const int a = rho(r) + 4 * h;
-                const bool in = a < A && live;
-                const float d = av[r] - (mu[r] + sm[T_B3 + a]);
-                const float term = -(d * d) * sm[T_IV2 + a] - sm[T_LS + a] - LOG_SQRT_2PI;
-                diff[r] = in ? d : 0.0f;
-                lp += in ? term : 0.0f;
-            }
-            const float logp = lp + __shfl_xor(lp, 32, 64);
-            float g_logp = 0.0f;
-            if (live) {
-                float an = x1;
-                if (p.norm_adv) an = (an - mean_f) / (std_f + p.adv_eps);
-                const float ratio = expf(logp - x0);
-                const float surr1 = ratio * an;
-                const float rc = fminf(fmaxf(ratio, p.lo), p.hi);
-                const float surr2 = rc * an;
-                const float in_rng = (ratio >= p.lo && ratio <= p.hi) ? 1.0f : 0.0f;
-                float clip1, d1;
-                if (surr1 < surr2) {
-                    clip1 = surr1;
-                    d1 = an;
-                } else if (surr2 < surr1) {
-                    clip1 = surr2;
-                    d1 = in_rng * an;
-                } else {
-                    clip1 = surr1;
-                    d1 = 0.5f * an + 0.5f * in_rng * an;
-                }
-                float obj = clip1, dobj = d1;
-                if (p.use_dual && an < 0.0f) {
-                    const float tt = p.dual * an;
-                    if (clip1 > tt) {
-                        obj = clip1;
-                    } else if (clip1 < tt) {
-                        obj = tt;
-                        dobj = 0.0f;
-                    } else {
-                        obj = clip1;
-                        dobj = 0.5f * d1;
-                    }
-                }
-                g_logp = (float)(-(double)dobj * (double)ratio * p.inv_b64);
-                if (h == 0) {
-                    loss_acc += -(double)obj;
-                    cnt_acc += 1.0;
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            float dmu[1][16], dls[16];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int a = rho(r) + 4 * h;
-                const float iv = sm[T_IV + a];
-                dmu[0][r] = g_logp * diff[r] * iv;
-                dls[r] = (a < A && live) ? g_logp * (diff[r] * diff[r] * iv - 1.0f) : 0.0f;
-            }
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                dls_l[r] += dls[r];
-                gb3_l[r] += dmu[0][r];
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            // dW3a = dMu^T . H2a over the 32 rows, two half passes
-            TAIL_STAMP(3)
-#pragma unroll
-            for (int half = 0; half < 2; ++half) {
-                __builtin_amdgcn_sched_barrier(0);
-                wave_sync_lds();
-                put_half<1>(S1, dmu, c, h, half);
-                put_half<2>(S2, h2, c, h, half);
-                wave_sync_lds();
-                acc_wgrad_x6<1, 2>(gW3, S1, S2, c, h);
-            }
-            // dZ2 = (W3a^T dMu) * (1 - H2^2)
-            TAIL_STAMP(4)
-            {
-                bf16x8 bd0[NPL], bd1[NPL];
-                split_frag(dmu[0], 0, bd0);
-                split_frag(dmu[0], 1, bd1);
-#pragma unroll
-                for (int ft = 0; ft < 2; ++ft) {
-                    f32x16 d = zero16();
-                    bf16x8 a[NPL];
-                    ld_img(img + IMG_W3T, 1, H, 0, 32 * ft + c, 0, h, a);
-                    d = mfma6(a, bd0, d);
-                    ld_img(img + IMG_W3T, 1, H, 0, 32 * ft + c, 1, h, a);
-                    d = mfma6(a, bd1, d);
-#pragma unroll
-                    for (int r = 0; r < 16; ++r)
-                        dz2[ft][r] = d[r] * (1.0f - h2[ft][r] * h2[ft][r]);
-                }
-            }
-        } else {
-            // ---- value head + value loss ----------------------------------------------------
-            float vpart = 0.0f;
-#pragma unroll
-            for (int it = 0; it < 2; ++it)
-#pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    vpart += sm[T_W3C + 32 * it + rho(r) + 4 * h] * h2[it][r];
-            const float value = vpart + __shfl_xor(vpart, 32, 64) + b3c;
-            float gv = 0.0f;
-            if (live) {
-                const float rt = x0;
-                float dv, vf;
-                if (p.value_clip) {
-                    const float vs = x1;
-                    const float dlt = value - vs;
-                    const float dcl = fminf(fmaxf(dlt, -p.eps_clip), p.eps_clip);
-                    const float vcl = vs + dcl;
-                    const float e1 = rt - value, e2 = rt - vcl;
-                    const float vf1 = e1 * e1, vf2 = e2 * e2;
-                    const float g1 = -2.0f * e1;
-                    const float g2 = (dlt >= -p.eps_clip && dlt <= p.eps_clip) ? -2.0f * e2 : 0.0f;
-                    if (vf1 > vf2) {
-                        vf = vf1;
-                        dv = g1;
-                    } else if (vf2 > vf1) {
-                        vf = vf2;
-                        dv = g2;
-                    } else {
-                        vf = vf1;
-                        dv = 0.5f * g1 + 0.5f * g2;
-                    }
-                } else {
-                    const float e1 = rt - value;
-                    vf = e1 * e1;
-                    dv = -2.0f * e1;
-                }
-                gv = (float)((double)p.vf_coef * (double)dv * p.inv_b64);
-                if (h == 0) loss_acc += (double)vf;
-            }
-            {
-#pragma unroll
-                for (int it = 0; it < 2; ++it)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) gw3c_l[it][r] += gv * h2[it][r];
-                gv_l += h == 0 ? gv : 0.0f;
-            }
-#pragma unroll
-            for (int ft = 0; ft < 2; ++ft)
-#pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    dz2[ft][r] = gv * sm[T_W3C + 32 * ft + rho(r) + 4 * h] *
-                                 (1.0f - h2[ft][r] * h2[ft][r]);
-        }
-        // ---- dZ1 = (W2^T dZ2) * (1 - H1^2) -> HBM (row-major [n][128]) -------------------
-        TAIL_STAMP(5)
-        f32x16 dd0 = zero16(), dd1 = zero16();
-#pragma unroll
-        for (int kc = 0; kc < 2; ++kc)
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                bf16x8 b[NPL], a[NPL];
-                split_frag(dz2[kc], s, b);
-                ld_img(img + IMG_W2T, 2, H, kc, c, s, h, a);
-                dd0 = mfma6(a, b, dd0);
-                ld_img(img + IMG_W2T, 2, H, kc, 32 + c, s, h, a);
-                dd1 = mfma6(a, b, dd1);
-            }
-#pragma unroll
-        for (int ft = 0; ft < 2; ++ft) {
-            __builtin_amdgcn_sched_barrier(0);
-            const f32x16 d = ft == 0 ? dd0 : dd1;
-            if (live) {
-                float v[16];
-#pragma unroll
-                for (int r = 0; r < 16; ++r) v[r] = d[r] * (1.0f - h1[ft][r] * h1[ft][r]);
-                float* o = dz1 + brow * HC + 64 * net + 32 * ft + 4 * h;
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    *reinterpret_cast<float4*>(o + 8 * q) =
-                        make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
-            }
-        }
-        // ---- db2, dW2 = dZ2^T . H1 ---------------------------------------------------------
-        TAIL_STAMP(6)
-#pragma unroll
-        for (int ot = 0; ot < 2; ++ot) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) gb2_l[ot][r] += dz2[ot][r];
-        }
-#pragma unroll
-        for (int half = 0; half < 2; ++half) {
-            __builtin_amdgcn_sched_barrier(0);
-            wave_sync_lds();
-            put_half<2>(S1, dz2, c, h, half);
-            put_half<2>(S2, h1, c, h, half);
-            wave_sync_lds();
-            acc_wgrad_x6<2, 2>(gW2, S1, S2, c, h);
-        }
-        TAIL_STAMP(7)
-#if TAIL_TRACE
-        ++tr_tile;
-#endif
-    }
-#undef TAIL_PREFETCH
-    // the deferred column sums: one reduce-scatter each (rs_sum16's lane ownership)
-#pragma unroll
-    for (int it = 0; it < 2; ++it) {
-        gb2[it] = rs_sum16(gb2_l[it], l);
-        if constexpr (!actor) gw3c[it] = rs_sum16(gw3c_l[it], l);
-    }
-    if constexpr (actor) {
-        gb3 = rs_sum16(gb3_l, l);
-        dls_acc = (double)rs_sum16(dls_l, l);
-    } else {
-        float gsum = gv_l;
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) gsum += __shfl_xor(gsum, off, 64);
-        gb3 = gsum;
-    }
-    // ---- fold the TAIL_NW waves (fixed order) into this workgroup's slab ---------------------
-    __syncthreads();
-    float* red = sm;  // T_END >= TAIL_NW * 32 * 64 floats
-    auto wsum = [&](int stride, int i) {
-        float v = red[i];
-#pragma unroll
-        for (int ww = 1; ww < TAIL_NW; ++ww) v += red[ww * stride + i];
-        return v;
-    };
-    float* slab = slab_f + (int64_t)blockIdx.x * SL_F;
-    auto fold = [&](const f32x16 (&g)[2], int o0, int base) {
-        // rows [o0, o0+32) of a [rows][64] matrix held as C layout (o = rho(r)+4h, f = 32ft+c)
-#pragma unroll
-        for (int ft = 0; ft < 2; ++ft)
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-                red[w * 32 * H + (rho(r) + 4 * h) * H + 32 * ft + c] = g[ft][r];
-        __syncthreads();
-        for (int i = t; i < 32 * H; i += TAIL_TPB)
-            slab[base + o0 * H + i] = wsum(32 * H, i);
-        __syncthreads();
-    };
-    const int base2 = actor ? SL_W2A : SL_W2C;
-    fold(gW2[0], 0, base2);
-    fold(gW2[1], 32, base2);
-    if constexpr (actor) fold(gW3[0], 0, SL_W3A);
-    // vectors: lanes with bit0 == 0 own feature rho(rs_reg(l)) + 4h of each tile
-    const int fr = rho(rs_reg(l)) + 4 * h;
-    constexpr int VW = 3 * H + 4;
-    if ((l & 1) == 0) {
-#pragma unroll
-        for (int it = 0; it < 2; ++it) {
-            red[w * VW + 32 * it + fr] = gb2[it];
-            red[w * VW + H + 32 * it + fr] = gw3c[it];
-        }
-        red[w * VW + 2 * H + fr] = gb3;  // actor: db3a[a]; critic: lane 0's gb3 is db3c
-    }
-    __syncthreads();
-    if (t < VW) {
-        const float v = wsum(VW, t);
-        if (t < H) {
-            slab[(actor ? SL_B2A : SL_B2C) + t] = v;
-        } else if (t < 2 * H) {
-            if (!actor) slab[SL_W3C + t - H] = v;
-        } else if (t < 2 * H + AMAX) {
-            if (actor) slab[SL_B3A + t - 2 * H] = v;
-        }
-    }
-    if (!actor && t == 0) {
-        // every lane of a critic wave holds the same gb3 (full-wave sum)
-        slab[SL_B3C] = wsum(VW, 2 * H);
-    }
-    loss_acc = wave_sum(loss_acc);
-    cnt_acc = wave_sum(cnt_acc);
-    if (actor && (l & 1) == 0) sred[w][4 + fr] = dls_acc;
-    if (l == 0) {
-        sred[w][0] = loss_acc;
-        sred[w][1] = cnt_acc;
-    }
-    __syncthreads();
-    double* sd = slab_d + (int64_t)blockIdx.x * SL_D;
-    if (t < SL_D) {
-        double v = sred[0][t];
-#pragma unroll
-        for (int ww = 1; ww < TAIL_NW; ++ww) v += sred[ww][t];
-        if (actor) {
-            if (t == 0) sd[0] = v;            // clip sum
-            else if (t == 1) sd[2] = v;       // row count
-            else if (t >= 4) sd[t] = v;       // d/dlog_std
-        } else if (t == 0) {
-            sd[1] = v;                        // vf sum
-        }
-    }
-    if (actor && t == 3) sd[3] = 0.0;
-}
-
 // ---------------------------------------------------------------------------------------
-// ppo_tail16_kernel: the same tail (layers 2-3, loss, backward to dZ1, layer-2/3 weight
-// gradients) on 16-row tiles at TWO waves per SIMD.  The 32-row kernel above runs one wave
-// per SIMD (505 / 384 VGPR+AGPR): its waves issue 54-56 % of their cycles and wait on their
-// own dependent MFMA -> tanh -> MFMA chains the rest (profiles/r03_learn_sq_pmc.txt), and a
-// quarter of its vector instructions move values between VGPRs and AGPRs.  Here a wave owns
-// 16 minibatch rows at a time: the chain products run on v_mfma_f32_16x16x32_bf16 (bf16x6,
-// 16 cycles each, the same matrix-core time per row), so the per-tile activations take half
-// the registers and the kernel fits 256 (8 waves per workgroup, one workgroup per CU, the
-// weight images shared by all 8).  The weight gradients still accumulate per wave on
-// v_mfma_f32_32x32x16_bf16 over the tile's 16 rows (acc_wgrad_x6, one K step).
+// ppo_tail16_kernel: layers 2-3 of one net, the clipped-surrogate / value loss, the backward
+// down to dZ1 and the layer-2/3 weight gradients, on 16-row tiles at TWO waves per SIMD.
+// Round 5 replaced the round-2..4 32-row kernel, which ran one wave per SIMD (505 / 384
+// VGPR+AGPR): its waves issued 54-56 % of their cycles and waited on their own dependent
+// MFMA -> tanh -> MFMA chains the rest (profiles/r03_learn_sq_pmc.txt), and a quarter of its
+// vector instructions moved values between VGPRs and AGPRs.  Here a wave owns 16 minibatch
+// rows at a time: the chain products run on v_mfma_f32_16x16x32_bf16 (bf16x6, 16 cycles
+// each, the same matrix-core time per row), so the per-tile activations take half the
+// registers and the kernel fits 256 (8 waves per workgroup, one workgroup per CU, the weight
+// images shared by all 8; no AGPR moves).  The weight gradients accumulate per wave on
+// v_mfma_f32_32x32x16_bf16 over the tile's 16 rows (acc_wgrad_x6, one K step).  Measured
+// (tools/mlp_kernel_bench.py --only tail, both nets + reduce, 262144 rows, A/B in one call,
+// profiles/r05_tail16_ab.log): 188-197 vs 210-222 us for the 32-row kernel.
 //
 // Layouts (lane l: row b = l & 15 of the tile, lane group g = l >> 4):
 //   H1: the 16 layer-1 features Fh1(g, r) = 32 (g >> 1) + rho(r) + 4 (g & 1), r = 0..15 --
@@ -1811,16 +1249,10 @@ TailParams make_tail_params(const tsrl_ppo_params& q, int A) {
     return p;
 }
 
-// 1: the 16-row-tile tail at two waves per SIMD (ppo_tail16_kernel); 0: the 32-row kernel
-#ifndef TAIL16
-#define TAIL16 1
-#endif
-
 int tail_grid(int64_t n) {
     // workgroups per net (one launch per net), one resident per CU
-    const int64_t tiles = TAIL16 ? (n + 15) / 16 : (n + 31) / 32;
-    const int64_t waves = TAIL16 ? T16_NW : TAIL_NW;
-    const int64_t g = (tiles + waves - 1) / waves;
+    const int64_t tiles = (n + 15) / 16;
+    const int64_t g = (tiles + T16_NW - 1) / T16_NW;
     return (int)std::min<int64_t>(g, 256);
 }
 
@@ -1860,8 +1292,7 @@ extern "C" int64_t tsrl_mlp_frag_floats(int64_t n) {
 
 extern "C" int64_t tsrl_ppo_tail_workspace_bytes(int64_t n) {
     const int g = tail_grid(n);
-    return (int64_t)g * (SL_F * (int64_t)sizeof(float) + SL_D * (int64_t)sizeof(double)) + 256 +
-           (TAIL_TRACE ? 256 + 2 * (int64_t)g * TAIL_NW * TAIL_TRACE_TILES * TAIL_NSTAMP * 8 : 0);
+    return (int64_t)g * (SL_F * (int64_t)sizeof(float) + SL_D * (int64_t)sizeof(double)) + 256;
 }
 
 static int ppo_tail_impl(const float* h1frag, int64_t n, const int64_t* idx,
@@ -1890,21 +1321,12 @@ static int ppo_tail_impl(const float* h1frag, int64_t n, const int64_t* idx,
     TailWeights w{wt->w2a, wt->b2a, wt->w2c, wt->b2c, wt->w3a, wt->b3a, wt->w3c, wt->b3c,
                   wt->log_std};
     const TailParams tp = make_tail_params(prm, (int)act_dim);
-    if ((stages & 1) && TAIL16) {
+    if (stages & 1) {
         hipLaunchKernelGGL(ppo_tail16_kernel<0>, dim3(g), dim3(T16_TPB), 0, as_stream(stream),
                            h1frag, n, idx, w, act, logp_old, adv, ret, v_s, adv_sums, tp, dz1,
                            slab_f, slab_d);
         TSRL_LAUNCH_CHECK("tsrl_ppo_tail(actor)");
         hipLaunchKernelGGL(ppo_tail16_kernel<1>, dim3(g), dim3(T16_TPB), 0, as_stream(stream),
-                           h1frag, n, idx, w, act, logp_old, adv, ret, v_s, adv_sums, tp, dz1,
-                           slab_f, slab_d);
-        TSRL_LAUNCH_CHECK("tsrl_ppo_tail");
-    } else if (stages & 1) {
-        hipLaunchKernelGGL(ppo_tail_kernel<0>, dim3(g), dim3(TAIL_TPB), 0, as_stream(stream),
-                           h1frag, n, idx, w, act, logp_old, adv, ret, v_s, adv_sums, tp, dz1,
-                           slab_f, slab_d);
-        TSRL_LAUNCH_CHECK("tsrl_ppo_tail(actor)");
-        hipLaunchKernelGGL(ppo_tail_kernel<1>, dim3(g), dim3(TAIL_TPB), 0, as_stream(stream),
                            h1frag, n, idx, w, act, logp_old, adv, ret, v_s, adv_sums, tp, dz1,
                            slab_f, slab_d);
         TSRL_LAUNCH_CHECK("tsrl_ppo_tail");

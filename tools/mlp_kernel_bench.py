@@ -30,9 +30,6 @@ def main():
                     help="minibatch rows contiguous (no permutation gather)")
     ap.add_argument("--sorted", action="store_true",
                     help="random minibatch rows, gathered in ascending row order")
-    ap.add_argument("--tail-trace", type=int, default=0,
-                    help="the library is a TAIL_TRACE=1 build with this many waves per workgroup: "
-                         "report the tail's per-phase s_memtime cycles")
     ap.add_argument("--eval-chunk", type=int, default=0,
                     help="rows per process_fn evaluation chunk (FusedActorCritic.EVAL_CHUNK)")
     a = ap.parse_args()
@@ -121,9 +118,6 @@ def main():
     def evaluate():  # process_fn: V(s) + logp_old of one 2M-row chunk (l1 + eval tail)
         fm.evaluate(obs_v[:EV], act[:EV])
 
-    if a.tail_trace:
-        tail_trace_report(tail, ws, B, a.tail_trace)
-        return
     for name, fn, flop in (("l1_fwd", l1, flop_l1), ("l1_fwd_x6(+split)", l1x6, flop_l1),
                            ("l1_x6_staged(rows)", l1x6_staged, flop_l1),
                            ("tail(+reduce)", tail, flop_tail),
@@ -144,43 +138,6 @@ def main():
         us = e0.elapsed_time(e1) * 1e3 / a.iters
         tf = f"  {flop / us / 1e6:7.1f} TFLOP/s" if flop else ""
         print(f"{name:16s} {us:9.1f} us{tf}", flush=True)
-
-
-def tail_trace_report(tail, ws, B, nw, tiles=8, nstamp=8):
-    """Per-phase cycles of ppo_tail_kernel from a TAIL_TRACE build (mlp.hip: trace area after
-    the f32 / f64 slabs, [net][block][wave][tile][stamp] of s_memtime)."""
-    import numpy as np
-    ws.zero_()  # unwritten stamps read 0 and are masked out
-    tail()
-    torch.cuda.synchronize()
-    SL_F = 2 * 64 * 64 + 2 * 64 + 32 * 64 + 32 + 64 + 4
-    SL_D = 4 + 32
-    g = min((B // 32 + nw - 1) // nw, 256)
-    base = ws.data_ptr()
-    dptr = (base + g * SL_F * 4 + 15) & ~15
-    tptr = (dptr + g * SL_D * 8 + 255) & ~255
-    off = tptr - base
-    n = 2 * g * nw * tiles * nstamp
-    raw = ws.view(torch.uint8)[off:off + n * 8].cpu().numpy().view(np.uint64).astype(np.int64)
-    raw = raw.reshape(2, g, nw, tiles, nstamp)
-    names = ["load issue", "layer2(+wait)", "head+loss", "dW3", "dZ2", "dZ1+store", "dW2"]
-    for net in (0, 1):
-        r = raw[net]
-        ok = r[..., 7] > 0
-        print(f"net {net}: tiles traced {int(ok.sum())}")
-        for i in range(7):
-            a, b = r[..., i], r[..., i + 1]
-            m = ok & (a > 0) & (b > 0)
-            if not m.any():
-                continue
-            d = (b - a)[m]
-            print(f"  {names[i]:14s} median {np.median(d):8.0f}  p90 {np.percentile(d, 90):8.0f} cycles")
-        tt = (r[..., 7] - r[..., 0])[ok]
-        print(f"  {'whole tile':14s} median {np.median(tt):8.0f}  p90 {np.percentile(tt, 90):8.0f}")
-        # kernel span per wave (first tile start -> last tile end)
-        st = r[..., 0][ok].min()
-        en = r[..., 7][ok].max()
-        print(f"  span first stamp -> last stamp {en - st} cycles")
 
 
 if __name__ == "__main__":
