@@ -62,7 +62,9 @@ def main():
     if rank != 0:
         for k in KEYS:
             t = getattr(buf, k).contiguous()
-            dist.send(t.to(torch.uint8) if t.dtype == torch.bool else t, 0)
+            # host copies: gloo moves host tensors (a CUDA tensor's copy is not ordered
+            # with this process's streams)
+            dist.send((t.to(torch.uint8) if t.dtype == torch.bool else t).cpu(), 0)
         dist.barrier()
         dist.destroy_process_group()
         return
@@ -70,9 +72,10 @@ def main():
     for r in range(1, world):
         for k in KEYS:
             like = getattr(buf, k)
-            t = torch.empty_like(like, dtype=torch.uint8 if like.dtype == torch.bool
-                                 else like.dtype)
+            t = torch.empty(like.shape, dtype=torch.uint8 if like.dtype == torch.bool
+                            else like.dtype)
             dist.recv(t, r)
+            t = t.to(like.device)
             parts[k].append(t.bool() if like.dtype == torch.bool else t)
     dist.barrier()
     dist.destroy_process_group()

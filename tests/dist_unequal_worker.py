@@ -69,9 +69,11 @@ def main():
     if rank != 0:
         for k in KEYS:
             t = getattr(buf, k).contiguous()
-            dist.send(t.to(torch.uint8) if t.dtype == torch.bool else t, 0)
-        dist.send(rms_state[0], 0)
-        dist.send(rms_state[1], 0)
+            # host copies: gloo moves host tensors (a CUDA tensor's copy is not ordered
+            # with this process's streams)
+            dist.send((t.to(torch.uint8) if t.dtype == torch.bool else t).cpu(), 0)
+        dist.send(rms_state[0].cpu(), 0)
+        dist.send(rms_state[1].cpu(), 0)
         for k in PF:
             dist.send(cap[k], 0)
         dist.barrier()
@@ -83,8 +85,9 @@ def main():
             like = getattr(buf, k)
             shape = (SHARDS[r] * T,) + tuple(like.shape[1:])
             t = torch.empty(shape, dtype=torch.uint8 if like.dtype == torch.bool
-                            else like.dtype, device=like.device)
+                            else like.dtype)
             dist.recv(t, r)
+            t = t.to(like.device)
             parts[k].append(t.bool() if like.dtype == torch.bool else t)
     other = [torch.empty(D), torch.empty(D)]
     dist.recv(other[0], 1)
