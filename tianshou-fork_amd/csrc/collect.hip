@@ -61,11 +61,6 @@ constexpr int KMAX = 512;      // observation columns handled (padded to 128)
 constexpr int XP = 17;         // LDS pitch of the live-obs tile sX[col][row]
 constexpr int HP = 16;         // h1 / h2 tiles [feature][row]
 constexpr int WP = 68;         // W2 / W3 rows (4i + k banks: conflict-free A fragments)
-// 1: the quantised env's hashes, raw-row stores and moment atomics issued in pieces between
-// the actor's stages (env_rows / env_reset_and_totals); 0: the whole env phase before the actor
-#ifndef COLLECT_ENV_IL
-#define COLLECT_ENV_IL 1
-#endif
 // diagnostic builds only: per-workgroup s_memrealtime stamps (100 MHz) after each phase,
 // stored behind the workspace (tools/collect_step_bench.py --trace)
 #ifndef COLLECT_TRACE
@@ -629,11 +624,15 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         for (int rw = 0; rw < nrows; ++rw) row_store1(s_row[rw] + t, sX[t * XP + rw]);
     // ---- C. env step + auto-reset of these rows (env.hip box_step_reset_kernel) -------------
     // The quantised synthetic env's transition does not read the action, so its step runs
-    // before the actor: its obs_rms atomics drain while the actor computes.  The
+    // before the actor: its obs_rms atomics drain while the actor computes.  (Round 5,
+    // measured and dropped: the env's hashes / raw-row stores / atomics issued in pieces under
+    // the actor's three MFMA chains instead -- 23.3-24.0 vs 21.3 us per step, two A/B rounds:
+    // the pieces outlast the chains they hide under and every stage barrier then waits for
+    // them.)  The
     // action-coupled env (CPL) steps after the actor, on the actions in sAr.  Phase A of
     // this launch has consumed the previous step's env rows of this workgroup (the barrier
     // above).
-    auto env_flags = [&]() {
+    auto env_phase = [&]() {
         if (t < nrows) {
             // keys, reward and flags came from the top of the launch (LDS)
             const int64_t r = r0 + t;
@@ -645,56 +644,6 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
             if (f & 4) a.ep_j[r] = s_jn[t];
             a.ep_t[r] = s_tn[t];
         }
-    };
-    // The quantised env's step rows in pieces: env_rows(rb, re) hashes rows [rb, re) of this
-    // thread's column (D <= KMAX = NT), stores them and adds their exact integer moments to
-    // registers; env_reset_and_totals() does the reset rows and issues the totals atomics.
-    // With COLLECT_ENV_IL the pieces are issued between the actor's stages (below), where the
-    // waves otherwise wait on their MFMA chains and the stage barriers: the hashes (64-bit
-    // integer VALU) fill those gaps instead of running ahead of the actor.
-    long long cs1 = 0, cq1 = 0, cs2 = 0, cq2 = 0;
-    auto env_rows = [&](int rb, int re) {
-        if (t < D) {
-            const int d = t;
-            const int e = re < nrows ? re : nrows;
-            for (int r = rb; r < e; ++r) {
-                const int m = box_m(rs[r].key, d);
-                a.raw[(r0 + r) * D + d] = (float)m * 0x1p-23f;  // == box_val(key, d), exactly
-                cs1 += m;
-                cq1 += (long long)m * m;
-            }
-        }
-    };
-    auto env_reset_and_totals = [&]() {
-        const int nd = s_nd;
-        long long* tc = ws.tot[tcur];
-        if (t < D && nd > 0) {
-            const int d = t;
-            for (int r = 0; r < nrows; ++r) {
-                if (!rr[r].active) continue;
-                const int m = box_m(rr[r].key, d);
-                a.reset_raw[(r0 + r) * D + d] = (float)m * 0x1p-23f;
-                cs2 += m;
-                cq2 += (long long)m * m;
-            }
-        }
-        if (defer) {
-            if (t < D) {
-                atomic_add_i64(tc + t, cs1);
-                atomic_add_i64(tc + D + t, cq1);
-                if (nd > 0) {
-                    atomic_add_i64(tc + 2 * D + t, cs2);
-                    atomic_add_i64(tc + 3 * D + t, cq2);
-                }
-            }
-            if (t == 0) {
-                if (nd > 0) atomic_add_i64(tc + 4 * D, nd);
-                atomic_add_i64(tc + 4 * D + 1, nrows);
-            }
-        }
-    };
-    auto env_phase = [&]() {
-        env_flags();
         const int nd = s_nd;
         long long* tc = ws.tot[tcur];
         if (CPL) {
@@ -738,11 +687,42 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
             }
             return;
         }
-        env_rows(0, R);
-        env_reset_and_totals();
+        // this thread's column (D <= KMAX = NT): its exact integer moments, added to the totals
+        // slot by atomics
+        long long cs1 = 0, cq1 = 0, cs2 = 0, cq2 = 0;
+        if (t < D) {
+            const int d = t;
+            for (int r = 0; r < nrows; ++r) {
+                const int m = box_m(rs[r].key, d);
+                a.raw[(r0 + r) * D + d] = (float)m * 0x1p-23f;  // == box_val(key, d), exactly
+                cs1 += m;
+                cq1 += (long long)m * m;
+            }
+            if (nd > 0)
+                for (int r = 0; r < nrows; ++r) {
+                    if (!rr[r].active) continue;
+                    const int m = box_m(rr[r].key, d);
+                    a.reset_raw[(r0 + r) * D + d] = (float)m * 0x1p-23f;
+                    cs2 += m;
+                    cq2 += (long long)m * m;
+                }
+        }
+        if (defer) {
+            if (t < D) {
+                atomic_add_i64(tc + t, cs1);
+                atomic_add_i64(tc + D + t, cq1);
+                if (nd > 0) {
+                    atomic_add_i64(tc + 2 * D + t, cs2);
+                    atomic_add_i64(tc + 3 * D + t, cq2);
+                }
+            }
+            if (t == 0) {
+                if (nd > 0) atomic_add_i64(tc + 4 * D, nd);
+                atomic_add_i64(tc + 4 * D + 1, nrows);
+            }
+        }
     };
-    if (!CPL && !COLLECT_ENV_IL) env_phase();
-    if (!CPL && COLLECT_ENV_IL) env_flags();
+    if (!CPL) env_phase();
     TSTAMP(2)
 
     // ---- B. actor: layer 1 (wave w: k in [w KW, (w+1) KW), all 64 features) -----------------
@@ -763,7 +743,6 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
                 acc[ft] = mfma4(wall[sq][ft].w, b3, acc[ft]);
             }
         }
-        if (!CPL && COLLECT_ENV_IL) env_rows(0, R / 2);  // under the layer-1 MFMA chain
         // red[w][ft][r][lane]
 #pragma unroll
         for (int ft = 0; ft < 4; ++ft)
@@ -793,7 +772,6 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         const float* hb = sH1 + (32 * kh + (l >> 4)) * HP + (l & 15);
 #pragma unroll
         for (int s = 0; s < 8; ++s) z = mfma4(wa[4 * s], hb[4 * s * HP], z);
-        if (!CPL && COLLECT_ENV_IL) env_rows(R / 2, R);  // under the layer-2 MFMA chain
 #pragma unroll
         for (int r = 0; r < 4; ++r) red[(w * 4 + r) * 64 + l] = z[r];
     }
@@ -816,7 +794,6 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         const float* hb = sH2 + (16 * kq + (l >> 4)) * HP + (l & 15);
 #pragma unroll
         for (int s = 0; s < 4; ++s) z = mfma4(wa[4 * s], hb[4 * s * HP], z);
-        if (!CPL && COLLECT_ENV_IL) env_reset_and_totals();  // under the mu-head MFMA chain
 #pragma unroll
         for (int r = 0; r < 4; ++r) red[(w * 4 + r) * 64 + l] = z[r];
     }
