@@ -396,18 +396,11 @@ __device__ __forceinline__ double load_scale(const GaeArgs& p) {
 // thread-owns-8-elements load touches) and are redistributed through LDS; after the scan the
 // same regions carry adv and ret (f32) back out as coalesced stores.  v_s and the u8 flags
 // keep per-thread loads (32 B and 8 B per lane).
-// 1: rew staged through LDS like v_s_ (lane l loads 16-byte vector l); 0: each thread loads
-// its own 8 consecutive rews (4 x 16 B, 64 B per lane: still whole lines per wave) and the
-// stage shrinks from 24 to 16 KB per workgroup (8 instead of 6 resident workgroups per CU)
-#ifndef GAE_STAGE_REW
-#define GAE_STAGE_REW 0
-#endif
+// (Round 5, measured and dropped: rew loaded per thread, 8 consecutive values, instead of
+// staged -- a 16 instead of 24 KB stage; 47.6-47.8 vs 47.6-48.1 us by events at 4096 x 2048,
+// two A/B rounds: no change, the kernel is VGPR-limited to 4 workgroups per CU either way.)
 struct Stage {
-#if GAE_STAGE_REW
     double rew[TILE];  // rew; after the scan, ret as f32 in the first half
-#else
-    float ret[TILE];   // ret as f32 after the scan
-#endif
     float vn[TILE];    // v_s_; after the scan, adv as f32
 };
 
@@ -415,31 +408,19 @@ template <bool F64V>
 __device__ double gae_tile_staged(const GaeArgs& p, int64_t tb, double carry, double scale,
                                   Stage& st, Aff* lds, double* wsh, Welford* acc) {
     const int t = threadIdx.x;
-#if !GAE_STAGE_REW
-    double2 rd[4];
     {
-        const double2* r2 = reinterpret_cast<const double2*>(p.rew + tb + (int64_t)t * EPT);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) rd[j] = r2[j];
-    }
-#endif
-    {
-        const float4* n4 = reinterpret_cast<const float4*>(p.vn + tb);
-        float4 nv[2];
-#if GAE_STAGE_REW
         const double2* r2 = reinterpret_cast<const double2*>(p.rew + tb);
+        const float4* n4 = reinterpret_cast<const float4*>(p.vn + tb);
         double2 r[4];
+        float4 nv[2];
 #pragma unroll
         for (int j = 0; j < 4; ++j) r[j] = r2[t + TPB * j];
-#endif
 #pragma unroll
         for (int j = 0; j < 2; ++j) nv[j] = n4[t + TPB * j];
-#if GAE_STAGE_REW
         double2* sr = reinterpret_cast<double2*>(st.rew);
+        float4* sn = reinterpret_cast<float4*>(st.vn);
 #pragma unroll
         for (int j = 0; j < 4; ++j) sr[t + TPB * j] = r[j];
-#endif
-        float4* sn = reinterpret_cast<float4*>(st.vn);
 #pragma unroll
         for (int j = 0; j < 2; ++j) sn[t + TPB * j] = nv[j];
     }
@@ -457,13 +438,9 @@ __device__ double gae_tile_staged(const GaeArgs& p, int64_t tb, double carry, do
     e.endb = 0;
     e.validb = 0;
     {
-#if GAE_STAGE_REW
         const double2* sr = reinterpret_cast<const double2*>(st.rew + t * EPT);
-        const double2 r0 = sr[0], r1 = sr[1], r2 = sr[2], r3 = sr[3];
-#else
-        const double2 r0 = rd[0], r1 = rd[1], r2 = rd[2], r3 = rd[3];
-#endif
         const float4* sn = reinterpret_cast<const float4*>(st.vn + t * EPT);
+        const double2 r0 = sr[0], r1 = sr[1], r2 = sr[2], r3 = sr[3];
         const float4 n0 = sn[0], n1 = sn[1];
         const double rv[8] = {r0.x, r0.y, r1.x, r1.y, r2.x, r2.y, r3.x, r3.y};
         const float nvv[8] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w};
@@ -493,11 +470,7 @@ __device__ double gae_tile_staged(const GaeArgs& p, int64_t tb, double carry, do
     const double rscale = 1.0 / scale;
     double ret[EPT];
     float* sadv = st.vn + t * EPT;
-#if GAE_STAGE_REW
     float* sret = reinterpret_cast<float*>(st.rew) + t * EPT;
-#else
-    float* sret = st.ret + t * EPT;
-#endif
 #pragma unroll
     for (int k = EPT - 1; k >= 0; --k) {
         const double c = (e.endb & (1u << k)) ? 0.0 : p.gl;
@@ -526,11 +499,7 @@ __device__ double gae_tile_staged(const GaeArgs& p, int64_t tb, double carry, do
     }
     {
         const float4* sn = reinterpret_cast<const float4*>(st.vn);
-#if GAE_STAGE_REW
         const float4* sr = reinterpret_cast<const float4*>(st.rew);
-#else
-        const float4* sr = reinterpret_cast<const float4*>(st.ret);
-#endif
         if (p.adv) {
             float4* o = reinterpret_cast<float4*>(p.adv + tb);
 #pragma unroll
