@@ -86,6 +86,13 @@ def parse():
     ap.add_argument("--exact-obs-rms", action="store_true",
                     help="VectorEnvNormObs with the reference's f32 obs_rms arithmetic bit for "
                          "bit (sequential f32 column sums; opt-in, measures its cost)")
+    ap.add_argument("--exact-pipeline", type=int, default=None,
+                    help="with --exact-obs-rms: env rows computed this many steps ahead and the "
+                         "f32 statistic on a second graph branch (Collector.exact_pipeline, "
+                         "default 2; 0: serial, one exact update between step launches)")
+    ap.add_argument("--exact-branches", type=int, default=None,
+                    help="diagnostic: concurrent statistics streams of the pipelined exact "
+                         "obs_rms (Collector.exact_branches, default 1)")
     ap.add_argument("--force-dp", action="store_true",
                     help="diagnostic: under torch.distributed.run with ONE rank, run the "
                          "data-parallel code path (RCCL collectives over a one-rank "
@@ -309,6 +316,10 @@ def main():
                            perm_device=args.perm in ("device", "sorted")).to(dev)
         buf = VectorReplayBuffer(n, E, device=dev)
         coll = Collector(policy, env, buf)
+        if args.exact_pipeline is not None:
+            coll.exact_pipeline = args.exact_pipeline
+        if args.exact_branches is not None:
+            coll.exact_branches = args.exact_branches
     torch.manual_seed(rank)  # per-rank action sampling streams
     policy.graph_learn = {"auto": None, "on": True, "off": False}[args.graph_learn]
     policy.sort_minibatch = args.perm in ("sorted", "numpy-sorted")
@@ -426,7 +437,9 @@ def main():
                                                    if world > 1 or args.force_dp else ""),
                        "rccl_world_size": world if distributed else None,
                        "learn_graph": args.graph_learn,
-                       "obs_rms": "exact f32 (reference arithmetic)" if args.exact_obs_rms
+                       "obs_rms": ("exact f32 (reference arithmetic), " + (
+                           f"pipelined {coll.exact_pipeline} steps ahead"
+                           if coll._xpipe_ok() else "serial")) if args.exact_obs_rms
                        else ("f64 moments (atomic), action-coupled env" if args.act_coef
                              else "exact int64 moments (quantised synthetic obs), f64 merge"),
                        "learn_graph_capture_failed": bool(getattr(policy, "_graph_failed",

@@ -297,6 +297,18 @@ typedef struct tsrl_collect_args {
                                 totals); c != 0: the action-coupled env (synth.h coupled_val:
                                 env phase after the actor, f64 totals; the act_dim action
                                 columns feed obs column d mod act_dim) */
+    /* Pipelined exact obs_rms (xpipe != 0; exact_obs_rms with the action-independent env,
+     * no_moments = 0): the env rows of step i + d are computed d launches ahead ("spec" env,
+     * counters spec_j / spec_t) into spec_raw / spec_reset_raw / spec_done, so that their f32
+     * batch statistics (tsrl_rms_exact_stats, on a second graph branch) are ready when
+     * launch i + d + 1 merges them.  Launch i merges `xstats` (step i - 1's batch statistics,
+     * when rms_step > 0) into the state slot in its prologue with the reference's f32
+     * update_from_moments; its own env phase writes flags / counters only.  spec_raw NULL:
+     * no spec step in this launch. */
+    int64_t xpipe;
+    const void* xstats;
+    int64_t* spec_j; int64_t* spec_t;
+    float* spec_raw; float* spec_reset_raw; uint8_t* spec_done;
 } tsrl_collect_args;
 int64_t tsrl_collect_pack_floats(int64_t dim);
 int tsrl_collect_pack_w1(const float* W, int64_t dim, float* packed, void* stream);
@@ -311,6 +323,26 @@ int tsrl_collect_rms_finalize(const tsrl_collect_args* a, void* stream);
  * chain accumulates ([4*dim] reset rows, [4*dim + 1] step rows; data parallel: all-reduce it
  * with SUM before the next launch, world * k <= 2^17 keeps the sums exact). */
 int64_t tsrl_collect_totals_offset(int64_t step);
+/* Pipelined exact obs_rms (see tsrl_collect_args.xpipe).
+ * tsrl_collect_spec_step: the spec env step alone (a pipeline's first d steps): with `init`
+ *   the spec counters start from the env's (ep_j / ep_t), then one step of them writes the
+ *   rows of that step to spec_raw / spec_reset_raw / spec_done.
+ * tsrl_collect_xpipe_finalize: after the chain's last launch (rms_step = its index), its
+ *   step's batch statistics `xstats` merged into the state that launch published -> mean /
+ *   var / count, snap_mean / snap_var = after its step rows (the closing tsrl_buffer_add's
+ *   obs_next statistics).
+ * tsrl_rms_exact_stats: the batch moments of one RunningMeanStd.update pair in the
+ *   reference's f32 arithmetic (statistics.py:93-101: np.mean / np.var over axis 0, sequential
+ *   f32 column sums in row order) -- rows x [k, dim] (all), then the rows of reset_x [k, dim]
+ *   whose done flag is set, in row order -- into `stats` (tsrl_rms_exact_stats_bytes(dim)):
+ *   float bm1[dim], bv1[dim], bm2[dim], bv2[dim], then int64 n1, nd at byte offset
+ *   16 * dim rounded up to 8.  Merging them with update_from_moments reproduces
+ *   tsrl_rms_exact_update bit for bit.  dim % 4 == 0, x / reset_x 16-byte aligned. */
+int tsrl_collect_spec_step(const tsrl_collect_args* a, int init, void* stream);
+int tsrl_collect_xpipe_finalize(const tsrl_collect_args* a, void* stream);
+int64_t tsrl_rms_exact_stats_bytes(int64_t dim);
+int tsrl_rms_exact_stats(const float* x, int64_t k, const float* reset_x, const uint8_t* done,
+                         int64_t dim, void* stats, void* stream);
 /* *rel_dev = (*rel_dev + 1) % ring_size (device-side ring cursor for graph-captured steps). */
 int tsrl_ring_advance(int64_t* rel_dev, int64_t ring_size, void* stream);
 

@@ -37,11 +37,13 @@ def test_ctypes_struct_layout_matches_header(tmp_path):
     from tianshou_amd import _C
     src = tmp_path / "probe.c"
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "tsrl.h"\n'
-                   'int main(){printf("%zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(tsrl_add_args), '
+                   'int main(){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\\n", '
+                   'sizeof(tsrl_add_args), '
                    'sizeof(tsrl_ppo_params), offsetof(tsrl_add_args, stat_idx), '
                    'offsetof(tsrl_ppo_params, norm_adv), sizeof(tsrl_collect_args), '
                    'offsetof(tsrl_collect_args, sample), offsetof(tsrl_collect_args, no_moments), '
-                   'offsetof(tsrl_collect_args, rms_step));}')
+                   'offsetof(tsrl_collect_args, rms_step), offsetof(tsrl_collect_args, xpipe), '
+                   'offsetof(tsrl_collect_args, spec_done));}')
     exe = tmp_path / "probe"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)],
                    check=True)
@@ -54,6 +56,8 @@ def test_ctypes_struct_layout_matches_header(tmp_path):
     assert int(out[5]) == _C.CollectArgs.sample.offset
     assert int(out[6]) == _C.CollectArgs.no_moments.offset
     assert int(out[7]) == _C.CollectArgs.rms_step.offset
+    assert int(out[8]) == _C.CollectArgs.xpipe.offset
+    assert int(out[9]) == _C.CollectArgs.spec_done.offset
 
 
 @pytest.mark.parametrize("name", ["manager", "ragged"])

@@ -38,8 +38,21 @@
 //      hand-off.  With `no_moments` set (exact obs_rms) the launch computes no moments at
 //      all: the caller runs tsrl_rms_exact_update on the raw step / reset rows between
 //      launches, and the pending add normalises with the caller's mean / var / snapshot.
+//   E. Pipelined exact obs_rms (`xpipe`, the action-independent env): the reference's f32
+//      statistic needs two k-long dependent f32 add chains per column and update (~30 us at
+//      4096 rows), which serialised between launches cost 3x the default collect.  The env
+//      does not read the action, so its rows of step i + d are computed d launches early by a
+//      "spec" env (its own counters spec_j / spec_t, started from the env's at the head of
+//      each captured graph by tsrl_collect_spec_step) into a ring slot; the chains of step
+//      i's rows (tsrl_rms_exact_stats, batch moments only) run on a second graph branch
+//      concurrently with launches i - d + 1 .. i, and launch i + 1 merges them in its
+//      prologue with update_from_moments' f32 arithmetic (rms_exact.h merge) -- the same
+//      state slots as the deferred merge of D, no totals, no moments.  This launch's own env
+//      phase then writes only the step's flags / reward / counters; the pending add reads the
+//      ring slot's rows.
 #include "add_row.h"
 #include "noise.h"
+#include "rms_exact.h"
 #include "synth.h"
 
 namespace tsrl {
@@ -155,6 +168,47 @@ struct Ws {
     uint64_t* trace;
 };
 
+// tsrl_rms_exact_stats's layout: float bm1[D], bv1[D], bm2[D], bv2[D]; int64 n1, nd at byte
+// offset 16 D rounded up to 8
+__device__ __forceinline__ const int64_t* xstats_counts(const void* xs, int D) {
+    return reinterpret_cast<const int64_t*>(reinterpret_cast<const char*>(xs) +
+                                            (16 * (int64_t)D + 7) / 8 * 8);
+}
+
+// The reference's two RunningMeanStd updates of a Collector step from their batch moments, in
+// f32 (statistics.py:103-114; rms_exact.h merge): (mean, var, cnt) -> snapshot after the n1
+// step rows -> final after the nd reset rows.  An update with no rows changes nothing.
+__device__ __forceinline__ void merge_column_x(float m, float v, double& cnt, float bm1,
+                                               float bv1, int64_t n1, float bm2, float bv2,
+                                               int64_t nd, float& snap_m, float& snap_v,
+                                               float& fin_m, float& fin_v) {
+    if (n1 > 0) exact::merge(m, v, cnt, bm1, bv1, n1);
+    snap_m = m;
+    snap_v = v;
+    if (nd > 0) exact::merge(m, v, cnt, bm2, bv2, nd);
+    fin_m = m;
+    fin_v = v;
+}
+
+// The spec env's counter step of env e (the same transition as the env phase's keys, see
+// the top of collect_box_step_kernel): (j, tt) after the previous step -> this step's key,
+// done flag and, when done, the reset key; (j, tt) advanced.
+__device__ __forceinline__ void spec_keys(uint64_t seed, int64_t ep_len, int64_t e, int64_t& j,
+                                          int64_t& tt, RowState& st, RowState& sr, bool& dn) {
+    tt += 1;
+    st.key = env_key(seed, (uint64_t)e, j, tt);
+    st.active = 1;
+    sr.key = 0ull;
+    sr.active = 0;
+    dn = tt >= ep_len;
+    if (dn) {
+        j += 1;
+        tt = (j == 0) ? (e % ep_len) : 0;
+        sr.key = env_key(seed, (uint64_t)e, j, tt);
+        sr.active = 1;
+    }
+}
+
 // m such that the synthetic env value is x = m 2^-23 exactly (box_val, synth.h)
 __device__ __forceinline__ int box_m(uint64_t key, int64_t d) {
     const uint64_t h = sm64(key + (uint64_t)d * synth::GOLD);
@@ -224,7 +278,7 @@ __device__ __forceinline__ double slot_f(const long long* p, int i) {
 // CPL: the action-coupled env (a.act_coef != 0, synth.h coupled_val): the env phase runs
 // AFTER the actor on this launch's actions, and the obs_rms moments are f64 sums (atomic f64
 // adds: the values are not 2^-23-quantised), the counts f64 too (one all-reducible f64 slot).
-template <int SQC, bool CPL>
+template <int SQC, bool CPL, bool LW>
 __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_args a, Ws ws) {
 #pragma clang fp contract(off)
     __shared__ float sX[KMAX * XP];
@@ -242,6 +296,9 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
     __shared__ int s_flg[R];
     __shared__ int64_t s_jn[R], s_tn[R];
     __shared__ float* s_row[R];  // this step's stored obs row of each env (obs_dst + pitch)
+    // xpipe: the spec env's keys of step i + d (E)
+    __shared__ RowState xs_rs[R], xs_rr[R];
+    __shared__ int xs_nd;
     // deferred obs_rms merge: the statistics after the previous step's step rows (obs_next
     // normalisation) and after its reset rows (reset rows, state)
     __shared__ __attribute__((aligned(16))) float sSnapM[KMAX], sSnapV[KMAX], sFinM[KMAX],
@@ -274,11 +331,12 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
     TSTAMP(0)
 
     // ---- deferred obs_rms merge of the previous step (see D) ----------------------------------
-    const bool defer = !a.no_moments;
+    const bool xp = a.xpipe != 0;               // pipelined exact obs_rms (E)
+    const bool defer = !a.no_moments && !xp;    // the integer-totals chain (D)
     const int step = a.rms_step;  // index of this launch in its chain of deferred steps
     const int par = step & 1;
     const int tcur = step % 3, tprev = (step + 2) % 3, tnext = (step + 1) % 3;
-    const bool merge = defer && step > 0;
+    const bool merge = (defer || xp) && step > 0;
     tsrl_add_args ad = a.add;
     // A1 (merge chain): every load of the pending add (raw rows, reset flag, act row, flags
     // and episode counters) and of the merge is issued first; they are consumed after the
@@ -303,6 +361,15 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
         kj = a.ep_j[r0 + ki];
         kt = a.ep_t[r0 + ki];
         koff = a.obs_offset[r0 + ki];
+    }
+    // xpipe: the spec env's counters of these rows (the R threads before the key threads)
+    const int si = t - (KT0 - R);
+    const bool sgrp = xp && a.spec_raw && si >= 0 && si < R;
+    const bool srow = sgrp && si < nrows;
+    int64_t sj = 0, stt = 0;
+    if (srow) {
+        sj = a.spec_j[r0 + si];
+        stt = a.spec_t[r0 + si];
     }
     const int64_t ar = r0 + arw;
     const bool arow = fast && arw < nrows;
@@ -329,7 +396,24 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
     float mm0 = 0.f, mv0 = 0.f;
     long long ms1 = 0, mq1 = 0, ms2 = 0, mq2 = 0;  // raw slot words (int64 or f64 bits)
     double mcount = 0.0, mnd = 0.0, mk = 0.0;
-    if (merge) {
+    float xb1 = 0.f, xv1 = 0.f, xb2 = 0.f, xv2 = 0.f;  // xpipe: the previous step's batch moments
+    int64_t xn1 = 0, xnd = 0;
+    if (merge && xp) {
+        const RmsState* sin = ws.st[par];
+        const int64_t* xc = xstats_counts(a.xstats, D);
+        const float* xf = reinterpret_cast<const float*>(a.xstats);
+        mcount = sin->count;
+        xn1 = xc[0];
+        xnd = xc[1];
+        if (t < D) {
+            mm0 = sin->mean[t];
+            mv0 = sin->var[t];
+            xb1 = xf[t];
+            xv1 = xf[D + t];
+            xb2 = xf[2 * D + t];
+            xv2 = xf[3 * D + t];
+        }
+    } else if (merge) {
         const RmsState* sin = ws.st[par];
         const long long* tp = ws.tot[tprev];
         mcount = sin->count;
@@ -394,12 +478,33 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
             s_row[ki] = a.obs_dst + (koff + uo) * (a.obs_pitch ? a.obs_pitch : D);
         }
     }
+    if (sgrp) {
+        // xpipe: the spec env's step (i + d) of these rows; its counters and done flags go to
+        // HBM now (nothing else in this launch reads them), its rows in the env phase
+        RowState st = {0ull, 0}, sr = {0ull, 0};
+        bool dn = false;
+        if (srow) {
+            const int64_t e = r0 + si;
+            spec_keys(a.env_seed, a.ep_len, e, sj, stt, st, sr, dn);
+            a.spec_j[e] = sj;
+            a.spec_t[e] = stt;
+            a.spec_done[e] = (uint8_t)dn;
+        }
+        xs_rs[si] = st;
+        xs_rr[si] = sr;
+        const uint64_t dm = __ballot(dn);
+        if (si == 0) xs_nd = __popcll(dm);
+    }
+    double xcnt = mcount;  // xpipe: the count after the merge
     if (merge) {
         // the step rows behind the totals (counted in the slot: k, or the sum of every
         // rank's k when the slot was all-reduced)
         const double kp = mk;
         if (t < D) {
-            if (CPL)
+            if (xp)
+                merge_column_x(mm0, mv0, xcnt, xb1, xv1, xn1, xb2, xv2, xnd, sSnapM[t],
+                               sSnapV[t], sFinM[t], sFinV[t]);
+            else if (CPL)
                 merge_column_f((double)mm0, (double)mv0, mcount, kp, __longlong_as_double(ms1),
                                __longlong_as_double(mq1), mnd, __longlong_as_double(ms2),
                                __longlong_as_double(mq2), sSnapM[t], sSnapV[t], sFinM[t],
@@ -419,10 +524,12 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
                 so->mean[t] = sFinM[t];
                 so->var[t] = sFinV[t];
             }
-            if (t == 0) so->count = mcount + kp + mnd;
-            // the slot the next launch accumulates: read by the launch before this one
-            long long* tz = ws.tot[tnext];
-            for (int i = t; i < 4 * D + 2; i += NT) tz[i] = 0;
+            if (t == 0) so->count = xp ? xcnt : mcount + kp + mnd;
+            if (defer) {
+                // the slot the next launch accumulates: read by the launch before this one
+                long long* tz = ws.tot[tnext];
+                for (int i = t; i < 4 * D + 2; i += NT) tz[i] = 0;
+            }
         }
         // the add reads the statistics from LDS, with sqrt(var + eps) per column
         // (add_row<true>)
@@ -434,7 +541,7 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
             ad.reset_mean = sFinM;
             ad.reset_var = sFinS;
         }
-    } else if (defer && blockIdx.x == 0) {
+    } else if ((defer || xp) && blockIdx.x == 0) {
         // first step of a chain: the caller's state seeds the state slot (slot 1 of the
         // totals ring is zero: tsrl_collect_rms_finalize cleared the ring)
         RmsState* so = ws.st[par ^ 1];
@@ -488,17 +595,21 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
             vhi = a.high[t];
         }
     }
+
     // layer-1 weight fragments of this wave (SQ == SQC): independent of the add phase, so
-    // their latency hides behind it
+    // their latency hides behind it.  LW (the pipelined exact kernels, E): issued after the
+    // add instead -- held across it they take the kernel to 241 VGPRs, two waves per SIMD
+    // then fill the register file, and the concurrent tsrl_rms_exact_stats workgroup (128
+    // VGPRs) finds no room on the CU; issued late, 190.  The default keeps the early issue:
+    // 22.5 vs 23.8 us per step (tools/collect_ab.sh, two rounds).
     float4 wall[SQC][4];
-    {
-        const float4* wp = reinterpret_cast<const float4*>(a.w1p) + (int64_t)w * SQ * 4 * 64 + l;
+    const float4* wp = reinterpret_cast<const float4*>(a.w1p) + (int64_t)w * SQ * 4 * 64 + l;
+    if constexpr (!LW) {
 #pragma unroll
         for (int sq = 0; sq < SQC; ++sq)
 #pragma unroll
             for (int ft = 0; ft < 4; ++ft) wall[sq][ft] = wp[(sq * 4 + ft) * 64];
     }
-
     TSTAMP(4)
     // ---- A. pending add of the previous step -> buffer rows + live obs (HBM and sX) ---------
     if (ad.k > 0) {
@@ -566,6 +677,12 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
             const int rw = i / D, c = i - rw * D;
             sX[c * XP + rw] = a.cur[(r0 + rw) * D + c];
         }
+    }
+    if constexpr (LW) {
+#pragma unroll
+        for (int sq = 0; sq < SQC; ++sq)
+#pragma unroll
+            for (int ft = 0; ft < 4; ++ft) wall[sq][ft] = wp[(sq * 4 + ft) * 64];
     }
     TSTAMP(1)
     // zero padding: columns [D, Kp) and rows past the last env of a partial tile
@@ -643,6 +760,22 @@ __global__ __launch_bounds__(NT, 1) void collect_box_step_kernel(tsrl_collect_ar
             a.done[r] = (uint8_t)((f >> 2) & 1);
             if (f & 4) a.ep_j[r] = s_jn[t];
             a.ep_t[r] = s_tn[t];
+        }
+        if (xp) {
+            // E: this step's rows were computed d launches ago; the spec env's rows of step
+            // i + d (one column per thread) go to the ring slot for tsrl_rms_exact_stats and
+            // the pending add of launch i + d + 1
+            if (a.spec_raw && t < D) {
+                const int d = t;
+                for (int r = 0; r < nrows; ++r)
+                    a.spec_raw[(r0 + r) * D + d] = (float)box_m(xs_rs[r].key, d) * 0x1p-23f;
+                if (xs_nd > 0)
+                    for (int r = 0; r < nrows; ++r)
+                        if (xs_rr[r].active)
+                            a.spec_reset_raw[(r0 + r) * D + d] =
+                                (float)box_m(xs_rr[r].key, d) * 0x1p-23f;
+            }
+            return;
         }
         const int nd = s_nd;
         long long* tc = ws.tot[tcur];
@@ -865,6 +998,68 @@ __global__ __launch_bounds__(NT) void rms_finalize_kernel(tsrl_collect_args a, W
     if (t == 0) *a.count = old_count + kp + nd;
 }
 
+// tsrl_collect_spec_step: the spec env step alone (E) -- the head of a pipelined chain computes
+// the rows of its first d steps with it.  Workgroup = R env rows, one column per thread.
+__global__ __launch_bounds__(NT) void spec_step_kernel(tsrl_collect_args a, int init) {
+    __shared__ RowState rs[R], rr[R];
+    __shared__ int s_nd;
+    const int t = threadIdx.x;
+    const int D = (int)a.dim;
+    const int64_t r0 = (int64_t)blockIdx.x * R;
+    const int nrows = (int)min((int64_t)R, a.k - r0);
+    if (t < R) {
+        RowState st = {0ull, 0}, sr = {0ull, 0};
+        bool dn = false;
+        if (t < nrows) {
+            const int64_t e = r0 + t;
+            int64_t j = init ? a.ep_j[e] : a.spec_j[e];
+            int64_t tt = init ? a.ep_t[e] : a.spec_t[e];
+            spec_keys(a.env_seed, a.ep_len, e, j, tt, st, sr, dn);
+            a.spec_j[e] = j;
+            a.spec_t[e] = tt;
+            a.spec_done[e] = (uint8_t)dn;
+        }
+        rs[t] = st;
+        rr[t] = sr;
+        const uint64_t dm = __ballot(dn);
+        if (t == 0) s_nd = __popcll(dm);
+    }
+    __syncthreads();
+    if (t < D) {
+        for (int r = 0; r < nrows; ++r)
+            a.spec_raw[(r0 + r) * D + t] = (float)box_m(rs[r].key, t) * 0x1p-23f;
+        if (s_nd > 0)
+            for (int r = 0; r < nrows; ++r)
+                if (rr[r].active)
+                    a.spec_reset_raw[(r0 + r) * D + t] = (float)box_m(rr[r].key, t) * 0x1p-23f;
+    }
+}
+
+// tsrl_collect_xpipe_finalize: the pipelined chain's last step -- its batch moments (xstats)
+// merged into the state its launch published -> the caller's mean / var / count and the
+// snapshot after its step rows.
+__global__ __launch_bounds__(NT) void xpipe_finalize_kernel(tsrl_collect_args a, Ws ws) {
+#pragma clang fp contract(off)
+    const int t = threadIdx.x;
+    const int D = (int)a.dim;
+    const RmsState* sin = ws.st[(a.rms_step + 1) & 1];
+    const int64_t* xc = xstats_counts(a.xstats, D);
+    const float* xf = reinterpret_cast<const float*>(a.xstats);
+    const int64_t n1 = xc[0], nd = xc[1];
+    double cnt = sin->count;
+    for (int d = t; d < D; d += NT) {
+        cnt = sin->count;
+        float sm, sv, fm, fv;
+        merge_column_x(sin->mean[d], sin->var[d], cnt, xf[d], xf[D + d], n1, xf[2 * D + d],
+                       xf[3 * D + d], nd, sm, sv, fm, fv);
+        a.snap_mean[d] = sm;
+        a.snap_var[d] = sv;
+        a.mean[d] = fm;
+        a.var[d] = fv;
+    }
+    if (t == 0) *a.count = cnt;
+}
+
 inline int64_t nblk_for(int64_t k) { return (k + R - 1) / R; }
 constexpr int64_t TICKET_BYTES = 256;
 constexpr int64_t TOT_BYTES = (TOT_N * 8 + 255) / 256 * 256;
@@ -952,6 +1147,16 @@ extern "C" int tsrl_collect_box_step(const tsrl_collect_args* a, void* stream) {
         TSRL_CHECK_ARG(!ad.obs_src, "tsrl_collect_box_step: the pending add copies no obs (the "
                                     "launch that produced it stored them)");
     }
+    if (a->xpipe) {
+        TSRL_CHECK_ARG(a->act_coef == 0.0f && !a->no_moments && (a->rms_step == 0 || a->xstats),
+                       "tsrl_collect_box_step: xpipe needs the action-independent env, "
+                       "no_moments = 0 and, past a chain's first launch, xstats");
+        TSRL_CHECK_ARG(!a->spec_raw || (a->spec_j && a->spec_t && a->spec_reset_raw && a->spec_done),
+                       "tsrl_collect_box_step: xpipe spec rows need spec_j / spec_t / "
+                       "spec_reset_raw / spec_done");
+        TSRL_CHECK_ARG(!a->xstats || (reinterpret_cast<uintptr_t>(a->xstats) & 7u) == 0,
+                       "tsrl_collect_box_step: xstats must be 8-byte aligned");
+    }
     // one row adds <= 2^46 to a column's int64 sum of m^2: exact for <= 2^17 rows per slot (the
     // data-parallel caller also checks world * k); the coupled env's f64 slot has no such bound
     TSRL_CHECK_ARG(a->act_coef != 0.0f || k <= (int64_t)1 << 17,
@@ -960,24 +1165,21 @@ extern "C" int tsrl_collect_box_step(const tsrl_collect_args* a, void* stream) {
     tsrl_collect_args p = *a;
     p.act_seed = sm64(a->act_seed);
     p.env_seed = sm64(a->env_seed);
-#define TSRL_COLLECT_LAUNCH(SQ, CP)                                                         \
-    hipLaunchKernelGGL((collect_box_step_kernel<SQ, CP>), dim3((unsigned)ws.nblk), dim3(NT), 0,  \
-                       as_stream(stream), p, ws)
+#define TSRL_COLLECT_LAUNCH(SQ, CP, LW)                                                     \
+    hipLaunchKernelGGL((collect_box_step_kernel<SQ, CP, LW>), dim3((unsigned)ws.nblk), dim3(NT), \
+                       0, as_stream(stream), p, ws)
+#define TSRL_COLLECT_SQ(SQ)                                                                 \
+    if (cpl) TSRL_COLLECT_LAUNCH(SQ, true, false);                                          \
+    else if (a->xpipe) TSRL_COLLECT_LAUNCH(SQ, false, true);                                \
+    else TSRL_COLLECT_LAUNCH(SQ, false, false);
     const bool cpl = a->act_coef != 0.0f;
     switch (kpad(D) / 128) {
-        case 1:
-            if (cpl) TSRL_COLLECT_LAUNCH(1, true); else TSRL_COLLECT_LAUNCH(1, false);
-            break;
-        case 2:
-            if (cpl) TSRL_COLLECT_LAUNCH(2, true); else TSRL_COLLECT_LAUNCH(2, false);
-            break;
-        case 3:
-            if (cpl) TSRL_COLLECT_LAUNCH(3, true); else TSRL_COLLECT_LAUNCH(3, false);
-            break;
-        default:
-            if (cpl) TSRL_COLLECT_LAUNCH(4, true); else TSRL_COLLECT_LAUNCH(4, false);
-            break;
+        case 1: TSRL_COLLECT_SQ(1) break;
+        case 2: TSRL_COLLECT_SQ(2) break;
+        case 3: TSRL_COLLECT_SQ(3) break;
+        default: TSRL_COLLECT_SQ(4) break;
     }
+#undef TSRL_COLLECT_SQ
 #undef TSRL_COLLECT_LAUNCH
     TSRL_LAUNCH_CHECK("tsrl_collect_box_step");
     return 0;
@@ -985,6 +1187,30 @@ extern "C" int tsrl_collect_box_step(const tsrl_collect_args* a, void* stream) {
 
 extern "C" int64_t tsrl_collect_totals_offset(int64_t step) {
     return TICKET_BYTES + (step % 3) * TOT_BYTES;
+}
+
+extern "C" int tsrl_collect_spec_step(const tsrl_collect_args* a, int init, void* stream) {
+    TSRL_CHECK_ARG(a != nullptr && a->k > 0 && a->dim > 0 && a->dim <= KMAX && a->ep_len > 0 &&
+                       a->spec_j && a->spec_t && a->spec_raw && a->spec_reset_raw &&
+                       a->spec_done && (!init || (a->ep_j && a->ep_t)),
+                   "tsrl_collect_spec_step: bad arguments");
+    tsrl_collect_args p = *a;
+    p.env_seed = sm64(a->env_seed);  // as tsrl_collect_box_step passes it
+    hipLaunchKernelGGL(spec_step_kernel, dim3((unsigned)nblk_for(a->k)), dim3(NT), 0,
+                       as_stream(stream), p, init);
+    TSRL_LAUNCH_CHECK("tsrl_collect_spec_step");
+    return 0;
+}
+
+extern "C" int tsrl_collect_xpipe_finalize(const tsrl_collect_args* a, void* stream) {
+    TSRL_CHECK_ARG(a != nullptr && a->workspace && a->mean && a->var && a->count &&
+                       a->snap_mean && a->snap_var && a->xstats && a->k > 0 && a->dim > 0 &&
+                       a->dim <= KMAX && (reinterpret_cast<uintptr_t>(a->xstats) & 7u) == 0,
+                   "tsrl_collect_xpipe_finalize: bad arguments");
+    hipLaunchKernelGGL(xpipe_finalize_kernel, dim3(1), dim3(NT), 0, as_stream(stream), *a,
+                       make_ws(a));
+    TSRL_LAUNCH_CHECK("tsrl_collect_xpipe_finalize");
+    return 0;
 }
 
 extern "C" int tsrl_collect_rms_finalize(const tsrl_collect_args* a, void* stream) {

@@ -55,6 +55,8 @@ class CollectArgs(ctypes.Structure):
         ("workspace", _p), ("mean", _p), ("var", _p), ("snap_mean", _p), ("snap_var", _p),
         ("count", _p), ("no_moments", _i64), ("rms_step", _i64), ("obs_pitch", _i64),
         ("act_coef", ctypes.c_float),
+        ("xpipe", _i64), ("xstats", _p), ("spec_j", _p), ("spec_t", _p), ("spec_raw", _p),
+        ("spec_reset_raw", _p), ("spec_done", _p),
     ]
 
 
@@ -122,6 +124,10 @@ _SIGS = {
     "tsrl_collect_box_step": ([ctypes.POINTER(CollectArgs), _p], ctypes.c_int),
     "tsrl_collect_rms_finalize": ([ctypes.POINTER(CollectArgs), _p], ctypes.c_int),
     "tsrl_collect_totals_offset": ([_i64], _i64),
+    "tsrl_collect_spec_step": ([ctypes.POINTER(CollectArgs), _i32, _p], ctypes.c_int),
+    "tsrl_collect_xpipe_finalize": ([ctypes.POINTER(CollectArgs), _p], ctypes.c_int),
+    "tsrl_rms_exact_stats_bytes": ([_i64], _i64),
+    "tsrl_rms_exact_stats": ([_p, _i64, _p, _p, _i64, _p, _p], ctypes.c_int),
     "tsrl_gather_rows": ([_p, _i64, _p, _i64, _p, _p], ctypes.c_int),
     "tsrl_gather_rows_pitched": ([_p, _i64, _i64, _p, _i64, _p, _p], ctypes.c_int),
     "tsrl_np_shuffle_draws": ([_p, _p, _i64, _p], ctypes.c_int),

@@ -72,6 +72,14 @@ class Collector:
         self._rms_chain = None
         self._rms_step = 0  # index of the next deferred launch in its chain
         self._pending = None
+        # exact_obs_rms on the fused step with the action-independent env: the reference's
+        # f32 statistic of step i runs on a second graph branch while the step launches go on,
+        # its env rows computed this many launches ahead (csrc/collect.hip E; 0: the serial
+        # form, one tsrl_rms_exact_update between launches)
+        self.exact_pipeline = 2
+        self.exact_branches = 1  # side streams of the statistics (concurrent statistics)
+        self._xp_streams = None
+        self._xp_keep = []
         from tianshou_amd.dist import default_dp
         self.dp = default_dp()
         if sync_obs_rms and self.dp.active and self._norm is not None:
@@ -291,10 +299,11 @@ class Collector:
         sc = self._scratch["step_ctr"]
         return bool(self.policy.fused_collect_fill(_C.CollectArgs(), (sc[0, 1:2], sc[1, 1:2])))
 
-    def _fused_box_step(self, cur, kk, add_kw) -> None:
+    def _fused_box_step(self, cur, kk, add_kw, xp=None) -> None:
         """One vector step as one launch: the pending add of the previous step, policy act,
         env step + auto-reset, both obs_rms updates (csrc/collect.hip).  This step's add is
-        left pending for the next launch or _flush()."""
+        left pending for the next launch or _flush().  ``xp``: launch i of a pipelined exact
+        chain (see _xpipe_steps): dict(i, stats_prev, spec, rows, reset_rows)."""
         s, b, buf = self._scratch, self._base, self.buffer
         rms = self._norm.obs_rms
         rms.ensure_snapshot()
@@ -324,10 +333,23 @@ class Collector:
         c.mean, c.var, c.count = _C.ptr(rms.mean_t), _C.ptr(rms.var_t), _C.ptr(rms.count_t)
         c.snap_mean, c.snap_var = _C.ptr(rms.snap_mean_t), _C.ptr(rms.snap_var_t)
         dp = rms.dp is not None and rms.dp.active
-        if rms.exact:
+        obs_next, reset_src = s["raw"], s["reset_raw"]
+        if xp is not None:
+            # pipelined exact obs_rms: merge step i - 1's batch moments in the prologue, write
+            # the spec env's rows of step i + d, read this step's rows from the ring slot
+            c.xpipe, c.rms_step = 1, xp["i"]
+            c.xstats = _C.ptr(xp["stats_prev"])
+            if xp["spec"] is not None:
+                sj, st_, sraw, sreset, sdone = xp["spec"]
+                c.spec_j, c.spec_t = _C.ptr(sj), _C.ptr(st_)
+                c.spec_raw, c.spec_reset_raw, c.spec_done = (_C.ptr(sraw), _C.ptr(sreset),
+                                                             _C.ptr(sdone))
+            obs_next, reset_src = xp["rows"], xp["reset_rows"]
+        elif rms.exact:
             # the launch computes no moments; the exact f32 update runs after it (below)
             c.no_moments = 1
-        c.rms_step = 0 if rms.exact else self._rms_step
+        if xp is None:
+            c.rms_step = 0 if rms.exact else self._rms_step
         _C.check(_C.lib().tsrl_collect_box_step(c, _C.stream_ptr(b.device)),
                  "tsrl_collect_box_step")
         if dp and not rms.exact:
@@ -343,16 +365,111 @@ class Collector:
         # step's obs_rms moments
         self._rms_chain = None if rms.exact else c
         self._rms_step = 0 if rms.exact else self._rms_step + 1
-        if rms.exact:
+        if rms.exact and xp is None:
             # both updates from the raw step / reset rows the launch wrote, in the
             # reference's f32 arithmetic
             rms.exact_update(s["raw"][:kk], None, s["reset_raw"][:kk], s["done"][:kk],
                              snapshot=True)
         self._pending = buf._launch_add(
-            ids=None, k=kk, obs=None, act=s["act"], obs_next=s["raw"], cur_obs=cur, norm=rms,
-            norm_snapshot=True, reset_src=s["reset_raw"], reset_mask=s["done"], reset_norm=rms,
+            ids=None, k=kk, obs=None, act=s["act"], obs_next=obs_next, cur_obs=cur, norm=rms,
+            norm_snapshot=True, reset_src=reset_src, reset_mask=s["done"], reset_norm=rms,
             rew=s["rew"], term=s["term"], trunc=s["trunc"], launch=False, **add_kw)
         self._parity ^= 1
+        return c
+
+    # -- pipelined exact obs_rms (csrc/collect.hip E) ---------------------------------------------
+    def _xpipe_ok(self) -> bool:
+        """exact_obs_rms on the one-launch step with the action-independent env (rows of a
+        multiple of 4 floats, one process): its f32 statistic can run beside the launches."""
+        if not (self.exact_pipeline and self._step_on and self._norm is not None):
+            return False
+        rms, b = self._norm.obs_rms, self._base
+        return bool(rms.exact and b.act_coef == 0.0 and b.obs_numel % 4 == 0
+                    and not (rms.dp is not None and rms.dp.active))
+
+    def _xpipe_scratch(self) -> None:
+        """Ring of d + 2 slots (a step's env rows, reset rows, done flags, batch moments),
+        the spec env counters and the side stream of the statistics branch."""
+        s, b = self._scratch, self._base
+        d = int(self.exact_pipeline)
+        nsl, k, D, dev = d + 2, self.env_num, b.obs_numel, b.device
+        if s.get("xp_raw") is None or s["xp_raw"].shape[0] != nsl:
+            s["xp_raw"] = torch.empty((nsl, k, D), device=dev)
+            s["xp_reset"] = torch.empty((nsl, k, D), device=dev)
+            s["xp_done"] = torch.zeros((nsl, k), dtype=torch.uint8, device=dev)
+            nb = -(-int(_C.lib().tsrl_rms_exact_stats_bytes(D)) // 256) * 256
+            s["xp_stats"] = torch.zeros((nsl, nb), dtype=torch.uint8, device=dev)
+            s["xp_spec"] = torch.zeros((2, k), dtype=torch.int64, device=dev)
+        nbr = max(1, min(int(self.exact_branches), d))
+        if self._xp_streams is None or len(self._xp_streams) != nbr:
+            self._xp_streams = [torch.cuda.Stream(device=dev) for _ in range(nbr)]
+
+    def _xpipe_steps(self, G: int, sc) -> None:
+        """G fused steps with the exact statistic pipelined (inside a graph capture): the spec
+        env computes step j's rows d launches before launch j + 1 needs their statistic;
+        tsrl_rms_exact_stats of step j runs on the side stream after the launch (or the
+        head's tsrl_collect_spec_step) that wrote them -- one statistic at a time: a
+        workgroup of it fits on a CU beside a step workgroup, two do not; launch j + 1 waits
+        for it and merges it; tsrl_collect_xpipe_finalize merges the last step's, then
+        _flush runs its add."""
+        s, b = self._scratch, self._base
+        rms = self._norm.obs_rms
+        lib = _C.lib()
+        d = int(self.exact_pipeline)
+        nsl, k, D = d + 2, self.env_num, b.obs_numel
+        main = torch.cuda.current_stream(b.device)
+        raw, rst, dn, st, spec = (s[x] for x in ("xp_raw", "xp_reset", "xp_done", "xp_stats",
+                                                 "xp_spec"))
+        ev_stats = {}
+        # the events outlive the capture (destroyed before the next one begins, not inside it)
+        keep = self._xp_keep
+
+        def spec_of(j):
+            return spec[0], spec[1], raw[j % nsl], rst[j % nsl], dn[j % nsl]
+
+        def stats(j):
+            ev = torch.cuda.Event()
+            ev.record(main)  # step j's rows are written
+            side = self._xp_streams[j % len(self._xp_streams)]
+            side.wait_event(ev)
+            keep.append(ev)
+            _C.check(lib.tsrl_rms_exact_stats(_C.ptr(raw[j % nsl]), k, _C.ptr(rst[j % nsl]),
+                                              _C.ptr(dn[j % nsl]), D, _C.ptr(st[j % nsl]),
+                                              side.cuda_stream), "tsrl_rms_exact_stats")
+            ev_stats[j] = torch.cuda.Event()
+            ev_stats[j].record(side)
+            keep.append(ev_stats[j])
+
+        for j in range(min(d, G)):
+            c = _C.CollectArgs()
+            c.k, c.dim, c.env_seed, c.ep_len = k, D, b.seed_, b.ep_len
+            c.ep_j, c.ep_t = _C.ptr(b.ep_j), _C.ptr(b.ep_t)
+            c.spec_j, c.spec_t, c.spec_raw, c.spec_reset_raw, c.spec_done = (
+                _C.ptr(x) for x in spec_of(j))
+            _C.check(lib.tsrl_collect_spec_step(c, int(j == 0), main.cuda_stream),
+                     "tsrl_collect_spec_step")
+            stats(j)
+        c = None
+        for i in range(G):
+            if i > 0:
+                main.wait_event(ev_stats[i - 1])
+            xp = dict(i=i, stats_prev=st[(i - 1) % nsl] if i > 0 else None,
+                      spec=spec_of(i + d) if i + d < G else None, rows=raw[i % nsl],
+                      reset_rows=rst[i % nsl])
+            c = self._fused_box_step(self._scratch["cur"], k, dict(
+                rel_dev=sc[i % 2, 0:1], rel_next=sc[(i + 1) % 2, 0:1]), xp=xp)
+            if i + d < G:
+                stats(i + d)
+        main.wait_event(ev_stats[G - 1])
+        c.xstats = _C.ptr(st[(G - 1) % nsl])
+        _C.check(lib.tsrl_collect_xpipe_finalize(c, main.cuda_stream),
+                 "tsrl_collect_xpipe_finalize")
+        self._flush()
+        for side in self._xp_streams[:min(len(self._xp_streams), G)]:  # join the forks
+            ev = torch.cuda.Event()
+            ev.record(side)
+            main.wait_event(ev)
+            keep.append(ev)
 
     def _flush(self) -> None:
         """Run the pending buffer add of the last fused step (tsrl_buffer_add), after merging
@@ -446,7 +563,7 @@ class Collector:
             ptrs += [r.mean_t.data_ptr(), r.var_t.data_ptr(), r.count_t.data_ptr(),
                      self._norm.update_obs_rms]
         return (G, self.policy.training, self.exploration_noise, self._fused_act_on,
-                self._step_on, tuple(ptrs))
+                self._step_on, self.exact_pipeline if self._xpipe_ok() else 0, tuple(ptrs))
 
     def _replay_steps(self, no_grad, n_steps: int, written: list) -> int:
         """Run up to n_steps uniform steps as replays of captured HIP graphs of G steps
@@ -467,6 +584,10 @@ class Collector:
             self._graphs = {}
         sc[0, 0].fill_(int(buf._ring.index[0]))
         done = 0
+        xpipe = self._xpipe_ok()
+        if xpipe:
+            self._xpipe_scratch()
+        self._xp_keep = []
         while n_steps - done >= 2:
             G = min(Gmax, (n_steps - done) // 2 * 2)
             key = self._graph_key(G)
@@ -476,11 +597,14 @@ class Collector:
                 torch.cuda.synchronize()
                 LOG.capture_begin()
                 with graph_capture(g):
-                    for i in range(G):
-                        self._device_step(self._scratch["cur"], self.env_num, None, False,
-                                          no_grad, dict(rel_dev=sc[i % 2, 0:1],
-                                                        rel_next=sc[(i + 1) % 2, 0:1]))
-                    self._flush()
+                    if xpipe:
+                        self._xpipe_steps(G, sc)
+                    else:
+                        for i in range(G):
+                            self._device_step(self._scratch["cur"], self.env_num, None, False,
+                                              no_grad, dict(rel_dev=sc[i % 2, 0:1],
+                                                            rel_next=sc[(i + 1) % 2, 0:1]))
+                        self._flush()
                 self._graphs[G] = graph = (key, g, LOG.capture_end())
                 self._parity = 0
             graph[1].replay()

@@ -34,7 +34,8 @@ for name, cnt, ms, us in c.execute(
     print(f"{ms:10.2f} ms {cnt:7d} x {us:10.1f} us  {name[:140]}")
 ALWAYS = ("gae_rows_staged_kernel", "collect_box_step_kernel", "l1_ring_kernel",
           "dw_x6_kernel", "dw_reduce_kernel", "ppo_tail_kernel", "tail_reduce_kernel",
-          "clip_adam_kernel", "rms_exact_kernel", "eval_tail_kernel")
+          "clip_adam_kernel", "rms_exact_kernel", "eval_tail_kernel", "rms_exact_stats_kernel",
+          "spec_step_kernel", "xpipe_finalize_kernel", "ppo_tail16_kernel")
 print("cited kernels (every launch in the window): total ms, calls, mean / min / max us")
 for pat in ALWAYS:
     for name, cnt, ms, us, lo, hi in c.execute(
