@@ -410,128 +410,32 @@ extern "C" int tsrl_rms_exact_update(const float* x, const uint8_t* mask, int64_
 
 // ---------------------------------------------------------------------------------------
 // tsrl_rms_exact_stats: the batch moments of one update pair alone, for the pipelined exact
-// collect (collect.hip, xpipe: the next step launch merges them in its prologue).  The same
-// f32 arithmetic as rms_exact_kernel (sum in row order, mean = S / k, squares about the mean
-// summed in row order, var = Q / k), but STREAMED rather than LDS-resident, so a workgroup
-// takes 32 KB of LDS and runs on a CU beside a collect-step workgroup (~118 KB):
-//   wave 0: the step rows of SXC = 16 columns, two passes (sums, then squares about the batch
-//           mean).  LDS-DMA (global_load_lds_dwordx4: 16 rows x 64 B per wave-instruction)
-//           into a 16-stage ring, 256 rows in flight; lanes 0-15 run the columns' chains,
-//           reading the next block out of LDS while they add the current one.  Per row the
-//           chain is one dependent v_add_f32, so a 4096-row pass is ~4096 x 8 cycles;
-//   wave 1: the reset rows (done flag set, in row order): the flags of up to 4096 rows to an
-//           LDS row list (ballots), then the listed rows' values by ordinary loads, 16 rows in
-//           flight.
-// Workgroup b takes column group (b % 8) * ceil(G / 8) + b / 8 (blocks b, b + 8, ... share an
-// XCD and its L2, so neighbouring column groups -- the same 128-B lines of every row -- are
-// read through one L2).
+// collect (collect.hip E: the next step launch merges them in its prologue).  The same f32
+// arithmetic as rms_exact_kernel (sum in row order, mean = S / k, squares about the mean summed
+// in row order, var = Q / k), in a form that runs on a CU BESIDE a collect-step workgroup
+// (~117 KB of LDS, 190 VGPRs in its LW form): RXC = 2 columns per workgroup (128 threads), a
+// span of RSPAN = 2048 rows of them in LDS ([column][row], 16 KB), loaded by LDS-DMA
+// (global_load_lds_dword: one column x 64 rows per wave-instruction, a span's instructions all
+// in flight -- one memory latency per span and pass), exact::chain over each column run (lanes
+// 0-1 of wave 0), the squares in place (wave w: column w), the var chains; wave 1 runs the
+// reset rows' two passes (row lists of RSEG = 1024 rows) while wave 0 chains.  20 KB and 128
+// VGPRs per workgroup: two statistics (two steps) fit on a CU beside a step workgroup, so the
+// pipeline keeps two in flight.  Workgroup b takes column pair (b % 8) * G / 8 + b / 8 (grid
+// G padded to a multiple of 8): blocks b, b + 8, ... share an XCD and its L2, and neighbouring
+// pairs read the same 128-B lines of every row.
+// Measured (round 5, bench --exact-obs-rms, collect per 2048-step iteration; serial form 142
+// ms, default obs_rms 41-42 ms): span 4096 / one statistic at a time 108-109 ms; XCD order 97;
+// two at a time 110-113 (they no longer fit beside the step); span 2048 + XCD order, two at a
+// time 79-80 (three: 80; span 1024: 87, three at depth 3: 80).  The first form streamed 16
+// columns through a 16-stage LDS-DMA ring (16 rows per instruction): 199 us per statistic
+// alone -- one DMA latency per 15 blocks -- against 38.8 us for the resident form alone.
 // ---------------------------------------------------------------------------------------
 namespace tsrl {
 namespace {
 
-constexpr int SXC = 16;     // columns per workgroup
-constexpr int SRB = 16;     // rows per DMA wave-instruction (16 x 64 B)
-#ifndef XSTATS_NS
-#define XSTATS_NS 16
-#endif
-constexpr int SNS = XSTATS_NS;  // ring stages
-constexpr int SSEG = 4096;  // reset-row flags per list segment (64 per lane)
-
-// One LDS-DMA wave-instruction: lane l copies 16 bytes from src to LDS byte lds + 16 l (M0 is
-// set and restored inside the statement; lds is wave-uniform).
-__device__ __forceinline__ void sdma16(const void* src, uint32_t lds) {
-    uint32_t keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %2\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, off\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(src), "s"(lds)
-        : "memory");
-}
-
-// s_waitcnt vmcnt(n) for a wave-uniform n < 64 (the count is an immediate)
-__device__ __forceinline__ void wait_vm(int n) {
-    switch (n < 63 ? n : 63) {
-#define WVM(i) \
-    case i: asm volatile("s_waitcnt vmcnt(" #i ")" ::: "memory"); break;
-        WVM(0) WVM(1) WVM(2) WVM(3) WVM(4) WVM(5) WVM(6) WVM(7) WVM(8) WVM(9) WVM(10) WVM(11)
-        WVM(12) WVM(13) WVM(14) WVM(15) WVM(16) WVM(17) WVM(18) WVM(19) WVM(20) WVM(21) WVM(22)
-        WVM(23) WVM(24) WVM(25) WVM(26) WVM(27) WVM(28) WVM(29) WVM(30) WVM(31) WVM(32) WVM(33)
-        WVM(34) WVM(35) WVM(36) WVM(37) WVM(38) WVM(39) WVM(40) WVM(41) WVM(42) WVM(43) WVM(44)
-        WVM(45) WVM(46) WVM(47) WVM(48) WVM(49) WVM(50) WVM(51) WVM(52) WVM(53) WVM(54) WVM(55)
-        WVM(56) WVM(57) WVM(58) WVM(59) WVM(60) WVM(61) WVM(62) WVM(63)
-#undef WVM
-    }
-}
-
-// One pass of wave 0 over rows [0, k) of columns [c0, c0 + 16): acc = ((0 + v0) + v1) + ...
-// with v = x (SQ false) or v = (x - bm)^2 (SQ true), lanes 0-15.
-template <bool SQ>
-__device__ float stream_pass(const float* __restrict__ x, int64_t dim, int64_t c0, int64_t k,
-                             float bm, const float* ring, uint32_t ring_lds) {
-#pragma clang fp contract(off)
-    const int l = threadIdx.x & 63;
-    const int64_t nblk = (k + SRB - 1) / SRB;
-    if (nblk == 0) return 0.0f;
-    // this lane's DMA piece of a block: row 16 b + l / 4, columns c0 + 4 (l % 4) .. + 3 (a
-    // piece past dim reads the row's column c0 instead: never added)
-    const int64_t pc = c0 + 4 * (l & 3) < dim ? c0 + 4 * (l & 3) : c0;
-    const int rl = l >> 2;
-    auto issue = [&](int64_t b) {
-        int64_t r = b * SRB + rl;
-        r = r < k ? r : k - 1;
-        sdma16(x + r * dim + pc, ring_lds + (uint32_t)((b % SNS) * SRB * SXC * 4));
-    };
-    const int64_t pre = nblk < SNS ? nblk : SNS;
-    for (int64_t b = 0; b < pre; ++b) issue(b);
-    const float* lp = ring + (l & 15);
-    float A[SRB], B[SRB];
-    wait_vm((int)(pre - 1));
-#pragma unroll
-    for (int j = 0; j < SRB; ++j) A[j] = lp[j * SXC];
-    float acc = 0.0f;
-    for (int64_t b = 0; b < nblk; ++b) {
-        const int64_t nb = b + 1;
-        if (nb < nblk) {
-            // issued so far: blocks [0, min(nblk, b + SNS)); block nb must have landed
-            const int64_t issued = nblk < b + SNS ? nblk : b + SNS;
-            wait_vm((int)(issued - nb - 1));
-            const float* q = lp + (nb % SNS) * SRB * SXC;
-#pragma unroll
-            for (int j = 0; j < SRB; ++j) B[j] = q[j * SXC];
-        }
-        const int64_t nr = k - b * SRB;
-        if (nr >= SRB) {
-#pragma unroll
-            for (int j = 0; j < SRB; ++j) {
-                float v = A[j];
-                if (SQ) {
-                    v = v - bm;
-                    v = v * v;
-                }
-                acc = acc + v;
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < SRB; ++j) {
-                float v = A[j];
-                if (SQ) {
-                    v = v - bm;
-                    v = v * v;
-                }
-                if (j < nr) acc = acc + v;
-            }
-        }
-        // block b's values are in registers (the adds consumed them): its stage is free
-        if (b + SNS < nblk) issue(b + SNS);
-#pragma unroll
-        for (int j = 0; j < SRB; ++j) A[j] = B[j];
-    }
-    return acc;
-}
+constexpr int RXC = 2;       // columns per workgroup
+constexpr int RSPAN = 2048;  // rows of a span held in LDS
+constexpr int RSEG = 1024;   // reset-row flags per list segment (64 lanes x 16)
 
 // Wave 1: the selected rows of segment [s0, s0 + n) (n <= SEG) -> list[0, cnt) in row order
 // (lane l holds rows s0 + 64 j + l); returns cnt.
@@ -595,74 +499,8 @@ __device__ float reset_pass(const float* __restrict__ xr, const uint8_t* __restr
     return acc;
 }
 
-__global__ __launch_bounds__(128) void rms_exact_stats_kernel(const float* __restrict__ x,
-                                                              int64_t k,
-                                                              const float* __restrict__ xr,
-                                                              const uint8_t* __restrict__ done,
-                                                              int64_t dim, float* __restrict__ st,
-                                                              int64_t* __restrict__ cnts) {
-#pragma clang fp contract(off)
-    __shared__ __attribute__((aligned(16))) float ring[SNS * SRB * SXC];
-    __shared__ int list[SSEG];
-    const int t = threadIdx.x, w = t >> 6, l = t & 63;
-    const int G = (int)gridDim.x, b = (int)blockIdx.x;
-    const int per = (G + 7) / 8;
-    int g = (b % 8) * per + b / 8;
-    if (G % 8 != 0) g = b;  // the remap is a permutation only for G a multiple of 8
-    const int64_t c0 = (int64_t)g * SXC;
-    const int64_t col = c0 + l;
-    if (w == 0) {
-        const uint32_t ring_lds = (uint32_t)(uintptr_t)ring;
-        const float S = stream_pass<false>(x, dim, c0, k, 0.0f, ring, ring_lds);
-        const float kf = (float)k;
-        const float bm = S / kf;
-        const float Q = stream_pass<true>(x, dim, c0, k, bm, ring, ring_lds);
-        if (l < SXC && col < dim) {
-            st[col] = bm;
-            st[dim + col] = Q / kf;
-        }
-        if (b == 0 && l == 0) cnts[0] = k;
-    } else {
-        int64_t nd = 0;
-        const int first =
-            (xr && done && k > 0) ? reset_list<SSEG>(done, 0, k < SSEG ? k : SSEG, list) : 0;
-        float bm2 = 0.0f, bv2 = 0.0f;
-        if (xr && done) {
-            const float S2 = reset_pass<false, SSEG, SXC>(xr, done, k, dim, col, 0.0f, list,
-                                                           k <= SSEG ? first : -1, &nd);
-            if (nd > 0) {
-                const float kf2 = (float)nd;
-                bm2 = S2 / kf2;
-                const float Q2 = reset_pass<true, SSEG, SXC>(xr, done, k, dim, col, bm2, list,
-                                                              k <= SSEG ? first : -1, &nd);
-                bv2 = Q2 / kf2;
-            }
-        }
-        if (l < SXC && col < dim) {
-            st[2 * dim + col] = bm2;
-            st[3 * dim + col] = bv2;
-        }
-        if (b == 0 && l == 0) cnts[1] = nd;
-    }
-}
-
-// The LDS-resident form: RXC = 2 columns per workgroup, the whole span of up to RSPAN rows of
-// them in LDS ([column][row], 33 KB), loaded by LDS-DMA (global_load_lds_dword: one column x
-// 64 rows per wave-instruction, every instruction of a span in flight at once -- one memory
-// latency per span), then exact::chain over each column run (lanes 0-1 of wave 0), the
-// squares in place (wave w: column w), the var chains.  Wave 1 runs the reset rows' two
-// passes (lists of RSEG = 1024 rows, 4 KB) while wave 0 chains.  188 workgroups of 37 KB at
-// D = 376: one fits beside a collect-step workgroup (117 KB) on a CU.
-#ifndef XSTATS_RSPAN
-#define XSTATS_RSPAN 4096
-#endif
-#ifndef XSTATS_XCD
-#define XSTATS_XCD 0
-#endif
-constexpr int RXC = 2;
-constexpr int RSPAN = XSTATS_RSPAN;
-constexpr int RSEG = 1024;
-
+// One LDS-DMA wave-instruction: lane l copies 4 bytes from src to LDS byte lds + 4 l (M0 set and
+// restored inside the statement; lds wave-uniform).
 __device__ __forceinline__ void sdma4(const void* src, uint32_t lds) {
     uint32_t keep;
     asm volatile(
@@ -676,7 +514,7 @@ __device__ __forceinline__ void sdma4(const void* src, uint32_t lds) {
         : "memory");
 }
 
-__global__ __launch_bounds__(128) void rms_exact_stats_res_kernel(
+__global__ __launch_bounds__(128) void rms_exact_stats_kernel(
     const float* __restrict__ x, int64_t k, const float* __restrict__ xr,
     const uint8_t* __restrict__ done, int64_t dim, float* __restrict__ st,
     int64_t* __restrict__ cnts) {
@@ -685,14 +523,10 @@ __global__ __launch_bounds__(128) void rms_exact_stats_res_kernel(
     __shared__ int list[RSEG];
     __shared__ float sbm[RXC];
     const int t = threadIdx.x, w = t >> 6, l = t & 63;
-    int g = (int)blockIdx.x;
-    if (XSTATS_XCD) {
-        // blocks b, b + 8, ... share an XCD: give them consecutive column pairs (the grid is
-        // padded to a multiple of 8; pairs past the last exit)
-        const int per = (int)gridDim.x / 8;
-        g = (g % 8) * per + g / 8;
-        if ((int64_t)g * RXC >= dim) return;
-    }
+    // XCD-aware column order (the grid is padded to a multiple of 8; pairs past the last
+    // exit before any barrier)
+    const int g = ((int)blockIdx.x % 8) * ((int)gridDim.x / 8) + (int)blockIdx.x / 8;
+    if ((int64_t)g * RXC >= dim) return;
     const int64_t c0 = (int64_t)g * RXC;
     const int64_t mycol = c0 + w;  // the column this wave loads and squares
     const int nspan = (int)((k + RSPAN - 1) / RSPAN);
@@ -792,19 +626,9 @@ extern "C" int tsrl_rms_exact_stats(const float* x, int64_t k, const float* rese
     float* st = reinterpret_cast<float*>(stats);
     int64_t* cnts = reinterpret_cast<int64_t*>(reinterpret_cast<char*>(stats) +
                                                (16 * dim + 7) / 8 * 8);
-#ifndef XSTATS_FORM
-#define XSTATS_FORM 2
-#endif
-    if (XSTATS_FORM == 2) {
-        unsigned grid = (unsigned)((dim + tsrl::RXC - 1) / tsrl::RXC);
-        if (XSTATS_XCD) grid = (grid + 7) / 8 * 8;
-        hipLaunchKernelGGL(tsrl::rms_exact_stats_res_kernel, dim3(grid), dim3(128), 0,
-                           as_stream(stream), x, k, reset_x, done, dim, st, cnts);
-    } else {
-        const unsigned grid = (unsigned)((dim + tsrl::SXC - 1) / tsrl::SXC);
-        hipLaunchKernelGGL(tsrl::rms_exact_stats_kernel, dim3(grid), dim3(128), 0,
-                           as_stream(stream), x, k, reset_x, done, dim, st, cnts);
-    }
+    const unsigned grid = (unsigned)(((dim + tsrl::RXC - 1) / tsrl::RXC + 7) / 8 * 8);
+    hipLaunchKernelGGL(tsrl::rms_exact_stats_kernel, dim3(grid), dim3(128), 0,
+                       as_stream(stream), x, k, reset_x, done, dim, st, cnts);
     TSRL_LAUNCH_CHECK("tsrl_rms_exact_stats");
     return 0;
 }

@@ -77,7 +77,10 @@ class Collector:
         # its env rows computed this many launches ahead (csrc/collect.hip E; 0: the serial
         # form, one tsrl_rms_exact_update between launches)
         self.exact_pipeline = 2
-        self.exact_branches = 1  # side streams of the statistics (concurrent statistics)
+        # statistics in flight at once (side streams): two fit on a CU beside a step
+        # workgroup (csrc/rms.hip tsrl_rms_exact_stats; 79-80 ms per 2048-step collect at the
+        # headline shape vs 108 with one and 142 serial)
+        self.exact_branches = 2
         self._xp_streams = None
         self._xp_keep = []
         from tianshou_amd.dist import default_dp
@@ -389,7 +392,7 @@ class Collector:
 
     def _xpipe_scratch(self) -> None:
         """Ring of d + 2 slots (a step's env rows, reset rows, done flags, batch moments),
-        the spec env counters and the side stream of the statistics branch."""
+        the spec env counters and the side streams of the statistics branches."""
         s, b = self._scratch, self._base
         d = int(self.exact_pipeline)
         nsl, k, D, dev = d + 2, self.env_num, b.obs_numel, b.device
@@ -407,11 +410,10 @@ class Collector:
     def _xpipe_steps(self, G: int, sc) -> None:
         """G fused steps with the exact statistic pipelined (inside a graph capture): the spec
         env computes step j's rows d launches before launch j + 1 needs their statistic;
-        tsrl_rms_exact_stats of step j runs on the side stream after the launch (or the
-        head's tsrl_collect_spec_step) that wrote them -- one statistic at a time: a
-        workgroup of it fits on a CU beside a step workgroup, two do not; launch j + 1 waits
-        for it and merges it; tsrl_collect_xpipe_finalize merges the last step's, then
-        _flush runs its add."""
+        tsrl_rms_exact_stats of step j runs on side stream j % exact_branches after the
+        launch (or the head's tsrl_collect_spec_step) that wrote them; launch j + 1 waits for
+        it and merges it; tsrl_collect_xpipe_finalize merges the last step's, then _flush
+        runs its add."""
         s, b = self._scratch, self._base
         rms = self._norm.obs_rms
         lib = _C.lib()

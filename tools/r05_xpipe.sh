@@ -1,13 +1,13 @@
 #!/bin/bash
-# Round-5 pipelined exact obs_rms (csrc/collect.hip E): the statistics kernel alone (resident
-# two-column form vs the streamed form), parity (the new tests, the exact reference goldens,
-# the wide and collect-step tests), then the exact-mode bench pipelined (depth 2, 1, 3) vs
-# serial, the default bench, and a kernel trace of the pipelined form.
+# Round-5 pipelined exact obs_rms (csrc/collect.hip E): the statistics kernel alone, parity
+# (the new tests, the exact reference goldens, the wide and collect-step tests), then the
+# exact-mode bench pipelined (depth 2, 1, 3) vs serial, the default bench, and a kernel trace
+# of the pipelined form.
 export TMPDIR=/tmp
 T="python -u -m pytest -q -x -rf --timeout 200 --timeout-method thread -p no:cacheprovider -m gpu"
 B="python3 bench.py --steps 3 --warmup 2 --no-cpu-baseline"
 tools/gpu_run.sh \
-  "xs:200:for v in main stream; do unset TSRL_LIB_PATH; [ \$v = main ] || export TSRL_LIB_PATH=variants/libtsrl_\$v.so; echo == \$v; timeout -k 10 100 python tools/xstats_bench.py || exit \$?; done" \
+  "xs:200:python tools/xstats_bench.py" \
   "t_x:400:$T tests/test_gpu_xpipe.py tests/test_gpu_rollout.py tests/test_gpu_wide.py tests/test_gpu_collect_step.py" \
   "b_xpipe:300:$B --exact-obs-rms" \
   "b_x1:300:$B --exact-obs-rms --exact-pipeline 1" \
