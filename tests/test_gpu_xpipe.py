@@ -5,8 +5,8 @@ next step launch.  The result must be the serial exact path's, bit for bit.
 
 * tsrl_rms_exact_stats against NumPy's own np.mean / np.var over axis 0 of the f32 rows --
   the reference's arithmetic (statistics.py:93-101) -- for the step rows and the done rows of
-  the reset array, bitwise, over row counts around the 16-row DMA blocks, the 256-row ring
-  and the 4096-row reset-list segment;
+  the reset array, bitwise, over row counts around the 64-row DMA instructions, the 2048-row
+  LDS span and the 1024-row reset-list segment;
 * whole collects (graph replay, several graph lengths and pipeline depths, short episodes so
   that many envs reset per step) against exact_pipeline = 0 (one tsrl_rms_exact_update
   between launches): buffer rows, flags, obs_rms state and the live obs identical.

@@ -206,7 +206,6 @@ constexpr int SH = 20;
 constexpr int IMG_W2 = 0;                              // W2   [64 out][64 in]
 constexpr int IMG_W2T = IMG_W2 + NPL * 2 * H * 64;     // W2^T [64 in][64 out]
 constexpr int IMG_W3 = IMG_W2T + NPL * 2 * H * 64;     // W3   [32 act][64]      (actor)
-constexpr int IMG_W3T = IMG_W3 + NPL * 2 * AMAX * 64;  // W3^T [64][32 act]      (actor)
 
 __device__ __forceinline__ int img_off(int p, int kc, int row, int q, int nkc, int rows) {
     return (p * nkc + kc) * rows * 64 + sw_off(row, q);
@@ -414,7 +413,7 @@ constexpr int I16_ACTOR = I16_W3T + NPL * 4 * 1024, I16_CRITIC = I16_W3;
 constexpr int T16_SCR = T16_NW * 2 * H * SH;
 static_assert(T16_SCR >= T16_NW * 32 * H, "fold scratch");
 static_assert(T16_SCR >= T16_NW * 64 * 18, "vector fold scratch");
-constexpr int T16_V = 0, T16_B2 = 0, T16_B3 = T16_B2 + H, T16_W3C = T16_B3 + AMAX,
+constexpr int T16_B2 = 0, T16_B3 = T16_B2 + H, T16_W3C = T16_B3 + AMAX,
               T16_LS = T16_W3C + H, T16_IV = T16_LS + AMAX, T16_IV2 = T16_IV + AMAX,
               T16_VEND = T16_IV2 + AMAX;
 
