@@ -203,9 +203,6 @@ constexpr int SH = 20;
 // LDS image of the matrix, split once per workgroup into 3 bf16 planes whose rows hold the
 // k in exactly that order.  Image of an [rows][32*nkc] matrix: plane p, 32-k chunk kc, row r
 // at byte ((p*nkc + kc)*rows)*64 + sw_off(r, q), q = 2s + h the 16-byte chunk of (s, h).
-constexpr int IMG_W2 = 0;                              // W2   [64 out][64 in]
-constexpr int IMG_W2T = IMG_W2 + NPL * 2 * H * 64;     // W2^T [64 in][64 out]
-constexpr int IMG_W3 = IMG_W2T + NPL * 2 * H * 64;     // W3   [32 act][64]      (actor)
 
 __device__ __forceinline__ int img_off(int p, int kc, int row, int q, int nkc, int rows) {
     return (p * nkc + kc) * rows * 64 + sw_off(row, q);
@@ -848,7 +845,7 @@ constexpr int E_B2A = 0, E_B2C = E_B2A + H, E_B3 = E_B2C + H, E_W3C = E_B3 + AMA
               E_LS = E_VAR + AMAX, E_END = E_LS + AMAX;
 
 // Round 3: layer 2 and the mu head as bf16x6 products against split weight images (the
-// learn tail's IMG_W2 / IMG_W3 layouts) instead of v_mfma_f32_32x32x2_f32 with one LDS read
+// 32-row image layout above) instead of v_mfma_f32_32x32x2_f32 with one LDS read
 // per MFMA: 2.7x fewer matrix-core cycles per tile.
 constexpr int EV_W2A = 0, EV_W2C = EV_W2A + NPL * 2 * H * 64, EV_W3 = EV_W2C + NPL * 2 * H * 64,
               EV_IMG = EV_W3 + NPL * 2 * AMAX * 64;  // 60 KB: two workgroups per CU
