@@ -30,7 +30,6 @@ import torch  # noqa: E402
 
 GAE_BYTES_PER_TRANSITION = 26  # rew f64 8 + v_s 4 + v_s_ 4 + term 1 + trunc 1 + adv 4 + ret 4
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
-SPIN_CYCLES = 100_000          # device spin ahead of the GAE start event (see GaeTimer)
 
 
 def parse():
@@ -120,12 +119,11 @@ def parse():
 
 
 class GaeTimer:
-    """HIP-event timing of every tsrl_gae launch (on the stream it is launched on).
-
-    A short device-side spin (``torch.cuda._sleep``) is queued before the start event so that
-    the GPU is still busy while the host enqueues the event and the kernel: the event pair
-    then brackets the kernel alone, not host launch latency (the spin costs ~50 us per
-    update, outside the bracket)."""
+    """HIP-event timing of every tsrl_gae launch, on the stream it is launched on: the two
+    events are handed to the library (tsrl_gae_time_next), which launches the GAE kernel with
+    hipExtLaunchKernel so that the events record the kernel's OWN start and stop -- the
+    duration rocprof reports, without the dispatch latency an event pair recorded around the
+    launch also holds (round 4-5: 44-58 us by such a pair vs 38-44 us by rocprof)."""
 
     def __init__(self):
         self.events = []
@@ -133,17 +131,16 @@ class GaeTimer:
         self.on = False
 
     def __call__(self, phase, n):
-        if not self.on:
+        if not self.on or phase != "start":
             return
-        if phase == "start":
-            torch.cuda._sleep(SPIN_CYCLES)
-        ev = torch.cuda.Event(enable_timing=True)
-        ev.record(torch.cuda.current_stream())
-        if phase == "start":
-            self.events.append([ev, None])
-            self.n = n
-        else:
-            self.events[-1][1] = ev
+        from tianshou_amd import _C
+        pair = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
+        for ev in pair:  # create the events (torch creates them at their first record)
+            ev.record(torch.cuda.current_stream())
+        _C.check(_C.lib().tsrl_gae_time_next(pair[0].cuda_event, pair[1].cuda_event),
+                 "tsrl_gae_time_next")
+        self.events.append(pair)
+        self.n = n
 
     def each_ms(self):
         return [a.elapsed_time(b) for a, b in self.events if b is not None]

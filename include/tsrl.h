@@ -67,6 +67,12 @@ int tsrl_gae_f64v(const double* v_s, const double* v_s_next, const double* rew,
                   double* adv64_out, double* ret64_out, void* workspace,
                   int64_t workspace_bytes, void* stream);
 
+/* Diagnostic (bench.py's roofline): the next row-path (row_len > 0) tsrl_gae call of this host
+ * thread launches its kernel with hipExtLaunchKernel, which records the kernel's own start /
+ * stop timestamps into these two HIP events (hipEvent_t, created with timing); NULL, NULL
+ * clears.  The 3-phase general path ignores them. */
+int tsrl_gae_time_next(void* start_event, void* stop_event);
+
 /* Merge (count, mean, M2) partials into a RunningMeanStd held on device as
  * double rms[3] = {mean, var, count}  (statistics.py:93-114, Chan parallel merge). */
 int tsrl_ret_rms_update(const double* partials, int64_t nparts, double* rms, void* stream);

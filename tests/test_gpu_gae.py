@@ -229,3 +229,32 @@ def test_gae_staged_rows_kernel(dev, envs, steps, scaled, monkeypatch):
         if scaled else v_s.cpu().numpy(), 0.99, 0.95)
     _tol(a0, adv_o)
     _tol(r0, ret_o / s)
+
+
+def test_gae_time_next_kernel_events(dev):
+    """tsrl_gae_time_next (bench.py's roofline timer): the next row-path launch records its
+    kernel's start / stop into the two HIP events (hipExtLaunchKernel) -- outputs unchanged,
+    a positive duration -- and the setting is consumed by that one launch."""
+    from tianshou_amd.policy.base import gae_device
+    from tianshou_amd import _C
+    envs, steps = 1024, 2048
+    g = torch.Generator(device=dev).manual_seed(5)
+    n = envs * steps
+    v_s = torch.randn(n, device=dev, generator=g)
+    v_n = torch.randn(n, device=dev, generator=g)
+    rew = torch.rand(n, device=dev, generator=g, dtype=torch.float64)
+    u = torch.rand(n, device=dev, generator=g)
+    term, trunc = u < 0.002, u > 0.998
+    plain = gae_device(v_s, v_n, rew, term, trunc, 0.99, 0.95, steps)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    b.record()
+    assert _C.lib().tsrl_gae_time_next(a.cuda_event, b.cuda_event) == 0
+    timed = gae_device(v_s, v_n, rew, term, trunc, 0.99, 0.95, steps)
+    again = gae_device(v_s, v_n, rew, term, trunc, 0.99, 0.95, steps)  # no events: consumed
+    torch.cuda.synchronize()
+    ms = a.elapsed_time(b)
+    assert 0.0 < ms < 50.0, ms
+    for x, y, z in zip(plain[:2], timed[:2], again[:2]):
+        assert torch.equal(x, y) and torch.equal(x, z)
+    assert _C.lib().tsrl_gae_time_next(a.cuda_event, None) != 0  # both or neither

@@ -15,6 +15,8 @@
 // reference's separately-rounded NumPy/Python operations.
 // Algorithmic traffic: 26 B/transition (rew f64, v_s f32, v_s_ f32, term u8, trunc u8,
 // adv f32, ret f32).
+#include <hip/hip_ext.h>
+
 #include "tsrl_common.h"
 
 #pragma clang fp contract(off)
@@ -670,6 +672,21 @@ extern "C" int64_t tsrl_gae_num_partials(int64_t n, int64_t row_len) {
     return (n + TILE - 1) / TILE;
 }
 
+// tsrl_gae_time_next: HIP events the NEXT row-path tsrl_gae launch of this host thread
+// records its kernel's start / stop into (bench.py's roofline: the kernel's own duration on
+// its launch stream, not an event pair around the launch, which also holds the dispatch)
+namespace {
+thread_local hipEvent_t g_time_start = nullptr, g_time_stop = nullptr;
+}
+
+extern "C" int tsrl_gae_time_next(void* start_event, void* stop_event) {
+    TSRL_CHECK_ARG((start_event == nullptr) == (stop_event == nullptr),
+                   "tsrl_gae_time_next: both events or neither");
+    g_time_start = reinterpret_cast<hipEvent_t>(start_event);
+    g_time_stop = reinterpret_cast<hipEvent_t>(stop_event);
+    return 0;
+}
+
 extern "C" int tsrl_gae(const float* v_s, const float* v_s_next, const double* rew,
                         const uint8_t* terminated, const uint8_t* truncated,
                         const uint8_t* end_extra, int64_t n, int64_t row_len,
@@ -716,22 +733,25 @@ extern "C" int tsrl_gae(const float* v_s, const float* v_s_next, const double* r
         TSRL_CHECK_ARG(grid < (1ll << 31), "tsrl_gae: too many ranges");
         const bool staged = vec_ok && !adv64_out && !ret64_out && r % TILE == 0 &&
                             n % r == 0 && !getenv("TSRL_GAE_UNSTAGED");
+        // tsrl_gae_time_next: the launch's own start / stop timestamps (hipExtLaunchKernel)
+        hipEvent_t t0 = g_time_start, t1 = g_time_stop;
+        g_time_start = g_time_stop = nullptr;
         if (staged) {
             if (f64v)
-                hipLaunchKernelGGL(gae_rows_staged_kernel<true>, dim3((unsigned)grid), dim3(TPB),
-                                   0, s, p, r);
+                hipExtLaunchKernelGGL(gae_rows_staged_kernel<true>, dim3((unsigned)grid),
+                                      dim3(TPB), 0, s, t0, t1, 0, p, r);
             else
-                hipLaunchKernelGGL(gae_rows_staged_kernel<false>, dim3((unsigned)grid), dim3(TPB),
-                                   0, s, p, r);
+                hipExtLaunchKernelGGL(gae_rows_staged_kernel<false>, dim3((unsigned)grid),
+                                      dim3(TPB), 0, s, t0, t1, 0, p, r);
             TSRL_LAUNCH_CHECK("tsrl_gae(rows, staged)");
             return 0;
         }
         if (f64v)
-            hipLaunchKernelGGL(gae_rows_kernel<true>, dim3((unsigned)grid), dim3(TPB), 0, s, p, r,
-                               vec_ok);
+            hipExtLaunchKernelGGL(gae_rows_kernel<true>, dim3((unsigned)grid), dim3(TPB), 0, s,
+                                  t0, t1, 0, p, r, vec_ok);
         else
-            hipLaunchKernelGGL(gae_rows_kernel<false>, dim3((unsigned)grid), dim3(TPB), 0, s, p,
-                               r, vec_ok);
+            hipExtLaunchKernelGGL(gae_rows_kernel<false>, dim3((unsigned)grid), dim3(TPB), 0, s,
+                                  t0, t1, 0, p, r, vec_ok);
         TSRL_LAUNCH_CHECK("tsrl_gae(rows)");
         return 0;
     }

@@ -89,6 +89,7 @@ _SIGS = {
     "tsrl_last_error": ([], ctypes.c_char_p),
     "tsrl_gae_workspace_bytes": ([_i64, _i64], _i64),
     "tsrl_gae_num_partials": ([_i64, _i64], _i64),
+    "tsrl_gae_time_next": ([_p, _p], ctypes.c_int),
     "tsrl_gae": ([_p, _p, _p, _p, _p, _p, _i64, _i64, _p, _d, _d, _p, _p, _p, _p, _p, _p, _i64,
                   _p], ctypes.c_int),
     "tsrl_gae_f64v": ([_p, _p, _p, _p, _p, _p, _i64, _i64, _d, _d, _p, _p, _p, _i64, _p],
