@@ -1252,9 +1252,12 @@ int tail_grid(int64_t n) {
     return (int)std::min<int64_t>(g, 256);
 }
 
+#ifndef DW_NSPLIT_MAX
+#define DW_NSPLIT_MAX 170
+#endif
 int dw_nsplit(int64_t n) {
     // ~512 resident workgroups on 256 CUs (3 column tiles at D=376), >= 64 rows per split
-    int64_t s = std::max<int64_t>(1, std::min<int64_t>(170, n / 64));
+    int64_t s = std::max<int64_t>(1, std::min<int64_t>(DW_NSPLIT_MAX, n / 64));
     // a multiple of 8 (XCD-aware tile order in dw_x6_kernel) once there are 8 or more
     if (s >= 8) s &= ~int64_t(7);
     return (int)s;
