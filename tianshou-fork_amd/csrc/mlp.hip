@@ -1252,12 +1252,11 @@ int tail_grid(int64_t n) {
     return (int)std::min<int64_t>(g, 256);
 }
 
-#ifndef DW_NSPLIT_MAX
-#define DW_NSPLIT_MAX 170
-#endif
 int dw_nsplit(int64_t n) {
-    // ~512 resident workgroups on 256 CUs (3 column tiles at D=376), >= 64 rows per split
-    int64_t s = std::max<int64_t>(1, std::min<int64_t>(DW_NSPLIT_MAX, n / 64));
+    // ~512 resident workgroups on 256 CUs (3 column tiles at D=376), >= 64 rows per split.
+    // Round 5 A/B of the cap (profiles/r05_learn_ab.log, dw + reduce per 262144 rows): 64 /
+    // 96 / 128 / 168 / 208 / 256 splits -> 340 / 306 / 263 / 228-241 / 291-298 / 273-278 us
+    int64_t s = std::max<int64_t>(1, std::min<int64_t>(170, n / 64));
     // a multiple of 8 (XCD-aware tile order in dw_x6_kernel) once there are 8 or more
     if (s >= 8) s &= ~int64_t(7);
     return (int)s;

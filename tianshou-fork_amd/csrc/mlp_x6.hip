@@ -325,13 +325,15 @@ template <bool TANH>
 __global__ __launch_bounds__(RNW * 64, 1) void l1_ring_kernel(
     const float* __restrict__ X, int64_t ldx, const int64_t* __restrict__ idx, int64_t n,
     int64_t ntiles, int Kp, int dq, const __bf16* __restrict__ wsp, const float* __restrict__ ba,
-    const float* __restrict__ bc, float* __restrict__ out, int64_t frag_tiles) {
+    const float* __restrict__ bc, float* __restrict__ out, int64_t frag_tiles, int tpw) {
     __shared__ __attribute__((aligned(16))) char sm[RLDS];
     const int t = threadIdx.x;
     const int w = __builtin_amdgcn_readfirstlane(t >> 6);
     const int l = t & 63, h = l >> 5, c = l & 31;
-    const int64_t tile0 = (int64_t)blockIdx.x * RTPW;
-    const int ntl = (int)min((int64_t)RTPW, ntiles - tile0);
+    // tpw (<= RTPW) tiles per workgroup: RTPW once the grid fills the chip, fewer for small
+    // row counts (more workgroups)
+    const int64_t tile0 = (int64_t)blockIdx.x * tpw;
+    const int ntl = (int)min((int64_t)tpw, ntiles - tile0);
     const int nch = Kp / KC;
     const int C = ntl * nch;
     float* sb = reinterpret_cast<float*>(sm + RBOFF);
@@ -549,17 +551,20 @@ extern "C" int tsrl_mlp_l1_fwd_x6(const float* X, int64_t ldx, const int64_t* id
         // of tsrl_mlp_frag_floats(n)
         const int64_t ntiles = (n + RROWS - 1) / RROWS;
         const int64_t frag_tiles = (n + XR - 1) / XR * (XR / 32);
-        const unsigned grid = (unsigned)((ntiles + RTPW - 1) / RTPW);
+        // tiles per workgroup: RTPW when that still gives a workgroup per CU, fewer below
+        // (config 2's 2048-row minibatches: 8 tiles on 8 workgroups instead of 2)
+        const int64_t tpw = std::max<int64_t>(1, std::min<int64_t>(RTPW, ntiles / n_cus()));
+        const unsigned grid = (unsigned)((ntiles + tpw - 1) / tpw);
         if (act_tanh)
             hipLaunchKernelGGL(l1_ring_kernel<true>, dim3(grid), dim3(RNW * 64), 0,
                                as_stream(stream), X, ldx, idx, n, ntiles, (int)kpad32(D),
                                (int)((D + 3) / 4 * 4), reinterpret_cast<const __bf16*>(wsplit),
-                               ba, bc, out, frag_tiles);
+                               ba, bc, out, frag_tiles, (int)tpw);
         else
             hipLaunchKernelGGL(l1_ring_kernel<false>, dim3(grid), dim3(RNW * 64), 0,
                                as_stream(stream), X, ldx, idx, n, ntiles, (int)kpad32(D),
                                (int)((D + 3) / 4 * 4), reinterpret_cast<const __bf16*>(wsplit),
-                               ba, bc, out, frag_tiles);
+                               ba, bc, out, frag_tiles, (int)tpw);
         TSRL_LAUNCH_CHECK("tsrl_mlp_l1_fwd_x6(ring)");
         return 0;
     }

@@ -240,15 +240,7 @@ extern "C" int tsrl_clip_adam(float* param, float* grad, float* exp_avg, float* 
     // the in-kernel slice-norm hand-off needs every workgroup resident at once: up to one
     // slice per CU of this device (hipDeviceAttributeMultiprocessorCount, 256 on MI355X);
     // larger parameter sets take the separate norm launch
-    static int n_cu = 0;
-    if (n_cu == 0) {
-        int dev = 0, cu = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            cu = 1;
-        n_cu = cu > 0 ? cu : 1;
-    }
-    const int fused_norm = grid <= n_cu;
+    const int fused_norm = grid <= n_cus();
     if (max_norm > 0.0f && !fused_norm) {
         hipLaunchKernelGGL(norm_partials_kernel, dim3((unsigned)grid), dim3(OTPB), 0,
                            as_stream(stream), grad, n, partials);

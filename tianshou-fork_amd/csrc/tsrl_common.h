@@ -35,6 +35,20 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 
 __host__ __device__ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+// Compute units of the current device (hipDeviceAttributeMultiprocessorCount: 256 on MI355X),
+// queried once per process; 1 if the query fails.
+inline int n_cus() {
+    static int n = 0;
+    if (n == 0) {
+        int dev = 0, cu = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cu = 1;
+        n = cu > 0 ? cu : 1;
+    }
+    return n;
+}
+
 // splitmix64 finaliser of (x + golden gamma): the counter-based hash of the synthetic env
 // (oracle/synth_env.py restates it on the CPU).
 __host__ __device__ __forceinline__ uint64_t sm64(uint64_t x) {
