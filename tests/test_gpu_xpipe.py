@@ -92,7 +92,9 @@ def _run(dev, depth, E, D, A, L, T, G, seed=3):
 
 
 @pytest.mark.parametrize("E,D,L,T,G", [(64, 8, 3, 12, 4), (512, 376, 5, 10, 4),
-                                       (4096, 376, 7, 16, 8)])
+                                       (4096, 376, 7, 16, 8),
+                                       # every env resets every step; a partial 16-row tile
+                                       (100, 20, 1, 9, 2), (37, 12, 2, 7, 6)])
 @pytest.mark.parametrize("depth", [1, 2, 3])
 def test_pipelined_exact_collect_equals_serial(dev, E, D, L, T, G, depth):
     ref = _run(dev, 0, E, D, 6, L, T, G)
