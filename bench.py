@@ -88,10 +88,13 @@ def parse():
     ap.add_argument("--exact-pipeline", type=int, default=None,
                     help="with --exact-obs-rms: env rows computed this many steps ahead and the "
                          "f32 statistic on a second graph branch (Collector.exact_pipeline, "
-                         "default 2; 0: serial, one exact update between step launches)")
+                         "default 5; 0: serial, one exact update between step launches)")
+    ap.add_argument("--exact-group", type=int, default=None,
+                    help="diagnostic: steps per statistics launch of the pipelined exact "
+                         "obs_rms (Collector.exact_group, default 2)")
     ap.add_argument("--exact-branches", type=int, default=None,
                     help="diagnostic: concurrent statistics streams of the pipelined exact "
-                         "obs_rms (Collector.exact_branches, default 1)")
+                         "obs_rms (Collector.exact_branches; one when groups > 1)")
     ap.add_argument("--force-dp", action="store_true",
                     help="diagnostic: under torch.distributed.run with ONE rank, run the "
                          "data-parallel code path (RCCL collectives over a one-rank "
@@ -317,6 +320,8 @@ def main():
             coll.exact_pipeline = args.exact_pipeline
         if args.exact_branches is not None:
             coll.exact_branches = args.exact_branches
+        if args.exact_group is not None:
+            coll.exact_group = args.exact_group
     torch.manual_seed(rank)  # per-rank action sampling streams
     policy.graph_learn = {"auto": None, "on": True, "off": False}[args.graph_learn]
     policy.sort_minibatch = args.perm in ("sorted", "numpy-sorted")
@@ -435,7 +440,8 @@ def main():
                        "rccl_world_size": world if distributed else None,
                        "learn_graph": args.graph_learn,
                        "obs_rms": ("exact f32 (reference arithmetic), " + (
-                           f"pipelined {coll.exact_pipeline} steps ahead"
+                           f"pipelined {coll.exact_pipeline} steps ahead, statistics "
+                           f"{coll._xpipe_group()} steps per launch"
                            if coll._xpipe_ok() else "serial")) if args.exact_obs_rms
                        else ("f64 moments (atomic), action-coupled env" if args.act_coef
                              else "exact int64 moments (quantised synthetic obs), f64 merge"),

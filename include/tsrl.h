@@ -349,6 +349,12 @@ int tsrl_collect_xpipe_finalize(const tsrl_collect_args* a, void* stream);
 int64_t tsrl_rms_exact_stats_bytes(int64_t dim);
 int tsrl_rms_exact_stats(const float* x, int64_t k, const float* reset_x, const uint8_t* done,
                          int64_t dim, void* stats, void* stream);
+/* The same for nsteps <= 4 steps in one launch (host arrays of the per-step pointers): the
+ * pipelined collect computes two steps' statistics per launch, one graph edge fewer per
+ * two steps. */
+int tsrl_rms_exact_stats_n(int nsteps, const float* const* x, const float* const* reset_x,
+                           const uint8_t* const* done, int64_t k, int64_t dim,
+                           void* const* stats, void* stream);
 /* *rel_dev = (*rel_dev + 1) % ring_size (device-side ring cursor for graph-captured steps). */
 int tsrl_ring_advance(int64_t* rel_dev, int64_t ring_size, void* stream);
 

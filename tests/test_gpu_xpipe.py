@@ -62,7 +62,8 @@ def test_exact_stats_equal_numpy(dev, k, D, p):
         assert np.array_equal(f[3], np.var(xr[done], axis=0)), "reset-row var"
 
 
-def _run(dev, depth, E, D, A, L, T, G, seed=3):
+def _run(dev, depth, E, D, A, L, T, G, seed=3, group=1):
+    """One collect of E * T steps at pipeline depth / statistics group (depth 0: serial)."""
     from tianshou_amd.data import Collector, VectorReplayBuffer
     from tianshou_amd.env import Box, SyntheticVectorEnv, VectorEnvNormObs
     from tianshou_amd.policy import PPOPolicy
@@ -78,6 +79,7 @@ def _run(dev, depth, E, D, A, L, T, G, seed=3):
     c = Collector(policy, env, buf)
     c.graph_steps = G
     c.exact_pipeline = depth
+    c.exact_group = group
     torch.manual_seed(seed + 1)
     res = c.collect(n_step=E * T)
     assert c._step_on
@@ -99,5 +101,17 @@ def _run(dev, depth, E, D, A, L, T, G, seed=3):
 def test_pipelined_exact_collect_equals_serial(dev, E, D, L, T, G, depth):
     ref = _run(dev, 0, E, D, 6, L, T, G)
     got = _run(dev, depth, E, D, 6, L, T, G)
+    for k in ref:
+        assert np.array_equal(np.asarray(got[k]), np.asarray(ref[k])), k
+
+
+@pytest.mark.parametrize("E,D,L,T,G", [(64, 8, 3, 12, 4), (512, 376, 5, 10, 6),
+                                       (4096, 376, 7, 16, 8), (100, 20, 1, 9, 2)])
+@pytest.mark.parametrize("depth,group", [(3, 2), (4, 2), (4, 3), (5, 2)])
+def test_pipelined_exact_grouped_equals_serial(dev, E, D, L, T, G, depth, group):
+    """Several steps' statistics per launch (tsrl_rms_exact_stats_n, Collector.exact_group):
+    the same bits as the serial form, for graph lengths that do and do not divide evenly."""
+    ref = _run(dev, 0, E, D, 6, L, T, G)
+    got = _run(dev, depth, E, D, 6, L, T, G, group=group)
     for k in ref:
         assert np.array_equal(np.asarray(got[k]), np.asarray(ref[k])), k

@@ -514,18 +514,34 @@ __device__ __forceinline__ void sdma4(const void* src, uint32_t lds) {
         : "memory");
 }
 
-__global__ __launch_bounds__(128) void rms_exact_stats_kernel(
-    const float* __restrict__ x, int64_t k, const float* __restrict__ xr,
-    const uint8_t* __restrict__ done, int64_t dim, float* __restrict__ st,
-    int64_t* __restrict__ cnts) {
+// Up to XSTEPS steps' statistics in one launch (tsrl_rms_exact_stats_n): workgroup b works on
+// step b / G8, column pair of (b % G8) (G8 = the per-step grid, a multiple of 8).
+constexpr int XSTEPS = 4;
+struct XSteps {
+    const float* x[XSTEPS];
+    const float* xr[XSTEPS];
+    const uint8_t* done[XSTEPS];
+    float* st[XSTEPS];
+    int64_t* cnts[XSTEPS];
+    int g8;
+};
+
+__global__ __launch_bounds__(128) void rms_exact_stats_kernel(XSteps P, int64_t k,
+                                                              int64_t dim) {
 #pragma clang fp contract(off)
     __shared__ __attribute__((aligned(16))) float col[RXC][RSPAN + 4];
     __shared__ int list[RSEG];
     __shared__ float sbm[RXC];
     const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    const int sidx = (int)blockIdx.x / P.g8, bl = (int)blockIdx.x % P.g8;
+    const float* __restrict__ x = P.x[sidx];
+    const float* __restrict__ xr = P.xr[sidx];
+    const uint8_t* __restrict__ done = P.done[sidx];
+    float* __restrict__ st = P.st[sidx];
+    int64_t* __restrict__ cnts = P.cnts[sidx];
     // XCD-aware column order (the grid is padded to a multiple of 8; pairs past the last
     // exit before any barrier)
-    const int g = ((int)blockIdx.x % 8) * ((int)gridDim.x / 8) + (int)blockIdx.x / 8;
+    const int g = (bl % 8) * (P.g8 / 8) + bl / 8;
     if ((int64_t)g * RXC >= dim) return;
     const int64_t c0 = (int64_t)g * RXC;
     const int64_t mycol = c0 + w;  // the column this wave loads and squares
@@ -615,20 +631,35 @@ extern "C" int64_t tsrl_rms_exact_stats_bytes(int64_t dim) {
     return dim > 0 ? (16 * dim + 7) / 8 * 8 + 16 : 0;
 }
 
-extern "C" int tsrl_rms_exact_stats(const float* x, int64_t k, const float* reset_x,
-                                    const uint8_t* done, int64_t dim, void* stats, void* stream) {
-    TSRL_CHECK_ARG(x && stats && dim > 0 && dim % 4 == 0 && k >= 0 && aligned16(x) &&
-                       (reset_x == nullptr) == (done == nullptr) &&
-                       (reset_x == nullptr || aligned16(reset_x)) &&
-                       (reinterpret_cast<uintptr_t>(stats) & 7u) == 0,
-                   "tsrl_rms_exact_stats: bad arguments (dim %% 4 == 0, 16-byte aligned rows, "
-                   "8-byte aligned stats)");
-    float* st = reinterpret_cast<float*>(stats);
-    int64_t* cnts = reinterpret_cast<int64_t*>(reinterpret_cast<char*>(stats) +
+extern "C" int tsrl_rms_exact_stats_n(int nsteps, const float* const* x,
+                                      const float* const* reset_x, const uint8_t* const* done,
+                                      int64_t k, int64_t dim, void* const* stats, void* stream) {
+    TSRL_CHECK_ARG(nsteps >= 1 && nsteps <= tsrl::XSTEPS && x && reset_x && done && stats &&
+                       dim > 0 && dim % 4 == 0 && k >= 0,
+                   "tsrl_rms_exact_stats_n: 1 <= nsteps <= %d, dim %% 4 == 0", tsrl::XSTEPS);
+    tsrl::XSteps S{};
+    for (int i = 0; i < nsteps; ++i) {
+        TSRL_CHECK_ARG(x[i] && stats[i] && aligned16(x[i]) &&
+                           (reset_x[i] == nullptr) == (done[i] == nullptr) &&
+                           (reset_x[i] == nullptr || aligned16(reset_x[i])) &&
+                           (reinterpret_cast<uintptr_t>(stats[i]) & 7u) == 0,
+                       "tsrl_rms_exact_stats: bad arguments (16-byte aligned rows, 8-byte "
+                       "aligned stats)");
+        S.x[i] = x[i];
+        S.xr[i] = reset_x[i];
+        S.done[i] = done[i];
+        S.st[i] = reinterpret_cast<float*>(stats[i]);
+        S.cnts[i] = reinterpret_cast<int64_t*>(reinterpret_cast<char*>(stats[i]) +
                                                (16 * dim + 7) / 8 * 8);
-    const unsigned grid = (unsigned)(((dim + tsrl::RXC - 1) / tsrl::RXC + 7) / 8 * 8);
-    hipLaunchKernelGGL(tsrl::rms_exact_stats_kernel, dim3(grid), dim3(128), 0,
-                       as_stream(stream), x, k, reset_x, done, dim, st, cnts);
+    }
+    S.g8 = (int)(((dim + tsrl::RXC - 1) / tsrl::RXC + 7) / 8 * 8);
+    hipLaunchKernelGGL(tsrl::rms_exact_stats_kernel, dim3((unsigned)(S.g8 * nsteps)), dim3(128),
+                       0, as_stream(stream), S, k, dim);
     TSRL_LAUNCH_CHECK("tsrl_rms_exact_stats");
     return 0;
+}
+
+extern "C" int tsrl_rms_exact_stats(const float* x, int64_t k, const float* reset_x,
+                                    const uint8_t* done, int64_t dim, void* stats, void* stream) {
+    return tsrl_rms_exact_stats_n(1, &x, &reset_x, &done, k, dim, &stats, stream);
 }

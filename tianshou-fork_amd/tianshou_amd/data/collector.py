@@ -11,6 +11,7 @@ Two paths behind the reference API:
   statistics are gathered once at the end.
 * generic (any other env): the reference's loop, with the buffer still in HBM.
 """
+import ctypes
 import time
 import warnings
 from typing import Any, Callable, Dict, Optional
@@ -76,11 +77,15 @@ class Collector:
         # f32 statistic of step i runs on a second graph branch while the step launches go on,
         # its env rows computed this many launches ahead (csrc/collect.hip E; 0: the serial
         # form, one tsrl_rms_exact_update between launches)
-        self.exact_pipeline = 2
-        # statistics in flight at once (side streams): two fit on a CU beside a step
-        # workgroup (csrc/rms.hip tsrl_rms_exact_stats; 79-80 ms per 2048-step collect at the
-        # headline shape vs 108 with one and 142 serial)
+        self.exact_pipeline = 5
+        # statistics launches in flight at once (side streams); with groups of 2 one branch
+        # (a group's workgroups already fill the room beside the step launches)
         self.exact_branches = 2
+        # steps per statistics launch (tsrl_rms_exact_stats_n; <= exact_pipeline - 1): one
+        # cross-branch graph edge per group.  Headline shape, collect per 2048 steps
+        # (profiles/r05_xpipe_ab.log): depth 2 / group 1 / 2 branches 79 ms, depth 4 / group 2
+        # 69, depth 5 / group 2 65, depth 6 / group 2 69, group 3 86, serial 142
+        self.exact_group = 2
         self._xp_streams = None
         self._xp_keep = []
         from tianshou_amd.dist import default_dp
@@ -404,43 +409,53 @@ class Collector:
             s["xp_stats"] = torch.zeros((nsl, nb), dtype=torch.uint8, device=dev)
             s["xp_spec"] = torch.zeros((2, k), dtype=torch.int64, device=dev)
         nbr = max(1, min(int(self.exact_branches), d))
+        if self._xpipe_group() > 1:
+            nbr = 1  # a group's workgroups already fill the room beside the step launches
         if self._xp_streams is None or len(self._xp_streams) != nbr:
             self._xp_streams = [torch.cuda.Stream(device=dev) for _ in range(nbr)]
 
     def _xpipe_steps(self, G: int, sc) -> None:
         """G fused steps with the exact statistic pipelined (inside a graph capture): the spec
-        env computes step j's rows d launches before launch j + 1 needs their statistic;
-        tsrl_rms_exact_stats of step j runs on side stream j % exact_branches after the
-        launch (or the head's tsrl_collect_spec_step) that wrote them; launch j + 1 waits for
-        it and merges it; tsrl_collect_xpipe_finalize merges the last step's, then _flush
-        runs its add."""
+        env computes step j's rows d launches before launch j + 1 needs their statistic; the
+        statistics of m = exact_group consecutive steps run as ONE tsrl_rms_exact_stats_n
+        launch (on side stream q % exact_branches for group q) after the launch (or the
+        head's tsrl_collect_spec_step) that wrote the group's last rows; launch j + 1 waits
+        for its group (one cross-branch graph edge per group, not per step) and merges step
+        j's; tsrl_collect_xpipe_finalize merges the last step's, then _flush runs its add."""
         s, b = self._scratch, self._base
-        rms = self._norm.obs_rms
         lib = _C.lib()
-        d = int(self.exact_pipeline)
+        d, m = int(self.exact_pipeline), self._xpipe_group()
         nsl, k, D = d + 2, self.env_num, b.obs_numel
         main = torch.cuda.current_stream(b.device)
         raw, rst, dn, st, spec = (s[x] for x in ("xp_raw", "xp_reset", "xp_done", "xp_stats",
                                                  "xp_spec"))
-        ev_stats = {}
+        ev_group = {}
         # the events outlive the capture (destroyed before the next one begins, not inside it)
         keep = self._xp_keep
 
         def spec_of(j):
             return spec[0], spec[1], raw[j % nsl], rst[j % nsl], dn[j % nsl]
 
-        def stats(j):
+        def group_stats(q):  # the rows of group q's steps are written (on main)
+            steps = range(m * q, min(m * q + m, G))
             ev = torch.cuda.Event()
-            ev.record(main)  # step j's rows are written
-            side = self._xp_streams[j % len(self._xp_streams)]
+            ev.record(main)
+            side = self._xp_streams[q % len(self._xp_streams)]
             side.wait_event(ev)
             keep.append(ev)
-            _C.check(lib.tsrl_rms_exact_stats(_C.ptr(raw[j % nsl]), k, _C.ptr(rst[j % nsl]),
-                                              _C.ptr(dn[j % nsl]), D, _C.ptr(st[j % nsl]),
-                                              side.cuda_stream), "tsrl_rms_exact_stats")
-            ev_stats[j] = torch.cuda.Event()
-            ev_stats[j].record(side)
-            keep.append(ev_stats[j])
+            n = len(steps)
+            arr = lambda ts: (ctypes.c_void_p * n)(*[_C.ptr(t) for t in ts])  # noqa: E731
+            _C.check(lib.tsrl_rms_exact_stats_n(
+                n, arr([raw[j % nsl] for j in steps]), arr([rst[j % nsl] for j in steps]),
+                arr([dn[j % nsl] for j in steps]), k, D, arr([st[j % nsl] for j in steps]),
+                side.cuda_stream), "tsrl_rms_exact_stats_n")
+            ev_group[q] = torch.cuda.Event()
+            ev_group[q].record(side)
+            keep.append(ev_group[q])
+
+        def rows_written(j):  # step j's rows now exist: launch its group once complete
+            if j == G - 1 or (j + 1) % m == 0:
+                group_stats(j // m)
 
         for j in range(min(d, G)):
             c = _C.CollectArgs()
@@ -450,28 +465,34 @@ class Collector:
                 _C.ptr(x) for x in spec_of(j))
             _C.check(lib.tsrl_collect_spec_step(c, int(j == 0), main.cuda_stream),
                      "tsrl_collect_spec_step")
-            stats(j)
+            rows_written(j)
         c = None
         for i in range(G):
-            if i > 0:
-                main.wait_event(ev_stats[i - 1])
+            if i > 0 and (i - 1) % m == 0:  # the group of step i - 1 (later members: waited)
+                main.wait_event(ev_group[(i - 1) // m])
             xp = dict(i=i, stats_prev=st[(i - 1) % nsl] if i > 0 else None,
                       spec=spec_of(i + d) if i + d < G else None, rows=raw[i % nsl],
                       reset_rows=rst[i % nsl])
             c = self._fused_box_step(self._scratch["cur"], k, dict(
                 rel_dev=sc[i % 2, 0:1], rel_next=sc[(i + 1) % 2, 0:1]), xp=xp)
             if i + d < G:
-                stats(i + d)
-        main.wait_event(ev_stats[G - 1])
+                rows_written(i + d)
+        if (G - 1) % m == 0:  # the last step opens its group: no launch waited for it
+            main.wait_event(ev_group[(G - 1) // m])
         c.xstats = _C.ptr(st[(G - 1) % nsl])
         _C.check(lib.tsrl_collect_xpipe_finalize(c, main.cuda_stream),
                  "tsrl_collect_xpipe_finalize")
         self._flush()
-        for side in self._xp_streams[:min(len(self._xp_streams), G)]:  # join the forks
+        for side in self._xp_streams[:min(len(self._xp_streams), -(-G // m))]:  # join forks
             ev = torch.cuda.Event()
             ev.record(side)
             main.wait_event(ev)
             keep.append(ev)
+
+    def _xpipe_group(self) -> int:
+        """Steps per statistics launch: the group's last rows must exist d launches before
+        its first step's statistic is merged, so m <= d - 1 (m = 1 below depth 2)."""
+        return max(1, min(int(self.exact_group), int(self.exact_pipeline) - 1))
 
     def _flush(self) -> None:
         """Run the pending buffer add of the last fused step (tsrl_buffer_add), after merging
@@ -565,7 +586,8 @@ class Collector:
             ptrs += [r.mean_t.data_ptr(), r.var_t.data_ptr(), r.count_t.data_ptr(),
                      self._norm.update_obs_rms]
         return (G, self.policy.training, self.exploration_noise, self._fused_act_on,
-                self._step_on, self.exact_pipeline if self._xpipe_ok() else 0, tuple(ptrs))
+                self._step_on, (self.exact_pipeline, self.exact_branches, self._xpipe_group())
+                if self._xpipe_ok() else 0, tuple(ptrs))
 
     def _replay_steps(self, no_grad, n_steps: int, written: list) -> int:
         """Run up to n_steps uniform steps as replays of captured HIP graphs of G steps
