@@ -880,80 +880,114 @@ __global__ __launch_bounds__(256, 2) void eval_tail_kernel(const float* __restri
     __syncthreads();
     const float b3c = wt.b3c[0];
     const int64_t ntiles = (n + 31) / 32;
-    for (int64_t bt = (int64_t)blockIdx.x * 4 + w; bt < ntiles; bt += (int64_t)gridDim.x * 4) {
+    // one net's two layer-1 tiles of row tile bt (fragment layout, 32 floats per lane)
+    auto load_unit = [&](int64_t bt, int net, float (&h1)[2][16]) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const float4* src = reinterpret_cast<const float4*>(
+                h1f + ((bt * NT + 2 * net + i) * 64 + l) * 16);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 v = src[q];
+                h1[i][4 * q] = v.x;
+                h1[i][4 * q + 1] = v.y;
+                h1[i][4 * q + 2] = v.z;
+                h1[i][4 * q + 3] = v.w;
+            }
+        }
+    };
+    auto run_net = [&](int64_t bt, int net, const float (&h1)[2][16]) {
         const int64_t brow = bt * 32 + c;
         const bool live = brow < n;
+        // the stored actions of the logp rows, loaded before the products they wait behind
+        float av[16];
+        if (net == 0) {
 #pragma unroll
-        for (int net = LOGP ? 0 : 1; net < 2; ++net) {
-            __builtin_amdgcn_sched_barrier(0);  // one net at a time (register pressure)
+            for (int r = 0; r < 16; ++r) {
+                const int a = rho(r) + 4 * h;
+                av[r] = 0.0f;
+                if (a < A && live) av[r] = act[brow * A + a];
+            }
+        }
+        const char* iw2 = img + (net ? EV_W2C : EV_W2A);
+        const float* sb2 = sm + (net ? E_B2C : E_B2A);
+        float h2[2][16];
+        {
+            f32x16 z0 = zero16(), z1 = zero16();
+#pragma unroll
+            for (int kc = 0; kc < 2; ++kc)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    bf16x8 b[NPL], a[NPL];
+                    split_frag(h1[kc], s, b);
+                    ld_img(iw2, 2, H, kc, c, s, h, a);
+                    z0 = mfma6(a, b, z0);
+                    ld_img(iw2, 2, H, kc, 32 + c, s, h, a);
+                    z1 = mfma6(a, b, z1);
+                }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                h2[0][r] = tanh_nb(z0[r] + sb2[rho(r) + 4 * h]);
+                h2[1][r] = tanh_nb(z1[r] + sb2[32 + rho(r) + 4 * h]);
+            }
+        }
+        if (net == 1) {
+            float vpart = 0.0f;
+#pragma unroll
+            for (int it = 0; it < 2; ++it)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    vpart += sm[E_W3C + 32 * it + rho(r) + 4 * h] * h2[it][r];
+            const float value = vpart + __shfl_xor(vpart, 32, 64) + b3c;
+            if (live && h == 0) value_out[brow] = value;
+        } else {
+            f32x16 mu = zero16();
+#pragma unroll
+            for (int kc = 0; kc < 2; ++kc)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    bf16x8 b[NPL], a[NPL];
+                    split_frag(h2[kc], s, b);
+                    ld_img(img + EV_W3, 2, AMAX, kc, c, s, h, a);
+                    mu = mfma6(a, b, mu);
+                }
+            float lp = 0.0f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int a = rho(r) + 4 * h;
+                if (a < A && live) {
+                    const float diff = av[r] - (mu[r] + sm[E_B3 + a]);
+                    lp += -(diff * diff) / (2.0f * sm[E_VAR + a]) - sm[E_LS + a] - LOG_SQRT_2PI;
+                }
+            }
+            const float logp = lp + __shfl_xor(lp, 32, 64);
+            if (live && h == 0) logp_out[brow] = logp;
+        }
+    };
+    const int64_t bstep = (int64_t)gridDim.x * 4;
+    int64_t bt = (int64_t)blockIdx.x * 4 + w;
+    if (LOGP) {
+        // Round 5: one net's layer-1 tiles in flight while the other's products run (the
+        // critic's of this row tile under the actor's, the next row tile's actor under this
+        // critic's) instead of every wave waiting for its loads: 623 -> 542 us per 2M rows
+        // (rocprof, profiles/r05_evtail_ab.log)
+        float ua[2][16], ub[2][16];
+        if (bt < ntiles) load_unit(bt, 0, ua);
+        for (; bt < ntiles; bt += bstep) {
+            load_unit(bt, 1, ub);
+            __builtin_amdgcn_sched_barrier(0);
+            run_net(bt, 0, ua);
+            __builtin_amdgcn_sched_barrier(0);
+            if (bt + bstep < ntiles) load_unit(bt + bstep, 0, ua);
+            __builtin_amdgcn_sched_barrier(0);
+            run_net(bt, 1, ub);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    } else {
+        for (; bt < ntiles; bt += bstep) {
             float h1[2][16];
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const float4* src = reinterpret_cast<const float4*>(
-                    h1f + ((bt * NT + 2 * net + i) * 64 + l) * 16);
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const float4 v = src[q];
-                    h1[i][4 * q] = v.x;
-                    h1[i][4 * q + 1] = v.y;
-                    h1[i][4 * q + 2] = v.z;
-                    h1[i][4 * q + 3] = v.w;
-                }
-            }
-            const char* iw2 = img + (net ? EV_W2C : EV_W2A);
-            const float* sb2 = sm + (net ? E_B2C : E_B2A);
-            float h2[2][16];
-            {
-                f32x16 z0 = zero16(), z1 = zero16();
-#pragma unroll
-                for (int kc = 0; kc < 2; ++kc)
-#pragma unroll
-                    for (int s = 0; s < 2; ++s) {
-                        bf16x8 b[NPL], a[NPL];
-                        split_frag(h1[kc], s, b);
-                        ld_img(iw2, 2, H, kc, c, s, h, a);
-                        z0 = mfma6(a, b, z0);
-                        ld_img(iw2, 2, H, kc, 32 + c, s, h, a);
-                        z1 = mfma6(a, b, z1);
-                    }
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    h2[0][r] = tanh_nb(z0[r] + sb2[rho(r) + 4 * h]);
-                    h2[1][r] = tanh_nb(z1[r] + sb2[32 + rho(r) + 4 * h]);
-                }
-            }
-            if (net == 1) {
-                float vpart = 0.0f;
-#pragma unroll
-                for (int it = 0; it < 2; ++it)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r)
-                        vpart += sm[E_W3C + 32 * it + rho(r) + 4 * h] * h2[it][r];
-                const float value = vpart + __shfl_xor(vpart, 32, 64) + b3c;
-                if (live && h == 0) value_out[brow] = value;
-            } else {
-                f32x16 mu = zero16();
-#pragma unroll
-                for (int kc = 0; kc < 2; ++kc)
-#pragma unroll
-                    for (int s = 0; s < 2; ++s) {
-                        bf16x8 b[NPL], a[NPL];
-                        split_frag(h2[kc], s, b);
-                        ld_img(img + EV_W3, 2, AMAX, kc, c, s, h, a);
-                        mu = mfma6(a, b, mu);
-                    }
-                float lp = 0.0f;
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int a = rho(r) + 4 * h;
-                    if (a < A && live) {
-                        const float diff = act[brow * A + a] - (mu[r] + sm[E_B3 + a]);
-                        lp += -(diff * diff) / (2.0f * sm[E_VAR + a]) - sm[E_LS + a] - LOG_SQRT_2PI;
-                    }
-                }
-                const float logp = lp + __shfl_xor(lp, 32, 64);
-                if (live && h == 0) logp_out[brow] = logp;
-            }
+            load_unit(bt, 1, h1);
+            run_net(bt, 1, h1);
         }
     }
 }

@@ -44,3 +44,14 @@ for pat in ALWAYS:
             "name like ? group by name order by name", params + (f"%{pat}%",)):
         print(f"{ms:10.2f} ms {cnt:7d} x {us:10.2f} us (min {lo:.2f}, max {hi:.2f})  "
               f"{name[:120]}")
+# the layer-1 kernel serves both the minibatch (learn) and process_fn's evaluation chunks:
+# split its launches by grid size when the database records it
+cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
+gcol = next((x for x in ("grid_size", "grid_size_x", "grid_x", "grid") if x in cols), None)
+if gcol:
+    print(f"l1_ring_kernel by {gcol}: calls, mean / min / max us")
+    for g, cnt, us, lo, hi in c.execute(
+            f"select {gcol}, count(*), avg(duration)/1e3, min(duration)/1e3, max(duration)/1e3 "
+            f"from kernels {where + (' and' if where else 'where')} name like ? "
+            f"group by {gcol} order by {gcol}", params + ("%l1_ring_kernel%",)):
+        print(f"  {gcol} {g}: {cnt:6d} x {us:10.2f} us (min {lo:.2f}, max {hi:.2f})")
