@@ -187,7 +187,7 @@ def test_ret_rms_update(dev):
 
 
 @pytest.mark.parametrize("envs,steps", [(4096, 2048), (64, 4096), (256, 128), (96, 512),
-                                        (80, 32), (48, 32)])
+                                        (80, 32), (48, 32), (600, 2048), (3, 6144)])
 @pytest.mark.parametrize("scaled", [False, True])
 def test_gae_staged_rows_kernel(dev, envs, steps, scaled, monkeypatch):
     """The LDS-staged row kernel (f32 outputs only, rows a multiple of the 2048-transition
@@ -206,8 +206,8 @@ def test_gae_staged_rows_kernel(dev, envs, steps, scaled, monkeypatch):
     scale = torch.tensor([1.37], dtype=torch.float64, device=dev) if scaled else None
     nparts = int(_C.lib().tsrl_gae_num_partials(n, steps))
     outs = []
-    for unstaged in (False, True):
-        if unstaged:
+    for mode in ("staged", "unstaged"):
+        if mode == "unstaged":
             monkeypatch.setenv("TSRL_GAE_UNSTAGED", "1")
         parts = torch.full((nparts * 3,), -1.0, dtype=torch.float64, device=dev) if scaled \
             else None
@@ -216,11 +216,12 @@ def test_gae_staged_rows_kernel(dev, envs, steps, scaled, monkeypatch):
         outs.append((adv32.cpu().numpy(), ret32.cpu().numpy(),
                      None if parts is None else parts.cpu().numpy()))
     monkeypatch.delenv("TSRL_GAE_UNSTAGED")
-    (a0, r0, p0), (a1, r1, p1) = outs
-    np.testing.assert_array_equal(a0, a1)
-    np.testing.assert_array_equal(r0, r1)
-    if scaled:
-        np.testing.assert_array_equal(p0, p1)
+    a0, r0, p0 = outs[0]
+    for a1, r1, p1 in outs[1:]:
+        np.testing.assert_array_equal(a0, a1)
+        np.testing.assert_array_equal(r0, r1)
+        if scaled:
+            np.testing.assert_array_equal(p0, p1)
     s = 1.37 if scaled else 1.0
     ret_o, adv_o = ref.compute_episodic_return(
         rew.cpu().numpy(), term.cpu().numpy(), trunc.cpu().numpy(), np.arange(n),
@@ -229,6 +230,37 @@ def test_gae_staged_rows_kernel(dev, envs, steps, scaled, monkeypatch):
         if scaled else v_s.cpu().numpy(), 0.99, 0.95)
     _tol(a0, adv_o)
     _tol(r0, ret_o / s)
+
+
+@pytest.mark.parametrize("envs,steps", [(700, 2048), (5, 4096), (256, 512)])
+def test_gae_row_kernels_end_extra(dev, envs, steps, monkeypatch):
+    """The extra end flags (process_fn's unfinished-episode mask) through the staged and the
+    per-thread-load row kernels: the same bits (adv, ret, partials)."""
+    from tianshou_amd.policy.base import gae_device
+    from tianshou_amd import _C
+    g = torch.Generator(device=dev).manual_seed(7 * envs + steps)
+    n = envs * steps
+    v_s = torch.randn(n, device=dev, generator=g)
+    v_n = torch.randn(n, device=dev, generator=g)
+    rew = torch.rand(n, device=dev, generator=g, dtype=torch.float64)
+    u = torch.rand(n, device=dev, generator=g)
+    term = u < 0.003
+    trunc = (u > 0.997) & ~term
+    extra = ((u > 0.5) & (u < 0.503)).to(torch.uint8)
+    scale = torch.tensor([0.71], dtype=torch.float64, device=dev)
+    nparts = int(_C.lib().tsrl_gae_num_partials(n, steps))
+    outs = []
+    for mode in ("staged", "unstaged"):
+        if mode == "unstaged":
+            monkeypatch.setenv("TSRL_GAE_UNSTAGED", "1")
+        parts = torch.full((nparts * 3,), -1.0, dtype=torch.float64, device=dev)
+        adv32, ret32, _, _ = gae_device(v_s, v_n, rew, term, trunc, 0.99, 0.95, steps, extra,
+                                        scale, ret_partials=parts)
+        outs.append((adv32.cpu().numpy(), ret32.cpu().numpy(), parts.cpu().numpy()))
+    monkeypatch.delenv("TSRL_GAE_UNSTAGED")
+    for o in outs[1:]:
+        for x, y in zip(outs[0], o):
+            np.testing.assert_array_equal(x, y)
 
 
 def test_gae_time_next_kernel_events(dev):

@@ -22,7 +22,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join("tianshou-fork_amd", "csrc", "gae.hip")
 
-KERNEL = "gae_rows_staged_kernel"
+KERNEL = os.environ.get("GAE_KERNEL", "gae_rows_staged_kernel")
 N = 4096 * 2048
 
 
