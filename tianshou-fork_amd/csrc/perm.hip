@@ -176,11 +176,21 @@ __global__ __launch_bounds__(RX_T) void radix_scatter_kernel(
     __syncthreads();
     const int64_t b0 = (int64_t)blockIdx.x * RX_TILE;
     const uint64_t below = lane == 0 ? 0ull : (~0ull >> (kWave - lane));
+    // the whole tile's pairs loaded up front (all loads in flight at once, not one memory
+    // latency per round)
+    uint32_t kr[RX_R], vr[RX_R];
+#pragma unroll
+    for (int r = 0; r < RX_R; ++r) {
+        const int64_t i = b0 + r * RX_T + t;
+        kr[r] = i < m ? kin[i] : 0u;
+        vr[r] = i < m ? (vin ? vin[i] : (uint32_t)(i + 1)) : 0u;
+    }
+#pragma unroll
     for (int r = 0; r < RX_R; ++r) {
         const int64_t i = b0 + r * RX_T + t;
         const bool valid = i < m;
-        const uint32_t key = valid ? kin[i] : 0u;
-        const uint32_t val = valid ? (vin ? vin[i] : (uint32_t)(i + 1)) : 0u;
+        const uint32_t key = kr[r];
+        const uint32_t val = vr[r];
         const uint32_t d = (key >> shift) & (RX_D - 1);
         uint64_t match = __ballot(valid);
 #pragma unroll
