@@ -628,7 +628,9 @@ int tsrl_ppo_tail_fin(const float* h1frag, int64_t n, const int64_t* idx,
 /* tsrl_ppo_tail_stage: the same work in two stages so the caller can run the reduction on a
  * second stream beside tsrl_mlp_dw (both only read what the tail kernels wrote):
  * stages & 1 = the actor and critic tail kernels, stages & 2 = the reduction (with the loss
- * finalisation when log_std/losses/grad_log_std are given — all three or none), 3 = both. */
+ * finalisation when log_std/losses/grad_log_std are given — all three or none), 3 = both;
+ * stages & 4 / & 8 = the actor's / the critic's tail kernel alone (disjoint outputs: two
+ * streams may run them concurrently, both before the reduction). */
 int tsrl_ppo_tail_stage(const float* h1frag, int64_t n, const int64_t* idx,
                         const tsrl_tail_weights* w, int64_t act_dim, const float* act,
                         const float* logp_old, const float* adv, const float* ret,

@@ -1334,7 +1334,8 @@ static int ppo_tail_impl(const float* h1frag, int64_t n, const int64_t* idx,
                          float* dz1, const tsrl_tail_grads* grads, double* sums,
                          void* workspace, int64_t ws_bytes, TailFin fin, int stages,
                          void* stream) {
-    TSRL_CHECK_ARG(stages >= 1 && stages <= 3, "tsrl_ppo_tail: stages must be 1, 2 or 3");
+    TSRL_CHECK_ARG((stages >= 1 && stages <= 3) || stages == 4 || stages == 8,
+                   "tsrl_ppo_tail: stages must be 1, 2, 3, 4 or 8");
     TSRL_CHECK_ARG(n > 0 && act_dim > 0 && act_dim <= AMAX,
                    "tsrl_ppo_tail: need n > 0 and 0 < act_dim <= %d", AMAX);
     TSRL_CHECK_ARG(h1frag && wt && grads && act && logp_old && adv && ret && dz1 && sums &&
@@ -1353,11 +1354,15 @@ static int ppo_tail_impl(const float* h1frag, int64_t n, const int64_t* idx,
     TailWeights w{wt->w2a, wt->b2a, wt->w2c, wt->b2c, wt->w3a, wt->b3a, wt->w3c, wt->b3c,
                   wt->log_std};
     const TailParams tp = make_tail_params(prm, (int)act_dim);
-    if (stages & 1) {
+    // stages: 1 both nets' tails, 4 / 8 the actor's / the critic's alone (they write disjoint
+    // slab entries and dZ1 halves, so two streams may run them side by side), 2 the reduction
+    if (stages & (1 | 4)) {
         hipLaunchKernelGGL(ppo_tail16_kernel<0>, dim3(g), dim3(T16_TPB), 0, as_stream(stream),
                            h1frag, n, idx, w, act, logp_old, adv, ret, v_s, adv_sums, tp, dz1,
                            slab_f, slab_d);
         TSRL_LAUNCH_CHECK("tsrl_ppo_tail(actor)");
+    }
+    if (stages & (1 | 8)) {
         hipLaunchKernelGGL(ppo_tail16_kernel<1>, dim3(g), dim3(T16_TPB), 0, as_stream(stream),
                            h1frag, n, idx, w, act, logp_old, adv, ret, v_s, adv_sums, tp, dz1,
                            slab_f, slab_d);

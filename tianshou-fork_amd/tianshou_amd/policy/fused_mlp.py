@@ -31,6 +31,10 @@ L1_X6 = True
 # the tail's reduction launch runs on a second stream beside tsrl_mlp_dw (TSRL_TAIL_OVERLAP=0:
 # one stream)
 TAIL_OVERLAP = os.environ.get("TSRL_TAIL_OVERLAP", "1") != "0"
+# minibatches of at most this many rows run the actor's and the critic's tail kernels on the
+# two streams side by side (each tail then fills at most half of a 256-CU device:
+# ceil(rows / 16 / 8) workgroups <= 128); TSRL_TAIL_SPLIT=0 keeps them on one stream
+TAIL_SPLIT_ROWS = 16384 if os.environ.get("TSRL_TAIL_SPLIT", "1") != "0" else 0
 
 
 def _seq(mlp) -> Optional[list]:
@@ -286,10 +290,19 @@ class FusedActorCritic(FlatAdam):
         if side is None:
             _C.check(lib.tsrl_ppo_tail_stage(*args, *fin, 3, s), "tsrl_ppo_tail_stage")
         else:
+            cur = torch.cuda.current_stream(dev)
+            if b <= TAIL_SPLIT_ROWS:
+                # small minibatches: each net's tail fills at most half the CUs, so the
+                # critic's runs on the second stream beside the actor's
+                side.wait_stream(cur)
+                _C.check(lib.tsrl_ppo_tail_stage(*args, *fin, 4, s), "tsrl_ppo_tail_stage")
+                _C.check(lib.tsrl_ppo_tail_stage(*args, *fin, 8, side.cuda_stream),
+                         "tsrl_ppo_tail_stage")
+                cur.wait_stream(side)
+            else:
+                _C.check(lib.tsrl_ppo_tail_stage(*args, *fin, 1, s), "tsrl_ppo_tail_stage")
             # the tail's reduction only reads the tail kernels' slabs and dw only their dz1:
             # the reduction runs on a second stream beside the first-layer weight gradients
-            _C.check(lib.tsrl_ppo_tail_stage(*args, *fin, 1, s), "tsrl_ppo_tail_stage")
-            cur = torch.cuda.current_stream(dev)
             side.wait_stream(cur)
             _C.check(lib.tsrl_ppo_tail_stage(*args, *fin, 2, side.cuda_stream),
                      "tsrl_ppo_tail_stage")
