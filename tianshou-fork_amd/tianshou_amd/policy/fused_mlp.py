@@ -243,15 +243,17 @@ class FusedActorCritic(FlatAdam):
     def minibatch(self, obs: torch.Tensor, idx: Optional[torch.Tensor], b: int,
                   act: torch.Tensor, logp_old: torch.Tensor, adv: torch.Tensor,
                   ret: torch.Tensor, v_s: torch.Tensor, params: "_C.PPOParams", dp,
-                  adv_sums: Optional[torch.Tensor] = None, split_w: bool = True
-                  ) -> torch.Tensor:
+                  adv_sums: Optional[torch.Tensor] = None, split_w: bool = True,
+                  terms_out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Gradients of the minibatch loss into the parameters' .grad; returns the device
         tensor [loss, clip, vf, ent] (ppo.py:140-142).  ``obs`` are the rows of ``rows()``;
         ``adv_sums`` = this minibatch's row of epoch_adv_moments (computed here when None).
         Under data parallelism ONE all-reduce carries the gradients and the loss sums; a rank
         whose share of the global minibatch is empty (b == 0) contributes zeros.
         ``split_w=False``: the bf16x6 planes of W1 are already current (split_w1(), or the
-        previous clip_adam(split_w1=True))."""
+        previous clip_adam(split_w1=True)).  ``terms_out``: a float32 [4] device tensor the
+        single-process loss finalisation writes into (a captured epoch's per-minibatch row: no
+        copy node per minibatch)."""
         self.bind_grads()
         L, lib = self.L, _C.lib()
         dev = obs.device
@@ -283,7 +285,9 @@ class FusedActorCritic(FlatAdam):
                 _C.ptr(ret), _C.ptr(v_s), _C.ptr(adv_sums) if adv_sums is not None else None,
                 params, _C.ptr(dz1), self._tail_grads, _C.ptr(sums), _C.ptr(ws), wsb)
         # single process: the loss finalisation rides the tail's reduction launch
-        terms = None if dp.active else torch.empty(4, dtype=torch.float32, device=dev)
+        terms = None if dp.active else (
+            terms_out if terms_out is not None else torch.empty(4, dtype=torch.float32,
+                                                                device=dev))
         fin = (None, None, None) if terms is None else (
             _C.ptr(L["sigma"]), _C.ptr(terms), _C.ptr(L["sigma"].grad))
         side = self._side_stream(dev)

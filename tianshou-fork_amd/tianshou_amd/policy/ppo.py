@@ -539,9 +539,10 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
                         t = self._mlp.minibatch(obs_all, sperm[s:e], e - s, *static,
                                                 self._params(b_glob), self.dp,
                                                 adv_sums=None if mom is None else mom[i],
-                                                split_w=not fused_opt)
+                                                split_w=not fused_opt, terms_out=sterms[i])
                         self._opt_step(last=(i == len(chunks) - 1))
-                        sterms[i].copy_(t)
+                        if t.data_ptr() != sterms[i].data_ptr():  # data parallel: reduced
+                            sterms[i].copy_(t)
             except RuntimeError as err:  # e.g. a collective backend that cannot be captured
                 import warnings
                 warnings.warn(f"learn-graph capture failed, running epochs eagerly: {err}")
