@@ -288,10 +288,13 @@ def test_fused_minibatch_matches_autograd(dev, D, A, B, kw):
         assert e_fused <= max(4 * e_torch, 2e-6), (k, e_fused, e_torch)
 
 
-@pytest.mark.parametrize("B", [262144 + 45, 1000])
+@pytest.mark.parametrize("B", [262144 + 45, 1000, 16384, 16385])
 def test_tail_reduction_on_side_stream_is_bitwise_single_stream(dev, monkeypatch, B):
-    """The tail's reduction on a second stream beside dW1 (TSRL_TAIL_OVERLAP, the default)
-    gives the same bits as the one-stream sequence: same kernels, only the stream differs."""
+    """The tail's reduction on a second stream beside dW1 (TSRL_TAIL_OVERLAP, the default) --
+    and, up to TAIL_SPLIT_ROWS rows, the critic's tail kernel on that stream beside the
+    actor's -- gives the same bits as the one-stream sequence: same kernels, only the streams
+    differ.  A third run writes the loss terms into a caller's buffer (terms_out, the
+    captured epochs' rows): same values, in place."""
     from tianshou_amd import _C
     from tianshou_amd.dist import DataParallel
     from tianshou_amd.policy import fused_mlp
@@ -320,10 +323,20 @@ def test_tail_reduction_on_side_stream_is_bitwise_single_stream(dev, monkeypatch
         torch.cuda.synchronize()
         out.append((terms.cpu().clone(),
                     [q.grad.detach().cpu().clone() for q in params if q.grad is not None]))
-    assert torch.equal(out[0][0], out[1][0])
-    assert len(out[0][1]) == len(out[1][1]) >= 13  # both nets' Linear weights/biases + log-std
-    for a, b in zip(out[0][1], out[1][1]):
-        assert torch.equal(a, b)
+    monkeypatch.setattr(fused_mlp, "TAIL_OVERLAP", True)
+    buf = torch.full((2, 4), -7.0, device=dev)
+    terms = fm.minibatch(obs, idx, B, act, logp_old, adv, ret, v_s, p, DataParallel(),
+                         terms_out=buf[1])
+    torch.cuda.synchronize()
+    assert terms.data_ptr() == buf[1].data_ptr()
+    out.append((buf[1].cpu().clone(),
+                [q.grad.detach().cpu().clone() for q in params if q.grad is not None]))
+    assert torch.equal(buf[0].cpu(), torch.full((4,), -7.0))
+    for o in out[1:]:
+        assert torch.equal(out[0][0], o[0])
+        assert len(out[0][1]) == len(o[1]) >= 13  # both nets' Linear weights/biases + log-std
+        for a, b in zip(out[0][1], o[1]):
+            assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("value_clip", [False, True])
