@@ -416,7 +416,10 @@ def main():
                    "sample": f"one iteration of {E} envs x {args.cpu_steps} steps "
                              f"(Box {D}/{A}), build CPU restatement "
                              f"(oracle/cpu_port.py: NumPy env+obs-norm+buffer, C GAE, "
-                             f"torch-CPU PPO), {dt:.1f}s"}
+                             f"torch-CPU PPO), {dt:.1f}s; parity-checked against the "
+                             f"reference Collector + VectorEnvNormObs + process_fn goldens "
+                             f"(tests/test_oracle.py::test_cpu_port_matches_reference_"
+                             f"collector)"}
         line = {
             "metric": "env-steps/sec through collect+GAE+PPO.learn",
             "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,

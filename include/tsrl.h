@@ -711,7 +711,9 @@ int tsrl_segtree_prefix_idx(const double* tree, int64_t bound, const void* value
  * tsrl_clip_adam_partials(n) entries) receive slice norms, norm_out[0] = gradient norm,
  * norm_out[1] = clip coefficient (max_norm <= 0: no clipping, partials / norm_out may be
  * NULL); step[0..nstep) (device f32 step counters, all equal) is
- * advanced by one.  ticket: two device uint32, zero-initialised, kept zero.
+ * advanced by one.  ticket: three device uint32, zero-initialised; [0] and [1] re-arm
+ * themselves, [2] is a sticky flag set to 1 when the in-kernel slice-norm hand-off timed
+ * out (the step is then invalid for EVERY slice: the caller must check it and reject it).
  * lr_dev (nullable device f32): the learning rate read at run time instead of `lr`, so a
  * captured learn graph follows an lr_scheduler (BasePolicy.update, base.py:312-313).
  * scale_grads: leave the gradient scaled by the clip coefficient in place (what p.grad holds

@@ -4,6 +4,12 @@ storage (NumPy) + critic values / GAE (C oracle) + PPO learn (torch CPU fp32), i
 reference algorithm (collector.py:184-402, a2c.py:83-117, ppo.py:87-162) restated for a
 bounded sample of the bench workload.  Timed on the GPU box's host cores by bench.py;
 never used by the product path.
+
+``tests/test_oracle.py::test_cpu_port_matches_reference_collector`` runs it at config 2's
+observation width (16 envs x 24 steps, D = 17) with the reference policy's initial weights
+and checks its obs_rms, stored rows, rewards and process_fn returns / advantages against the
+reference Collector + VectorEnvNormObs + process_fn goldens (``collector_d17.npz``): the
+baseline the bench reports is a parity-checked restatement.
 """
 import time
 
@@ -13,7 +19,21 @@ import torch
 from oracle import ref, synth_env
 
 
-def run_iteration(E, T, D, A, repeat=4, minibatches=32, ep_len=1000, threads=None, seed=0):
+# reference state-dict keys (policy.state_dict(), utils/net/common.py Net.model, continuous.py
+# ActorProb.mu / Critic.last) -> (net, layer index) of the nn.Sequential nets below
+_REF_KEYS = {"actor.preprocess.model.model.0": ("actor", 0),
+             "actor.preprocess.model.model.2": ("actor", 2),
+             "actor.mu.model.0": ("actor", 4),
+             "critic.preprocess.model.model.0": ("critic", 0),
+             "critic.preprocess.model.model.2": ("critic", 2),
+             "critic.last.model.0": ("critic", 4)}
+
+
+def run_iteration(E, T, D, A, repeat=4, minibatches=32, ep_len=1000, threads=None, seed=0,
+                  init=None, record=None):
+    """One iteration; returns (env-steps/s, seconds).  ``init``: the reference policy's
+    state-dict arrays (keys as _REF_KEYS + "actor.sigma_param") to start from; ``record``: a
+    dict that receives obs_rms, the stored rows, rewards and process_fn's returns / adv."""
     if threads:
         torch.set_num_threads(threads)
     torch.manual_seed(seed)
@@ -26,6 +46,13 @@ def run_iteration(E, T, D, A, repeat=4, minibatches=32, ep_len=1000, threads=Non
                              nn.Linear(64, out))
     actor, critic = mlp(A), mlp(1)
     sigma = nn.Parameter(torch.full((A,), -0.5))
+    if init is not None:
+        with torch.no_grad():
+            nets = {"actor": actor, "critic": critic}
+            for k, (net, i) in _REF_KEYS.items():
+                nets[net][i].weight.copy_(torch.as_tensor(init[k + ".weight"]))
+                nets[net][i].bias.copy_(torch.as_tensor(init[k + ".bias"]))
+            sigma.copy_(torch.as_tensor(init["actor.sigma_param"]).reshape(-1))
     params = list(actor.parameters()) + list(critic.parameters()) + [sigma]
     optim = torch.optim.Adam(params, lr=3e-4)
     env = synth_env.SynthVecEnvNP(E, (D,), A, ep_len, seed=seed)
@@ -71,6 +98,11 @@ def run_iteration(E, T, D, A, repeat=4, minibatches=32, ep_len=1000, threads=Non
                                            0.99, 0.95)
     returns = torch.as_tensor((ret / scale).astype(np.float32))
     adv_t = torch.as_tensor(adv.astype(np.float32))
+    if record is not None:
+        record.update(rms_mean=np.asarray(rms.mean), rms_var=np.asarray(rms.var),
+                      rms_count=rms.count, obs=S_obs.reshape(n, D),
+                      obs_next=S_next.reshape(n, D), rew=S_rew.reshape(-1), v_s=v_s,
+                      returns=returns.numpy(), adv=adv_t.numpy())
     ret_rms.update(ret)
     with torch.no_grad():
         mu = actor(o)

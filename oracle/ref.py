@@ -298,6 +298,53 @@ def ppo_gaussian_loss_torch(mu, sigma_param, value, act, logp_old, adv, returns,
             dict(mu=mu.grad, sigma_param=sp.grad, value=value.grad))
 
 
+def ppo_learn_torch(actor, critic, optim, obs, act, logp_old, adv, returns, batch_size,
+                    repeat, perm_fn, eps_clip=0.2, vf_coef=0.5, ent_coef=0.01,
+                    max_grad_norm=None, norm_adv=True, eps=1e-8):
+    """PPOPolicy.learn restated (ppo.py:99-162) for the Gaussian Independent(Normal) actor
+    over plain torch modules in fp32 (no dual / value clip, no advantage recomputation):
+    ``repeat`` epochs of Batch.split(batch_size, shuffle=True, merge_last=True)
+    (batch.py:896-912; ``perm_fn(n)`` = np.random.permutation(n)), per minibatch the
+    advantage normalisation, clipped surrogate, value and entropy losses, loss.backward(),
+    nn.utils.clip_grad_norm_ over the actor-critic parameters and optim.step().  Tensors live
+    on the caller's device; returns the [n_minibatch, 4] (loss, clip, vf, ent) terms."""
+    import torch
+    from torch.distributions import Independent, Normal
+    params = list(actor.parameters()) + list(critic.parameters())
+    n = len(adv)
+    out = []
+    for _ in range(repeat):
+        perm = torch.as_tensor(perm_fn(n), device=adv.device)
+        bounds = [(s, min(s + batch_size, n)) for s in range(0, n, batch_size)]
+        if n % batch_size and len(bounds) > 1:   # merge_last
+            bounds = bounds[:-2] + [(bounds[-2][0], n)]
+        for s, e in bounds:
+            idx = perm[s:e]
+            o = obs[idx]
+            (mu, sigma), _ = actor(o)
+            dist = Independent(Normal(mu, sigma), 1)
+            a = adv[idx]
+            if norm_adv:
+                mean, std = a.mean(), a.std()
+                a = (a - mean) / (std + eps)
+            ratio = (dist.log_prob(act[idx]) - logp_old[idx]).exp().float()
+            ratio = ratio.reshape(ratio.size(0), -1).transpose(0, 1)
+            surr1 = ratio * a
+            surr2 = ratio.clamp(1.0 - eps_clip, 1.0 + eps_clip) * a
+            clip_loss = -torch.min(surr1, surr2).mean()
+            value = critic(o).flatten()
+            vf_loss = (returns[idx] - value).pow(2).mean()
+            ent_loss = dist.entropy().mean()
+            loss = clip_loss + vf_coef * vf_loss - ent_coef * ent_loss
+            optim.zero_grad()
+            loss.backward()
+            if max_grad_norm:
+                torch.nn.utils.clip_grad_norm_(params, max_norm=max_grad_norm)
+            optim.step()
+            out.append(torch.stack([loss, clip_loss, vf_loss, ent_loss]).detach())
+    return torch.stack(out)
+
+
 # ---------------------------------------------------------------------------------------
 # PPO minibatch loss (ppo.py:106-151) for Categorical policies: Categorical(logits=x)
 # (examples/atari/atari_ppo.py:136-137) or Categorical(probs=x) (test/discrete/test_ppo.py:95).

@@ -82,6 +82,30 @@ def _worker(rank, world, port, out):
     rg = dp.all_gather_cat(torch.arange(rank + 1, dtype=torch.float64) + 10 * rank,
                            kind="ret_rms", ragged=True)
     assert rg.tolist() == [10.0 * r + i for r in range(world) for i in range(r + 1)], rg
+    # known lengths (the shard table's ret_rms partial counts): no length exchange
+    kg = dp.all_gather_known(torch.arange(rank + 1, dtype=torch.float64) + 10 * rank,
+                             [r + 1 for r in range(world)], kind="ret_rms")
+    assert kg.tolist() == rg.tolist(), kg
+    # the once-per-update shard table and the equal-shard requirement of the local-split
+    # learn paths (unequal shards must raise, not hang)
+    import types
+    from tianshou_amd.policy.a2c import A2CPolicy
+    stub = types.SimpleNamespace(dp=dp)
+    for name in ("_shard_table", "_learn_shards", "_require_equal_shards"):
+        setattr(stub, name, types.MethodType(getattr(A2CPolicy, name), stub))
+    np.random.seed(7)
+    tab = stub._shard_table(100 + rank, 5, torch.device("cpu"))
+    assert tab["n"] == [100 + r for r in range(world)] and tab["row_len"] == [5] * world
+    assert tab["hash_equal"] and tab["fresh"]
+    raised = False
+    try:
+        stub._require_equal_shards(100 + rank, torch.device("cpu"), "learn")
+    except ValueError as e:
+        raised = "unequal data-parallel shards" in str(e)
+    assert raised and not stub._shards["fresh"]
+    stub._require_equal_shards(64, torch.device("cpu"), "learn")  # equal: no error
+    np.random.seed(rank)  # different global streams are detected
+    assert not stub._shard_table(64, 0, torch.device("cpu"))["hash_equal"]
     out[rank] = (grads_sum, grads_avg, sums, flat, (int(hmax), int(hmin), moved, log, replayed))
     dist.destroy_process_group()
 

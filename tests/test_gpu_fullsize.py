@@ -181,3 +181,110 @@ def test_atari_stack_gather_full_size_buffer():
     assert np.array_equal(got.obs.cpu().numpy(), ref.stack_get(fr, idx, S, ix.prev))
     assert np.array_equal(got.obs_next.cpu().numpy(),
                           ref.stack_get(fr, ix.next(idx), S, ix.prev))
+
+
+def _headline_setup(dev, exact):
+    from tianshou_amd.data import Collector, VectorReplayBuffer
+    from tianshou_amd.env import SyntheticVectorEnv, VectorEnvNormObs
+    from tianshou_amd.policy import PPOPolicy
+    from tianshou_amd.utils.models import fixed_std_normal, get_actor_critic, init_and_get_optim
+    torch.manual_seed(0)
+    np.random.seed(0)
+    env = VectorEnvNormObs(SyntheticVectorEnv(E, (D,), A, ep_len=L, device=dev),
+                           exact_obs_rms=exact)
+    actor, critic = get_actor_critic((D,), (64, 64), (A,), dev)
+    actor, critic = actor.to(dev), critic.to(dev)
+    optim = init_and_get_optim(actor, critic, 3e-4)
+    policy = PPOPolicy(actor, critic, optim, fixed_std_normal, action_space=env.action_space,
+                       discount_factor=0.99, gae_lambda=0.95, max_grad_norm=0.5, vf_coef=0.25,
+                       ent_coef=0.0, reward_normalization=True, advantage_normalization=True,
+                       eps_clip=0.2).to(dev)
+    buf = VectorReplayBuffer(E * T, E, device=dev)
+    return env, policy, buf, Collector(policy, env, buf)
+
+
+def _ratio(got, want, rtol, atol):
+    """max |got - want| / (rtol |want| + atol): <= 1 passes assert_allclose(rtol, atol)."""
+    got, want = np.asarray(got, np.float64), np.asarray(want, np.float64)
+    return float((np.abs(got - want) / (rtol * np.abs(want) + atol)).max())
+
+
+@pytest.mark.parametrize("exact", [True, False])
+def test_headline_obs_rms_full_collect_matches_reference(golden_dir, exact):
+    """the headline collect (4096 envs x 2048 steps, D = 376, L = 1000,
+    seed 0 -- bench.py's config 3) against the REFERENCE VectorEnvNormObs's own trajectory
+    over the same 2048 steps (tests/golden/rms_fullT.npz, ~4100 f32 Chan merges,
+    statistics.py:99-114, venv_wrappers.py:77-99):
+
+    * obs_rms after the collect: exact_obs_rms=True bit for bit; the default (exact int64
+      moments, f64 merge) within rtol 1e-5, atol 1e-7 (the max ratio to that bound printed);
+    * the stored obs / obs_next rows of 24 envs (every row of their 2048 steps, rebuilt by
+      oracle.headline from the env's closed form and the reference's per-step statistics,
+      the rebuild itself pinned bitwise by test_oracle.py): exact bitwise, default within
+      A2's rtol 2e-4, atol 2e-5 (ratio printed);
+    * process_fn's returns / advantages of those envs against a torch-fp32 critic
+      (the policy's own nn.Linear layers) on the REFERENCE rows and the C-oracle GAE on its
+      values: north_star's rtol 1e-5, atol 1e-6 * max|ref|, both modes (ratio printed)."""
+    import os
+    from oracle import headline, ref
+    dev = torch.device("cuda", 0)
+    z = np.load(os.path.join(golden_dir, "rms_fullT.npz"))
+    assert (int(z["E"]), int(z["T"]), int(z["D"]), int(z["L"])) == (E, T, D, L)
+    env, policy, buf, coll = _headline_setup(dev, exact)
+    res = coll.collect(n_step=E * T)
+    assert res["n/st"] == E * T
+    rms = env.get_obs_rms()
+    assert rms.count == int(z["counts"][T, 1])
+    want_mean, want_var = z["reset_mean"][T - 1], z["reset_var"][T - 1]
+    rm = _ratio(rms.mean, want_mean, 1e-5, 1e-7)
+    rv = _ratio(rms.var, want_var, 1e-5, 1e-7)
+    print(f"exact={exact}: obs_rms after 2048 steps vs reference, max err / (rtol 1e-5 + "
+          f"atol 1e-7): mean {rm:.3g}, var {rv:.3g}; max |d mean| "
+          f"{np.abs(rms.mean - want_mean).max():.3g}, max |d var| / var "
+          f"{(np.abs(rms.var - want_var) / want_var).max():.3g}")
+    if exact:
+        assert np.array_equal(rms.mean, want_mean) and np.array_equal(rms.var, want_var)
+    else:
+        np.testing.assert_allclose(rms.mean, want_mean, rtol=1e-5, atol=1e-7)
+        np.testing.assert_allclose(rms.var, want_var, rtol=1e-5, atol=1e-7)
+    rng = np.random.default_rng(11)
+    envs = np.unique(np.concatenate([z["keep_envs"], rng.choice(E, 16, replace=False)]))
+    obs_ref, nxt_ref = headline.rebuild_rows(z, envs)
+    rows = (envs[:, None] * T + np.arange(T)[None]).reshape(-1)
+    rows_t = torch.as_tensor(rows, device=dev)
+    m = buf._meta
+    got_obs = m.obs[rows_t][:, :D].cpu().numpy().reshape(len(envs), T, D)
+    got_nxt = m.obs_next[rows_t][:, :D].cpu().numpy().reshape(len(envs), T, D)
+    if exact:
+        assert np.array_equal(got_obs, obs_ref)
+        assert np.array_equal(got_nxt, nxt_ref)
+    else:
+        print(f"default rows of {len(envs)} envs x {T} steps, max err / (rtol 2e-4 + atol "
+              f"2e-5): obs {_ratio(got_obs, obs_ref, 2e-4, 2e-5):.3g}, obs_next "
+              f"{_ratio(got_nxt, nxt_ref, 2e-4, 2e-5):.3g}; bit-exact fraction "
+              f"{np.mean(got_nxt == nxt_ref):.4f}")
+        np.testing.assert_allclose(got_obs, obs_ref, rtol=2e-4, atol=2e-5)
+        np.testing.assert_allclose(got_nxt, nxt_ref, rtol=2e-4, atol=2e-5)
+    # process_fn on the device vs torch-fp32 critic + C-oracle GAE on the reference rows
+    batch, idx = buf.sample(0)
+    assert np.array_equal(np.asarray(idx), np.arange(E * T))  # full buffer: batch row = row
+    var0 = policy.ret_rms.var
+    batch = policy.process_fn(batch, buf, idx)
+    with torch.no_grad():
+        v_s = policy.critic(torch.as_tensor(obs_ref.reshape(-1, D), device=dev)).flatten()
+        v_n = policy.critic(torch.as_tensor(nxt_ref.reshape(-1, D), device=dev)).flatten()
+    v_s, v_n = v_s.cpu().numpy(), v_n.cpu().numpy()
+    rew, term, trunc = _closed_form_env()
+    scale = np.sqrt(var0 + policy._eps)
+    ret_o, adv_o = ref.compute_episodic_return(
+        rew[rows], term[rows], trunc[rows], rows, buf.unfinished_index(),
+        v_n.astype(np.float64) * scale, v_s.astype(np.float64) * scale, 0.99, 0.95)
+    want = {"returns": (ret_o / scale).astype(np.float32), "adv": adv_o.astype(np.float32),
+            "v_s": v_s}
+    for k in ("v_s", "returns", "adv"):
+        g = batch[k][rows_t].cpu().numpy()
+        w = want[k]
+        r = _ratio(g, w, 1e-5, 1e-6 * np.abs(w).max())
+        print(f"exact={exact} {k} of {len(envs)} envs vs torch-fp32 critic + C-oracle GAE on "
+              f"the reference rows: max err / (rtol 1e-5 + atol 1e-6 max) {r:.3g}")
+        np.testing.assert_allclose(g, w, rtol=1e-5, atol=1e-6 * np.abs(w).max(), err_msg=k)

@@ -251,3 +251,80 @@ def test_synth_env_obs_rms_production_rows(golden_dir):
             rms.update(env.reset(done))
         check(t + 1)
     assert np.array_equal(rew.reshape(-1), z["c1_rew"])
+
+
+def test_headline_rows_rebuild_matches_reference(golden_dir):
+    """The full-length headline obs_rms trajectory (gen_rms_fullT: the reference
+    VectorEnvNormObs over 4096 synthetic envs x 2048 steps, D = 376, L = 1000): the done ids of
+    every step follow the env's closed form, the counts add up, the first steps' statistics
+    equal the NumPy restatement (ref.RMS over oracle.synth_env rows) bit for bit, and
+    oracle.headline.rebuild_rows -- the rows the GPU test compares the device buffer with --
+    reproduces every normalised row the reference wrapper returned for the kept envs and steps
+    (obs_next, reset rows, initial obs) bit for bit."""
+    from oracle import headline
+    z = _load(golden_dir, "rms_fullT.npz")
+    E, D, L, T = (int(z[k]) for k in ("E", "D", "L", "T"))
+    e = np.arange(E)
+    cnt = z["counts"]
+    assert cnt[0, 0] == E
+    for s in range(T):
+        _, t = headline.step_coords(e, s, L)
+        done = np.flatnonzero(t == L)
+        assert np.array_equal(headline.done_ids(z, s), done), s
+        prev = cnt[s, 1] if s else cnt[0, 0]  # row 0: the initial reset's update only
+        assert cnt[s + 1, 0] == prev + E and cnt[s + 1, 1] == cnt[s + 1, 0] + len(done)
+    # the first 3 steps through the NumPy restatement (the env's own step / reset calls)
+    env = synth_env.SynthVecEnvNP(E, (D,), int(z["A"]), L)
+    rms = ref.RMS()
+    rms.update(env.reset())
+    assert np.array_equal(np.asarray(rms.mean, np.float32), z["step_mean"][0])
+    for s in range(3):
+        nxt, _, term, trunc = env.step()
+        rms.update(nxt)
+        assert np.array_equal(np.asarray(rms.mean, np.float32), z["step_mean"][s + 1])
+        assert np.array_equal(np.asarray(rms.var, np.float32), z["step_var"][s + 1])
+        done = np.flatnonzero(term | trunc)
+        if len(done):
+            rms.update(env.reset(done))
+        assert np.array_equal(np.asarray(rms.var, np.float32), z["reset_var"][s])
+    keep, steps = z["keep_envs"], z["keep_steps"]
+    obs, obs_next = headline.rebuild_rows(z, keep)
+    assert np.array_equal(obs[:, 0], z["kept_obs0"])
+    for i, s in enumerate(steps):
+        assert np.array_equal(obs_next[:, s], z["kept_obs_next"][i]), s
+    n_reset = 0
+    for name in z.files:
+        if name.startswith("kept_reset_"):
+            s, env_id = (int(v) for v in name.split("_")[2:])
+            if s + 1 < T:
+                a = int(np.flatnonzero(keep == env_id)[0])
+                assert np.array_equal(obs[a, s + 1], z[name]), name
+                n_reset += 1
+    assert n_reset >= 6
+
+
+def test_cpu_port_matches_reference_collector(golden_dir):
+    """bench.py's cpu_baseline (oracle/cpu_port.py) is a parity-checked restatement: one
+    iteration at config 2's width (16 envs x 24 steps, Box 17/6, L = 7) from the reference
+    policy's initial weights reproduces the reference Collector + VectorEnvNormObs run of
+    collector_d17.npz -- obs_rms and every stored obs / obs_next row and reward bit for bit
+    (actions do not enter the synthetic env), and process_fn's V(s), returns and advantages
+    (rew_norm GAE, a2c.py:83-117) within north_star's rtol 1e-5, atol 1e-6 * max."""
+    from oracle import cpu_port
+    z = _load(golden_dir, "collector_d17.npz")
+    E, D, A, L, T = (int(z[k]) for k in ("E", "D", "A", "L", "T"))
+    init = {k[len("init_"):]: z[k] for k in z.files if k.startswith("init_actor.") or
+            k.startswith("init_critic.")}
+    rec = {}
+    cpu_port.run_iteration(E, T, D, A, repeat=1, minibatches=4, ep_len=L, threads=1,
+                           init=init, record=rec)
+    assert np.array_equal(rec["rms_mean"].astype(np.float32), z["c1_rms_mean"])
+    assert np.array_equal(rec["rms_var"].astype(np.float32), z["c1_rms_var"])
+    assert rec["rms_count"] == int(z["c1_rms_count"])
+    assert np.array_equal(rec["obs"], z["c1_buf_obs"])
+    assert np.array_equal(rec["obs_next"], z["c1_buf_obs_next"])
+    assert np.array_equal(rec["rew"], z["c1_buf_rew"])
+    for k in ("v_s", "returns", "adv"):
+        want = z["pf_" + k]
+        np.testing.assert_allclose(rec[k], want, rtol=1e-5, atol=1e-6 * np.abs(want).max(),
+                                   err_msg=k)

@@ -694,6 +694,11 @@ extern "C" int tsrl_gae(const float* v_s, const float* v_s_next, const double* r
                         float* adv_out, float* ret_out, double* adv64_out, double* ret64_out,
                         double* ret_partials, void* workspace, int64_t workspace_bytes,
                         void* stream) {
+    // tsrl_gae_time_next's events belong to THIS call whichever path runs (or returns
+    // early): taken and cleared before anything can return, so they never reach a later,
+    // unrelated launch (e.g. one inside a graph capture)
+    hipEvent_t t0 = g_time_start, t1 = g_time_stop;
+    g_time_start = g_time_stop = nullptr;
     TSRL_CHECK_ARG(n >= 0, "tsrl_gae: n < 0");
     if (n == 0) return 0;
     TSRL_CHECK_ARG(v_s && v_s_next && rew && terminated && truncated,
@@ -733,9 +738,8 @@ extern "C" int tsrl_gae(const float* v_s, const float* v_s_next, const double* r
         TSRL_CHECK_ARG(grid < (1ll << 31), "tsrl_gae: too many ranges");
         const bool staged = vec_ok && !adv64_out && !ret64_out && r % TILE == 0 &&
                             n % r == 0 && !getenv("TSRL_GAE_UNSTAGED");
-        // tsrl_gae_time_next: the launch's own start / stop timestamps (hipExtLaunchKernel)
-        hipEvent_t t0 = g_time_start, t1 = g_time_stop;
-        g_time_start = g_time_stop = nullptr;
+        // tsrl_gae_time_next: the launch's own start / stop timestamps (hipExtLaunchKernel);
+        // the general path below launches three kernels and records none
         if (staged) {
             if (f64v)
                 hipExtLaunchKernelGGL(gae_rows_staged_kernel<true>, dim3((unsigned)grid),

@@ -148,6 +148,11 @@ __global__ __launch_bounds__(OTPB) void clip_adam_kernel(float* __restrict__ p,
                 __builtin_amdgcn_s_sleep(1);
             }
             s_late = late;
+            // the late slice alone would step with a NaN coefficient while the others may
+            // have seen every arrival: publish the timeout to a sticky device flag the host
+            // checks (FlatAdam.check_handoff), so the whole step is rejected, not one slice
+            if (late)
+                __hip_atomic_store(&ticket[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     if (clip) {

@@ -111,6 +111,24 @@ class DataParallel:
         dist.all_gather(out, t, group=self.group)
         return torch.cat(out)
 
+    def all_gather_known(self, t: torch.Tensor, lengths, kind: str = "other") -> torch.Tensor:
+        """all_gather_cat of 1-D tensors whose per-rank lengths every rank already knows
+        (``lengths[r]`` = rank r's numel, e.g. from the once-per-update shard table): each
+        rank pads to the longest, no length exchange and no host read."""
+        if not self.active:
+            return t
+        lengths = [int(k) for k in lengths]
+        assert lengths[self.rank] == t.numel(), (lengths, t.numel())
+        m = max(lengths)
+        if len(set(lengths)) == 1:
+            return self.all_gather_cat(t, kind)
+        pad = torch.zeros(m, dtype=t.dtype, device=t.device)
+        pad[:t.numel()] = t.reshape(-1)
+        LOG.note(kind, pad, "all_gather")
+        out = [torch.empty_like(pad) for _ in range(self.world)]
+        dist.all_gather(out, pad, group=self.group)
+        return torch.cat([o[:k] for o, k in zip(out, lengths)])
+
     def broadcast_params_(self, params: Iterable[torch.nn.Parameter], src: int = 0) -> None:
         """Make every rank's replica rank ``src``'s (one bucketed broadcast): data-parallel
         learning keeps identical replicas by applying the same all-reduced step, which needs

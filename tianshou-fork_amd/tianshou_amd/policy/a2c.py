@@ -1,4 +1,5 @@
 """A2CPolicy (tianshou/policy/modelfree/a2c.py:14-160): critic values + GAE on device."""
+import zlib
 from typing import Any, Callable, Dict, List, Optional
 
 import numpy as np
@@ -110,6 +111,52 @@ class A2CPolicy(PGPolicy):
             self.dp.broadcast_params_(self._actor_critic.parameters())
             self._replicas_synced = True
 
+    def _shard_table(self, n: int, row_len: int, dev) -> dict:
+        """Data parallel: every rank's row count, GAE row length and global np.random state
+        hash, exchanged with ONE all-gather of three int64 per rank and one host read.
+        process_fn makes it (``fresh``) and the update's learn() consumes it, so an update
+        reads the shard layout from the host once: the ret_rms partial counts of every rank
+        follow from it (no ragged length exchange), learn() checks the shared RandomState and
+        whether the shards are equal with it."""
+        st = np.random.get_state()
+        h = zlib.crc32(np.ascontiguousarray(st[1]).tobytes() + int(st[2]).to_bytes(4, "little"))
+        W = self.dp.world
+        hs = self.dp.all_gather_cat(torch.tensor([h, n, row_len], dtype=torch.int64,
+                                                 device=dev), kind="shard_table")
+        hs = hs.view(W, 3).cpu()
+        t = {"hash_equal": bool((hs[:, 0] == hs[0, 0]).all()), "n": hs[:, 1].tolist(),
+             "row_len": hs[:, 2].tolist(), "n_local": n, "fresh": True}
+        assert t["n"][self.dp.rank] == n
+        self._shards = t
+        return t
+
+    def _learn_shards(self, n: int, dev) -> dict:
+        """The shard table for this learn(): process_fn's of the same update if there is one,
+        else a new exchange (learn() called on its own).  Consumed here: the next update makes
+        its own."""
+        t = getattr(self, "_shards", None)
+        if t is None or not t["fresh"]:
+            t = self._shard_table(n, 0, dev)
+        elif t["n_local"] != n:
+            raise RuntimeError(f"learn() got {n} rows, this update's process_fn "
+                               f"{t['n_local']}")
+        t["fresh"] = False
+        return t
+
+    def _require_equal_shards(self, n: int, dev, path: str) -> None:
+        """Local minibatch splits (``split_indices`` over this rank's rows, b_global =
+        world x local size) need every rank to hold the same row count: otherwise the ranks
+        run different numbers of minibatches and their per-minibatch all-reduces stop
+        matching (a hang, or mixed payloads).  Raise instead."""
+        if not self.dp.active or self.dp.world == 1:
+            return
+        t = self._learn_shards(n, dev)
+        if len(set(t["n"])) > 1:
+            raise ValueError(
+                f"{type(self).__name__}.{path}: unequal data-parallel shards {t['n']} rows per "
+                f"rank; only the fused-MLP PPO update with dp_permutation='global' splits the "
+                f"global batch -- give every rank the same number of envs and steps")
+
     def _compute_returns(self, batch: Batch, buffer, indices: np.ndarray) -> Batch:
         self._sync_replicas()
         obs = torch.as_tensor(batch.obs)
@@ -124,17 +171,20 @@ class A2CPolicy(PGPolicy):
         trunc = torch.as_tensor(batch.truncated).to(dev).bool().contiguous()
         row_len, extra = self._gae_layout(buffer, indices)
         n = len(v_s)
+        tab = self._shard_table(n, row_len, dev) if self.dp.active else None
         if self._rew_norm:
             st = self.ret_rms.state
             scale = (st[1:2] + self._eps).sqrt()
-            nparts = int(_C.lib().tsrl_gae_num_partials(n, row_len))
+            num = _C.lib().tsrl_gae_num_partials
+            nparts = int(num(n, row_len))
             partials = torch.empty(max(nparts, 1) * 3, dtype=torch.float64, device=dev)
             adv, ret, _, _ = gae_device(v_s, v_s_, rew, term, trunc, self._gamma, self._lambda,
                                         row_len, extra, scale, ret_partials=partials)
             if self.dp.active:  # every rank folds every rank's partials in rank order
-                # (unequal env shards give unequal partial counts: ragged all-gather)
-                partials = self.dp.all_gather_cat(partials[:nparts * 3], kind="ret_rms",
-                                                  ragged=True)
+                # (unequal env shards give unequal partial counts, known from the table)
+                counts = [3 * int(num(nr, rl)) for nr, rl in zip(tab["n"], tab["row_len"])]
+                partials = self.dp.all_gather_known(partials[:nparts * 3], counts,
+                                                    kind="ret_rms")
                 nparts = partials.numel() // 3
             self.ret_rms.update_from_partials(partials, nparts)
         else:
@@ -147,6 +197,7 @@ class A2CPolicy(PGPolicy):
     def learn(self, batch: Batch, batch_size: int, repeat: int, **kwargs: Any
               ) -> Dict[str, List[float]]:
         """a2c.py:119-160 (generic torch path on device)."""
+        self._require_equal_shards(len(batch), next(self.critic.parameters()).device, "learn")
         losses, actor_losses, vf_losses, ent_losses = [], [], [], []
         for _ in range(repeat):
             for part in split_indices(len(batch), batch_size, True, True):

@@ -181,7 +181,7 @@ class FlatAdam:
             o += k
         self._adam = dict(optim=optim, p=flat_p, m=flat_m, v=flat_v, steps=steps, pviews=pviews,
                           mviews=mviews, vviews=vviews,
-                          ticket=torch.zeros(2, dtype=torch.int32, device=dev),
+                          ticket=torch.zeros(3, dtype=torch.int32, device=dev),
                           partials=torch.zeros(
                               max(int(_C.lib().tsrl_clip_adam_partials(n)), 1),
                               dtype=torch.float64, device=dev),
@@ -224,3 +224,15 @@ class FlatAdam:
             _C.ptr(st["partials"]), _C.ptr(st["norm"]), _C.ptr(st["ticket"]), _C.ptr(st["lr"]),
             split, int(bool(scale_grads)), _C.stream_ptr(st["p"].device)),
             "tsrl_clip_adam")
+
+    def check_handoff(self) -> None:
+        """Raise if any clip_adam launch since the last check timed out waiting for the slice
+        norms of the other workgroups (tsrl_clip_adam's sticky ticket[2]): its step used a
+        NaN clip coefficient in some slices only, so the parameters are invalid.  One 4-byte
+        read, after learn() has read its loss terms back anyway."""
+        st = self._adam
+        if st is not None and int(st["ticket"][2].item()) != 0:
+            st["ticket"][2].zero_()
+            raise RuntimeError("tsrl_clip_adam: the in-kernel gradient-norm hand-off timed out "
+                               "(workgroups not co-resident); this learn()'s parameters are "
+                               "invalid")

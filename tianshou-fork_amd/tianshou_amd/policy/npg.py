@@ -103,6 +103,7 @@ class NPGPolicy(FusedEvalMixin, A2CPolicy):
 
     def learn(self, batch: Batch, batch_size: int, repeat: int, **kwargs: Any
               ) -> Dict[str, List[float]]:
+        self._require_equal_shards(len(batch), next(self.critic.parameters()).device, "learn")
         actor_losses, vf_losses, kls = [], [], []
         for _ in range(repeat):
             for part in split_indices(len(batch), batch_size, True, True):

@@ -10,7 +10,6 @@ read back once at the end).  Other actor/dist combinations run the reference's t
 formulation on the GPU.
 """
 import contextlib
-import zlib
 from typing import Any, Callable, Dict, List, Optional
 
 import numpy as np
@@ -267,6 +266,8 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
         f32 = dict(device=dev, dtype=torch.float32)
         mlp_ok = self._mlp is not None and batch.obs.is_cuda and \
             batch.obs.dtype == torch.float32 and batch.obs.dim() == 2
+        if not self._global_perm(n, dev, mlp_ok):
+            self._require_equal_shards(n, dev, "learn")
         plans = self._plan_pipeline(n, dev, batch_size, repeat, mlp_ok)
         for step in range(repeat):
             if self._recompute_adv and step > 0:
@@ -320,6 +321,8 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
                 terms.append(t)
         vals = torch.cat([t.reshape(-1, 4) for t in terms]).cpu().numpy() if terms else \
             np.zeros((0, 4), np.float32)
+        if self._mlp is not None:
+            self._mlp.check_handoff()
         return {"loss": vals[:, 0].tolist(), "loss/clip": vals[:, 1].tolist(),
                 "loss/vf": vals[:, 2].tolist(), "loss/ent": vals[:, 3].tolist()}
 
@@ -382,19 +385,14 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
         cuda = dev.type == "cuda"
         if self._global_perm(n, dev, allow_global):
             if not self._np_perm_used:  # once per learn(): every rank holds the same stream
-                st = np.random.get_state()
-                h = zlib.crc32(np.ascontiguousarray(st[1]).tobytes() +
-                               int(st[2]).to_bytes(4, "little"))
-                hs = self.dp.all_gather_cat(torch.tensor([h, n], dtype=torch.int64,
-                                                         device=dev),
-                                                kind="perm_check").view(W, 2).cpu()
-                if not bool((hs[:, 0] == hs[0, 0]).all()):
+                # (the shard table of this update's process_fn: no second exchange)
+                tab = self._learn_shards(n, dev)
+                if not tab["hash_equal"]:
                     raise RuntimeError(
                         "dp_permutation='global' needs the same global np.random state on "
                         "every rank (seed np.random identically, or set "
                         "dp_permutation='local')")
-                sizes = hs[:, 1].tolist()
-                assert sizes[self.dp.rank] == n
+                sizes = tab["n"]
                 self._dp_shards = (sum(sizes[:self.dp.rank]), sum(sizes))
             lo, N = self._dp_shards
             B = batch_size * W
@@ -575,6 +573,7 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
         terms = []
         f32 = dict(device=dev, dtype=torch.float32)
         fa = self._cat_flat_adam()
+        self._require_equal_shards(n, dev, "learn")
         for step in range(repeat):
             if self._recompute_adv and step > 0:
                 batch = self._compute_returns(batch, self._buffer, self._indices)
@@ -603,6 +602,8 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
             self._cat_warm = True
         vals = torch.cat([t.reshape(-1, 4) for t in terms]).cpu().numpy() if terms else \
             np.zeros((0, 4), np.float32)
+        if fa is not None:
+            fa.check_handoff()
         return {"loss": vals[:, 0].tolist(), "loss/clip": vals[:, 1].tolist(),
                 "loss/vf": vals[:, 2].tolist(), "loss/ent": vals[:, 3].tolist()}
 
@@ -687,6 +688,7 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
     def _learn_generic(self, batch: Batch, batch_size: int, repeat: int
                        ) -> Dict[str, List[float]]:
         """ppo.py:99-162 as written, on device tensors."""
+        self._require_equal_shards(len(batch), next(self.critic.parameters()).device, "learn")
         losses, clip_losses, vf_losses, ent_losses = [], [], [], []
         for step in range(repeat):
             if self._recompute_adv and step > 0:

@@ -614,6 +614,76 @@ def gen_collector_wide():
     _save("collector_wide.npz", **out)
 
 
+RMS_FULL_ENVS = (0, 1, 7, 24, 999, 1000, 2047, 4095)  # envs whose normalised rows are kept
+RMS_FULL_STEPS = (0, 1, 2, 511, 904, 905, 952, 953, 975, 976, 992, 993, 998, 999, 1000, 1001,
+                  1999, 2000, 2046, 2047)  # around the kept envs' resets
+
+
+def gen_rms_fullT():
+    """obs_rms of the HEADLINE collect at full length: the reference
+    VectorEnvNormObs over a reference DummyVectorEnv of 4096 synthetic envs (D = 376, L = 1000,
+    seed 0: bench.py's config 3) driven for 2048 vector steps in the Collector's order
+    (collector.py:282-354: venv.step of every env, then venv.reset(done ids) of the envs that
+    finished -- venv_wrappers.py:77-99 updates RunningMeanStd on each, statistics.py:99-114).
+    The Collector, policy and buffer do not change the statistic (the env ignores actions), so
+    zero actions are sent.  Stored: the statistic after the initial reset and after every step
+    update and every reset update (f32 mean / var, ~4100 states), the done ids of every step,
+    and the normalised rows the wrapper returned for a few envs and steps (pins the test's
+    rebuild of buffer rows from the stored states)."""
+    import time as _time
+    E, D, A, L, T = 4096, 376, 17, 1000, 2048
+    venv = VectorEnvNormObs(DummyVectorEnv(
+        [lambda e=e: SynthGymEnv(e, D, A, L) for e in range(E)]))
+    keep = np.array(RMS_FULL_ENVS)
+    steps = set(RMS_FULL_STEPS)
+    out = dict(E=np.array(E), D=np.array(D), A=np.array(A), L=np.array(L), T=np.array(T),
+               keep_envs=keep, keep_steps=np.array(RMS_FULL_STEPS))
+    step_mean = np.zeros((T + 1, D), np.float32)
+    step_var = np.zeros((T + 1, D), np.float32)
+    reset_mean = np.zeros((T, D), np.float32)
+    reset_var = np.zeros((T, D), np.float32)
+    counts = np.zeros((T + 1, 2), np.int64)
+    done_ids, done_ptr = [], [0]
+    kept_obs_next = np.zeros((len(RMS_FULL_STEPS), len(keep), D), np.float32)
+    kept_reset = {}
+
+    def state(m, v, i):
+        rms = venv.get_obs_rms()
+        assert rms.mean.dtype == np.float32 and rms.var.dtype == np.float32
+        m[i], v[i] = rms.mean, rms.var
+        return rms.count
+
+    obs0, _ = venv.reset()
+    out["kept_obs0"] = np.asarray(obs0, np.float32)[keep]
+    counts[0, 0] = state(step_mean, step_var, 0)
+    act = np.zeros((E, A), np.float32)
+    t0 = _time.time()
+    for s in range(T):
+        obs_next, rew, term, trunc, _ = venv.step(act)
+        counts[s + 1, 0] = state(step_mean, step_var, s + 1)
+        if s in steps:
+            kept_obs_next[RMS_FULL_STEPS.index(s)] = np.asarray(obs_next, np.float32)[keep]
+        done = np.where(np.logical_or(term, trunc))[0]
+        done_ids.append(done)
+        done_ptr.append(done_ptr[-1] + len(done))
+        if len(done):
+            obs_r, _ = venv.reset(done)
+            counts[s + 1, 1] = state(reset_mean, reset_var, s)
+            for e in np.intersect1d(done, keep):
+                kept_reset[f"kept_reset_{s}_{e}"] = np.asarray(obs_r, np.float32)[
+                    int(np.where(done == e)[0][0])]
+        else:
+            reset_mean[s], reset_var[s] = step_mean[s + 1], step_var[s + 1]
+            counts[s + 1, 1] = counts[s + 1, 0]
+        if s % 128 == 0:
+            print(f"  rms_fullT step {s} ({_time.time() - t0:.0f}s)", flush=True)
+    out.update(step_mean=step_mean, step_var=step_var, reset_mean=reset_mean,
+               reset_var=reset_var, counts=counts,
+               done_ids=np.concatenate(done_ids).astype(np.int32),
+               done_ptr=np.array(done_ptr, np.int64), kept_obs_next=kept_obs_next, **kept_reset)
+    _save("rms_fullT.npz", **out)
+
+
 def gen_rms_wide():
     """One RunningMeanStd.update on a [4096, 376] batch of the synthetic env's raw rows, then
     a second one (the merge), stats only: the batch is regenerated from the env keys
@@ -1216,7 +1286,7 @@ if __name__ == "__main__":
     table = dict(returns=gen_returns_known, gae=gen_gae_random, buffer=gen_buffer_traces,
                  split=gen_split, rms=gen_rms, ppo=gen_ppo, collector=gen_collector,
                  collector_fused=gen_collector_fused, collector_wide=gen_collector_wide,
-                 rms_wide=gen_rms_wide,
+                 rms_wide=gen_rms_wide, rms_fullT=gen_rms_fullT,
                  stack=gen_stack, ppo_discrete=gen_ppo_discrete, npg=gen_npg, replay=gen_replay,
                  cartpole=gen_cartpole, sched=gen_sched,
                  persist=gen_persist, trainer=gen_trainer)
