@@ -295,15 +295,18 @@ __global__ __launch_bounds__(256, X6_OCC) void l1_fwd_x6_kernel(
 // Waits are counted `s_waitcnt vmcnt(N)` in inline asm (the LDS-DMA loads are inline asm
 // too, so the compiler inserts no drain of its own); the per-tile epilogue stores count in
 // vmcnt and are skipped by the count of the wait that follows them.
+// Round 6 (tools/r06_l1diag.sh, profiles/r06_l1_diag.log; diagnostic builds since removed,
+// standalone 262144 gathered rows at pitch 384, two passes each): this kernel 224-235 us;
+// without the X split (plane 0 reused) 218-223; without any MFMA 150-154; three of the six
+// products 176-180; without the W reloads 221-222; without the X reloads 184-186; without the
+// per-chunk barrier 223-225; LDS-DMA issue spread over the first MFMA pairs 226-228;
+// s_setprio around the MFMAs 243-246.  SQ counters (profiles/r06_l1_pmc.txt): MFMA busy 43 %
+// of the wave lifetime, waves issue-stalled 43 %, parked 32 %.  So neither the split VALU nor
+// the weight stream nor the barrier bounds it; the MFMA time and the gathered X rows add
+// rather than overlap.  A 16-k-chunk form with an 8-stage X ring (twice the chunks in flight,
+// 112 KB per CU; bit-identical, 53 MLP / PPO tests green) measured SLOWER, 246-256 us gathered
+// and 247-249 contiguous (profiles/r06_l1_deep_ab.log): in-flight depth is not the limit.
 // ---------------------------------------------------------------------------------------
-// L1D: diagnostic builds only (tools/build_variant.sh ... -DL1D=n; wrong results for n > 0):
-// 1 no X split (plane 0 reused), 2 no MFMA, 3 no per-chunk barrier, 4 weight fragments read
-// once per chunk, 5 s_setprio 1 around each k-step's MFMAs, 6 weight chunks loaded for the
-// first two chunks only, 7 X chunks loaded for the first two chunks only, 8 three of the six
-// products, 9 the chunk's LDS-DMA issue spread over its first MFMA pairs
-#ifndef L1D
-#define L1D 0
-#endif
 constexpr int RNW = 8;                   // waves per workgroup
 constexpr int RROWS = 32 * RNW;          // rows per tile
 constexpr int RTPW = 4;                  // tiles per workgroup (at most)
@@ -443,19 +446,9 @@ __global__ __launch_bounds__(RNW * 64, 1) void l1_ring_kernel(
             if (nx) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-#if L1D != 3
         __builtin_amdgcn_s_barrier();
-#endif
-#if L1D == 6
-        if (nx && cc < 1) issue_w();
-#elif L1D != 9
         if (nx) issue_w();
-#endif
-#if L1D == 7
-        if (cc + 2 < C && cc < 1) issue_x();
-#elif L1D != 9
         if (cc + 2 < C) issue_x();
-#endif
         const char* Xs = sm + cs_x * RXSTAGE;
         const char* Ws = sm + RWOFF + cs_w * RWSTAGE;
         cs_x = cs_x == RXS - 1 ? 0 : cs_x + 1;
@@ -468,75 +461,30 @@ __global__ __launch_bounds__(RNW * 64, 1) void l1_ring_kernel(
                 const float4 u = *reinterpret_cast<const float4*>(&Xs[swf_off(xr, 4 * s + 2 * h)]);
                 const float4 v = *reinterpret_cast<const float4*>(
                     &Xs[swf_off(xr, 4 * s + 2 * h + 1)]);
-#if L1D == 1
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    b[0][e] = (__bf16)(&u.x)[e];
-                    b[0][4 + e] = (__bf16)(&v.x)[e];
-                }
-                b[1] = b[0];
-                b[2] = b[0];
-#else
                 split4(u, b[0], b[1], b[2], 0);
                 split4(v, b[0], b[1], b[2], 4);
-#endif
             }
-#if L1D == 5
-            __builtin_amdgcn_s_setprio(1);
-#endif
 #pragma unroll
             for (int ip = 0; ip < NT; ip += 2) {
                 bf16x8 a0[NPL], a1[NPL];
                 const int ao0 = sw_off(32 * ip + c, 2 * s + h);
                 const int ao1 = sw_off(32 * (ip + 1) + c, 2 * s + h);
-#if L1D == 4
-                const int ip_r = 0, s_r = 0;
-                const int ar0 = sw_off(32 * ip_r + c, 2 * s_r + h);
-                const int ar1 = sw_off(32 * (ip_r + 1) + c, 2 * s_r + h);
-                (void)ao0;
-                (void)ao1;
-#else
-                const int ar0 = ao0, ar1 = ao1;
-#endif
 #pragma unroll
                 for (int p = 0; p < NPL; ++p) {
-                    a0[p] = *reinterpret_cast<const bf16x8*>(&Ws[p * HC * ROWB + ar0]);
-                    a1[p] = *reinterpret_cast<const bf16x8*>(&Ws[p * HC * ROWB + ar1]);
+                    a0[p] = *reinterpret_cast<const bf16x8*>(&Ws[p * HC * ROWB + ao0]);
+                    a1[p] = *reinterpret_cast<const bf16x8*>(&Ws[p * HC * ROWB + ao1]);
                 }
-#if L1D == 2
-#define RX6_PAIR(pa, pb)                                                                    \
-    acc[ip][pa] += (float)a0[pa][pb];                                                       \
-    acc[ip + 1][pb] += (float)a1[pa][pb] + (float)b[pb][pa];
-#else
 #define RX6_PAIR(pa, pb)                                                                    \
     acc[ip] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[pa], b[pb], acc[ip], 0, 0, 0);     \
     acc[ip + 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[pa], b[pb], acc[ip + 1], 0, 0, 0);
-#endif
                 RX6_PAIR(0, 0)
-#if L1D == 9
-                if (s == 0 && ip == 0) {
-                    __builtin_amdgcn_sched_barrier(0);
-                    if (nx) issue_w();
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-                if (s == 0 && ip == 2) {
-                    __builtin_amdgcn_sched_barrier(0);
-                    if (cc + 2 < C) issue_x();
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-#endif
                 RX6_PAIR(0, 1)
                 RX6_PAIR(1, 0)
-#if L1D != 8
                 RX6_PAIR(0, 2)
                 RX6_PAIR(1, 1)
                 RX6_PAIR(2, 0)
-#endif
 #undef RX6_PAIR
             }
-#if L1D == 5
-            __builtin_amdgcn_s_setprio(0);
-#endif
         }
         epi_prev = kc == nch - 1;
         if (epi_prev) {
