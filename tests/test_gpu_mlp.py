@@ -28,9 +28,11 @@ def _rho(r):
 
 
 def frag_to_rows(frag, n, nt=4):
-    """[row tile][feature tile][lane][16] MFMA-fragment layout -> [n, 32*nt]."""
+    """MFMA-fragment layout ([row tile][feature tile][q][lane][4], x6.h frag_off4: lane l's
+    16 values as four float4 pieces) -> [n, 32*nt]."""
     ntile = (n + 31) // 32
-    f = frag[:ntile * nt * 64 * 16].view(ntile, nt, 64, 16).cpu()
+    f = frag[:ntile * nt * 64 * 16].view(ntile, nt, 4, 64, 4).permute(0, 1, 3, 2, 4)
+    f = f.reshape(ntile, nt, 64, 16).cpu()
     out = torch.empty(ntile * 32, nt * 32)
     lane = torch.arange(64)
     for r in range(16):
@@ -106,7 +108,8 @@ def test_l1_fwd_x6_f32_accuracy(dev, D, n):
 def frag_to_rows_dev(frag, n, nt=4):
     """frag_to_rows on the device (for large n)."""
     ntile = (n + 31) // 32
-    f = frag[:ntile * nt * 64 * 16].view(ntile, nt, 64, 16)
+    f = frag[:ntile * nt * 64 * 16].view(ntile, nt, 4, 64, 4).permute(0, 1, 3, 2, 4)
+    f = f.reshape(ntile, nt, 64, 16)
     lane = torch.arange(64, device=frag.device)
     r = torch.arange(16, device=frag.device)
     feat = (r[None, :] & 3) + 8 * (r[None, :] >> 2) + 4 * (lane[:, None] >> 5)  # [64, 16]

@@ -143,7 +143,7 @@ __global__ __launch_bounds__(256, 2) void l1_fwd_kernel(
         if (kc + 1 < nchunks) store(buf ^ 1);
         __syncthreads();
     }
-    // epilogue: bias + tanh; frag layout [row tile][feature tile][lane][16] or row-major
+    // epilogue: bias + tanh; fragment layout (x6::frag_off4) or row-major
     const int64_t bt = (row0 >> 5) + w;
     const int64_t brow = row0 + 32 * w + c;
 #pragma unroll
@@ -156,10 +156,10 @@ __global__ __launch_bounds__(256, 2) void l1_fwd_kernel(
             v[r] = act_tanh ? tanh_nb(z) : z;
         }
         if (frag_out) {
-            float4* o = reinterpret_cast<float4*>(out + ((bt * NT + i) * 64 + l) * 16);
 #pragma unroll
             for (int q = 0; q < 4; ++q)
-                o[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+                *reinterpret_cast<float4*>(out + x6::frag_off4(bt * NT + i, l, q)) =
+                    make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
         } else if (brow < n) {
 #pragma unroll
             for (int q = 0; q < 4; ++q)
@@ -509,11 +509,12 @@ __global__ __launch_bounds__(T16_TPB, 1) void ppo_tail16_kernel(
         // ---- inputs ----------------------------------------------------------------------
         float h1[16];
         {
-            const float4* src = reinterpret_cast<const float4*>(
-                h1f + ((bt * NT + 2 * net + (g >> 1)) * 64 + 16 * half + b + 32 * (g & 1)) * 16);
+            const int64_t ftile = bt * NT + 2 * net + (g >> 1);
+            const int flane = 16 * half + b + 32 * (g & 1);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const float4 v = src[q];
+                const float4 v =
+                    *reinterpret_cast<const float4*>(h1f + x6::frag_off4(ftile, flane, q));
                 h1[4 * q] = v.x;
                 h1[4 * q + 1] = v.y;
                 h1[4 * q + 2] = v.z;
@@ -884,11 +885,10 @@ __global__ __launch_bounds__(256, 2) void eval_tail_kernel(const float* __restri
     auto load_unit = [&](int64_t bt, int net, float (&h1)[2][16]) {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-            const float4* src = reinterpret_cast<const float4*>(
-                h1f + ((bt * NT + 2 * net + i) * 64 + l) * 16);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const float4 v = src[q];
+                const float4 v = *reinterpret_cast<const float4*>(
+                    h1f + x6::frag_off4(bt * NT + 2 * net + i, l, q));
                 h1[i][4 * q] = v.x;
                 h1[i][4 * q + 1] = v.y;
                 h1[i][4 * q + 2] = v.z;

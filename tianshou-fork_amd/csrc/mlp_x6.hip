@@ -250,7 +250,7 @@ __global__ __launch_bounds__(256, X6_OCC) void l1_fwd_x6_kernel(
     }
 #undef X6_LOAD
 #undef X6_STORE
-    // epilogue: bias + tanh; frag layout [row tile][feature tile][lane][16] or row-major
+    // epilogue: bias + tanh; fragment layout (x6::frag_off4) or row-major
     const int64_t bt = (row0 >> 5) + w;
     const int64_t brow = row0 + 32 * w + c;
 #pragma unroll
@@ -263,10 +263,10 @@ __global__ __launch_bounds__(256, X6_OCC) void l1_fwd_x6_kernel(
             v[r] = act_tanh ? tanh_nb(z) : z;
         }
         if (frag_out) {
-            float4* o = reinterpret_cast<float4*>(out + ((bt * NT + i) * 64 + l) * 16);
 #pragma unroll
             for (int q = 0; q < 4; ++q)
-                o[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+                *reinterpret_cast<float4*>(out + x6::frag_off4(bt * NT + i, l, q)) =
+                    make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
         } else if (brow < n) {
 #pragma unroll
             for (int q = 0; q < 4; ++q)
@@ -488,7 +488,7 @@ __global__ __launch_bounds__(RNW * 64, 1) void l1_ring_kernel(
         }
         epi_prev = kc == nch - 1;
         if (epi_prev) {
-            // bias + tanh -> fragment layout [row tile][feature tile][lane][16]
+            // bias + tanh -> fragment layout (x6::frag_off4)
             const int64_t bt = (tile0 + tl) * (RROWS / 32) + w;
             const bool keep = bt < frag_tiles;
 #pragma unroll
@@ -506,10 +506,10 @@ __global__ __launch_bounds__(RNW * 64, 1) void l1_ring_kernel(
                     }
                 }
                 if (keep) {
-                    float4* o = reinterpret_cast<float4*>(out + ((bt * NT + i) * 64 + l) * 16);
 #pragma unroll
                     for (int q = 0; q < 4; ++q)
-                        o[q] = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+                        *reinterpret_cast<float4*>(out + x6::frag_off4(bt * NT + i, l, q)) =
+                            make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
                 }
             }
             // a tile whose fragments lie past the buffer issues no stores: keep the counted

@@ -40,5 +40,14 @@ __device__ __forceinline__ int sw_off(int row, int q) {
     return row * 64 + 16 * (q ^ ((row >> 2) & 3));
 }
 
+// Layer-1 activations in MFMA-fragment order (l1 kernels -> tail / eval-tail kernels): 32x32
+// fragment tile `tile` (= row tile * 4 + feature tile) holds lane l's 16 accumulator values
+// as four float4 pieces q = 0..3, piece q of all 64 lanes contiguous ([tile][q][lane][4]), so
+// each of the writer's four 16-byte stores covers one contiguous KB (round 6: the earlier
+// [tile][lane][16] order wrote 64-byte-strided pieces; -9.5 us per 262144-row layer-1 launch).
+__device__ __forceinline__ int64_t frag_off4(int64_t tile, int lane, int q) {
+    return tile * 1024 + (int64_t)(q * 64 + lane) * 4;
+}
+
 }  // namespace x6
 }  // namespace tsrl
