@@ -58,9 +58,13 @@ __host__ __device__ __forceinline__ uint64_t sm64(uint64_t x) {
     return z ^ (z >> 31);
 }
 
-// tanhf without branches: both halves of ROCm's __ocml_tanh_f32 (the |x| < 0.625 polynomial
-// and 1 - 2/(exp(2|x|) + 1)) are evaluated and selected, so the result is bit-identical to
-// tanhf while unrolled MFMA code keeps one basic block (ocml's branch splits it per call).
+// tanh without branches: both halves of ROCm's __ocml_tanh_f32 (the |x| < 0.625 polynomial
+// and 1 - 2/(exp(2|x|) + 1)) are evaluated and selected, so unrolled MFMA code keeps one basic
+// block (ocml's branch splits it per call).  Round 6: exp(2|x|) is one v_exp_f32 of
+// 2|x| log2(e) instead of expf's range-reduced form -- within 1.6 ulp of tanh (emulated
+// with correctly rounded exp2 / rcp over 3M points; expf's form 1.05 ulp), no longer
+// bit-identical to tanhf; layer 1 222 -> 208 us per 262144-row minibatch, the evaluation
+// of 2M rows 1800 -> 1688 us (tools/r06_tanh.sh, profiles/r06_tanh_ab.log).
 __device__ __forceinline__ float tanh_nb(float x) {
     const float ax = __builtin_fabsf(x);
     const float x2 = x * x;
@@ -69,7 +73,7 @@ __device__ __forceinline__ float tanh_nb(float x) {
     p = __builtin_fmaf(x2, p, 0x1.110704p-3f);
     p = __builtin_fmaf(x2, p, -0x1.555532p-2f);
     const float small = __builtin_fmaf(x2, ax * p, ax);
-    const float e = __builtin_expf(ax * 2.0f);
+    const float e = __builtin_amdgcn_exp2f(ax * 2.8853900817779268f);  // 2^(2|x| log2 e)
     const float large = __builtin_fmaf(-2.0f, __builtin_amdgcn_rcpf(e + 1.0f), 1.0f);
     return __builtin_copysignf(ax < 0.625f ? small : large, x);
 }
