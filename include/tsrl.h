@@ -355,6 +355,8 @@ int tsrl_rms_exact_stats(const float* x, int64_t k, const float* reset_x, const 
 int tsrl_rms_exact_stats_n(int nsteps, const float* const* x, const float* const* reset_x,
                            const uint8_t* const* done, int64_t k, int64_t dim,
                            void* const* stats, void* stream);
+/* The largest nsteps tsrl_rms_exact_stats_n accepts (the Collector clamps its exact_group). */
+int tsrl_rms_exact_stats_max_steps(void);
 /* *rel_dev = (*rel_dev + 1) % ring_size (device-side ring cursor for graph-captured steps). */
 int tsrl_ring_advance(int64_t* rel_dev, int64_t ring_size, void* stream);
 

@@ -173,3 +173,21 @@ def test_sorted_minibatch_device_labels(n, bs):
     np.testing.assert_array_equal(np.sort(got), np.arange(n))
     for s, e in split_bounds(n, bs, merge_last=True):
         assert np.all(np.diff(got[s:e]) > 0)
+
+
+def test_exact_group_clamped_to_library_bound():
+    """the pipelined exact obs_rms carries at most tsrl_rms_exact_stats_max_steps()
+    steps per statistics launch (rms.hip XSTEPS) and at most exact_pipeline - 1 (the group's
+    last rows must exist before its first step is merged); Collector._xpipe_group clamps to
+    both (no GPU call: the bound is a host-side constant of the library)."""
+    import types
+    from tianshou_amd import _C
+    from tianshou_amd.data.collector import Collector
+    cap = int(_C.lib().tsrl_rms_exact_stats_max_steps())
+    assert cap >= 2
+    grp = lambda g, d: Collector._xpipe_group(types.SimpleNamespace(  # noqa: E731
+        exact_group=g, exact_pipeline=d))
+    assert grp(2, 5) == 2
+    assert grp(cap + 3, cap + 10) == cap
+    assert grp(6, 3) == 2
+    assert grp(4, 1) == 1

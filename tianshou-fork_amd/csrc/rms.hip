@@ -631,6 +631,8 @@ extern "C" int64_t tsrl_rms_exact_stats_bytes(int64_t dim) {
     return dim > 0 ? (16 * dim + 7) / 8 * 8 + 16 : 0;
 }
 
+extern "C" int tsrl_rms_exact_stats_max_steps(void) { return tsrl::XSTEPS; }
+
 extern "C" int tsrl_rms_exact_stats_n(int nsteps, const float* const* x,
                                       const float* const* reset_x, const uint8_t* const* done,
                                       int64_t k, int64_t dim, void* const* stats, void* stream) {

@@ -130,6 +130,7 @@ _SIGS = {
     "tsrl_rms_exact_stats_bytes": ([_i64], _i64),
     "tsrl_rms_exact_stats": ([_p, _i64, _p, _p, _i64, _p, _p], ctypes.c_int),
     "tsrl_rms_exact_stats_n": ([_i32, _p, _p, _p, _i64, _i64, _p, _p], ctypes.c_int),
+    "tsrl_rms_exact_stats_max_steps": ([], ctypes.c_int),
     "tsrl_gather_rows": ([_p, _i64, _p, _i64, _p, _p], ctypes.c_int),
     "tsrl_gather_rows_pitched": ([_p, _i64, _i64, _p, _i64, _p, _p], ctypes.c_int),
     "tsrl_np_shuffle_draws": ([_p, _p, _i64, _p], ctypes.c_int),

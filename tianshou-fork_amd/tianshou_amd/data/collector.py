@@ -34,9 +34,6 @@ def _empty_data() -> Batch:
 
 
 class Collector:
-    # most steps one tsrl_rms_exact_stats_n launch takes (csrc/rms.hip XSTEPS)
-    XSTEPS_MAX = 4
-
     def __init__(self, policy, env, buffer: Optional[ReplayBuffer] = None,
                  preprocess_fn: Optional[Callable[..., Batch]] = None,
                  exploration_noise: bool = False, sync_obs_rms: bool = True) -> None:
@@ -495,9 +492,9 @@ class Collector:
     def _xpipe_group(self) -> int:
         """Steps per statistics launch: the group's last rows must exist d launches before
         its first step's statistic is merged, so m <= d - 1 (m = 1 below depth 2), and one
-        tsrl_rms_exact_stats_n launch carries at most XSTEPS_MAX steps (csrc/rms.hip XSTEPS)."""
+        tsrl_rms_exact_stats_n launch carries at most tsrl_rms_exact_stats_max_steps() steps."""
         return max(1, min(int(self.exact_group), int(self.exact_pipeline) - 1,
-                          self.XSTEPS_MAX))
+                          int(_C.lib().tsrl_rms_exact_stats_max_steps())))
 
     def _flush(self) -> None:
         """Run the pending buffer add of the last fused step (tsrl_buffer_add), after merging
