@@ -25,6 +25,13 @@
 
 #include "x6.h"
 
+#ifndef DQN_C1_GATHER
+#define DQN_C1_GATHER 0
+#endif
+#ifndef DQN_C2_GATHER
+#define DQN_C2_GATHER 0
+#endif
+
 namespace tsrl {
 namespace {
 
@@ -144,6 +151,134 @@ __global__ __launch_bounds__(256, 2) void dqn_conv1_fwd_kernel(
     }
 }
 
+// Round 6: the same products with each sample's frame stack staged in LDS.  The kernel above
+// gathers every B fragment from global memory: 8-byte loads whose 32 lanes overlap at a 4-byte
+// stride (each frame byte is fetched 4 times), so the address units, not the matrix cores, set
+// its pace (0.45 ms per 8192 samples, 0.14 of the bf16 rate).  Here a workgroup (4 waves, 2 per
+// CU: 48 KB weight planes + one 28224-byte frame stack) walks whole samples: the next sample's
+// stack is loaded into registers (16-byte coalesced loads) during the current sample's MFMAs and
+// written to LDS between two barriers; a lane's B fragment is one ds_read2_b32 of the staged
+// bytes.  The 400 output pixels of a sample are 13 tiles of 32 (the last half-full): wave w
+// takes tiles w, w + 4, w + 8 and wave 0 tile 12 as well.  Every accumulator sees the same
+// products in the same order as dqn_conv1_fwd_kernel (k-step j = 0..15, planes 0, 1, 2), so the
+// outputs are bit-identical to it.
+constexpr int C1L_TILES = (C1_PIX + 31) / 32;   // 13
+constexpr int C1L_V4 = C1_FRAME / 16;           // 1764 16-byte pieces per frame stack
+constexpr int C1L_PER = (C1L_V4 + 255) / 256;   // 7 per thread
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <bool A16>
+__global__ __launch_bounds__(256, 2) void dqn_conv1_fwd_lds_kernel(
+    const uint8_t* __restrict__ X, int64_t n, const float* __restrict__ W, int64_t sw0,
+    int64_t sw1, int64_t sw2, int64_t sw3, const float* __restrict__ bias, float scale,
+    int relu, float* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) char Ws[NPL][C1_OC * C1_ROWB];
+    __shared__ __attribute__((aligned(16))) uint8_t Fs[C1_FRAME];
+    __shared__ float sb[C1_OC];
+    const int t = threadIdx.x;
+    const int w = t >> 6, l = t & 63, h = l >> 5, c = l & 31;
+    for (int i = t; i < C1_OC * C1_KK; i += 256) {
+        const int m = i / C1_KK, k = i - m * C1_KK;
+        const int ci = k >> 6, kh = (k >> 3) & 7, kw = k & 7;
+        const float v = W[m * sw0 + ci * sw1 + kh * sw2 + kw * sw3];
+        __bf16 a0, a1, a2;
+        x6::split1(v, a0, a1, a2);
+        const int o = c1_off(m, k >> 3) + 2 * (k & 7);
+        *reinterpret_cast<__bf16*>(&Ws[0][o]) = a0;
+        *reinterpret_cast<__bf16*>(&Ws[1][o]) = a1;
+        *reinterpret_cast<__bf16*>(&Ws[2][o]) = a2;
+    }
+    if (t < C1_OC) sb[t] = bias ? bias[t] : 0.0f;
+    // frame staging: the 16-byte pieces t + 256 i of the next sample held in registers during
+    // the current sample's products (a frame base that is only 4-byte aligned: copied word by
+    // word between the barriers instead); macros, not lambdas: a lambda capturing fr put it in
+    // scratch memory
+    u32x4 fr[C1L_PER];  // a native vector type: an array of HIP's uint4 stays in scratch
+#define C1L_LOAD(smp)                                                                       \
+    if constexpr (A16) {                                                                    \
+        const u32x4* src_ = reinterpret_cast<const u32x4*>(X + (smp) * C1_FRAME);             \
+        _Pragma("unroll") for (int i = 0; i < C1L_PER; ++i)                                 \
+            fr[i] = src_[t + 256 * i < C1L_V4 ? t + 256 * i : 0];                           \
+    }
+#define C1L_STORE(smp)                                                                      \
+    if constexpr (A16) {                                                                    \
+        _Pragma("unroll") for (int i = 0; i < C1L_PER; ++i)                                 \
+            if (t + 256 * i < C1L_V4) reinterpret_cast<u32x4*>(Fs)[t + 256 * i] = fr[i];    \
+    } else {                                                                                \
+        const uint32_t* src_ = reinterpret_cast<const uint32_t*>(X + (smp) * C1_FRAME);     \
+        for (int q = t; q < C1L_V4 * 4; q += 256) reinterpret_cast<uint32_t*>(Fs)[q] = src_[q]; \
+    }
+    // one or two 32-pixel tiles of the staged sample smp: the 16 k-steps of 3 (+ 3) MFMAs
+    auto run_tiles = [out, scale, relu, c, h](int64_t smp, int ta, int tb) {
+        const bool two = tb < C1L_TILES;
+        const int pa = 32 * ta + c, pb = 32 * tb + c;
+        const bool va = pa < C1_PIX, vb = two && pb < C1_PIX;
+        int ba, bb;
+        {
+            const int qa = va ? pa : 0, qb = vb ? pb : 0;
+            const int oha = qa / C1_OUT, owa = qa - oha * C1_OUT;
+            const int ohb = qb / C1_OUT, owb = qb - ohb * C1_OUT;
+            ba = (C1_S * oha + h) * C1_HW + C1_S * owa;
+            bb = (C1_S * ohb + h) * C1_HW + C1_S * owb;
+        }
+        f32x16 acc0, acc1;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0.0f;
+        // partial unroll: a full one hoists all 16 k-steps' LDS reads (192 registers of
+        // weight fragments) and spills
+#pragma unroll 4
+        for (int j = 0; j < 16; ++j) {
+            const int off = (j >> 2) * (C1_HW * C1_HW) + 2 * (j & 3) * C1_HW;
+            const int ao = c1_off(c, 2 * j + h);
+            const bf16x8 w0 = *reinterpret_cast<const bf16x8*>(&Ws[0][ao]);
+            const bf16x8 w1 = *reinterpret_cast<const bf16x8*>(&Ws[1][ao]);
+            const bf16x8 w2 = *reinterpret_cast<const bf16x8*>(&Ws[2][ao]);
+            const uint32_t* fa = reinterpret_cast<const uint32_t*>(Fs + ba + off);
+            const bf16x8 b0 = bytes_to_bf16(fa[0], fa[1]);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0, b0, acc0, 0, 0, 0);
+            if (two) {
+                const uint32_t* fb = reinterpret_cast<const uint32_t*>(Fs + bb + off);
+                const bf16x8 b1 = bytes_to_bf16(fb[0], fb[1]);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0, b1, acc1, 0, 0, 0);
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1, b0, acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1, b1, acc1, 0, 0, 0);
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2, b0, acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2, b1, acc1, 0, 0, 0);
+            } else {
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1, b0, acc0, 0, 0, 0);
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2, b0, acc0, 0, 0, 0);
+            }
+        }
+#define C1L_EPI(ACC, P, V)                                                                  \
+        if (V) {                                                                            \
+            float4* o_ = reinterpret_cast<float4*>(out + (smp * C1_PIX + (P)) * C1_OC);     \
+            _Pragma("unroll") for (int q = 0; q < 4; ++q) {                                 \
+                float v_[4];                                                                \
+                _Pragma("unroll") for (int e = 0; e < 4; ++e) {                             \
+                    const float z_ = ACC[4 * q + e] / scale + sb[8 * q + 4 * h + e];        \
+                    v_[e] = relu ? fmaxf(z_, 0.0f) : z_;                                    \
+                }                                                                           \
+                o_[2 * q + h] = make_float4(v_[0], v_[1], v_[2], v_[3]);                    \
+            }                                                                               \
+        }
+        C1L_EPI(acc0, pa, va)
+        C1L_EPI(acc1, pb, vb)
+#undef C1L_EPI
+    };
+    int64_t smp = blockIdx.x;
+    if (smp < n) C1L_LOAD(smp)
+    for (; smp < n; smp += gridDim.x) {
+        __syncthreads();  // the previous sample's B reads are done (and, first, Ws / sb)
+        C1L_STORE(smp)
+        __syncthreads();
+        if (smp + gridDim.x < n) C1L_LOAD(smp + gridDim.x)
+        run_tiles(smp, w, w + 4);
+        run_tiles(smp, w + 8, w == 0 ? 12 : C1L_TILES);
+    }
+#undef C1L_LOAD
+#undef C1L_STORE
+}
+
 // ---------------------------------------------------------------------------------------
 // Data gradient of the second convolution (Conv2d(32, 64, 4, stride 2): [n,32,20,20] ->
 // [n,64,9,9]) as a bf16x6 implicit GEMM, the ReLU mask of its input (the first layer's
@@ -252,6 +387,151 @@ __global__ __launch_bounds__(256, 2) void dqn_conv2_dgrad_kernel(
             }
         }
     }
+}
+
+// Round 6: the same products with each sample's gy2 staged in LDS, split once.  The kernel
+// above gathers 32 16-byte pieces of gy2 per lane and tile from global memory (each gy2 element
+// fetched by 16 lanes across the 4 classes and taps) and splits every piece it uses.  Here a
+// workgroup of class cls (4 waves, 2 per CU: the class's 48 KB split sub-kernel + 31.5 KB of
+// gy2 planes) walks whole samples: the next sample's 81 x 64 gy2 values are loaded into
+// registers (16-byte coalesced) during the current sample's MFMAs, then split into the three
+// bf16 planes of an LDS image [82 pixels][64 co] (row 81 stays zero: the taps that fall
+// outside the 9 x 9 map read it) between two barriers.  A lane's B fragment is one
+// ds_read_b128 per plane (16-byte chunks XOR-swizzled by pixel, so the 16 lanes of a read
+// phase -- 16 different pixels -- hit distinct banks).  The 100 input pixels of the class
+// are 4 tiles of 32, one per wave (the last holds 4).  Every accumulator sees the same split
+// values and products in the same order as dqn_conv2_dgrad_kernel: bit-identical outputs.
+constexpr int C2L_PX = C2_OUT * C2_OUT;         // 81 gy2 pixels per sample
+constexpr int C2L_ROW = C2_CO * 2;              // 128 bytes per image row (64 bf16)
+constexpr int C2L_PLANE = (C2L_PX + 1) * C2L_ROW;
+constexpr int C2L_V4 = C2L_PX * C2_CO / 4;      // 1296 float4 pieces per sample
+constexpr int C2L_PER = (C2L_V4 + 255) / 256;   // 6 per thread
+typedef float f32x4n __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int c2l_off(int px, int q) { return px * C2L_ROW + 16 * (q ^ (px & 7)); }
+__device__ __forceinline__ uint32_t bf2(__bf16 lo, __bf16 hi) {
+    return (uint32_t)__builtin_bit_cast(uint16_t, lo) |
+           ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+}
+
+__global__ __launch_bounds__(256, 2) void dqn_conv2_dgrad_lds_kernel(
+    const float* __restrict__ gy, int64_t n, const float* __restrict__ W, int64_t sw0,
+    int64_t sw1, int64_t sw2, int64_t sw3, const float* __restrict__ z1,
+    float* __restrict__ dx) {
+    __shared__ __attribute__((aligned(16))) char Ws[NPL][C2_CI * C1_ROWB];
+    __shared__ __attribute__((aligned(16))) char Gs[NPL][C2L_PLANE];
+    const int t = threadIdx.x;
+    const int w = t >> 6, l = t & 63, h = l >> 5, c = l & 31;
+    const int cls = blockIdx.y, ph = cls >> 1, pw = cls & 1;
+    for (int i = t; i < C2_CI * 256; i += 256) {
+        const int ci = i >> 8, k = i & 255;
+        const int tap = k >> 6, co = k & 63;
+        const int kh = ph + 2 * (tap >> 1), kw = pw + 2 * (tap & 1);
+        const float v = W[co * sw0 + ci * sw1 + kh * sw2 + kw * sw3];
+        __bf16 a0, a1, a2;
+        x6::split1(v, a0, a1, a2);
+        const int o = c1_off(ci, k >> 3) + 2 * (k & 7);
+        *reinterpret_cast<__bf16*>(&Ws[0][o]) = a0;
+        *reinterpret_cast<__bf16*>(&Ws[1][o]) = a1;
+        *reinterpret_cast<__bf16*>(&Ws[2][o]) = a2;
+    }
+    if (t < C2L_ROW / 4) {  // the zero row
+#pragma unroll
+        for (int p = 0; p < NPL; ++p)
+            *reinterpret_cast<uint32_t*>(&Gs[p][C2L_PX * C2L_ROW + 4 * t]) = 0u;
+    }
+    // this wave's tile of the class: input pixel p = 32 w + c, and the gy2 pixel of each tap
+    const int p = 32 * w + c;
+    const bool live = p < C2_CPIX;
+    const int ih = 2 * ((live ? p : 0) / 10) + ph, iw = 2 * ((live ? p : 0) % 10) + pw;
+    int tpx[4];
+#pragma unroll
+    for (int tap = 0; tap < 4; ++tap) {
+        const int oh = (ih >> 1) - (tap >> 1), ow = (iw >> 1) - (tap & 1);
+        const bool ok = live && oh >= 0 && oh < C2_OUT && ow >= 0 && ow < C2_OUT;
+        tpx[tap] = ok ? oh * C2_OUT + ow : C2L_PX;
+    }
+    f32x4n gr[C2L_PER];
+#define C2L_LOAD(smp)                                                                       \
+    {                                                                                       \
+        const f32x4n* src_ = reinterpret_cast<const f32x4n*>(gy + (smp) * (C2L_PX * C2_CO)); \
+        _Pragma("unroll") for (int i = 0; i < C2L_PER; ++i)                                 \
+            gr[i] = src_[t + 256 * i < C2L_V4 ? t + 256 * i : 0];                           \
+    }
+    /* piece i: pixel q / 16, channels 4 (q % 16) .. + 3 -> 8 bytes of each plane */        \
+#define C2L_STORE()                                                                         \
+    {                                                                                       \
+        _Pragma("unroll") for (int i = 0; i < C2L_PER; ++i) {                               \
+            const int q_ = t + 256 * i;                                                     \
+            if (q_ < C2L_V4) {                                                              \
+                const int px_ = q_ >> 4, c4_ = q_ & 15;                                     \
+                const int o_ = c2l_off(px_, c4_ >> 1) + 8 * (c4_ & 1);                      \
+                uint32_t pk_[NPL][2];                                                       \
+                _Pragma("unroll") for (int e = 0; e < 4; e += 2) {                          \
+                    __bf16 x0_, x1_, x2_, y0_, y1_, y2_;                                    \
+                    x6::split1(gr[i][e], x0_, x1_, x2_);                                    \
+                    x6::split1(gr[i][e + 1], y0_, y1_, y2_);                                \
+                    pk_[0][e >> 1] = bf2(x0_, y0_);                                         \
+                    pk_[1][e >> 1] = bf2(x1_, y1_);                                         \
+                    pk_[2][e >> 1] = bf2(x2_, y2_);                                         \
+                }                                                                           \
+                _Pragma("unroll") for (int pp = 0; pp < NPL; ++pp)                          \
+                    *reinterpret_cast<uint2*>(&Gs[pp][o_]) = make_uint2(pk_[pp][0], pk_[pp][1]); \
+            }                                                                               \
+        }                                                                                   \
+    }
+    int64_t smp = blockIdx.x;
+    if (smp < n) C2L_LOAD(smp)
+    for (; smp < n; smp += gridDim.x) {
+        __syncthreads();  // the previous sample's B reads are done (and, first, Ws / zero row)
+        C2L_STORE()
+        __syncthreads();
+        if (smp + gridDim.x < n) C2L_LOAD(smp + gridDim.x)
+        const int64_t o = ((smp * C2_IN + ih) * C2_IN + iw) * C2_CI;
+        f32x4n zm[4];
+        if (live && z1) {
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq)
+                zm[qq] = reinterpret_cast<const f32x4n*>(z1 + o)[2 * qq + h];
+        }
+        f32x16 acc;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[e] = 0.0f;
+#pragma unroll 1
+        for (int tap = 0; tap < 4; ++tap) {
+          const int tp = tap == 0 ? tpx[0] : tap == 1 ? tpx[1] : tap == 2 ? tpx[2] : tpx[3];
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            const int j = 4 * tap + jj;
+            const int bo = c2l_off(tp, 2 * jj + h);
+            const int ao = c1_off(c, 2 * j + h);
+            bf16x8 a[NPL], b[NPL];
+#pragma unroll
+            for (int pl = 0; pl < NPL; ++pl) {
+                b[pl] = *reinterpret_cast<const bf16x8*>(&Gs[pl][bo]);
+                a[pl] = *reinterpret_cast<const bf16x8*>(&Ws[pl][ao]);
+            }
+            acc = x6::mfma6(a, b, acc);
+          }
+        }
+        if (live) {
+            float4* d = reinterpret_cast<float4*>(dx + o);
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq) {
+                float4 v = make_float4(acc[4 * qq], acc[4 * qq + 1], acc[4 * qq + 2],
+                                       acc[4 * qq + 3]);
+                if (z1) {
+                    v.x = zm[qq][0] > 0.0f ? v.x : 0.0f;
+                    v.y = zm[qq][1] > 0.0f ? v.y : 0.0f;
+                    v.z = zm[qq][2] > 0.0f ? v.z : 0.0f;
+                    v.w = zm[qq][3] > 0.0f ? v.w : 0.0f;
+                }
+                d[2 * qq + h] = v;
+            }
+        }
+    }
+#undef C2L_LOAD
+#undef C2L_STORE
 }
 
 // ---------------------------------------------------------------------------------------
@@ -467,15 +747,28 @@ extern "C" int tsrl_dqn_conv1_fwd(const uint8_t* frames, int64_t n, const float*
     TSRL_CHECK_ARG((((uintptr_t)frames) & 3) == 0 && aligned16(out),
                    "tsrl_dqn_conv1_fwd: frames must be 4-byte and out 16-byte aligned");
     TSRL_CHECK_ARG(scale > 0.0f, "tsrl_dqn_conv1_fwd: scale must be > 0");
-    const int64_t npix = n * C1_PIX;
-    const int64_t pairs = (npix + 63) / 64;
     int dev = 0, ncu = 256;
     if (hipGetDevice(&dev) == hipSuccess)
         (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+#if DQN_C1_GATHER
+    const int64_t npix = n * C1_PIX;
+    const int64_t pairs = (npix + 63) / 64;
     const int64_t grid = std::min<int64_t>((pairs + 3) / 4, (int64_t)ncu * 3);
     hipLaunchKernelGGL(dqn_conv1_fwd_kernel, dim3((unsigned)grid), dim3(256), 0,
                        as_stream(stream), frames, npix, w, sw0, sw1, sw2, sw3, bias, scale, relu,
                        out);
+#else
+    // one persistent workgroup per sample up to two per CU
+    const int64_t grid = std::min<int64_t>(n, (int64_t)ncu * 2);
+    if (aligned16(frames))
+        hipLaunchKernelGGL(dqn_conv1_fwd_lds_kernel<true>, dim3((unsigned)grid), dim3(256), 0,
+                           as_stream(stream), frames, n, w, sw0, sw1, sw2, sw3, bias, scale,
+                           relu, out);
+    else
+        hipLaunchKernelGGL(dqn_conv1_fwd_lds_kernel<false>, dim3((unsigned)grid), dim3(256), 0,
+                           as_stream(stream), frames, n, w, sw0, sw1, sw2, sw3, bias, scale,
+                           relu, out);
+#endif
     TSRL_LAUNCH_CHECK("tsrl_dqn_conv1_fwd");
     return 0;
 }
@@ -488,14 +781,21 @@ extern "C" int tsrl_dqn_conv2_dgrad(const float* gy, int64_t n, const float* w, 
     TSRL_CHECK_ARG(gy && w && dx, "tsrl_dqn_conv2_dgrad: null pointer");
     TSRL_CHECK_ARG(aligned16(gy) && aligned16(dx) && (!z1 || aligned16(z1)),
                    "tsrl_dqn_conv2_dgrad: gy / dx / z1 must be 16-byte aligned");
-    const int64_t ntile = (n * C2_CPIX + 31) / 32;
     int dev = 0, ncu = 256;
     if (hipGetDevice(&dev) == hipSuccess)
         (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+#if DQN_C2_GATHER
+    const int64_t ntile = (n * C2_CPIX + 31) / 32;
     // 4 parity classes x gx workgroups, 2 per CU in total
     const int64_t gx = std::max<int64_t>(1, std::min<int64_t>((ntile + 3) / 4, (int64_t)ncu / 2));
     hipLaunchKernelGGL(dqn_conv2_dgrad_kernel, dim3((unsigned)gx, 4), dim3(256), 0,
                        as_stream(stream), gy, n, w, sw0, sw1, sw2, sw3, z1, dx);
+#else
+    // 4 parity classes x gx persistent workgroups (samples bx, bx + gx, ...), 2 per CU
+    const int64_t gx = std::max<int64_t>(1, std::min<int64_t>(n, (int64_t)ncu / 2));
+    hipLaunchKernelGGL(dqn_conv2_dgrad_lds_kernel, dim3((unsigned)gx, 4), dim3(256), 0,
+                       as_stream(stream), gy, n, w, sw0, sw1, sw2, sw3, z1, dx);
+#endif
     TSRL_LAUNCH_CHECK("tsrl_dqn_conv2_dgrad");
     return 0;
 }
