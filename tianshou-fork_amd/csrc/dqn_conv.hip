@@ -397,8 +397,9 @@ __global__ __launch_bounds__(256, 2) void dqn_conv2_dgrad_kernel(
 // registers (16-byte coalesced) during the current sample's MFMAs, then split into the three
 // bf16 planes of an LDS image [82 pixels][64 co] (row 81 stays zero: the taps that fall
 // outside the 9 x 9 map read it) between two barriers.  A lane's B fragment is one
-// ds_read_b128 per plane (16-byte chunks XOR-swizzled by pixel, so the 16 lanes of a read
-// phase -- 16 different pixels -- hit distinct banks).  The 100 input pixels of the class
+// ds_read_b128 per plane (16-byte chunks XOR-swizzled by pixel / 2: a 128-byte row spans half
+// the 64 banks, so the 16 lanes of a read phase -- 16 different pixels -- hit distinct banks
+// when both the row parity and the swizzled chunk differ).  The 100 input pixels of the class
 // are 4 tiles of 32, one per wave (the last holds 4).  Every accumulator sees the same split
 // values and products in the same order as dqn_conv2_dgrad_kernel: bit-identical outputs.
 constexpr int C2L_PX = C2_OUT * C2_OUT;         // 81 gy2 pixels per sample
@@ -408,7 +409,9 @@ constexpr int C2L_V4 = C2L_PX * C2_CO / 4;      // 1296 float4 pieces per sample
 constexpr int C2L_PER = (C2L_V4 + 255) / 256;   // 6 per thread
 typedef float f32x4n __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ int c2l_off(int px, int q) { return px * C2L_ROW + 16 * (q ^ (px & 7)); }
+__device__ __forceinline__ int c2l_off(int px, int q) {
+    return px * C2L_ROW + 16 * (q ^ ((px >> 1) & 7));
+}
 __device__ __forceinline__ uint32_t bf2(__bf16 lo, __bf16 hi) {
     return (uint32_t)__builtin_bit_cast(uint16_t, lo) |
            ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
