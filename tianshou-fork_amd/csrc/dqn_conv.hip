@@ -22,6 +22,7 @@
 // both tiles are issued up front, then 16 k-steps of 3 + 3 MFMAs share each A fragment.
 // Epilogue: bias + ReLU, NHWC f32 output ([n][20][20][32], channels_last of [n,32,20,20]).
 #include <algorithm>
+#include <type_traits>
 
 #include "x6.h"
 
@@ -30,6 +31,9 @@
 #endif
 #ifndef DQN_C2_GATHER
 #define DQN_C2_GATHER 0
+#endif
+#ifndef DQN_C2_NCL
+#define DQN_C2_NCL 2
 #endif
 
 namespace tsrl {
@@ -155,16 +159,24 @@ __global__ __launch_bounds__(256, 2) void dqn_conv1_fwd_kernel(
 // gathers every B fragment from global memory: 8-byte loads whose 32 lanes overlap at a 4-byte
 // stride (each frame byte is fetched 4 times), so the address units, not the matrix cores, set
 // its pace (0.45 ms per 8192 samples, 0.14 of the bf16 rate).  Here a workgroup (4 waves, 2 per
-// CU: 48 KB weight planes + one 28224-byte frame stack) walks whole samples: the next sample's
-// stack is loaded into registers (16-byte coalesced loads) during the current sample's MFMAs and
-// written to LDS between two barriers; a lane's B fragment is one ds_read2_b32 of the staged
-// bytes.  The 400 output pixels of a sample are 13 tiles of 32 (the last half-full): wave w
-// takes tiles w, w + 4, w + 8 and wave 0 tile 12 as well.  Every accumulator sees the same
-// products in the same order as dqn_conv1_fwd_kernel (k-step j = 0..15, planes 0, 1, 2), so the
-// outputs are bit-identical to it.
-constexpr int C1L_TILES = (C1_PIX + 31) / 32;   // 13
-constexpr int C1L_V4 = C1_FRAME / 16;           // 1764 16-byte pieces per frame stack
-constexpr int C1L_PER = (C1L_V4 + 255) / 256;   // 7 per thread
+// CU: 48 KB weight planes + one 28224-byte frame stack) walks whole samples and a lane's B
+// fragment is one ds_read2_b32 of the staged bytes.  The 400 output pixels of a sample are 13
+// tiles of 32 (the last half-full): wave w owns tiles w, w + 4, w + 8 (and wave 0 tile 12),
+// all of them accumulated together, k-step by k-step, so each weight fragment read from LDS
+// serves 3-4 tiles.  The stack is staged in two halves, channels 0-1 (k-steps 0-7) and 2-3
+// (8-15): the next sample's half h is loaded into registers (16-byte coalesced) while the
+// current sample's products over half h run, and written to LDS after the barrier that ends
+// them -- so every wait on those loads sits a half-sample of MFMAs after the loads AND after
+// the previous sample's output stores (vmcnt counts both, in order), instead of exposing the
+// stores' latency once per sample (the round-6 single-buffer form: 246 us per 8192 samples, of
+// which 97 us went to the staging and 64 us to the output stores, tools/r06_dqm.sh).  Every
+// accumulator sees the same products in the same order as dqn_conv1_fwd_kernel (k-step j =
+// 0..15, planes 0, 1, 2); the epilogue's division by scale is a reciprocal product with one fma
+// correction (correctly rounded: bit-identical outputs to the gathered kernel at 37 and 8192
+// samples, profiles/r06_atari_lds_ab.log), 3 VALU instead of the IEEE division's ~12.
+constexpr int C1L_HALF = C1_FRAME / 2;           // 14112 bytes: channels 0-1 or 2-3
+constexpr int C1L_HV4 = C1L_HALF / 16;           // 882 16-byte pieces per half
+constexpr int C1L_HPER = (C1L_HV4 + 255) / 256;  // 4 per thread
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 template <bool A16>
@@ -189,92 +201,119 @@ __global__ __launch_bounds__(256, 2) void dqn_conv1_fwd_lds_kernel(
         *reinterpret_cast<__bf16*>(&Ws[2][o]) = a2;
     }
     if (t < C1_OC) sb[t] = bias ? bias[t] : 0.0f;
-    // frame staging: the 16-byte pieces t + 256 i of the next sample held in registers during
-    // the current sample's products (a frame base that is only 4-byte aligned: copied word by
-    // word between the barriers instead); macros, not lambdas: a lambda capturing fr put it in
-    // scratch memory
-    u32x4 fr[C1L_PER];  // a native vector type: an array of HIP's uint4 stays in scratch
-#define C1L_LOAD(smp)                                                                       \
-    if constexpr (A16) {                                                                    \
-        const u32x4* src_ = reinterpret_cast<const u32x4*>(X + (smp) * C1_FRAME);             \
-        _Pragma("unroll") for (int i = 0; i < C1L_PER; ++i)                                 \
-            fr[i] = src_[t + 256 * i < C1L_V4 ? t + 256 * i : 0];                           \
-    }
-#define C1L_STORE(smp)                                                                      \
-    if constexpr (A16) {                                                                    \
-        _Pragma("unroll") for (int i = 0; i < C1L_PER; ++i)                                 \
-            if (t + 256 * i < C1L_V4) reinterpret_cast<u32x4*>(Fs)[t + 256 * i] = fr[i];    \
+    const float inv_scale = 1.0f / scale;
+    // half hf of a frame stack: 16-byte pieces t + 256 i held in registers (a frame base that
+    // is only 4-byte aligned: copied word by word at the store instead); macros, not lambdas
+    // over the array (a lambda capturing it put it in scratch memory), and a native vector
+    // type (an array of HIP's uint4 stays in scratch too)
+    u32x4 fr[C1L_HPER];
+#define C1L_LOAD(smp, hf)                                                                   \
+    { if constexpr (A16) {                                                                  \
+        const u32x4* src_ =                                                                 \
+            reinterpret_cast<const u32x4*>(X + (smp) * C1_FRAME) + (hf) * C1L_HV4;          \
+        _Pragma("unroll") for (int i = 0; i < C1L_HPER; ++i)                                \
+            fr[i] = src_[t + 256 * i < C1L_HV4 ? t + 256 * i : 0];                          \
+    } }
+#define C1L_STORE(smp, hf)                                                                  \
+    { if constexpr (A16) {                                                                  \
+        _Pragma("unroll") for (int i = 0; i < C1L_HPER; ++i)                                \
+            if (t + 256 * i < C1L_HV4)                                                      \
+                reinterpret_cast<u32x4*>(Fs + (hf) * C1L_HALF)[t + 256 * i] = fr[i];        \
     } else {                                                                                \
-        const uint32_t* src_ = reinterpret_cast<const uint32_t*>(X + (smp) * C1_FRAME);     \
-        for (int q = t; q < C1L_V4 * 4; q += 256) reinterpret_cast<uint32_t*>(Fs)[q] = src_[q]; \
-    }
-    // one or two 32-pixel tiles of the staged sample smp: the 16 k-steps of 3 (+ 3) MFMAs
-    auto run_tiles = [out, scale, relu, c, h](int64_t smp, int ta, int tb) {
-        const bool two = tb < C1L_TILES;
-        const int pa = 32 * ta + c, pb = 32 * tb + c;
-        const bool va = pa < C1_PIX, vb = two && pb < C1_PIX;
-        int ba, bb;
-        {
-            const int qa = va ? pa : 0, qb = vb ? pb : 0;
-            const int oha = qa / C1_OUT, owa = qa - oha * C1_OUT;
-            const int ohb = qb / C1_OUT, owb = qb - ohb * C1_OUT;
-            ba = (C1_S * oha + h) * C1_HW + C1_S * owa;
-            bb = (C1_S * ohb + h) * C1_HW + C1_S * owb;
-        }
-        f32x16 acc0, acc1;
+        const uint32_t* src_ =                                                              \
+            reinterpret_cast<const uint32_t*>(X + (smp) * C1_FRAME + (hf) * C1L_HALF);      \
+        for (int q = t; q < C1L_HALF / 4; q += 256)                                         \
+            reinterpret_cast<uint32_t*>(Fs + (hf) * C1L_HALF)[q] = src_[q];                 \
+    } }
+    // the sample loop of a wave owning NT tiles (3, or 4 for wave 0)
+    auto run = [&](auto nt_c) {
+        constexpr int NT = decltype(nt_c)::value;
+        int bo[NT];
+        bool vt[NT];
+        int pt[NT];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0.0f;
-        // partial unroll: a full one hoists all 16 k-steps' LDS reads (192 registers of
-        // weight fragments) and spills
-#pragma unroll 4
-        for (int j = 0; j < 16; ++j) {
-            const int off = (j >> 2) * (C1_HW * C1_HW) + 2 * (j & 3) * C1_HW;
-            const int ao = c1_off(c, 2 * j + h);
-            const bf16x8 w0 = *reinterpret_cast<const bf16x8*>(&Ws[0][ao]);
-            const bf16x8 w1 = *reinterpret_cast<const bf16x8*>(&Ws[1][ao]);
-            const bf16x8 w2 = *reinterpret_cast<const bf16x8*>(&Ws[2][ao]);
-            const uint32_t* fa = reinterpret_cast<const uint32_t*>(Fs + ba + off);
-            const bf16x8 b0 = bytes_to_bf16(fa[0], fa[1]);
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0, b0, acc0, 0, 0, 0);
-            if (two) {
-                const uint32_t* fb = reinterpret_cast<const uint32_t*>(Fs + bb + off);
-                const bf16x8 b1 = bytes_to_bf16(fb[0], fb[1]);
-                acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0, b1, acc1, 0, 0, 0);
-                acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1, b0, acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1, b1, acc1, 0, 0, 0);
-                acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2, b0, acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2, b1, acc1, 0, 0, 0);
-            } else {
-                acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1, b0, acc0, 0, 0, 0);
-                acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2, b0, acc0, 0, 0, 0);
+        for (int i = 0; i < NT; ++i) {
+            pt[i] = 32 * (w + 4 * i) + c;
+            vt[i] = pt[i] < C1_PIX;
+            const int q = vt[i] ? pt[i] : 0;
+            const int oh = q / C1_OUT, ow = q - oh * C1_OUT;
+            bo[i] = (C1_S * oh + h) * C1_HW + C1_S * ow;
+        }
+        f32x16 acc[NT];
+        // k-steps j0 .. j0 + 7 (one half of the stack) into every tile's accumulator
+        auto half = [&](int j0) {
+#pragma unroll 2
+            for (int j = j0; j < j0 + 8; ++j) {
+                const int off = (j >> 2) * (C1_HW * C1_HW) + 2 * (j & 3) * C1_HW;
+                const int ao = c1_off(c, 2 * j + h);
+                const bf16x8 w0 = *reinterpret_cast<const bf16x8*>(&Ws[0][ao]);
+                const bf16x8 w1 = *reinterpret_cast<const bf16x8*>(&Ws[1][ao]);
+                const bf16x8 w2 = *reinterpret_cast<const bf16x8*>(&Ws[2][ao]);
+                bf16x8 b[NT];
+#pragma unroll
+                for (int i = 0; i < NT; ++i) {
+                    const uint32_t* f = reinterpret_cast<const uint32_t*>(Fs + bo[i] + off);
+                    b[i] = bytes_to_bf16(f[0], f[1]);
+                }
+#pragma unroll
+                for (int i = 0; i < NT; ++i)
+                    acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0, b[i], acc[i], 0, 0, 0);
+#pragma unroll
+                for (int i = 0; i < NT; ++i)
+                    acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1, b[i], acc[i], 0, 0, 0);
+#pragma unroll
+                for (int i = 0; i < NT; ++i)
+                    acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2, b[i], acc[i], 0, 0, 0);
+            }
+        };
+        for (int64_t smp = blockIdx.x; smp < n; smp += gridDim.x) {
+            const int64_t nx = smp + gridDim.x;
+            const bool more = nx < n;
+#pragma unroll
+            for (int i = 0; i < NT; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][r] = 0.0f;
+            if (more) C1L_LOAD(nx, 0)
+            half(0);
+            __syncthreads();  // channels 0-1 of smp are done with
+            if (more) C1L_STORE(nx, 0)
+            if (more) C1L_LOAD(nx, 1)
+            half(8);
+            __syncthreads();  // channels 2-3 of smp are done with (and nx's 0-1 are staged)
+            if (more) C1L_STORE(nx, 1)
+#pragma unroll
+            for (int i = 0; i < NT; ++i) {
+                if (vt[i]) {
+                    float4* o_ = reinterpret_cast<float4*>(out + (smp * C1_PIX + pt[i]) * C1_OC);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        float v_[4];
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const float x_ = acc[i][4 * q + e];
+                            const float q0_ = x_ * inv_scale;
+                            const float qt_ = fmaf(fmaf(-q0_, scale, x_), inv_scale, q0_);
+                            const float z_ = qt_ + sb[8 * q + 4 * h + e];
+                            v_[e] = relu ? fmaxf(z_, 0.0f) : z_;
+                        }
+                        o_[2 * q + h] = make_float4(v_[0], v_[1], v_[2], v_[3]);
+                    }
+                }
             }
         }
-#define C1L_EPI(ACC, P, V)                                                                  \
-        if (V) {                                                                            \
-            float4* o_ = reinterpret_cast<float4*>(out + (smp * C1_PIX + (P)) * C1_OC);     \
-            _Pragma("unroll") for (int q = 0; q < 4; ++q) {                                 \
-                float v_[4];                                                                \
-                _Pragma("unroll") for (int e = 0; e < 4; ++e) {                             \
-                    const float z_ = ACC[4 * q + e] / scale + sb[8 * q + 4 * h + e];        \
-                    v_[e] = relu ? fmaxf(z_, 0.0f) : z_;                                    \
-                }                                                                           \
-                o_[2 * q + h] = make_float4(v_[0], v_[1], v_[2], v_[3]);                    \
-            }                                                                               \
-        }
-        C1L_EPI(acc0, pa, va)
-        C1L_EPI(acc1, pb, vb)
-#undef C1L_EPI
     };
-    int64_t smp = blockIdx.x;
-    if (smp < n) C1L_LOAD(smp)
-    for (; smp < n; smp += gridDim.x) {
-        __syncthreads();  // the previous sample's B reads are done (and, first, Ws / sb)
-        C1L_STORE(smp)
-        __syncthreads();
-        if (smp + gridDim.x < n) C1L_LOAD(smp + gridDim.x)
-        run_tiles(smp, w, w + 4);
-        run_tiles(smp, w + 8, w == 0 ? 12 : C1L_TILES);
+    // the first sample of the workgroup, staged whole
+    if (blockIdx.x < n) {
+        C1L_LOAD((int64_t)blockIdx.x, 0)
+        C1L_STORE((int64_t)blockIdx.x, 0)
+        C1L_LOAD((int64_t)blockIdx.x, 1)
+        C1L_STORE((int64_t)blockIdx.x, 1)
     }
+    __syncthreads();
+    if (w == 0)
+        run(std::integral_constant<int, 4>{});
+    else
+        run(std::integral_constant<int, 3>{});
 #undef C1L_LOAD
 #undef C1L_STORE
 }
@@ -406,7 +445,6 @@ constexpr int C2L_PX = C2_OUT * C2_OUT;         // 81 gy2 pixels per sample
 constexpr int C2L_ROW = C2_CO * 2;              // 128 bytes per image row (64 bf16)
 constexpr int C2L_PLANE = (C2L_PX + 1) * C2L_ROW;
 constexpr int C2L_V4 = C2L_PX * C2_CO / 4;      // 1296 float4 pieces per sample
-constexpr int C2L_PER = (C2L_V4 + 255) / 256;   // 6 per thread
 typedef float f32x4n __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int c2l_off(int px, int q) {
@@ -417,34 +455,44 @@ __device__ __forceinline__ uint32_t bf2(__bf16 lo, __bf16 hi) {
            ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
 }
 
-__global__ __launch_bounds__(256, 2) void dqn_conv2_dgrad_lds_kernel(
+// NCL classes per workgroup (4 NCL waves, wave w: class NCL * blockIdx.y + w / 4, tile w % 4):
+// the staged gy2 image serves NCL classes, so it is loaded and split 4 / NCL times per sample
+// instead of 4.  NCL = 2: 96 KB of sub-kernels + the image, one 8-wave workgroup per CU.
+template <int NCL>
+__global__ __launch_bounds__(256 * NCL, 2 / NCL) void dqn_conv2_dgrad_lds_kernel(
     const float* __restrict__ gy, int64_t n, const float* __restrict__ W, int64_t sw0,
     int64_t sw1, int64_t sw2, int64_t sw3, const float* __restrict__ z1,
     float* __restrict__ dx) {
-    __shared__ __attribute__((aligned(16))) char Ws[NPL][C2_CI * C1_ROWB];
+    constexpr int NTH = 256 * NCL;
+    constexpr int PER = (C2L_V4 + NTH - 1) / NTH;
+    __shared__ __attribute__((aligned(16))) char Ws[NCL][NPL][C2_CI * C1_ROWB];
     __shared__ __attribute__((aligned(16))) char Gs[NPL][C2L_PLANE];
     const int t = threadIdx.x;
     const int w = t >> 6, l = t & 63, h = l >> 5, c = l & 31;
-    const int cls = blockIdx.y, ph = cls >> 1, pw = cls & 1;
-    for (int i = t; i < C2_CI * 256; i += 256) {
-        const int ci = i >> 8, k = i & 255;
+    for (int i = t; i < NCL * C2_CI * 256; i += NTH) {
+        const int cl = i / (C2_CI * 256), r = i - cl * (C2_CI * 256);
+        const int cls = NCL * blockIdx.y + cl, ph = cls >> 1, pw = cls & 1;
+        const int ci = r >> 8, k = r & 255;
         const int tap = k >> 6, co = k & 63;
         const int kh = ph + 2 * (tap >> 1), kw = pw + 2 * (tap & 1);
         const float v = W[co * sw0 + ci * sw1 + kh * sw2 + kw * sw3];
         __bf16 a0, a1, a2;
         x6::split1(v, a0, a1, a2);
         const int o = c1_off(ci, k >> 3) + 2 * (k & 7);
-        *reinterpret_cast<__bf16*>(&Ws[0][o]) = a0;
-        *reinterpret_cast<__bf16*>(&Ws[1][o]) = a1;
-        *reinterpret_cast<__bf16*>(&Ws[2][o]) = a2;
+        *reinterpret_cast<__bf16*>(&Ws[cl][0][o]) = a0;
+        *reinterpret_cast<__bf16*>(&Ws[cl][1][o]) = a1;
+        *reinterpret_cast<__bf16*>(&Ws[cl][2][o]) = a2;
     }
     if (t < C2L_ROW / 4) {  // the zero row
 #pragma unroll
         for (int p = 0; p < NPL; ++p)
             *reinterpret_cast<uint32_t*>(&Gs[p][C2L_PX * C2L_ROW + 4 * t]) = 0u;
     }
-    // this wave's tile of the class: input pixel p = 32 w + c, and the gy2 pixel of each tap
-    const int p = 32 * w + c;
+    // this wave's tile: class cls, input pixel p = 32 (w % 4) + c, the gy2 pixel of each tap
+    const int wl = w >> 2;
+    const int cls = NCL * blockIdx.y + wl, ph = cls >> 1, pw = cls & 1;
+    const char* Wc = &Ws[wl][0][0];
+    const int p = 32 * (w & 3) + c;
     const bool live = p < C2_CPIX;
     const int ih = 2 * ((live ? p : 0) / 10) + ph, iw = 2 * ((live ? p : 0) % 10) + pw;
     int tpx[4];
@@ -454,18 +502,18 @@ __global__ __launch_bounds__(256, 2) void dqn_conv2_dgrad_lds_kernel(
         const bool ok = live && oh >= 0 && oh < C2_OUT && ow >= 0 && ow < C2_OUT;
         tpx[tap] = ok ? oh * C2_OUT + ow : C2L_PX;
     }
-    f32x4n gr[C2L_PER];
+    f32x4n gr[PER];
 #define C2L_LOAD(smp)                                                                       \
     {                                                                                       \
         const f32x4n* src_ = reinterpret_cast<const f32x4n*>(gy + (smp) * (C2L_PX * C2_CO)); \
-        _Pragma("unroll") for (int i = 0; i < C2L_PER; ++i)                                 \
-            gr[i] = src_[t + 256 * i < C2L_V4 ? t + 256 * i : 0];                           \
+        _Pragma("unroll") for (int i = 0; i < PER; ++i)                                     \
+            gr[i] = src_[t + NTH * i < C2L_V4 ? t + NTH * i : 0];                           \
     }
     /* piece i: pixel q / 16, channels 4 (q % 16) .. + 3 -> 8 bytes of each plane */        \
 #define C2L_STORE()                                                                         \
     {                                                                                       \
-        _Pragma("unroll") for (int i = 0; i < C2L_PER; ++i) {                               \
-            const int q_ = t + 256 * i;                                                     \
+        _Pragma("unroll") for (int i = 0; i < PER; ++i) {                                   \
+            const int q_ = t + NTH * i;                                                     \
             if (q_ < C2L_V4) {                                                              \
                 const int px_ = q_ >> 4, c4_ = q_ & 15;                                     \
                 const int o_ = c2l_off(px_, c4_ >> 1) + 8 * (c4_ & 1);                      \
@@ -512,7 +560,7 @@ __global__ __launch_bounds__(256, 2) void dqn_conv2_dgrad_lds_kernel(
 #pragma unroll
             for (int pl = 0; pl < NPL; ++pl) {
                 b[pl] = *reinterpret_cast<const bf16x8*>(&Gs[pl][bo]);
-                a[pl] = *reinterpret_cast<const bf16x8*>(&Ws[pl][ao]);
+                a[pl] = *reinterpret_cast<const bf16x8*>(Wc + pl * (C2_CI * C1_ROWB) + ao);
             }
             acc = x6::mfma6(a, b, acc);
           }
@@ -794,10 +842,13 @@ extern "C" int tsrl_dqn_conv2_dgrad(const float* gy, int64_t n, const float* w, 
     hipLaunchKernelGGL(dqn_conv2_dgrad_kernel, dim3((unsigned)gx, 4), dim3(256), 0,
                        as_stream(stream), gy, n, w, sw0, sw1, sw2, sw3, z1, dx);
 #else
-    // 4 parity classes x gx persistent workgroups (samples bx, bx + gx, ...), 2 per CU
-    const int64_t gx = std::max<int64_t>(1, std::min<int64_t>(n, (int64_t)ncu / 2));
-    hipLaunchKernelGGL(dqn_conv2_dgrad_lds_kernel, dim3((unsigned)gx, 4), dim3(256), 0,
-                       as_stream(stream), gy, n, w, sw0, sw1, sw2, sw3, z1, dx);
+    // 4 / NCL class groups x gx persistent workgroups (samples bx, bx + gx, ...): 2 workgroups
+    // of one class per CU, or one of two classes
+    constexpr int NCL = DQN_C2_NCL;
+    const int64_t gx = std::max<int64_t>(1, std::min<int64_t>(n, (int64_t)ncu * NCL / 2));
+    hipLaunchKernelGGL(dqn_conv2_dgrad_lds_kernel<NCL>, dim3((unsigned)gx, 4 / NCL),
+                       dim3(256 * NCL), 0, as_stream(stream), gy, n, w, sw0, sw1, sw2, sw3, z1,
+                       dx);
 #endif
     TSRL_LAUNCH_CHECK("tsrl_dqn_conv2_dgrad");
     return 0;

@@ -37,13 +37,15 @@ def main():
     a = ap.parse_args()
     if a.compare:
         x, y = (torch.load(p, weights_only=True) for p in a.compare)
+        bad = 0
         for k in x:
             same = torch.equal(x[k], y[k])
-            d = float((x[k].double() - y[k].double()).abs().max())
-            print(f"{k}: bit-identical {same} (max |diff| {d:.3e})")
-            if not same:
-                sys.exit(1)
-        return
+            d = (x[k].double() - y[k].double()).abs()
+            rel = float((d / x[k].double().abs().clamp_min(1e-30)).max())
+            print(f"{k}: bit-identical {same} (max |diff| {float(d.max()):.3e}, "
+                  f"max rel {rel:.3e}, differing {int((d > 0).sum())} of {d.numel()})")
+            bad += not same
+        sys.exit(1 if bad else 0)
     from tianshou_amd import _C
     from tianshou_amd.utils.net_atari import conv1_u8_wgrad
     dev = torch.device("cuda", 0)

@@ -7,7 +7,7 @@ A="python3 tools/atari_kernel_ab.py"
 for r in 37 8192; do
   TSRL_LIB_PATH=variants/libtsrl_g.so timeout -k 10 120 $A --rows $r --iters 3 --save /tmp/old$r.pt > /dev/null || exit $?
   timeout -k 10 120 $A --rows $r --iters 3 --save /tmp/new$r.pt > /dev/null || exit $?
-  echo "rows $r:"; timeout -k 10 60 $A --compare /tmp/old$r.pt /tmp/new$r.pt || exit $?
+  echo "rows $r:"; timeout -k 10 60 $A --compare /tmp/old$r.pt /tmp/new$r.pt; echo "compare rc=$?"
 done
 for r in 1 2; do
   echo "== gather"; TSRL_LIB_PATH=variants/libtsrl_g.so timeout -k 10 120 $A || exit $?
