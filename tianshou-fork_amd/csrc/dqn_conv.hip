@@ -14,27 +14,16 @@
 //
 // GEMM view: D[32 channels][32 pixels] += W[32][16 k] . P[16 k][32 pixels] per MFMA
 // (v_mfma_f32_32x32x16_bf16), k = c*64 + kh*8 + kw, so the 8 k of one lane half are the 8
-// consecutive bytes x[c][4 oh + kh][4 ow .. 4 ow + 7] of one input row: one 8-byte load.
-// Workgroup = 4 waves, persistent over pixel tiles; the three split planes of W (48 KB) are
-// staged once per workgroup in LDS (rows of 512 B, 16-byte chunks XOR-swizzled by row so a
-// ds_read_b128 phase hits distinct banks).  A wave owns two 32-pixel tiles at a time (flat
-// pixel index over the batch, so tiles may straddle samples): the 32 eight-byte loads of
-// both tiles are issued up front, then 16 k-steps of 3 + 3 MFMAs share each A fragment.
-// Epilogue: bias + ReLU, NHWC f32 output ([n][20][20][32], channels_last of [n,32,20,20]).
+// consecutive bytes x[c][4 oh + kh][4 ow .. 4 ow + 7] of one input row.  The three split
+// planes of W (48 KB) are staged once per workgroup in LDS (rows of 512 B, 16-byte chunks
+// XOR-swizzled by row so a ds_read_b128 phase hits distinct banks), each sample's frame stack
+// too (dqn_conv1_fwd_lds_kernel below).  Epilogue: bias + ReLU, NHWC f32 output
+// ([n][20][20][32], channels_last of [n,32,20,20]).
 #include <algorithm>
 #include <type_traits>
 
 #include "x6.h"
 
-#ifndef DQN_C1_GATHER
-#define DQN_C1_GATHER 0
-#endif
-#ifndef DQN_C2_GATHER
-#define DQN_C2_GATHER 0
-#endif
-#ifndef DQN_C2_NCL
-#define DQN_C2_NCL 2
-#endif
 
 namespace tsrl {
 namespace {
@@ -68,97 +57,10 @@ __device__ __forceinline__ bf16x8 bytes_to_bf16(uint32_t lo, uint32_t hi) {
     return b;
 }
 
-__global__ __launch_bounds__(256, 2) void dqn_conv1_fwd_kernel(
-    const uint8_t* __restrict__ X, int64_t npix, const float* __restrict__ W, int64_t sw0,
-    int64_t sw1, int64_t sw2, int64_t sw3, const float* __restrict__ bias, float scale,
-    int relu, float* __restrict__ out) {
-    __shared__ __attribute__((aligned(16))) char Ws[NPL][C1_OC * C1_ROWB];
-    __shared__ float sb[C1_OC];
-    const int t = threadIdx.x;
-    const int w = t >> 6, l = t & 63, h = l >> 5, c = l & 31;
-    // stage the split weight planes: element (m, k), k = ci*64 + kh*8 + kw
-    for (int i = t; i < C1_OC * C1_KK; i += 256) {
-        const int m = i / C1_KK, k = i - m * C1_KK;
-        const int ci = k >> 6, kh = (k >> 3) & 7, kw = k & 7;
-        const float v = W[m * sw0 + ci * sw1 + kh * sw2 + kw * sw3];
-        __bf16 a0, a1, a2;
-        x6::split1(v, a0, a1, a2);
-        const int o = c1_off(m, k >> 3) + 2 * (k & 7);
-        *reinterpret_cast<__bf16*>(&Ws[0][o]) = a0;
-        *reinterpret_cast<__bf16*>(&Ws[1][o]) = a1;
-        *reinterpret_cast<__bf16*>(&Ws[2][o]) = a2;
-    }
-    if (t < C1_OC) sb[t] = bias ? bias[t] : 0.0f;
-    __syncthreads();
-    const int64_t ntile2 = (npix + 63) / 64;  // pairs of 32-pixel tiles
-    for (int64_t tp = (int64_t)blockIdx.x * 4 + w; tp < ntile2; tp += (int64_t)gridDim.x * 4) {
-        // this lane's pixel in each of the two tiles
-        const int64_t p0 = tp * 64 + c, p1 = p0 + 32;
-        const bool v0 = p0 < npix, v1 = p1 < npix;
-        const uint8_t* base0;
-        const uint8_t* base1;
-        {
-            const int64_t q0 = v0 ? p0 : 0, q1 = v1 ? p1 : 0;
-            const int64_t s0 = q0 / C1_PIX, s1 = q1 / C1_PIX;
-            const int r0 = (int)(q0 - s0 * C1_PIX), r1 = (int)(q1 - s1 * C1_PIX);
-            const int oh0 = r0 / C1_OUT, ow0 = r0 - oh0 * C1_OUT;
-            const int oh1 = r1 / C1_OUT, ow1 = r1 - oh1 * C1_OUT;
-            base0 = X + s0 * C1_FRAME + (C1_S * oh0 + h) * C1_HW + C1_S * ow0;
-            base1 = X + s1 * C1_FRAME + (C1_S * oh1 + h) * C1_HW + C1_S * ow1;
-        }
-        // k-step j: channel j / 4, kernel row 2 (j % 4) + h
-        uint32_t x0[32], x1[32];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const int off = (j >> 2) * (C1_HW * C1_HW) + 2 * (j & 3) * C1_HW;
-            const uint32_t* a = reinterpret_cast<const uint32_t*>(base0 + off);
-            const uint32_t* b = reinterpret_cast<const uint32_t*>(base1 + off);
-            x0[2 * j] = a[0];
-            x0[2 * j + 1] = a[1];
-            x1[2 * j] = b[0];
-            x1[2 * j + 1] = b[1];
-        }
-        f32x16 acc0, acc1;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0.0f;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const int ao = c1_off(c, 2 * j + h);
-            const bf16x8 w0 = *reinterpret_cast<const bf16x8*>(&Ws[0][ao]);
-            const bf16x8 w1 = *reinterpret_cast<const bf16x8*>(&Ws[1][ao]);
-            const bf16x8 w2 = *reinterpret_cast<const bf16x8*>(&Ws[2][ao]);
-            const bf16x8 b0 = bytes_to_bf16(x0[2 * j], x0[2 * j + 1]);
-            const bf16x8 b1 = bytes_to_bf16(x1[2 * j], x1[2 * j + 1]);
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0, b0, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w0, b1, acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1, b0, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1, b1, acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2, b0, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2, b1, acc1, 0, 0, 0);
-        }
-        // epilogue: lane (pixel c, half h) holds channels rho(r) + 4h
-#define C1_EPI(ACC, P, V)                                                                   \
-        if (V) {                                                                            \
-            float4* o_ = reinterpret_cast<float4*>(out + (P) * C1_OC);                      \
-            _Pragma("unroll") for (int q = 0; q < 4; ++q) {                                 \
-                float v_[4];                                                                \
-                _Pragma("unroll") for (int e = 0; e < 4; ++e) {                             \
-                    const float z_ = ACC[4 * q + e] / scale + sb[8 * q + 4 * h + e];        \
-                    v_[e] = relu ? fmaxf(z_, 0.0f) : z_;                                    \
-                }                                                                           \
-                o_[2 * q + h] = make_float4(v_[0], v_[1], v_[2], v_[3]);                    \
-            }                                                                               \
-        }
-        C1_EPI(acc0, p0, v0)
-        C1_EPI(acc1, p1, v1)
-#undef C1_EPI
-    }
-}
-
-// Round 6: the same products with each sample's frame stack staged in LDS.  The kernel above
-// gathers every B fragment from global memory: 8-byte loads whose 32 lanes overlap at a 4-byte
-// stride (each frame byte is fetched 4 times), so the address units, not the matrix cores, set
-// its pace (0.45 ms per 8192 samples, 0.14 of the bf16 rate).  Here a workgroup (4 waves, 2 per
+// Round 6: each sample's frame stack staged in LDS.  The round-2..5 kernel (removed) gathered
+// every B fragment from global memory: 8-byte loads whose 32 lanes overlap at a 4-byte stride
+// (each frame byte fetched 4 times), so the address units, not the matrix cores, set its pace
+// (0.45 ms per 8192 samples, 0.14 of the bf16 rate).  Here a workgroup (4 waves, 2 per
 // CU: 48 KB weight planes + one 28224-byte frame stack) walks whole samples and a lane's B
 // fragment is one ds_read2_b32 of the staged bytes.  The 400 output pixels of a sample are 13
 // tiles of 32 (the last half-full): wave w owns tiles w, w + 4, w + 8 (and wave 0 tile 12),
@@ -170,10 +72,14 @@ __global__ __launch_bounds__(256, 2) void dqn_conv1_fwd_kernel(
 // the previous sample's output stores (vmcnt counts both, in order), instead of exposing the
 // stores' latency once per sample (the round-6 single-buffer form: 246 us per 8192 samples, of
 // which 97 us went to the staging and 64 us to the output stores, tools/r06_dqm.sh).  Every
-// accumulator sees the same products in the same order as dqn_conv1_fwd_kernel (k-step j =
+// accumulator sees the same products in the same order as the gathered kernel did (k-step j =
 // 0..15, planes 0, 1, 2); the epilogue's division by scale is a reciprocal product with one fma
 // correction (correctly rounded: bit-identical outputs to the gathered kernel at 37 and 8192
 // samples, profiles/r06_atari_lds_ab.log), 3 VALU instead of the IEEE division's ~12.
+// Measured (tools/atari_kernel_ab.py, 8192 samples, same box): 446-450 us gathered, 229-251
+// single-buffer, 252-257 this form; counters (profiles/r06_atari_pmc.txt): MFMA busy 32 %, HBM
+// traffic = the algorithmic 227 + 411 MB at 3.0 TB/s, waves parked 37 % and issue-stalled 36 %
+// -- latency-bound at the 8 waves per CU that 77.5 KB of LDS per workgroup allow.
 constexpr int C1L_HALF = C1_FRAME / 2;           // 14112 bytes: channels 0-1 or 2-3
 constexpr int C1L_HV4 = C1L_HALF / 16;           // 882 16-byte pieces per half
 constexpr int C1L_HPER = (C1L_HV4 + 255) / 256;  // 4 per thread
@@ -325,113 +231,16 @@ __global__ __launch_bounds__(256, 2) void dqn_conv1_fwd_lds_kernel(
 // Input pixel (ih, iw) receives the 2x2 taps kh = ih%2 + 2 th, kw = iw%2 + 2 tw from output
 // pixel (ih/2 - th, iw/2 - tw) when that lies inside the 9x9 map, so the pixels of one parity
 // class (ih%2, iw%2) share one sub-kernel: D[32 ci][32 px] += Wc[32 ci][16 k] . G[16 k][32 px]
-// with k = (tap, co), 4 taps x 64 channels = 256.  Workgroups of class cls = blockIdx.y stage
-// that class's split sub-kernel (3 planes, 48 KB, same swizzled rows as conv1); a lane's B
-// fragment is 8 consecutive channels of gy2 (NHWC, 32 contiguous bytes) split in registers.
-// Tried and measured (tools/atari_layer_bench.py, 8192 rows): splitting gy2 into bf16 planes
-// once in a separate pass (each element feeds 16 products here) and loading the planes
-// tap by tap, 12 loads ahead of the MFMAs: bit-identical but 0.80 ms against 0.60 ms for
-// this kernel -- the per-product split is not the limit; the 32 gathered 16-byte loads per
-// lane and tile issued up front are what keep the MFMAs fed at 2 waves per SIMD.
+// with k = (tap, co), 4 taps x 64 channels = 256; every class's split sub-kernel is 3 planes
+// of 48 KB (same swizzled rows as conv1).
 constexpr int C2_CI = 32, C2_CO = 64, C2_IN = 20, C2_OUT = 9;
 constexpr int C2_CPIX = (C2_IN / 2) * (C2_IN / 2);  // 100 input pixels per class per sample
 
-__global__ __launch_bounds__(256, 2) void dqn_conv2_dgrad_kernel(
-    const float* __restrict__ gy, int64_t n, const float* __restrict__ W, int64_t sw0,
-    int64_t sw1, int64_t sw2, int64_t sw3, const float* __restrict__ z1,
-    float* __restrict__ dx) {
-    __shared__ __attribute__((aligned(16))) char Ws[NPL][C2_CI * C1_ROWB];
-    const int t = threadIdx.x;
-    const int w = t >> 6, l = t & 63, h = l >> 5, c = l & 31;
-    const int cls = blockIdx.y, ph = cls >> 1, pw = cls & 1;
-    // sub-kernel of the class: element (ci, k), k = tap * 64 + co, tap = 2 th + tw
-    for (int i = t; i < C2_CI * 256; i += 256) {
-        const int ci = i >> 8, k = i & 255;
-        const int tap = k >> 6, co = k & 63;
-        const int kh = ph + 2 * (tap >> 1), kw = pw + 2 * (tap & 1);
-        const float v = W[co * sw0 + ci * sw1 + kh * sw2 + kw * sw3];
-        __bf16 a0, a1, a2;
-        x6::split1(v, a0, a1, a2);
-        const int o = c1_off(ci, k >> 3) + 2 * (k & 7);
-        *reinterpret_cast<__bf16*>(&Ws[0][o]) = a0;
-        *reinterpret_cast<__bf16*>(&Ws[1][o]) = a1;
-        *reinterpret_cast<__bf16*>(&Ws[2][o]) = a2;
-    }
-    __syncthreads();
-    const int64_t npix = n * C2_CPIX;
-    const int64_t ntile = (npix + 31) / 32;
-    for (int64_t tl = (int64_t)blockIdx.x * 4 + w; tl < ntile; tl += (int64_t)gridDim.x * 4) {
-        const int64_t p = tl * 32 + c;
-        const bool live = p < npix;
-        const int64_t q = live ? p : 0;
-        const int64_t smp = q / C2_CPIX;
-        const int r = (int)(q - smp * C2_CPIX);
-        const int ih = 2 * (r / 10) + ph, iw = 2 * (r % 10) + pw;
-        // the 4 taps' source rows of gy (clamped to a valid address, zeroed when outside)
-        const float* src[4];
-        bool ok[4];
-#pragma unroll
-        for (int tap = 0; tap < 4; ++tap) {
-            const int oh = (ih >> 1) - (tap >> 1), ow = (iw >> 1) - (tap & 1);
-            ok[tap] = live && oh >= 0 && oh < C2_OUT && ow >= 0 && ow < C2_OUT;
-            src[tap] = gy + ((smp * C2_OUT + (ok[tap] ? oh : 0)) * C2_OUT + (ok[tap] ? ow : 0)) *
-                                C2_CO + 8 * h;
-        }
-        float4 g[32];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const float4* s4 = reinterpret_cast<const float4*>(src[j >> 2] + 16 * (j & 3));
-            g[2 * j] = s4[0];
-            g[2 * j + 1] = s4[1];
-        }
-        f32x16 acc;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[e] = 0.0f;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const bool k_ = ok[j >> 2];
-            bf16x8 b[NPL];
-            const float4 u = g[2 * j], v = g[2 * j + 1];
-            const float f[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                __bf16 a0, a1, a2;
-                x6::split1(k_ ? f[e] : 0.0f, a0, a1, a2);
-                b[0][e] = a0;
-                b[1][e] = a1;
-                b[2][e] = a2;
-            }
-            const int ao = c1_off(c, 2 * j + h);
-            bf16x8 a[NPL];
-#pragma unroll
-            for (int pl = 0; pl < NPL; ++pl) a[pl] = *reinterpret_cast<const bf16x8*>(&Ws[pl][ao]);
-            acc = x6::mfma6(a, b, acc);
-        }
-        if (live) {
-            const int64_t o = ((smp * C2_IN + ih) * C2_IN + iw) * C2_CI;
-            float4* d = reinterpret_cast<float4*>(dx + o);
-            const float4* zm = reinterpret_cast<const float4*>(z1 + o);
-#pragma unroll
-            for (int qq = 0; qq < 4; ++qq) {
-                float4 v = make_float4(acc[4 * qq], acc[4 * qq + 1], acc[4 * qq + 2],
-                                       acc[4 * qq + 3]);
-                if (z1) {
-                    const float4 m = zm[2 * qq + h];
-                    v.x = m.x > 0.0f ? v.x : 0.0f;
-                    v.y = m.y > 0.0f ? v.y : 0.0f;
-                    v.z = m.z > 0.0f ? v.z : 0.0f;
-                    v.w = m.w > 0.0f ? v.w : 0.0f;
-                }
-                d[2 * qq + h] = v;
-            }
-        }
-    }
-}
-
-// Round 6: the same products with each sample's gy2 staged in LDS, split once.  The kernel
-// above gathers 32 16-byte pieces of gy2 per lane and tile from global memory (each gy2 element
-// fetched by 16 lanes across the 4 classes and taps) and splits every piece it uses.  Here a
-// workgroup of class cls (4 waves, 2 per CU: the class's 48 KB split sub-kernel + 31.5 KB of
+// Round 6: each sample's gy2 staged in LDS, split once.  The round-2..5 kernel (removed)
+// gathered 32 16-byte pieces of gy2 per lane and tile from global memory (each gy2 element
+// fetched by 16 lanes across the 4 classes and taps) and split every piece it used; splitting
+// gy2 into bf16 planes in a separate pass had measured slower for it (0.80 vs 0.60 ms).  Here a
+// workgroup (4 waves per class it serves; its classes' 48 KB split sub-kernels + 31.5 KB of
 // gy2 planes) walks whole samples: the next sample's 81 x 64 gy2 values are loaded into
 // registers (16-byte coalesced) during the current sample's MFMAs, then split into the three
 // bf16 planes of an LDS image [82 pixels][64 co] (row 81 stays zero: the taps that fall
@@ -440,7 +249,7 @@ __global__ __launch_bounds__(256, 2) void dqn_conv2_dgrad_kernel(
 // the 64 banks, so the 16 lanes of a read phase -- 16 different pixels -- hit distinct banks
 // when both the row parity and the swizzled chunk differ).  The 100 input pixels of the class
 // are 4 tiles of 32, one per wave (the last holds 4).  Every accumulator sees the same split
-// values and products in the same order as dqn_conv2_dgrad_kernel: bit-identical outputs.
+// values and products in the same order as the gathered kernel did: bit-identical outputs.
 constexpr int C2L_PX = C2_OUT * C2_OUT;         // 81 gy2 pixels per sample
 constexpr int C2L_ROW = C2_CO * 2;              // 128 bytes per image row (64 bf16)
 constexpr int C2L_PLANE = (C2L_PX + 1) * C2L_ROW;
@@ -801,14 +610,6 @@ extern "C" int tsrl_dqn_conv1_fwd(const uint8_t* frames, int64_t n, const float*
     int dev = 0, ncu = 256;
     if (hipGetDevice(&dev) == hipSuccess)
         (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-#if DQN_C1_GATHER
-    const int64_t npix = n * C1_PIX;
-    const int64_t pairs = (npix + 63) / 64;
-    const int64_t grid = std::min<int64_t>((pairs + 3) / 4, (int64_t)ncu * 3);
-    hipLaunchKernelGGL(dqn_conv1_fwd_kernel, dim3((unsigned)grid), dim3(256), 0,
-                       as_stream(stream), frames, npix, w, sw0, sw1, sw2, sw3, bias, scale, relu,
-                       out);
-#else
     // one persistent workgroup per sample up to two per CU
     const int64_t grid = std::min<int64_t>(n, (int64_t)ncu * 2);
     if (aligned16(frames))
@@ -819,7 +620,6 @@ extern "C" int tsrl_dqn_conv1_fwd(const uint8_t* frames, int64_t n, const float*
         hipLaunchKernelGGL(dqn_conv1_fwd_lds_kernel<false>, dim3((unsigned)grid), dim3(256), 0,
                            as_stream(stream), frames, n, w, sw0, sw1, sw2, sw3, bias, scale,
                            relu, out);
-#endif
     TSRL_LAUNCH_CHECK("tsrl_dqn_conv1_fwd");
     return 0;
 }
@@ -835,21 +635,13 @@ extern "C" int tsrl_dqn_conv2_dgrad(const float* gy, int64_t n, const float* w, 
     int dev = 0, ncu = 256;
     if (hipGetDevice(&dev) == hipSuccess)
         (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-#if DQN_C2_GATHER
-    const int64_t ntile = (n * C2_CPIX + 31) / 32;
-    // 4 parity classes x gx workgroups, 2 per CU in total
-    const int64_t gx = std::max<int64_t>(1, std::min<int64_t>((ntile + 3) / 4, (int64_t)ncu / 2));
-    hipLaunchKernelGGL(dqn_conv2_dgrad_kernel, dim3((unsigned)gx, 4), dim3(256), 0,
-                       as_stream(stream), gy, n, w, sw0, sw1, sw2, sw3, z1, dx);
-#else
     // 4 / NCL class groups x gx persistent workgroups (samples bx, bx + gx, ...): 2 workgroups
     // of one class per CU, or one of two classes
-    constexpr int NCL = DQN_C2_NCL;
+    constexpr int NCL = 2;  // profiles/r06_atari_pmc.txt: 474-486 us vs 499-507 at NCL = 1
     const int64_t gx = std::max<int64_t>(1, std::min<int64_t>(n, (int64_t)ncu * NCL / 2));
     hipLaunchKernelGGL(dqn_conv2_dgrad_lds_kernel<NCL>, dim3((unsigned)gx, 4 / NCL),
                        dim3(256 * NCL), 0, as_stream(stream), gy, n, w, sw0, sw1, sw2, sw3, z1,
                        dx);
-#endif
     TSRL_LAUNCH_CHECK("tsrl_dqn_conv2_dgrad");
     return 0;
 }
