@@ -432,9 +432,14 @@ __global__ __launch_bounds__(256, 2) void dqn_conv1_wgrad_kernel(
     const int64_t c1 = min(nchunk, c0 + cpw);
     // staging roles: im2col run q = t >> 3 (ci = q >> 3, kh = q & 7) of the pixel quads
     // 4 (pg + 8 j) .. + 3, pg = t & 7: 8 bytes per pixel, re-packed as 4-pixel dwords of the 8
-    // rows k = 8q + kw; gradient float4 (t & 7) (channels 4gq..4gq+3) of pixels gp + 32 j
+    // rows k = 8q + kw; gradient float4s (channels 4gq..4gq+3, gq = (t >> 4) & 7) of the pixel
+    // pairs 2 gp + 32 (2 jj + hf) + {0, 1}, gp = t & 15, hf = t >> 7, jj = 0, 1 -- so each
+    // split plane takes one 4-byte store per channel and pair, and the 32 lanes of a store
+    // phase (16 pairs x 2 channel groups) hit 32 distinct banks (round 6: the earlier 2-byte
+    // store per pixel and plane, lanes spread over channels, made 52 % of this kernel's LDS
+    // cycles bank conflicts, profiles/r06_atari_pmc.txt)
     const int q = t >> 3, pg = t & 7;
-    const int gq = t & 7, gp = t >> 3;
+    const int gq = (t >> 4) & 7, gp = t & 15, hf = t >> 7;
     const int qoff = (q >> 3) * (C1_HW * C1_HW) + (q & 7) * C1_HW;  // channel + kernel row
     // A pixel quad 4m..4m+3 never straddles an output row or a sample (20 and 400 are
     // multiples of 4, and so is npix), so its 4 eight-byte runs are the 20-byte window
@@ -456,7 +461,7 @@ __global__ __launch_bounds__(256, 2) void dqn_conv1_wgrad_kernel(
             const uint32_t* a_ = reinterpret_cast<const uint32_t*>(                         \
                 X + (int64_t)s_ * C1_FRAME + qoff + C1_S * oh_ * C1_HW + C1_S * ow_);        \
             _Pragma("unroll") for (int d = 0; d < 5; ++d) rb[j][d] = a_[d];                 \
-            const int64_t g_ = (ch) * C1W_CH + gp + 32 * j;                                 \
+            const int64_t g_ = (ch) * C1W_CH + 2 * gp + 32 * (2 * (j >> 1) + hf) + (j & 1); \
             gv[j] = *reinterpret_cast<const float4*>(gy + (g_ < npix ? g_ : 0) * C1_OC + 4 * gq); \
         }                                                                                   \
     }
@@ -475,17 +480,25 @@ __global__ __launch_bounds__(256, 2) void dqn_conv1_wgrad_kernel(
                 *reinterpret_cast<uint32_t*>(&Pb[(8 * q + e) * C1W_PR + px0_]) =            \
                     (lo_ | hi_) & m_;                                                       \
             }                                                                               \
-            const bool ok_ = (ch) * C1W_CH + gp + 32 * j < npix;                            \
-            const float g_[4] = {ok_ ? gv[j].x : 0.f, ok_ ? gv[j].y : 0.f,                  \
-                                 ok_ ? gv[j].z : 0.f, ok_ ? gv[j].w : 0.f};                 \
+        }                                                                                   \
+        _Pragma("unroll") for (int jj = 0; jj < 2; ++jj) {                                  \
+            const int px_ = 2 * gp + 32 * (2 * jj + hf);                                    \
+            const bool ok0_ = (ch) * C1W_CH + px_ < npix;                                   \
+            const bool ok1_ = (ch) * C1W_CH + px_ + 1 < npix;                               \
+            const float4 u_ = gv[2 * jj], v_ = gv[2 * jj + 1];                              \
+            const float ga_[4] = {ok0_ ? u_.x : 0.f, ok0_ ? u_.y : 0.f,                     \
+                                  ok0_ ? u_.z : 0.f, ok0_ ? u_.w : 0.f};                    \
+            const float gb_[4] = {ok1_ ? v_.x : 0.f, ok1_ ? v_.y : 0.f,                     \
+                                  ok1_ ? v_.z : 0.f, ok1_ ? v_.w : 0.f};                    \
             _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                 \
-                __bf16 a0_, a1_, a2_;                                                       \
-                x6::split1(g_[e], a0_, a1_, a2_);                                           \
-                const int o_ = (4 * gq + e) * C1W_GR + 2 * (gp + 32 * j);                   \
-                *reinterpret_cast<__bf16*>(&Gs[0][o_]) = a0_;                               \
-                *reinterpret_cast<__bf16*>(&Gs[1][o_]) = a1_;                               \
-                *reinterpret_cast<__bf16*>(&Gs[2][o_]) = a2_;                               \
-                db[e] += g_[e];                                                             \
+                __bf16 a0_, a1_, a2_, b0_, b1_, b2_;                                        \
+                x6::split1(ga_[e], a0_, a1_, a2_);                                          \
+                x6::split1(gb_[e], b0_, b1_, b2_);                                          \
+                const int o_ = (4 * gq + e) * C1W_GR + 2 * px_;                             \
+                *reinterpret_cast<uint32_t*>(&Gs[0][o_]) = bf2(a0_, b0_);                   \
+                *reinterpret_cast<uint32_t*>(&Gs[1][o_]) = bf2(a1_, b1_);                   \
+                *reinterpret_cast<uint32_t*>(&Gs[2][o_]) = bf2(a2_, b2_);                   \
+                db[e] += ga_[e] + gb_[e];                                                   \
             }                                                                               \
         }                                                                                   \
     }
@@ -537,7 +550,7 @@ __global__ __launch_bounds__(256, 2) void dqn_conv1_wgrad_kernel(
     __syncthreads();
     float* red = reinterpret_cast<float*>(Pb);  // [32 slots][32 co]
 #pragma unroll
-    for (int e = 0; e < 4; ++e) red[gp * C1_OC + 4 * gq + e] = db[e];
+    for (int e = 0; e < 4; ++e) red[(gp + 16 * hf) * C1_OC + 4 * gq + e] = db[e];
     __syncthreads();
     if (t < C1_OC) {
         float sacc = 0.0f;
