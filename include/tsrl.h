@@ -646,6 +646,21 @@ int tsrl_ppo_tail_stage(const float* h1frag, int64_t n, const int64_t* idx,
  * are not read). */
 int tsrl_ppo_eval(const float* h1frag, int64_t n, const tsrl_tail_weights* w, int64_t act_dim,
                   const float* act, float* value_out, float* logp_out, void* stream);
+
+/* tsrl_ppo_eval_fused: tsrl_mlp_l1_fwd_x6 (tanh, fragment layout) followed by tsrl_ppo_eval in
+ * ONE launch: the layer-1 activations of each 32-row tile stay in registers and are evaluated
+ * there (process_fn's values and log-probs, reference a2c.py:83-100 / ppo.py:95-96), with the
+ * same products in the same order -- bit-identical outputs, without the 512 B per row of H1
+ * written and read back.  X / ldx / idx / n / D / wsplit / ba / bc as tsrl_mlp_l1_fwd_x6; wt /
+ * act_dim / act / value_out / logp_out as tsrl_ppo_eval; workspace: >=
+ * tsrl_ppo_eval_fused_workspace_bytes() bytes of device memory, 16-byte aligned (rebuilt by
+ * every call).  Enqueues two kernels on `stream`. */
+int64_t tsrl_ppo_eval_fused_workspace_bytes(void);
+int tsrl_ppo_eval_fused(const float* X, int64_t ldx, const int64_t* idx, int64_t n, int64_t D,
+                        const void* wsplit, const float* ba, const float* bc,
+                        const tsrl_tail_weights* wt, int64_t act_dim, const float* act,
+                        float* value_out, float* logp_out, void* workspace, int64_t ws_bytes,
+                        void* stream);
 int64_t tsrl_mlp_dw_workspace_bytes(int64_t n, int64_t D);
 int tsrl_mlp_dw(const float* dz1, const float* X, int64_t ldx, const int64_t* idx, int64_t n,
                 int64_t D, float* gWa, float* gba, float* gWc, float* gbc, void* workspace,

@@ -483,3 +483,45 @@ def test_learn_graph_replay_matches_eager(dev):
             assert a[k] == b[k], k
     for k in states[0]:
         assert torch.equal(states[0][k], states[1][k]), k
+
+
+@pytest.mark.parametrize("D,n,with_act,gathered", [
+    (376, 2 * 262144 + 77, True, False), (376, 5000, False, False), (376, 3001, True, True),
+    (17, 1000, True, False), (40, 257, True, True)])
+def test_fused_eval_bit_identical_to_two_kernel_eval(dev, D, n, with_act, gathered):
+    """tsrl_ppo_eval_fused (layer 1 and process_fn's evaluation in one launch, H1 kept in
+    registers) against tsrl_mlp_l1_fwd_x6 + tsrl_ppo_eval on the same rows: values and
+    log-probs bit for bit (same products in the same order), ragged row counts, contiguous
+    and gathered rows, with and without the stored actions."""
+    import tianshou_amd.policy.fused_mlp as fm
+    from tianshou_amd.policy import PPOPolicy
+    from tianshou_amd.env import Box
+    from tianshou_amd.utils.models import fixed_std_normal
+    A = 6
+    actor, critic = _nets(D, A, dev, 21)
+    optim = torch.optim.Adam(list(actor.parameters()) + list(critic.parameters()), lr=1e-4)
+    pol = PPOPolicy(actor, critic, optim, fixed_std_normal, action_space=Box(-1.0, 1.0, (A,)),
+                    fused_mlp=True)
+    mlp = pol._mlp
+    assert mlp is not None
+    g = torch.Generator(device=dev).manual_seed(n)
+    rows = n + 123 if gathered else n
+    obs = torch.randn(rows, D, device=dev, generator=g)
+    act = torch.randn(n, A, device=dev, generator=g) if with_act else None
+    idx = torch.randperm(rows, device=dev, generator=g)[:n] if gathered else None
+    prev = fm.EVAL_FUSED
+    try:
+        fm.EVAL_FUSED = True
+        v1, l1 = mlp.evaluate(obs, act, idx)
+        fm.EVAL_FUSED = False
+        v2, l2 = mlp.evaluate(obs, act, idx)
+    finally:
+        fm.EVAL_FUSED = prev
+    torch.cuda.synchronize()
+    assert torch.isfinite(v1).all()
+    assert torch.equal(v1, v2), float((v1 - v2).abs().max())
+    if with_act:
+        assert torch.isfinite(l1).all()
+        assert torch.equal(l1, l2), float((l1 - l2).abs().max())
+    else:
+        assert l1 is None and l2 is None

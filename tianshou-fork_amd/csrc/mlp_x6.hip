@@ -310,12 +310,223 @@ __global__ __launch_bounds__(256, X6_OCC) void l1_fwd_x6_kernel(
 constexpr int RNW = 8;                   // waves per workgroup
 constexpr int RROWS = 32 * RNW;          // rows per tile
 constexpr int RTPW = 4;                  // tiles per workgroup (at most)
-constexpr int RXS = 3, RWS = 2;          // X / W ring stages
+constexpr int RWS = 2;                   // W ring stages
 constexpr int RXSTAGE = RROWS * XROWB;   // 32 KB
 constexpr int RWSTAGE = NPL * HC * ROWB;  // 24 KB
-constexpr int RWOFF = RXS * RXSTAGE;
-constexpr int RBOFF = RWOFF + RWS * RWSTAGE;
-constexpr int RLDS = RBOFF + HC * 4;
+
+// ---------------------------------------------------------------------------------------
+// Fused process_fn evaluation (EVAL = true): the layer-1 ring with the evaluation of
+// tsrl_ppo_eval (mlp.hip eval_tail_kernel: layer 2 of both nets, the critic's value head, the
+// actor's mu head and the Gaussian log-prob of the stored action) run on each finished tile's
+// activations in registers, so H1 never leaves the chip (round 6; the
+// two-kernel form writes and re-reads 512 B per row, 1 GB per 2M-row chunk, past the 256 MB
+// Infinity Cache).  LDS: a 2-stage X ring (measured as fast as 3 stages, tools/r06_rxs.sh,
+// profiles/r06_fused_eval_ab.log), the W ring, and the two layer-2 images (48 KB) = 160 KB;
+// the mu-head image and the small constants live in a global workspace built once per call
+// (L1 / L2-resident), the layer-1 bias is read from global memory.  Same products in the same
+// order as l1_ring_kernel + eval_tail_kernel: bit-identical values and log-probs.
+constexpr int EH = 64, EAMAX = 32;
+constexpr float E_LOG_SQRT_2PI = 0.91893853320467274178f;
+constexpr int EV_W2 = NPL * 2 * EH * 64;         // one layer-2 image (2 chunks of 32 k)
+constexpr int EV_W3 = NPL * 2 * EAMAX * 64;      // the mu-head image
+// constants (floats): b2a, b2c, b3a (padded), w3c, sigma^2, log sigma
+constexpr int EC_B2A = 0, EC_B2C = EC_B2A + EH, EC_B3 = EC_B2C + EH, EC_W3C = EC_B3 + EAMAX,
+              EC_VAR = EC_W3C + EH, EC_LS = EC_VAR + EAMAX, EC_B1 = EC_LS + EAMAX,
+              EC_END = EC_B1 + 2 * EH;  // + the layer-1 biases (actor, critic), 16-byte aligned
+constexpr int EV_WS = EV_W3 + EC_END * 4;        // workspace bytes
+
+template <bool EVAL>
+struct RingLds {
+    static constexpr int XS = EVAL ? 2 : 3;       // X ring stages
+    static constexpr int WOFF = XS * RXSTAGE;
+    static constexpr int BOFF = WOFF + RWS * RWSTAGE;  // layer-1 bias / layer-2 images
+    static constexpr int SIZE = EVAL ? BOFF + 2 * EV_W2 : BOFF + HC * 4;
+};
+static_assert(RingLds<true>::SIZE <= 163840, "fused evaluation LDS");
+
+struct EvalArgs {
+    const float *w2a, *w2c, *b3c;  // raw layer-2 weights (images built per workgroup)
+    const char* w3img;             // workspace: mu-head image, then the constants
+    const float* act;              // stored actions [n][A] (null: values only)
+    float *value_out, *logp_out;
+    int A;
+};
+
+__device__ __forceinline__ int ev_img_off(int p, int kc, int row, int q, int nkc, int rows) {
+    return (p * nkc + kc) * rows * 64 + sw_off(row, q);
+}
+
+// M(row, k) split into an image (layout of mlp.hip build_img_n); TPB threads
+template <int TPB, typename F>
+__device__ __forceinline__ void ev_build_img(char* img, int rows, int nkc, int t, F val) {
+    for (int i = t; i < rows * nkc * 4; i += TPB) {
+        const int q = i & 3, kc = (i >> 2) % nkc, row = (i >> 2) / nkc;
+        bf16x8 p0, p1, p2;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = 32 * kc + 16 * (q >> 1) + 8 * (j >> 2) + 4 * (q & 1) + (j & 3);
+            __bf16 a, b, c;
+            split1(val(row, k), a, b, c);
+            p0[j] = a;
+            p1[j] = b;
+            p2[j] = c;
+        }
+        *reinterpret_cast<bf16x8*>(img + ev_img_off(0, kc, row, q, nkc, rows)) = p0;
+        *reinterpret_cast<bf16x8*>(img + ev_img_off(1, kc, row, q, nkc, rows)) = p1;
+        *reinterpret_cast<bf16x8*>(img + ev_img_off(2, kc, row, q, nkc, rows)) = p2;
+    }
+}
+
+__device__ __forceinline__ void ev_ld_img(const char* img, int nkc, int rows, int kc, int row,
+                                          int s, int h, bf16x8 (&a)[NPL]) {
+#pragma unroll
+    for (int p = 0; p < NPL; ++p)
+        a[p] = *reinterpret_cast<const bf16x8*>(img + ev_img_off(p, kc, row, 2 * s + h, nkc, rows));
+}
+
+__device__ __forceinline__ void ev_split_frag(const float (&v)[16], int s, bf16x8 (&b)[NPL]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        __bf16 x0, x1, x2;
+        split1(v[8 * s + j], x0, x1, x2);
+        b[0][j] = x0;
+        b[1][j] = x1;
+        b[2][j] = x2;
+    }
+}
+
+__device__ __forceinline__ f32x16 ev_zero16() {
+    f32x16 z;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) z[i] = 0.0f;
+    return z;
+}
+
+// The workspace of a call: the mu-head image (zero rows past A) and the constants, exactly as
+// eval_tail_kernel stages them in its LDS.
+__global__ __launch_bounds__(256) void eval_ws_kernel(const float* __restrict__ w3a,
+                                                      const float* __restrict__ b3a,
+                                                      const float* __restrict__ w3c,
+                                                      const float* __restrict__ b2a,
+                                                      const float* __restrict__ b2c,
+                                                      const float* __restrict__ log_std,
+                                                      const float* __restrict__ b1a,
+                                                      const float* __restrict__ b1c, int A,
+                                                      char* __restrict__ ws) {
+    const int t = threadIdx.x;
+    ev_build_img<256>(ws, EAMAX, 2, t,
+                      [=](int r, int k) { return (w3a && r < A) ? w3a[r * EH + k] : 0.0f; });
+    float* ec = reinterpret_cast<float*>(ws + EV_W3);
+    if (t < EH) {
+        ec[EC_B2C + t] = b2c[t];
+        ec[EC_W3C + t] = w3c[t];
+        ec[EC_B2A + t] = b2a ? b2a[t] : 0.0f;
+    }
+    if (t < 2 * EH) ec[EC_B1 + t] = t < EH ? b1a[t] : b1c[t - EH];
+    if (t < EAMAX) {
+        ec[EC_B3 + t] = (b3a && t < A) ? b3a[t] : 0.0f;
+        const float sig = (log_std && t < A) ? expf(log_std[t]) : 1.0f;
+        ec[EC_VAR + t] = sig * sig;
+        ec[EC_LS + t] = logf(sig);
+    }
+}
+
+// One net of eval_tail_kernel's run_net on a wave's 32 rows: h1 = the net's two layer-1 tiles
+// (C layout, after bias and tanh); iw2 = the net's layer-2 image (LDS).
+__device__ __forceinline__ void ev_net(int net, const float (&h1a)[16], const float (&h1b)[16],
+                                       int64_t brow, bool live, int c, int h, const char* iw2,
+                                       const char* iw3, const float* __restrict__ ec,
+                                       float b3c, const EvalArgs& ea) {
+    const int A = ea.A;
+    float av[16];
+    if (net == 0) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int a = rho(r) + 4 * h;
+            av[r] = 0.0f;
+            if (a < A && live) av[r] = ea.act[brow * A + a];
+        }
+    }
+    const float* sb2 = ec + (net ? EC_B2C : EC_B2A);
+    float h2[2][16];
+    {
+        f32x16 z0 = ev_zero16(), z1 = ev_zero16();
+#pragma unroll
+        for (int kc = 0; kc < 2; ++kc)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                bf16x8 b[NPL], a[NPL];
+                ev_split_frag(kc == 0 ? h1a : h1b, s, b);
+                ev_ld_img(iw2, 2, EH, kc, c, s, h, a);
+                z0 = mfma6(a, b, z0);
+                ev_ld_img(iw2, 2, EH, kc, 32 + c, s, h, a);
+                z1 = mfma6(a, b, z1);
+            }
+        // constants of rows rho(r) + 4h, r = 4g..4g+3: 4 consecutive floats, one 16-byte load
+        // (the workspace is 16-byte aligned)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const float4 u = *reinterpret_cast<const float4*>(sb2 + 8 * g + 4 * h);
+            const float4 v = *reinterpret_cast<const float4*>(sb2 + 32 + 8 * g + 4 * h);
+            const float uu[4] = {u.x, u.y, u.z, u.w}, vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                h2[0][4 * g + e] = tanh_nb(z0[4 * g + e] + uu[e]);
+                h2[1][4 * g + e] = tanh_nb(z1[4 * g + e] + vv[e]);
+            }
+        }
+    }
+    if (net == 1) {
+        float w3[2][16];
+#pragma unroll
+        for (int it = 0; it < 2; ++it)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const float4 u = *reinterpret_cast<const float4*>(ec + EC_W3C + 32 * it + 8 * g + 4 * h);
+                w3[it][4 * g] = u.x, w3[it][4 * g + 1] = u.y, w3[it][4 * g + 2] = u.z,
+                w3[it][4 * g + 3] = u.w;
+            }
+        float vpart = 0.0f;
+#pragma unroll
+        for (int it = 0; it < 2; ++it)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) vpart += w3[it][r] * h2[it][r];
+        const float value = vpart + __shfl_xor(vpart, 32, 64) + b3c;
+        if (live && h == 0) ea.value_out[brow] = value;
+    } else {
+        f32x16 mu = ev_zero16();
+#pragma unroll
+        for (int kc = 0; kc < 2; ++kc)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                bf16x8 b[NPL], a[NPL];
+                ev_split_frag(h2[kc], s, b);
+                ev_ld_img(iw3, 2, EAMAX, kc, c, s, h, a);
+                mu = mfma6(a, b, mu);
+            }
+        float b3[16], vr[16], ls[16];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const float4 u = *reinterpret_cast<const float4*>(ec + EC_B3 + 8 * g + 4 * h);
+            const float4 v = *reinterpret_cast<const float4*>(ec + EC_VAR + 8 * g + 4 * h);
+            const float4 q = *reinterpret_cast<const float4*>(ec + EC_LS + 8 * g + 4 * h);
+            b3[4 * g] = u.x, b3[4 * g + 1] = u.y, b3[4 * g + 2] = u.z, b3[4 * g + 3] = u.w;
+            vr[4 * g] = v.x, vr[4 * g + 1] = v.y, vr[4 * g + 2] = v.z, vr[4 * g + 3] = v.w;
+            ls[4 * g] = q.x, ls[4 * g + 1] = q.y, ls[4 * g + 2] = q.z, ls[4 * g + 3] = q.w;
+        }
+        float lp = 0.0f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int a = rho(r) + 4 * h;
+            if (a < A && live) {
+                const float diff = av[r] - (mu[r] + b3[r]);
+                lp += -(diff * diff) / (2.0f * vr[r]) - ls[r] - E_LOG_SQRT_2PI;
+            }
+        }
+        const float logp = lp + __shfl_xor(lp, 32, 64);
+        if (live && h == 0) ea.logp_out[brow] = logp;
+    }
+}
 
 // One LDS-DMA wave-instruction: lane l copies 16 bytes from src to LDS byte lds + 16 l (M0 is
 // set and restored inside the statement; lds is wave-uniform).
@@ -332,12 +543,15 @@ __device__ __forceinline__ void glds16(const void* src, uint32_t lds) {
         : "memory");
 }
 
-template <bool TANH>
+template <bool TANH, bool EVAL>
 __global__ __launch_bounds__(RNW * 64, 1) void l1_ring_kernel(
     const float* __restrict__ X, int64_t ldx, const int64_t* __restrict__ idx, int64_t n,
     int64_t ntiles, int Kp, int dq, const __bf16* __restrict__ wsp, const float* __restrict__ ba,
-    const float* __restrict__ bc, float* __restrict__ out, int64_t frag_tiles, int tpw) {
-    __shared__ __attribute__((aligned(16))) char sm[RLDS];
+    const float* __restrict__ bc, float* __restrict__ out, int64_t frag_tiles, int tpw,
+    EvalArgs ea) {
+    using L = RingLds<EVAL>;
+    constexpr int RXS = L::XS, RWOFF = L::WOFF, RBOFF = L::BOFF;
+    __shared__ __attribute__((aligned(16))) char sm[L::SIZE];
     const int t = threadIdx.x;
     const int w = __builtin_amdgcn_readfirstlane(t >> 6);
     const int l = t & 63, h = l >> 5, c = l & 31;
@@ -348,7 +562,14 @@ __global__ __launch_bounds__(RNW * 64, 1) void l1_ring_kernel(
     const int nch = Kp / KC;
     const int C = ntl * nch;
     float* sb = reinterpret_cast<float*>(sm + RBOFF);
-    if (t < HC) sb[t] = t < H ? ba[t] : bc[t - H];
+    if constexpr (EVAL) {
+        // the two layer-2 images (actor, critic), split once per workgroup
+        ev_build_img<RNW * 64>(sm + RBOFF, EH, 2, t, [=](int r, int k) { return ea.w2a[r * EH + k]; });
+        ev_build_img<RNW * 64>(sm + RBOFF + EV_W2, EH, 2, t,
+                               [=](int r, int k) { return ea.w2c[r * EH + k]; });
+    } else {
+        if (t < HC) sb[t] = t < H ? ba[t] : bc[t - H];
+    }
     // source rows of this lane's X pieces: tile tl, instruction i -> local row 32w + 8i + l/8
     // (rows past n, and tiles past ntl, read a real row; the index loads are unconditional)
     uint32_t rid[RTPW][4];
@@ -431,24 +652,26 @@ __global__ __launch_bounds__(RNW * 64, 1) void l1_ring_kernel(
     if (C > 0) {
         issue_w();
         issue_x();
-        if (C > 1) issue_x();
+        if (RXS > 2 && C > 1) issue_x();
     }
     bool epi_prev = false;
     int cs_x = 0, cs_w = 0;  // ring slots of the chunk being computed
     for (int cc = 0, tl = 0, kc = 0; cc < C; ++cc) {
         // retire W(cc) and X(cc): younger in flight are X(cc + 1) (4) and the previous tile's
         // epilogue stores (16), when they were issued
+        // (EVAL: X(cc) is the youngest load -- X is issued one chunk ahead -- and the
+        // evaluation epilogue drains everything it issued, so every wait is vmcnt(0))
         const bool nx = cc + 1 < C;
-        if (epi_prev) {
-            if (nx) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-        } else {
-            if (nx) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        if (RXS == 2 || !nx) {
+            if (epi_prev) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+            if (epi_prev) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         }
         __builtin_amdgcn_s_barrier();
         if (nx) issue_w();
-        if (cc + 2 < C) issue_x();
+        if (cc + RXS - 1 < C) issue_x();
         const char* Xs = sm + cs_x * RXSTAGE;
         const char* Ws = sm + RWOFF + cs_w * RWSTAGE;
         cs_x = cs_x == RXS - 1 ? 0 : cs_x + 1;
@@ -487,7 +710,41 @@ __global__ __launch_bounds__(RNW * 64, 1) void l1_ring_kernel(
             }
         }
         epi_prev = kc == nch - 1;
-        if (epi_prev) {
+        if (EVAL && epi_prev) {
+            // bias + tanh, then the evaluation of the wave's 32 rows (eval_tail_kernel's
+            // run_net, actor then critic).  The loads issued here are younger than the ring's
+            // LDS-DMA loads, so the compiler's waits for them also retire those (vmcnt retires
+            // in order); the next chunk's wait is vmcnt(0) (epi_prev = false, X ring of 2)
+            const int64_t bt = (tile0 + tl) * (RROWS / 32) + w;
+            const int64_t brow = bt * 32 + c;
+            const bool live = brow < n;
+            const float* ec = reinterpret_cast<const float*>(ea.w3img + EV_W3);
+            const float b3c = ea.b3c[0];
+            // one net at a time (its two tiles' activations, then its accumulators are
+            // free): the register peak of the epilogue
+#pragma unroll
+            for (int net = 0; net < 2; ++net) {
+                float hv[2][16];
+#pragma unroll
+                for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const float4 b4 = *reinterpret_cast<const float4*>(
+                            ec + EC_B1 + 64 * net + 32 * ii + 8 * g + 4 * h);
+                        const float bb[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const float z = acc[2 * net + ii][4 * g + e] + bb[e];
+                            hv[ii][4 * g + e] = TANH ? tanh_nb(z) : z;
+                            acc[2 * net + ii][4 * g + e] = 0.0f;
+                        }
+                    }
+                if (net == 1 || ea.logp_out)
+                    ev_net(net, hv[0], hv[1], brow, live, c, h, sm + RBOFF + net * EV_W2,
+                           ea.w3img, ec, b3c, ea);
+            }
+            epi_prev = false;
+        } else if (epi_prev) {
             // bias + tanh -> fragment layout (x6::frag_off4)
             const int64_t bt = (tile0 + tl) * (RROWS / 32) + w;
             const bool keep = bt < frag_tiles;
@@ -566,16 +823,17 @@ extern "C" int tsrl_mlp_l1_fwd_x6(const float* X, int64_t ldx, const int64_t* id
         // (config 2's 2048-row minibatches: 8 tiles on 8 workgroups instead of 2)
         const int64_t tpw = std::max<int64_t>(1, std::min<int64_t>(RTPW, ntiles / n_cus()));
         const unsigned grid = (unsigned)((ntiles + tpw - 1) / tpw);
+        const EvalArgs none{};
         if (act_tanh)
-            hipLaunchKernelGGL(l1_ring_kernel<true>, dim3(grid), dim3(RNW * 64), 0,
+            hipLaunchKernelGGL((l1_ring_kernel<true, false>), dim3(grid), dim3(RNW * 64), 0,
                                as_stream(stream), X, ldx, idx, n, ntiles, (int)kpad32(D),
                                (int)((D + 3) / 4 * 4), reinterpret_cast<const __bf16*>(wsplit),
-                               ba, bc, out, frag_tiles, (int)tpw);
+                               ba, bc, out, frag_tiles, (int)tpw, none);
         else
-            hipLaunchKernelGGL(l1_ring_kernel<false>, dim3(grid), dim3(RNW * 64), 0,
+            hipLaunchKernelGGL((l1_ring_kernel<false, false>), dim3(grid), dim3(RNW * 64), 0,
                                as_stream(stream), X, ldx, idx, n, ntiles, (int)kpad32(D),
                                (int)((D + 3) / 4 * 4), reinterpret_cast<const __bf16*>(wsplit),
-                               ba, bc, out, frag_tiles, (int)tpw);
+                               ba, bc, out, frag_tiles, (int)tpw, none);
         TSRL_LAUNCH_CHECK("tsrl_mlp_l1_fwd_x6(ring)");
         return 0;
     }
@@ -585,5 +843,46 @@ extern "C" int tsrl_mlp_l1_fwd_x6(const float* X, int64_t ldx, const int64_t* id
                        reinterpret_cast<const __bf16*>(wsplit), ba, bc, act_tanh, out,
                        frag_out);
     TSRL_LAUNCH_CHECK("tsrl_mlp_l1_fwd_x6");
+    return 0;
+}
+
+extern "C" int64_t tsrl_ppo_eval_fused_workspace_bytes(void) { return EV_WS; }
+
+extern "C" int tsrl_ppo_eval_fused(const float* X, int64_t ldx, const int64_t* idx, int64_t n,
+                                   int64_t D, const void* wsplit, const float* ba,
+                                   const float* bc, const tsrl_tail_weights* wt,
+                                   int64_t act_dim, const float* act, float* value_out,
+                                   float* logp_out, void* workspace, int64_t ws_bytes,
+                                   void* stream) {
+    TSRL_CHECK_ARG(n >= 0 && D > 0 && ldx >= D && act_dim > 0 && act_dim <= EAMAX,
+                   "tsrl_ppo_eval_fused: bad sizes");
+    if (n == 0) return 0;
+    TSRL_CHECK_ARG(X && wsplit && ba && bc && wt && value_out && (!logp_out || act) &&
+                       workspace,
+                   "tsrl_ppo_eval_fused: null pointer");
+    TSRL_CHECK_ARG(wt->w2c && wt->b2c && wt->w3c && wt->b3c &&
+                       (!logp_out || (wt->w2a && wt->b2a && wt->w3a && wt->b3a && wt->log_std)),
+                   "tsrl_ppo_eval_fused: null weight");
+    TSRL_CHECK_ARG(ws_bytes >= EV_WS && aligned16(workspace),
+                   "tsrl_ppo_eval_fused: workspace too small or not 16-byte aligned");
+    TSRL_CHECK_ARG(aligned16(X) && ldx % 4 == 0 && ldx >= (D + 3) / 4 * 4 && aligned16(wsplit),
+                   "tsrl_ppo_eval_fused: X/wsplit must be 16-byte aligned, ldx a multiple of 4 "
+                   "and >= roundup(D, 4)");
+    hipLaunchKernelGGL(eval_ws_kernel, dim3(1), dim3(256), 0, as_stream(stream),
+                       logp_out ? wt->w3a : nullptr, logp_out ? wt->b3a : nullptr, wt->w3c,
+                       logp_out ? wt->b2a : nullptr, wt->b2c, logp_out ? wt->log_std : nullptr,
+                       ba, bc, (int)act_dim, reinterpret_cast<char*>(workspace));
+    TSRL_LAUNCH_CHECK("tsrl_ppo_eval_fused(workspace)");
+    const int64_t ntiles = (n + RROWS - 1) / RROWS;
+    const int64_t tpw = std::max<int64_t>(1, std::min<int64_t>(RTPW, ntiles / n_cus()));
+    const unsigned grid = (unsigned)((ntiles + tpw - 1) / tpw);
+    EvalArgs ea{logp_out ? wt->w2a : wt->w2c, wt->w2c, wt->b3c,
+                reinterpret_cast<const char*>(workspace), act, value_out, logp_out,
+                (int)act_dim};
+    hipLaunchKernelGGL((l1_ring_kernel<true, true>), dim3(grid), dim3(RNW * 64), 0,
+                       as_stream(stream), X, ldx, idx, n, ntiles, (int)kpad32(D),
+                       (int)((D + 3) / 4 * 4), reinterpret_cast<const __bf16*>(wsplit), ba, bc,
+                       nullptr, (int64_t)0, (int)tpw, ea);
+    TSRL_LAUNCH_CHECK("tsrl_ppo_eval_fused");
     return 0;
 }

@@ -198,6 +198,9 @@ _SIGS = {
                              _p, _p, ctypes.c_int, _p], ctypes.c_int),
     "tsrl_ppo_eval": ([_p, _i64, ctypes.POINTER(TailWeights), _i64, _p, _p, _p, _p],
                       ctypes.c_int),
+    "tsrl_ppo_eval_fused_workspace_bytes": ([], _i64),
+    "tsrl_ppo_eval_fused": ([_p, _i64, _p, _i64, _i64, _p, _p, _p, ctypes.POINTER(TailWeights),
+                             _i64, _p, _p, _p, _p, _i64, _p], ctypes.c_int),
     "tsrl_mlp_dw_workspace_bytes": ([_i64, _i64], _i64),
     "tsrl_policy_pack_floats": ([_i64], _i64),
     "tsrl_gauss_policy_act_rng": ([_p, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p, _p, _i64, _u64,

@@ -31,6 +31,9 @@ L1_X6 = True
 # the tail's reduction launch runs on a second stream beside tsrl_mlp_dw (TSRL_TAIL_OVERLAP=0:
 # one stream)
 TAIL_OVERLAP = os.environ.get("TSRL_TAIL_OVERLAP", "1") != "0"
+# process_fn's evaluation as one launch per call, layer 1 and the evaluation fused
+# (tsrl_ppo_eval_fused; TSRL_EVAL_FUSED=0: tsrl_mlp_l1_fwd_x6 + tsrl_ppo_eval per 2M-row chunk)
+EVAL_FUSED = os.environ.get("TSRL_EVAL_FUSED", "1") != "0"
 # minibatches of at most this many rows run the actor's and the critic's tail kernels on the
 # two streams side by side (each tail then fills at most half of a 256-CU device:
 # ceil(rows / 16 / 8) workgroups <= 128); TSRL_TAIL_SPLIT=0 keeps them on one stream
@@ -198,6 +201,20 @@ class FusedActorCritic(FlatAdam):
         values = torch.empty(n, dtype=torch.float32, device=dev)
         logp = torch.empty(n, dtype=torch.float32, device=dev) if act is not None else None
         w = self._weights()
+        if L1_X6 and EVAL_FUSED:
+            # layer 1 + the evaluation in one launch over all rows (tsrl_ppo_eval_fused):
+            # no layer-1 activations in memory, so no chunking either
+            self.split_w1()
+            ws = self._buf("w1split", (int(lib.tsrl_mlp_split_bytes(D)) + 3) // 4)
+            nb = int(lib.tsrl_ppo_eval_fused_workspace_bytes())
+            evw = self._buf("eval_ws", (nb + 3) // 4)
+            _C.check(lib.tsrl_ppo_eval_fused(
+                obs.data_ptr(), ldx, None if idx is None else idx.data_ptr(), n, D, _C.ptr(ws),
+                _C.ptr(L["w1a"].bias), _C.ptr(L["w1c"].bias), w, A,
+                None if act is None else act.data_ptr(), values.data_ptr(),
+                None if logp is None else logp.data_ptr(), _C.ptr(evw), nb, s),
+                "tsrl_ppo_eval_fused")
+            return values, logp
         for s0 in range(0, n, self.EVAL_CHUNK):
             e0 = min(n, s0 + self.EVAL_CHUNK)
             m = e0 - s0
