@@ -397,13 +397,16 @@ int tsrl_frames_to_f32_nhwc(const uint8_t* src, int64_t n, int64_t c, int64_t hw
                             const float* lut, float* dst, void* stream);
 
 /* First convolution + ReLU of the Nature-DQN trunk straight from uint8 frame stacks:
- * out = relu(conv(frames, w) / scale + bias), frames [n][4][84][84] u8 (contiguous, 4-byte
- * aligned), w [32][4][8][8] f32 addressed through its element strides (sw0..sw3, so a
+ * out = relu(conv(frames, w) / scale + bias), frames [*][4][84][84] u8 (contiguous, 4-byte
+ * aligned); output sample s reads frame stack rows[s] (rows: n int64 indices, nullable =
+ * identity, so a minibatch is read in place from the whole batch -- round 6), w
+ * [32][4][8][8] f32 addressed through its element strides (sw0..sw3, so a
  * channels_last weight needs no copy), bias [32] (nullable), out [n][20][20][32] f32 (NHWC,
  * 16-byte aligned).  Replaces scale_obs + Conv2d(4, 32, 8, 4) + ReLU of
  * examples/atari/atari_network.py:18-30,53-90 in DQN.forward (:84): bytes are exact bf16
  * operands, weights split exactly into 3 bf16 planes (f32 GEMM error). */
-int tsrl_dqn_conv1_fwd(const uint8_t* frames, int64_t n, const float* w, int64_t sw0,
+int tsrl_dqn_conv1_fwd(const uint8_t* frames, int64_t n, const int64_t* rows, const float* w,
+                       int64_t sw0,
                        int64_t sw1, int64_t sw2, int64_t sw3, const float* bias, float scale,
                        int relu, float* out, void* stream);
 
@@ -424,7 +427,8 @@ int tsrl_dqn_conv2_dgrad(const float* gy, int64_t n, const float* w, int64_t sw0
  * scale_obs(frames) (examples/atari/atari_network.py:18-30,53-90) in loss.backward()
  * (ppo.py:146) and the u8 -> f32 frame conversion it needs: bytes exact in bf16, gy split
  * into 3 bf16 planes (f32 GEMM error), per-workgroup partials folded in fixed order (f64).
- * workspace: tsrl_dqn_conv1_wgrad_workspace_bytes(n) bytes. */
+ * workspace: tsrl_dqn_conv1_wgrad_workspace_bytes(n) bytes.  rows: as tsrl_dqn_conv1_fwd
+ * (gradient row s belongs to frame stack rows[s]; nullable). */
 /* y = max(y + bias, 0) in place over rows x C f32 (NHWC activations of a convolution run
  * without bias; C % 4 == 0, 16-byte aligned; bias nullable): the bias add + ReLU of the
  * trunk's Conv2d + ReLU pairs (examples/atari/atari_network.py:53-90) in one pass. */
@@ -442,7 +446,8 @@ int tsrl_relu_bwd_rows(const float* gz, const float* z, float* gy, int64_t rows,
                        float* gb, void* ws, int64_t ws_bytes, void* stream);
 
 int64_t tsrl_dqn_conv1_wgrad_workspace_bytes(int64_t n);
-int tsrl_dqn_conv1_wgrad(const uint8_t* frames, int64_t n, const float* gy, float scale,
+int tsrl_dqn_conv1_wgrad(const uint8_t* frames, int64_t n, const int64_t* rows,
+                         const float* gy, float scale,
                          float* gw, float* gb, void* workspace, int64_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------

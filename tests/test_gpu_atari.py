@@ -547,3 +547,39 @@ def test_gumbel_categorical_sample_distribution(dev):
     assert not bool(((a[:, 2] == 1) | (a[:, 2] == 3)).any())
     torch.manual_seed(0)
     assert torch.equal(gumbel_sample(rep).view(m, 3), a)
+
+
+@pytest.mark.parametrize("n,rows_n", [(300, 257), (64, 64)])
+def test_dqn_rows_in_place_matches_gathered(dev, n, rows_n):
+    """DQN.forward(obs, rows=idx) -- the uint8 first-layer kernels reading the minibatch's
+    frame stacks in place from the whole batch (tsrl_dqn_conv1_fwd / tsrl_dqn_conv1_wgrad with
+    rows) -- against forward(obs[idx]) on the gathered copy: outputs and conv1's weight and
+    bias gradients bit for bit (the same bytes reach the same kernels); the other gradients
+    come from MIOpen / hipBLASLt, whose split-K weight gradients accumulate with atomics in a
+    run-dependent order, so they are compared at rtol 1e-5 of their magnitude."""
+    import copy
+    from tianshou_amd.utils.net_atari import DQN, layer_init
+    torch.manual_seed(7)
+    net = DQN(4, 84, 84, (6,), device=dev, features_only=True, output_dim=512,
+              layer_init=layer_init).to(dev)
+    net2 = copy.deepcopy(net)
+    g = torch.Generator(device=dev).manual_seed(n)
+    obs = torch.randint(0, 256, (n, 4, 84, 84), dtype=torch.uint8, device=dev, generator=g)
+    idx = torch.randint(0, n, (rows_n,), device=dev, generator=g)
+    assert net.reads_rows(obs)
+    y1, _ = net(obs, rows=idx)
+    y2, _ = net2(obs[idx])
+    gy = torch.randn(y1.shape, device=dev, generator=g)
+    y1.backward(gy)
+    y2.backward(gy)
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2)
+    conv1 = {n_ for n_, p in net.named_parameters() if p is net._conv1_parts()[0].weight or
+             p is net._conv1_parts()[0].bias}
+    assert len(conv1) == 2
+    for (k, p1), (_, p2) in zip(net.named_parameters(), net2.named_parameters()):
+        if k in conv1:
+            assert torch.equal(p1.grad, p2.grad), k
+        else:
+            err = float((p1.grad - p2.grad).abs().max())
+            assert err <= 1e-5 * float(p2.grad.abs().max()) + 1e-12, (k, err)

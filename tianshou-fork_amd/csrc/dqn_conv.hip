@@ -87,7 +87,8 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 template <bool A16>
 __global__ __launch_bounds__(256, 2) void dqn_conv1_fwd_lds_kernel(
-    const uint8_t* __restrict__ X, int64_t n, const float* __restrict__ W, int64_t sw0,
+    const uint8_t* __restrict__ X, int64_t n, const int64_t* __restrict__ rows,
+    const float* __restrict__ W, int64_t sw0,
     int64_t sw1, int64_t sw2, int64_t sw3, const float* __restrict__ bias, float scale,
     int relu, float* __restrict__ out) {
     __shared__ __attribute__((aligned(16))) char Ws[NPL][C1_OC * C1_ROWB];
@@ -113,10 +114,11 @@ __global__ __launch_bounds__(256, 2) void dqn_conv1_fwd_lds_kernel(
     // over the array (a lambda capturing it put it in scratch memory), and a native vector
     // type (an array of HIP's uint4 stays in scratch too)
     u32x4 fr[C1L_HPER];
+#define C1L_SRC(smp) (X + (rows ? rows[smp] : (smp)) * C1_FRAME)
 #define C1L_LOAD(smp, hf)                                                                   \
     { if constexpr (A16) {                                                                  \
         const u32x4* src_ =                                                                 \
-            reinterpret_cast<const u32x4*>(X + (smp) * C1_FRAME) + (hf) * C1L_HV4;          \
+            reinterpret_cast<const u32x4*>(C1L_SRC(smp)) + (hf) * C1L_HV4;                  \
         _Pragma("unroll") for (int i = 0; i < C1L_HPER; ++i)                                \
             fr[i] = src_[t + 256 * i < C1L_HV4 ? t + 256 * i : 0];                          \
     } }
@@ -127,7 +129,7 @@ __global__ __launch_bounds__(256, 2) void dqn_conv1_fwd_lds_kernel(
                 reinterpret_cast<u32x4*>(Fs + (hf) * C1L_HALF)[t + 256 * i] = fr[i];        \
     } else {                                                                                \
         const uint32_t* src_ =                                                              \
-            reinterpret_cast<const uint32_t*>(X + (smp) * C1_FRAME + (hf) * C1L_HALF);      \
+            reinterpret_cast<const uint32_t*>(C1L_SRC(smp) + (hf) * C1L_HALF);              \
         for (int q = t; q < C1L_HALF / 4; q += 256)                                         \
             reinterpret_cast<uint32_t*>(Fs + (hf) * C1L_HALF)[q] = src_[q];                 \
     } }
@@ -220,6 +222,7 @@ __global__ __launch_bounds__(256, 2) void dqn_conv1_fwd_lds_kernel(
         run(std::integral_constant<int, 4>{});
     else
         run(std::integral_constant<int, 3>{});
+#undef C1L_SRC
 #undef C1L_LOAD
 #undef C1L_STORE
 }
@@ -421,8 +424,8 @@ constexpr int C1W_GR = 2 * C1W_CH + 16;       // Gs row pitch (bytes; 68 dwords:
                                               // b128 phases)
 
 __global__ __launch_bounds__(256, 2) void dqn_conv1_wgrad_kernel(
-    const uint8_t* __restrict__ X, const float* __restrict__ gy, int64_t npix, int64_t cpw,
-    float* __restrict__ part) {
+    const uint8_t* __restrict__ X, const int64_t* __restrict__ rows, const float* __restrict__ gy,
+    int64_t npix, int64_t cpw, float* __restrict__ part) {
     __shared__ __attribute__((aligned(16))) uint8_t Pb[C1_KK * C1W_PR];        // [k][px]
     __shared__ __attribute__((aligned(16))) uint8_t Gs[NPL][C1_OC * C1W_GR];   // [co][px] bf16
     const int t = threadIdx.x;
@@ -458,8 +461,9 @@ __global__ __launch_bounds__(256, 2) void dqn_conv1_wgrad_kernel(
             const uint32_t s_ = pp_ / (uint32_t)C1_PIX;                                     \
             const uint32_t rr_ = pp_ - s_ * C1_PIX, oh_ = rr_ / (uint32_t)C1_OUT;           \
             const uint32_t ow_ = rr_ - oh_ * C1_OUT;                                        \
+            const int64_t fs_ = rows ? rows[s_] : (int64_t)s_;                              \
             const uint32_t* a_ = reinterpret_cast<const uint32_t*>(                         \
-                X + (int64_t)s_ * C1_FRAME + qoff + C1_S * oh_ * C1_HW + C1_S * ow_);        \
+                X + fs_ * C1_FRAME + qoff + C1_S * oh_ * C1_HW + C1_S * ow_);                \
             _Pragma("unroll") for (int d = 0; d < 5; ++d) rb[j][d] = a_[d];                 \
             const int64_t g_ = (ch) * C1W_CH + 2 * gp + 32 * (2 * (j >> 1) + hf) + (j & 1); \
             gv[j] = *reinterpret_cast<const float4*>(gy + (g_ < npix ? g_ : 0) * C1_OC + 4 * gq); \
@@ -611,9 +615,10 @@ __global__ __launch_bounds__(256) void bias_relu_rows_kernel(float4* __restrict_
 
 using namespace tsrl;
 
-extern "C" int tsrl_dqn_conv1_fwd(const uint8_t* frames, int64_t n, const float* w, int64_t sw0,
-                                  int64_t sw1, int64_t sw2, int64_t sw3, const float* bias,
-                                  float scale, int relu, float* out, void* stream) {
+extern "C" int tsrl_dqn_conv1_fwd(const uint8_t* frames, int64_t n, const int64_t* rows,
+                                  const float* w, int64_t sw0, int64_t sw1, int64_t sw2,
+                                  int64_t sw3, const float* bias, float scale, int relu,
+                                  float* out, void* stream) {
     TSRL_CHECK_ARG(n >= 0, "tsrl_dqn_conv1_fwd: n < 0");
     if (n == 0) return 0;
     TSRL_CHECK_ARG(frames && w && out, "tsrl_dqn_conv1_fwd: null pointer");
@@ -627,12 +632,12 @@ extern "C" int tsrl_dqn_conv1_fwd(const uint8_t* frames, int64_t n, const float*
     const int64_t grid = std::min<int64_t>(n, (int64_t)ncu * 2);
     if (aligned16(frames))
         hipLaunchKernelGGL(dqn_conv1_fwd_lds_kernel<true>, dim3((unsigned)grid), dim3(256), 0,
-                           as_stream(stream), frames, n, w, sw0, sw1, sw2, sw3, bias, scale,
-                           relu, out);
+                           as_stream(stream), frames, n, rows, w, sw0, sw1, sw2, sw3, bias,
+                           scale, relu, out);
     else
         hipLaunchKernelGGL(dqn_conv1_fwd_lds_kernel<false>, dim3((unsigned)grid), dim3(256), 0,
-                           as_stream(stream), frames, n, w, sw0, sw1, sw2, sw3, bias, scale,
-                           relu, out);
+                           as_stream(stream), frames, n, rows, w, sw0, sw1, sw2, sw3, bias,
+                           scale, relu, out);
     TSRL_LAUNCH_CHECK("tsrl_dqn_conv1_fwd");
     return 0;
 }
@@ -666,9 +671,9 @@ extern "C" int64_t tsrl_dqn_conv1_wgrad_workspace_bytes(int64_t n) {
     return nwg * (C1_OC * C1_KK + C1_OC) * (int64_t)sizeof(float);
 }
 
-extern "C" int tsrl_dqn_conv1_wgrad(const uint8_t* frames, int64_t n, const float* gy,
-                                    float scale, float* gw, float* gb, void* workspace,
-                                    int64_t ws_bytes, void* stream) {
+extern "C" int tsrl_dqn_conv1_wgrad(const uint8_t* frames, int64_t n, const int64_t* rows,
+                                    const float* gy, float scale, float* gw, float* gb,
+                                    void* workspace, int64_t ws_bytes, void* stream) {
     TSRL_CHECK_ARG(n >= 0, "tsrl_dqn_conv1_wgrad: n < 0");
     TSRL_CHECK_ARG(frames && gy && gw && (n == 0 || workspace), "tsrl_dqn_conv1_wgrad: null pointer");
     TSRL_CHECK_ARG((((uintptr_t)frames) & 3) == 0 && aligned16(gy),
@@ -691,7 +696,7 @@ extern "C" int tsrl_dqn_conv1_wgrad(const uint8_t* frames, int64_t n, const floa
     const int64_t nwg = (nchunk + cpw - 1) / cpw;  // every workgroup has >= 1 chunk
     float* part = reinterpret_cast<float*>(workspace);
     hipLaunchKernelGGL(dqn_conv1_wgrad_kernel, dim3((unsigned)nwg), dim3(256), 0,
-                       as_stream(stream), frames, gy, npix, cpw, part);
+                       as_stream(stream), frames, rows, gy, npix, cpw, part);
     TSRL_LAUNCH_CHECK("tsrl_dqn_conv1_wgrad");
     hipLaunchKernelGGL(dqn_conv1_wgrad_reduce_kernel, dim3((W + 63) / 64), dim3(256), 0,
                        as_stream(stream), part, (int)nwg, 1.0f / scale, gw, gb);

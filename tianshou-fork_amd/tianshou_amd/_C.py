@@ -143,14 +143,15 @@ _SIGS = {
     "tsrl_stack_gather": ([_p, _i64, _p, _i64, _i64, _p, _p, _p, _i64, _i64, _p, _p, _p],
                           ctypes.c_int),
     "tsrl_frames_to_f32_nhwc": ([_p, _i64, _i64, _i64, _p, _p, _p], ctypes.c_int),
-    "tsrl_dqn_conv1_fwd": ([_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _f, ctypes.c_int, _p, _p],
+    "tsrl_dqn_conv1_fwd": ([_p, _i64, _p, _p, _i64, _i64, _i64, _i64, _p, _f, ctypes.c_int, _p,
+                            _p],
                            ctypes.c_int),
     "tsrl_dqn_conv2_dgrad": ([_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _p, _p], ctypes.c_int),
     "tsrl_relu_bwd_rows_workspace_bytes": ([_i64, _i64], _i64),
     "tsrl_relu_bwd_rows": ([_p, _p, _p, _i64, _i64, _p, _p, _i64, _p], ctypes.c_int),
     "tsrl_bias_relu_rows": ([_p, _p, _i64, _i64, _p], ctypes.c_int),
     "tsrl_dqn_conv1_wgrad_workspace_bytes": ([_i64], _i64),
-    "tsrl_dqn_conv1_wgrad": ([_p, _i64, _p, _f, _p, _p, _p, _i64, _p], ctypes.c_int),
+    "tsrl_dqn_conv1_wgrad": ([_p, _i64, _p, _p, _f, _p, _p, _p, _i64, _p], ctypes.c_int),
     "tsrl_nstep_return": ([_p, _p, _p, _p, _p, _i64, _i64, _p, _i64, _i64, _d, _p, _i64,
                            ctypes.c_int, _p, _p], ctypes.c_int),
     "tsrl_clip_adam_partials": ([_i64], _i64),

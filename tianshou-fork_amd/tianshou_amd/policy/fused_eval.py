@@ -140,14 +140,18 @@ class FusedEvalMixin:
                                        _C.ptr(out[s:e]), _C.stream_ptr(dev)), "tsrl_gauss_logp")
         return out
 
-    def _trunk_heads(self, obs: torch.Tensor):
+    def _trunk_heads(self, obs: torch.Tensor, rows: Optional[torch.Tensor] = None):
         """(actor output, V) of a shared-trunk DiscreteActor / DiscreteCritic pair with ONE
         trunk pass: actor.forward (utils/net.py DiscreteActor, discrete.py:52-71) and
         critic.forward (discrete.py:111-121) both start with preprocess(obs, None) on the same
         module, so the features are computed once and fed to both heads.  Forward values are
         those of the two separate passes; in backward the two heads' feature gradients are
-        summed before the trunk instead of after it (float summation order only)."""
-        h, _ = self.actor.preprocess(obs, None)
+        summed before the trunk instead of after it (float summation order only).  rows: the
+        minibatch is obs[rows], read in place when the trunk can (DQN.reads_rows)."""
+        if rows is not None:
+            h, _ = self.actor.preprocess(obs, None, rows=rows)
+        else:
+            h, _ = self.actor.preprocess(obs, None)
         x = self.actor.last(h)
         if self.actor.softmax_output:
             x = torch.softmax(x, dim=-1)

@@ -10,6 +10,7 @@ read back once at the end).  Other actor/dist combinations run the reference's t
 formulation on the GPU.
 """
 import contextlib
+import os
 from typing import Any, Callable, Dict, List, Optional
 
 import numpy as np
@@ -24,6 +25,10 @@ from tianshou_amd.policy.a2c import A2CPolicy
 from tianshou_amd.policy.flat_adam import FlatAdam
 from tianshou_amd.policy.fused_eval import FusedEvalMixin, cat_logp, cat_mode  # noqa: F401
 from tianshou_amd.utils.np_perm import LegacyPermutation
+
+# a shared uint8 conv trunk reads each minibatch's frame stacks in place from the whole batch
+# (DQN.forward(..., rows=idx)); TSRL_TRUNK_ROWS=0: gather them into a minibatch copy first
+TRUNK_ROWS = os.environ.get("TSRL_TRUNK_ROWS", "1") != "0"
 
 
 def split_bounds(length: int, size: int, merge_last: bool):
@@ -621,10 +626,14 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
                        b_glob: int, arrays, last: bool) -> torch.Tensor:
         """One Categorical minibatch (ppo.py:107-151): forward, fused loss, backward,
         gradient all-reduce, clip_grad_norm_ + Adam.step(); returns the [4] loss terms."""
-        obs_mb = gather_rows(obs, idx)
-        if self._shared_trunk:
-            x, value = self._trunk_heads(obs_mb)
+        pre = self.actor.preprocess if self._shared_trunk else None
+        if TRUNK_ROWS and pre is not None and hasattr(pre, "reads_rows") and pre.reads_rows(obs):
+            # the trunk's uint8 kernels read the minibatch's frame stacks in place (round 6)
+            x, value = self._trunk_heads(obs, rows=idx)
+        elif self._shared_trunk:
+            x, value = self._trunk_heads(gather_rows(obs, idx))
         else:
+            obs_mb = gather_rows(obs, idx)
             x, _ = self.actor(obs_mb)
             value = self.critic(obs_mb).flatten()
         loss, t = _CatPPOLoss.apply(x, value, (*arrays, idx, self._params(b_glob), self.dp,

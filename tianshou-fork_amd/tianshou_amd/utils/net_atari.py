@@ -33,12 +33,21 @@ def frames_to_f32_nhwc(obs: torch.Tensor, lut: torch.Tensor) -> torch.Tensor:
     return out.permute(0, 3, 1, 2)
 
 
-def conv1_u8(obs: torch.Tensor, conv: nn.Conv2d, scale: float) -> torch.Tensor:
+def _gather(t: torch.Tensor, rows: torch.Tensor) -> torch.Tensor:
+    from tianshou_amd.data.batch import gather_rows
+    return gather_rows(t, rows)
+
+
+def conv1_u8(obs: torch.Tensor, conv: nn.Conv2d, scale: float,
+             rows: Optional[torch.Tensor] = None) -> torch.Tensor:
     """relu(conv(obs / scale)) of the trunk's first layer straight from uint8 frame stacks
     [n, 4, 84, 84] (tsrl_dqn_conv1_fwd: bytes as exact bf16 operands, the weight split into
-    three bf16 planes; f32 GEMM error).  Returns [n, 32, 20, 20] in channels_last memory."""
+    three bf16 planes; f32 GEMM error).  Returns [n, 32, 20, 20] in channels_last memory.
+    rows (int64, on the device): the output rows are obs[rows], read in place."""
     obs = obs.contiguous()
-    n = obs.shape[0]
+    if rows is not None:
+        rows = rows.to(torch.int64).contiguous()
+    n = obs.shape[0] if rows is None else rows.numel()
     w = conv.weight.detach()
     if not (w.is_cuda and w.dtype == torch.float32 and w.device == obs.device):
         raise _C.TsrlError("conv1_u8: the conv weight must be an f32 tensor on the frames' "
@@ -46,7 +55,8 @@ def conv1_u8(obs: torch.Tensor, conv: nn.Conv2d, scale: float) -> torch.Tensor:
     out = torch.empty((n, 20, 20, 32), dtype=torch.float32, device=obs.device)
     b = conv.bias.detach() if conv.bias is not None else None
     # the weight is addressed through its strides (channels_last needs no copy)
-    _C.check(_C.lib().tsrl_dqn_conv1_fwd(_C.ptr(obs), n, w.data_ptr(), *w.stride(),
+    _C.check(_C.lib().tsrl_dqn_conv1_fwd(_C.ptr(obs), n, _C.ptr(rows) if rows is not None
+                                         else None, w.data_ptr(), *w.stride(),
                                          _C.ptr(b) if b is not None else None, float(scale), 1,
                                          _C.ptr(out), _C.stream_ptr(obs.device)),
              "tsrl_dqn_conv1_fwd")
@@ -59,10 +69,13 @@ CONV1_WGRAD_U8 = True
 
 
 def conv1_u8_wgrad(obs: torch.Tensor, gy_nhwc: torch.Tensor, weight: torch.Tensor,
-                   scale: float, bias: bool):
+                   scale: float, bias: bool, rows: Optional[torch.Tensor] = None):
     """(dW1, db1 or None) of relu-masked gradient rows gy [n, 20, 20, 32] (NHWC) w.r.t.
-    conv(obs / scale, W1) + b1, straight from the uint8 frames (tsrl_dqn_conv1_wgrad)."""
-    n = obs.shape[0]
+    conv(obs / scale, W1) + b1, straight from the uint8 frames (tsrl_dqn_conv1_wgrad); with
+    rows, gradient row s belongs to frame stack obs[rows[s]]."""
+    if rows is not None:
+        rows = rows.to(torch.int64).contiguous()
+    n = obs.shape[0] if rows is None else rows.numel()
     dev = obs.device
     lib = _C.lib()
     gw = torch.empty((32, 4, 8, 8), dtype=torch.float32, device=dev)
@@ -70,7 +83,9 @@ def conv1_u8_wgrad(obs: torch.Tensor, gy_nhwc: torch.Tensor, weight: torch.Tenso
     ws = torch.empty(max(1, (int(lib.tsrl_dqn_conv1_wgrad_workspace_bytes(n)) + 3) // 4),
                      dtype=torch.float32, device=dev)
     gy_nhwc = gy_nhwc.contiguous()
-    _C.check(lib.tsrl_dqn_conv1_wgrad(_C.ptr(obs.contiguous()), n, _C.ptr(gy_nhwc), float(scale),
+    _C.check(lib.tsrl_dqn_conv1_wgrad(_C.ptr(obs.contiguous()), n,
+                                      _C.ptr(rows) if rows is not None else None,
+                                      _C.ptr(gy_nhwc), float(scale),
                                       _C.ptr(gw), _C.ptr(gb) if gb is not None else None,
                                       _C.ptr(ws), ws.numel() * 4, _C.stream_ptr(dev)),
              "tsrl_dqn_conv1_wgrad")
@@ -86,9 +101,9 @@ class _Conv1U8(torch.autograd.Function):
     the frames themselves need no gradient."""
 
     @staticmethod
-    def forward(ctx, obs, weight, bias, conv, lut, scale):
-        z = conv1_u8(obs, conv, scale)
-        ctx.save_for_backward(obs, weight, z)
+    def forward(ctx, obs, rows, weight, bias, conv, lut, scale):
+        z = conv1_u8(obs, conv, scale, rows)
+        ctx.save_for_backward(obs, rows, weight, z)
         ctx.lut = lut
         ctx.scale = scale
         ctx.has_bias = bias is not None
@@ -96,16 +111,16 @@ class _Conv1U8(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gz):
-        obs, weight, z = ctx.saved_tensors
+        obs, rows, weight, z = ctx.saved_tensors
         gy = torch.ops.aten.threshold_backward(gz, z, 0.0)
         if CONV1_WGRAD_U8:
-            gw, gb = conv1_u8_wgrad(obs, _nhwc(gy), weight, ctx.scale, ctx.has_bias)
-            return None, gw, gb, None, None, None
-        x = frames_to_f32_nhwc(obs, ctx.lut)
+            gw, gb = conv1_u8_wgrad(obs, _nhwc(gy), weight, ctx.scale, ctx.has_bias, rows)
+            return None, None, gw, gb, None, None, None
+        x = frames_to_f32_nhwc(obs if rows is None else _gather(obs, rows), ctx.lut)
         _, gw, gb = torch.ops.aten.convolution_backward(
             gy, x, weight, [weight.shape[0]] if ctx.has_bias else None, (4, 4), (0, 0), (1, 1),
             False, (0, 0), 1, (False, True, ctx.has_bias))
-        return None, gw, gb, None, None, None
+        return None, None, gw, gb, None, None, None
 
 
 def bias_relu_(y: torch.Tensor, bias: Optional[torch.Tensor]) -> torch.Tensor:
@@ -236,10 +251,10 @@ class _Conv12U8(torch.autograd.Function):
     weight/bias gradient straight from the frames (tsrl_dqn_conv1_wgrad)."""
 
     @staticmethod
-    def forward(ctx, obs, w1, b1, w2, b2, conv1, conv2, lut, scale):
-        z1 = conv1_u8(obs, conv1, scale)
+    def forward(ctx, obs, rows, w1, b1, w2, b2, conv1, conv2, lut, scale):
+        z1 = conv1_u8(obs, conv1, scale, rows)
         z2 = bias_relu_(torch.nn.functional.conv2d(z1, w2, None, conv2.stride), b2)
-        ctx.save_for_backward(obs, w1, w2, z1, z2)
+        ctx.save_for_backward(obs, rows, w1, w2, z1, z2)
         ctx.lut = lut
         ctx.scale = scale
         ctx.bias = (b1 is not None, b2 is not None)
@@ -247,8 +262,8 @@ class _Conv12U8(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gz2):
-        obs, w1, w2, z1, z2 = ctx.saved_tensors
-        n = obs.shape[0]
+        obs, rows, w1, w2, z1, z2 = ctx.saved_tensors
+        n = z1.shape[0]
         gy2, gb2 = relu_bwd_bias(gz2, z2, ctx.bias[1])
         gy2 = gy2.contiguous(memory_format=torch.channels_last)
         lib_bias = ctx.bias[1] and gb2 is None
@@ -264,13 +279,13 @@ class _Conv12U8(torch.autograd.Function):
                                                _C.stream_ptr(obs.device)),
                  "tsrl_dqn_conv2_dgrad")
         if CONV1_WGRAD_U8:
-            gw1, gb1 = conv1_u8_wgrad(obs, gy1, w1, ctx.scale, ctx.bias[0])
+            gw1, gb1 = conv1_u8_wgrad(obs, gy1, w1, ctx.scale, ctx.bias[0], rows)
         else:
-            x = frames_to_f32_nhwc(obs, ctx.lut)
+            x = frames_to_f32_nhwc(obs if rows is None else _gather(obs, rows), ctx.lut)
             _, gw1, gb1 = torch.ops.aten.convolution_backward(
                 gy1.permute(0, 3, 1, 2), x, w1, [w1.shape[0]] if ctx.bias[0] else None, (4, 4),
                 (0, 0), (1, 1), False, (0, 0), 1, (False, True, ctx.bias[0]))
-        return None, gw1, gb1, gw2, gb2, None, None, None, None
+        return None, None, gw1, gb1, gw2, gb2, None, None, None, None
 
 
 def layer_init(layer: nn.Module, std: float = np.sqrt(2), bias_const: float = 0.0):
@@ -351,8 +366,24 @@ class DQN(nn.Module):
                                  outer[1:] if outer is not None else None) if ok else False
         return self._conv1_split or None
 
-    def forward(self, obs, state: Any = None, info: Dict[str, Any] = {}):
+    def reads_rows(self, obs) -> bool:
+        """Whether forward(obs, rows=...) reads obs[rows] in place (the uint8 first-layer
+        path on a contiguous frame-stack batch) instead of needing the rows gathered."""
+        return (self.fused_conv1 and self._conv1_parts() is not None and
+                isinstance(obs, torch.Tensor) and obs.dim() == 4 and
+                obs.dtype == torch.uint8 and obs.is_cuda and obs.is_contiguous() and
+                tuple(obs.shape[1:]) == (4, 84, 84) and bool(self.scale) and
+                obs.data_ptr() % 4 == 0)
+
+    def forward(self, obs, state: Any = None, info: Dict[str, Any] = {},
+                rows: Optional[torch.Tensor] = None):
+        """atari_network.py:84-90.  rows (int64 device indices, this repo's extension):
+        the output rows are those of obs[rows]; the uint8 first-layer kernels read them in
+        place (round 6: no gathered copy of the minibatch's frame stacks), any other path
+        gathers them first."""
         obs = torch.as_tensor(obs, device=self.device)
+        if rows is not None and not self.reads_rows(obs):
+            obs, rows = _gather(obs, rows), None
         parts = self._conv1_parts() if self.fused_conv1 else None
         if parts is not None and obs.dim() == 4 and obs.dtype == torch.uint8 and obs.is_cuda \
                 and tuple(obs.shape[1:]) == (4, 84, 84) and self.scale and \
@@ -360,10 +391,10 @@ class DQN(nn.Module):
             conv, conv2, rest, outer = parts
             lut = self._scale_lut(obs.device)
             if conv2 is not None:
-                h = _Conv12U8.apply(obs.contiguous(), conv.weight, conv.bias, conv2.weight,
+                h = _Conv12U8.apply(obs.contiguous(), rows, conv.weight, conv.bias, conv2.weight,
                                     conv2.bias, conv, conv2, lut, float(self.scale))
             else:
-                h = _Conv1U8.apply(obs.contiguous(), conv.weight, conv.bias, conv, lut,
+                h = _Conv1U8.apply(obs.contiguous(), rows, conv.weight, conv.bias, conv, lut,
                                    float(self.scale))
             if (outer is not None and len(rest) and isinstance(rest[-1], nn.Flatten) and
                     rest[-1].start_dim == 1 and rest[-1].end_dim == -1 and len(outer) and

@@ -58,7 +58,7 @@ def main():
     out1 = torch.empty(N, 20, 20, 32, device=dev)
     s_ = _C.stream_ptr(dev)
     lib = _C.lib()
-    f1 = lambda: lib.tsrl_dqn_conv1_fwd(_C.ptr(u8), N, w1.data_ptr(), *w1.stride(),  # noqa: E731
+    f1 = lambda: lib.tsrl_dqn_conv1_fwd(_C.ptr(u8), N, None, w1.data_ptr(), *w1.stride(),  # noqa
                                         _C.ptr(b1), 255.0, 1, _C.ptr(out1), s_)
     t1 = timed(f1, a.iters)
     flop1 = 2.0 * N * 400 * 32 * 256
