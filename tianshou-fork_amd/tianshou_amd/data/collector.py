@@ -572,8 +572,13 @@ class Collector:
             buf._launch_add(ids=ids_t, k=kk, obs=cur, act=act, obs_next=raw, cur_obs=cur,
                             norm=norm, rew=rew, term=term, trunc=trunc, **add_kw)
         torch.logical_or(term, trunc, out=done)
-        b._reset_raw(ids_t, done, kk, s["reset_raw"][:kk], s["part2"])
-        self._finish_obs(s["reset_raw"][:kk], cur, s["part2"], done, kk)
+        if b.u8:
+            # the reset kernel writes only the finished envs' rows: straight into cur (which
+            # now holds the stepped rows), no masked select pass over all rows
+            b._reset_raw(ids_t, done, kk, cur, s["part2"])
+        else:
+            b._reset_raw(ids_t, done, kk, s["reset_raw"][:kk], s["part2"])
+            self._finish_obs(s["reset_raw"][:kk], cur, s["part2"], done, kk)
         self._parity ^= 1
 
     def _graph_key(self, G: int):
