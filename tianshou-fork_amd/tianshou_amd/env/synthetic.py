@@ -143,6 +143,9 @@ class SyntheticVectorEnv(DeviceVectorEnv):
 
     def _reset_raw(self, ids: Optional[torch.Tensor], mask: Optional[torch.Tensor], k: int,
                    obs_out, partials=None) -> None:
+        """Reset the rows selected by mask (all k without one) into obs_out.  Rows not
+        selected are left untouched -- the fused collector relies on it for uint8 obs, whose
+        resets are written straight into its current observations."""
         L = _C.lib()
         s = _C.stream_ptr(self.device)
         if self.u8:
