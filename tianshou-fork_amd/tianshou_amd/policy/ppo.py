@@ -655,17 +655,22 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
     def _cat_epoch_graph(self, fa: FlatAdam, obs, arrays, perm, chunks, first: bool):
         """One Categorical epoch replayed from a captured HIP graph (the torch forward /
         autograd backward, the fused loss kernels and the flat Adam pass of every minibatch).
-        Static copies of the per-update arrays and the permutation feed it; the obs rows are
-        read in place (their address is part of the key).  None if the capture failed."""
+        Static copies of the per-update arrays and the permutation feed it, and of the obs
+        rows when they are small (≤ 64 MB: a buffer whose sample returns fresh rows every
+        update -- CartPoleVectorEnv's -- would otherwise re-capture the graph every update,
+        ~100 ms each, round 6); larger obs rows are read in place (their address is part of
+        the key).  None if the capture failed."""
         n = perm.numel()
-        key = (n, tuple(chunks), obs.data_ptr(), tuple(obs.shape), obs.dtype,
-               tuple(a.shape for a in arrays), fa.flat_grad.data_ptr(),
+        static_obs = obs.numel() * obs.element_size() <= (64 << 20)
+        key = (n, tuple(chunks), "static" if static_obs else obs.data_ptr(), tuple(obs.shape),
+               obs.dtype, tuple(a.shape for a in arrays), fa.flat_grad.data_ptr(),
                tuple(p.data_ptr() for p in fa.params))
         st = self._learn_graph
         if st is None or st["key"] != key:
             self._learn_graph = None
             dev = perm.device
             static = [a.clone() for a in arrays]
+            sobs = obs.clone() if static_obs else obs
             sperm = perm.clone()
             sterms = torch.empty(len(chunks), 4, dtype=torch.float32, device=dev)
             torch.cuda.synchronize()
@@ -674,7 +679,7 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
             try:
                 with graph_capture(graph):
                     for i, (s, e, b_glob) in enumerate(chunks):
-                        t = self._cat_minibatch(fa, obs, sperm[s:e], b_glob, static,
+                        t = self._cat_minibatch(fa, sobs, sperm[s:e], b_glob, static,
                                                 last=(i == len(chunks) - 1))
                         sterms[i].copy_(t)
             except RuntimeError as err:
@@ -684,11 +689,14 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
                 torch.cuda.synchronize()
                 return None
             st = self._learn_graph = dict(key=key, graph=graph, static=static, perm=sperm,
-                                          terms=sterms, tally=LOG.capture_end())
+                                          terms=sterms, tally=LOG.capture_end(),
+                                          obs=sobs if static_obs else None)
             first = False
         if first:
             for d, a in zip(st["static"], arrays):
                 d.copy_(a)
+            if st["obs"] is not None and st["obs"].data_ptr() != obs.data_ptr():
+                st["obs"].copy_(obs)
         st["perm"].copy_(perm)
         st["graph"].replay()
         LOG.replayed(st["tally"])
