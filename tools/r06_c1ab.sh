@@ -1,4 +1,6 @@
 #!/bin/bash
+# (the build flags this recipe names were removed after the measurement; the recipe documents
+# how the committed log was produced -- rebuild the variants from the commit it cites to rerun)
 # Round-6 A/B: conv1 forward and conv2 data gradient from LDS-staged samples (this build) vs the gathered form
 # (variants/libtsrl_g.so = -DDQN_C1_GATHER=1 -DDQN_C2_GATHER=1): atari GPU tests on this build, bit-identity of
 # the outputs at 8192 and 37 samples, timings twice interleaved.

@@ -1,4 +1,6 @@
 #!/bin/bash
+# (the build flags this recipe names were removed after the measurement; the recipe documents
+# how the committed log was produced -- rebuild the variants from the commit it cites to rerun)
 # Round-6 A/B: conv2 data gradient with two classes per 8-wave workgroup (this build) vs one
 # class per 4-wave workgroup (variants/libtsrl_n1.so = -DDQN_C2_NCL=1) and the gathered form
 # (variants/libtsrl_g.so); atari GPU tests on this build, bit-identity at 37 / 8192 samples.

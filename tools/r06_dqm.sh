@@ -1,4 +1,6 @@
 #!/bin/bash
+# (the build flags this recipe names were removed after the measurement; the recipe documents
+# how the committed log was produced -- rebuild the variants from the commit it cites to rerun)
 # Round-6 decomposition of the LDS-staged config-5 trunk kernels (dqn_conv.hip -DDQM=<bit>
 # builds, wrong results by design): conv1 forward -- 1 no MFMA, 2 no byte->bf16 conversion,
 # 4 no output stores, 8 no frame staging; conv2 data gradient -- 1 no MFMA, 2 no z1 mask loads,

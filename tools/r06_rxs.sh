@@ -1,4 +1,6 @@
 #!/bin/bash
+# (the build flags this recipe names were removed after the measurement; the recipe documents
+# how the committed log was produced -- rebuild the variants from the commit it cites to rerun)
 # Round-6 probe: the layer-1 ring with a 2-stage X ring (X issued one chunk ahead;
 # variants/libtsrl_x2.so = -DL1_RXS=2) vs the shipped 3 stages -- would a fused process_fn
 # evaluation (layer-2 images beside the ring) fit?  MLP tests on the variant, then the kernel
