@@ -583,3 +583,42 @@ def test_dqn_rows_in_place_matches_gathered(dev, n, rows_n):
         else:
             err = float((p1.grad - p2.grad).abs().max())
             assert err <= 1e-5 * float(p2.grad.abs().max()) + 1e-12, (k, err)
+
+
+def test_dqn_fused_trunk_grads_accumulate(dev):
+    """The fused trunk's gradients against the plain NCHW module over two backward passes:
+    the first assigns every .grad, the second accumulates -- the Flatten + Linear weight
+    gradient then goes straight into the existing .grad through its permuted view (round 6),
+    and the bias gradient is the HIP column sum.  Summation order only (rtol 1e-3)."""
+    from tianshou_amd.utils import net_atari
+    from tianshou_amd.utils.net_atari import DQN, layer_init
+    torch.manual_seed(0)
+    a = DQN(4, 84, 84, (6,), device=dev, features_only=True, output_dim=512,
+            layer_init=layer_init).to(dev)
+    torch.manual_seed(0)
+    b = DQN(4, 84, 84, (6,), device=dev, features_only=True, output_dim=512,
+            layer_init=layer_init, channels_last=False).to(dev)
+    b.fused_conv1 = False
+    taken = []
+    orig = net_atari._FlattenLinear._grad_slot
+
+    def spy(*args):
+        s = orig(*args)
+        taken.append(s is not None)
+        return s
+    net_atari._FlattenLinear._grad_slot = staticmethod(spy)
+    try:
+        for seed in (1, 2):
+            g = torch.Generator(device=dev).manual_seed(seed)
+            x = torch.randint(0, 256, (64, 4, 84, 84), dtype=torch.uint8, device=dev,
+                              generator=g)
+            ya, yb = a(x)[0], b(x)[0]
+            gy = torch.randn(ya.shape, device=dev, generator=g)
+            ya.backward(gy)
+            yb.backward(gy)
+    finally:
+        net_atari._FlattenLinear._grad_slot = staticmethod(orig)
+    assert taken == [False, True]
+    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+        torch.testing.assert_close(pa.grad, pb.grad, rtol=1e-3,
+                                   atol=1e-4 * float(pb.grad.abs().max()), msg=n)

@@ -255,3 +255,57 @@ def test_flat_adam_refuses_mixed_step_counts():
     # a uniform state dict binds again
     opt.load_state_dict(full)
     assert fm.bind_adam(opt)
+
+
+def test_flat_adam_keeps_channels_last_conv_weights():
+    """FlatAdam's flat slots keep each parameter's memory format (round 6): a channels_last
+    conv weight stays channels_last as a parameter, as a .grad slot and in the Adam moments
+    (MIOpen would otherwise copy it to the input's format on every convolution, and autograd
+    would accumulate its channels_last gradient with a strided add).  Convolution backward
+    into the slots + clip_adam over 4 steps = torch's clip_grad_norm_ + Adam on a twin;
+    a loaded optimiser state re-binds into the same formats."""
+    import copy
+    from tianshou_amd.policy.flat_adam import FlatAdam
+    dev = torch.device("cuda", 0)
+    cl = torch.channels_last
+    torch.manual_seed(4)
+
+    def make():
+        return torch.nn.Sequential(torch.nn.Conv2d(4, 8, 3, stride=2), torch.nn.ReLU(),
+                                   torch.nn.Conv2d(8, 8, 3), torch.nn.Flatten(),
+                                   torch.nn.Linear(8 * 4 * 4, 3)).to(dev).to(memory_format=cl)
+    m0 = make()
+    m1 = copy.deepcopy(m0)
+    opt_ref = torch.optim.Adam(m0.parameters(), lr=1e-3)
+    opt = torch.optim.Adam(m1.parameters(), lr=1e-3)
+    fa = FlatAdam(m1.parameters())
+    assert fa.bind_adam(opt) and fa.adam_bound(opt)
+    for p0, p1 in zip(m0.parameters(), m1.parameters()):
+        assert p1.stride() == p0.stride(), "memory format lost"
+        assert torch.equal(p1.detach(), p0.detach())
+        assert opt.state[p1]["exp_avg"].stride() == p0.stride()
+    g = torch.Generator(device=dev).manual_seed(5)
+    for step in range(4):
+        x = torch.randn(16, 4, 13, 13, device=dev, generator=g).contiguous(memory_format=cl)
+        opt_ref.zero_grad()
+        m0(x).square().sum().backward()
+        torch.nn.utils.clip_grad_norm_(m0.parameters(), max_norm=0.5)
+        opt_ref.step()
+        fa.zero_grad()
+        m1(x).square().sum().backward()
+        for p0, p1 in zip(m0.parameters(), m1.parameters()):
+            assert p1.grad.stride() == p0.stride()
+        fa.clip_adam(0.5)
+        torch.cuda.synchronize()
+        for (n0, p0), p1 in zip(m0.named_parameters(), m1.parameters()):
+            np.testing.assert_allclose(p1.detach().cpu().numpy(), p0.detach().cpu().numpy(),
+                                       rtol=1e-5, atol=1e-7, err_msg=f"step {step} {n0}")
+    # a loaded state dict re-binds into the same (channels_last) slots
+    sd = copy.deepcopy(opt.state_dict())
+    opt.load_state_dict(sd)
+    assert fa.bind_adam(opt)
+    for p0, p1 in zip(m0.parameters(), m1.parameters()):
+        assert opt.state[p1]["exp_avg_sq"].stride() == p0.stride()
+        np.testing.assert_allclose(opt.state[p1]["exp_avg_sq"].cpu().numpy(),
+                                   opt_ref.state[p0]["exp_avg_sq"].cpu().numpy(),
+                                   rtol=5e-5, atol=1e-12)

@@ -20,6 +20,18 @@ import torch
 from tianshou_amd import _C
 
 
+def _slot(flat: torch.Tensor, o: int, p: torch.Tensor) -> torch.Tensor:
+    """The numel(p) words of ``flat`` from offset o viewed with p's shape AND memory format
+    (a channels_last conv weight stays channels_last: MIOpen would otherwise copy an NCHW
+    weight to the input's format on every convolution, and autograd would accumulate its
+    channels_last gradients into NCHW slots with a strided add)."""
+    k = p.numel()
+    if p.is_contiguous():
+        return flat[o:o + k].view_as(p)
+    stride = torch.empty_like(p, memory_format=torch.preserve_format).stride()
+    return flat.as_strided(p.shape, stride, flat.storage_offset() + o)
+
+
 class FlatAdam:
     # extra f32 words after the flat gradients in the bucket (data-parallel loss sums ride
     # in the same all-reduce as the gradients)
@@ -47,7 +59,7 @@ class FlatAdam:
         self._views = []
         o = 0
         for p in self.params:
-            v = self._flat[o:o + p.numel()].view_as(p)
+            v = _slot(self._flat, o, p)
             p.grad = v
             self._views.append(v)
             o += p.numel()
@@ -128,21 +140,18 @@ class FlatAdam:
         """Copy whatever ``optim.state`` now holds into the flat moments / step counts (zeros
         for a parameter without state) and point ``optim.state`` back at the flat views."""
         st = self._adam
-        o = 0
         for i, p in enumerate(self.params):
-            k = p.numel()
             s = optim.state.get(p, {})
             if "exp_avg" in s:
-                st["m"][o:o + k].copy_(s["exp_avg"].reshape(-1))
-                st["v"][o:o + k].copy_(s["exp_avg_sq"].reshape(-1))
+                st["mviews"][i].copy_(s["exp_avg"])
+                st["vviews"][i].copy_(s["exp_avg_sq"])
                 st["steps"][i].copy_(torch.as_tensor(s["step"], dtype=torch.float32))
             else:
-                st["m"][o:o + k].zero_()
-                st["v"][o:o + k].zero_()
+                st["mviews"][i].zero_()
+                st["vviews"][i].zero_()
                 st["steps"][i].zero_()
             optim.state[p] = {"step": st["steps"][i], "exp_avg": st["mviews"][i],
                               "exp_avg_sq": st["vviews"][i]}
-            o += k
         st["lr_host"] = None  # load_state_dict may also have changed the param-group lr
 
     def bind_adam(self, optim) -> bool:
@@ -164,17 +173,16 @@ class FlatAdam:
         o = 0
         for i, p in enumerate(self.params):
             k = p.numel()
-            flat_p[o:o + k].copy_(p.detach().reshape(-1))
+            pv, mv, vv = _slot(flat_p, o, p), _slot(flat_m, o, p), _slot(flat_v, o, p)
+            pv.copy_(p.detach())
             st = optim.state.get(p, {})
             if "exp_avg" in st:
-                flat_m[o:o + k].copy_(st["exp_avg"].reshape(-1))
-                flat_v[o:o + k].copy_(st["exp_avg_sq"].reshape(-1))
+                mv.copy_(st["exp_avg"])
+                vv.copy_(st["exp_avg_sq"])
                 steps[i] = float(st["step"])
             with torch.no_grad():
-                p.data = flat_p[o:o + k].view_as(p)
-            optim.state[p] = {"step": steps[i],
-                              "exp_avg": flat_m[o:o + k].view_as(p),
-                              "exp_avg_sq": flat_v[o:o + k].view_as(p)}
+                p.data = pv
+            optim.state[p] = {"step": steps[i], "exp_avg": mv, "exp_avg_sq": vv}
             pviews.append(p.data)
             mviews.append(optim.state[p]["exp_avg"])
             vviews.append(optim.state[p]["exp_avg_sq"])

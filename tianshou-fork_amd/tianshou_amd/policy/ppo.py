@@ -138,6 +138,7 @@ class _CatPPOLoss(torch.autograd.Function):
         _C.check(L.tsrl_ppo_cat_finalize(_C.ptr(sums), params, _C.ptr(terms), s),
                  "tsrl_ppo_cat_finalize")
         ctx.save_for_backward(grad_x, grad_value)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the terms output
         loss = terms[0].clone()
         ctx.mark_non_differentiable(terms)
         return loss, terms
@@ -145,7 +146,30 @@ class _CatPPOLoss(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_loss, g_terms):
         grad_x, grad_value = ctx.saved_tensors
+        if g_loss is None:
+            return None, None, None
+        if _is_unit_seed(g_loss):
+            # loss.backward(UNIT): the gradients are the kernel's as they are (x * 1.0 is x)
+            return grad_x, grad_value, None
         return grad_x * g_loss, grad_value * g_loss, None
+
+
+_UNIT = {}
+
+
+def _unit_seed(dev: torch.device) -> torch.Tensor:
+    """A constant f32 1.0 on dev, the seed gradient of the Categorical minibatch's
+    loss.backward(): it spares autograd's ones_like fill, and _CatPPOLoss recognises it and
+    skips two scaling passes (round 6).  Never written."""
+    t = _UNIT.get(dev)
+    if t is None:
+        t = _UNIT[dev] = torch.ones((), dtype=torch.float32, device=dev)
+    return t
+
+
+def _is_unit_seed(g: torch.Tensor) -> bool:
+    t = _UNIT.get(g.device)
+    return t is not None and g.dim() == 0 and g.data_ptr() == t.data_ptr()
 
 
 class PPOPolicy(FusedEvalMixin, A2CPolicy):
@@ -640,7 +664,7 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
                                                self._cat))
         if fa is not None:
             fa.zero_grad()  # autograd accumulates into the flat bucket in place
-            loss.backward()
+            loss.backward(_unit_seed(loss.device))
             self.dp.all_reduce_(fa.flat_grad, kind="grad")
             fa.clip_adam(self._grad_norm, scale_grads=last)
             return t
