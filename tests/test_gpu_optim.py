@@ -309,3 +309,35 @@ def test_flat_adam_keeps_channels_last_conv_weights():
         np.testing.assert_allclose(opt.state[p1]["exp_avg_sq"].cpu().numpy(),
                                    opt_ref.state[p0]["exp_avg_sq"].cpu().numpy(),
                                    rtol=5e-5, atol=1e-12)
+
+
+def test_flat_adam_release_gather_grads():
+    """release_grads() + backward + gather_grads() (the eager Categorical minibatch, round 6)
+    leaves the same flat bucket as zero_grad() + backward: every gradient in its slot, a
+    parameter that received no gradient zeroed, every .grad the slot view again."""
+    from tianshou_amd.policy.flat_adam import FlatAdam
+    dev = torch.device("cuda", 0)
+    cl = torch.channels_last
+    torch.manual_seed(6)
+    m = torch.nn.Sequential(torch.nn.Conv2d(4, 8, 3, stride=2), torch.nn.ReLU(),
+                            torch.nn.Flatten(), torch.nn.Linear(8 * 6 * 6, 3)).to(dev)
+    m = m.to(memory_format=cl)
+    unused = torch.nn.Parameter(torch.randn(5, device=dev))
+    params = list(m.parameters()) + [unused]
+    fa = FlatAdam(params)
+    x = torch.randn(16, 4, 13, 13, device=dev).contiguous(memory_format=cl)
+    fa.zero_grad()
+    m(x).square().sum().backward()
+    want = fa.flat_grad.clone()
+    ptrs = [p.grad.data_ptr() for p in params]
+    # stale values in the bucket must not leak into the gathered gradients
+    fa.flat_grad.fill_(7.0)
+    fa.release_grads()
+    assert all(p.grad is None for p in params)
+    m(x).square().sum().backward()
+    fa.gather_grads()
+    assert [p.grad.data_ptr() for p in params] == ptrs
+    # (MIOpen's weight gradient may sum in another order run to run)
+    torch.testing.assert_close(fa.flat_grad, want, rtol=1e-5,
+                               atol=1e-6 * float(want.abs().max()))
+    assert torch.count_nonzero(unused.grad) == 0

@@ -78,6 +78,36 @@ class FlatAdam:
         self.bind_grads()
         self._flat.zero_()
 
+    def release_grads(self) -> None:
+        """zero_grad() for an eager backward followed by gather_grads(): the slots stay bound
+        (their addresses are the ones the optimiser pass and the collectives use), every .grad
+        is set to None, and autograd then hands each parameter its gradient tensor as it is
+        instead of adding it into a zero-filled slot -- the fill and one add per parameter
+        saved (round 6; 12 of each per config-5 minibatch)."""
+        self.bind_grads()
+        for p in self.params:
+            p.grad = None
+
+    def gather_grads(self) -> None:
+        """After a backward that began with release_grads(): every parameter's gradient copied
+        into its slot in one multi-tensor pass (a slot whose parameter received no gradient is
+        zeroed, as zero_grad() would have left it) and every .grad pointed back at its slot."""
+        dst, src = [], []
+        for p, v in zip(self.params, self._views):
+            g = p.grad
+            if g is None:
+                v.zero_()
+            elif g.data_ptr() != v.data_ptr():
+                if g.shape != v.shape or g.dtype != v.dtype:
+                    raise RuntimeError("FlatAdam.gather_grads: a gradient does not match its "
+                                       f"parameter ({tuple(g.shape)} {g.dtype} vs "
+                                       f"{tuple(v.shape)} {v.dtype})")
+                dst.append(v)
+                src.append(g)
+            p.grad = v
+        if dst:
+            torch._foreach_copy_(dst, src)
+
     # -- clip_grad_norm_ + Adam as one HIP pass ---------------------------------------------------
     @staticmethod
     def _plain_adam(optim, params) -> bool:

@@ -663,8 +663,16 @@ class PPOPolicy(FusedEvalMixin, A2CPolicy):
         loss, t = _CatPPOLoss.apply(x, value, (*arrays, idx, self._params(b_glob), self.dp,
                                                self._cat))
         if fa is not None:
-            fa.zero_grad()  # autograd accumulates into the flat bucket in place
+            # eager: autograd hands over each gradient and one pass gathers them into the flat
+            # bucket; under graph capture it accumulates into the zeroed bucket in place
+            gather = loss.is_cuda and not torch.cuda.is_current_stream_capturing()
+            if gather:
+                fa.release_grads()
+            else:
+                fa.zero_grad()
             loss.backward(_unit_seed(loss.device))
+            if gather:
+                fa.gather_grads()
             self.dp.all_reduce_(fa.flat_grad, kind="grad")
             fa.clip_adam(self._grad_norm, scale_grads=last)
             return t

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-6 A/B: config-5 glue cuts (flat Adam slots keep channels_last, the FC bias gradient as a
+# Round-6 A/B: config-5 glue cuts (first: flat Adam slots keep channels_last, the FC bias gradient as a
 # HIP column sum, the FC weight gradient added straight into .grad, the Categorical loss's
 # seed / zero fill / scaling passes skipped) -- this tree vs variants/oldtree (the previous
 # commit's Python package, same libtsrl.so): the affected GPU tests on this tree, then the
