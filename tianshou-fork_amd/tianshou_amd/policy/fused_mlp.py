@@ -36,8 +36,10 @@ TAIL_OVERLAP = os.environ.get("TSRL_TAIL_OVERLAP", "1") != "0"
 EVAL_FUSED = os.environ.get("TSRL_EVAL_FUSED", "1") != "0"
 # minibatches of at most this many rows run the actor's and the critic's tail kernels on the
 # two streams side by side (each tail then fills at most half of a 256-CU device:
-# ceil(rows / 16 / 8) workgroups <= 128); TSRL_TAIL_SPLIT=0 keeps them on one stream
-TAIL_SPLIT_ROWS = 16384 if os.environ.get("TSRL_TAIL_SPLIT", "1") != "0" else 0
+# ceil(rows / 16 / 8) workgroups <= 128); TSRL_TAIL_SPLIT=0 keeps them on one stream,
+# TSRL_TAIL_SPLIT_ROWS moves the threshold
+TAIL_SPLIT_ROWS = int(os.environ.get("TSRL_TAIL_SPLIT_ROWS", "16384")) \
+    if os.environ.get("TSRL_TAIL_SPLIT", "1") != "0" else 0
 
 
 def _seq(mlp) -> Optional[list]:
