@@ -589,7 +589,9 @@ def test_dqn_fused_trunk_grads_accumulate(dev):
     """The fused trunk's gradients against the plain NCHW module over two backward passes:
     the first assigns every .grad, the second accumulates -- the Flatten + Linear weight
     gradient then goes straight into the existing .grad through its permuted view (round 6),
-    and the bias gradient is the HIP column sum.  Summation order only (rtol 1e-3)."""
+    and the bias gradient is the HIP column sum -- then a third behind FlatAdam's
+    release_grads / gather_grads (the weight gradient written into its flat slot).
+    Summation order only (rtol 1e-3)."""
     from tianshou_amd.utils import net_atari
     from tianshou_amd.utils.net_atari import DQN, layer_init
     torch.manual_seed(0)
@@ -604,21 +606,36 @@ def test_dqn_fused_trunk_grads_accumulate(dev):
 
     def spy(*args):
         s = orig(*args)
-        taken.append(s is not None)
+        taken.append((s[0] is not None, s[1]))
         return s
+
+    def step(seed):
+        g = torch.Generator(device=dev).manual_seed(seed)
+        x = torch.randint(0, 256, (64, 4, 84, 84), dtype=torch.uint8, device=dev, generator=g)
+        ya, yb = a(x)[0], b(x)[0]
+        gy = torch.randn(ya.shape, device=dev, generator=g)
+        ya.backward(gy)
+        yb.backward(gy)
+
+    def check():
+        for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+            torch.testing.assert_close(pa.grad, pb.grad, rtol=1e-3,
+                                       atol=1e-4 * float(pb.grad.abs().max()), msg=n)
     net_atari._FlattenLinear._grad_slot = staticmethod(spy)
     try:
-        for seed in (1, 2):
-            g = torch.Generator(device=dev).manual_seed(seed)
-            x = torch.randint(0, 256, (64, 4, 84, 84), dtype=torch.uint8, device=dev,
-                              generator=g)
-            ya, yb = a(x)[0], b(x)[0]
-            gy = torch.randn(ya.shape, device=dev, generator=g)
-            ya.backward(gy)
-            yb.backward(gy)
+        step(1)
+        step(2)
+        check()
+        # FlatAdam's hand-over (release_grads / gather_grads): the Flatten + Linear weight
+        # gradient is written into its published flat slot
+        from tianshou_amd.policy.flat_adam import FlatAdam
+        fa = FlatAdam(a.parameters())
+        fa.release_grads()
+        b.zero_grad()
+        step(3)
+        fa.gather_grads()
+        assert all(p.grad.data_ptr() == v.data_ptr() for p, v in zip(fa.params, fa._views))
+        check()
     finally:
         net_atari._FlattenLinear._grad_slot = staticmethod(orig)
-    assert taken == [False, True]
-    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
-        torch.testing.assert_close(pa.grad, pb.grad, rtol=1e-3,
-                                   atol=1e-4 * float(pb.grad.abs().max()), msg=n)
+    assert taken == [(False, False), (True, False), (True, True)]

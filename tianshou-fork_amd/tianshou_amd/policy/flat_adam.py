@@ -85,8 +85,11 @@ class FlatAdam:
         instead of adding it into a zero-filled slot -- the fill and one add per parameter
         saved (round 6; 12 of each per config-5 minibatch)."""
         self.bind_grads()
-        for p in self.params:
+        for p, v in zip(self.params, self._views):
             p.grad = None
+            # a custom backward that can write a gradient in place (net_atari's Flatten +
+            # Linear) finds its slot here, writes it and makes it the .grad
+            p._tsrl_flat_slot = v
 
     def gather_grads(self) -> None:
         """After a backward that began with release_grads(): every parameter's gradient copied
@@ -94,6 +97,7 @@ class FlatAdam:
         zeroed, as zero_grad() would have left it) and every .grad pointed back at its slot."""
         dst, src = [], []
         for p, v in zip(self.params, self._views):
+            p.__dict__.pop("_tsrl_flat_slot", None)
             g = p.grad
             if g is None:
                 v.zero_()

@@ -205,9 +205,11 @@ class _FlattenLinear(torch.autograd.Function):
     features permuted to (h, w, C) order -- the same products, summed in another order -- and
     the input gradient comes back as a channels_last view.  Backward: the bias gradient is one
     HIP column sum (tsrl_sum_rows_f32; torch's reduction took 23 us per 8192 rows), and the
-    (h, w, C)-ordered weight gradient is added straight into an existing ``weight.grad``
-    through a permuted view -- one strided add instead of the (C, h, w) reshape copy plus
-    autograd's accumulation (round 6) -- when the weight has no gradient hooks."""
+    (h, w, C)-ordered weight gradient goes straight into an existing ``weight.grad`` (added)
+    or into the flat-bucket slot FlatAdam.release_grads() published (written, and made the
+    .grad) through a permuted view -- one strided pass instead of the (C, h, w) reshape copy
+    plus autograd's accumulation or hand-over copy (round 6) -- when the weight has no
+    gradient hooks."""
 
     @staticmethod
     def forward(ctx, x, weight, bias):
@@ -223,14 +225,18 @@ class _FlattenLinear(torch.autograd.Function):
 
     @staticmethod
     def _grad_slot(weight: torch.Tensor, O: int, C: int, H: int, W: int):
-        """weight.grad as an [O, h, w, C] view when the weight gradient may be accumulated
-        into it directly (a plain dense .grad, no hooks on the weight), else None."""
-        g = weight.grad
+        """(g, fresh): the gradient tensor the weight gradient may be written into directly
+        (a plain dense .grad, no hooks on the weight) and whether it is to be overwritten --
+        the flat-bucket slot FlatAdam.release_grads() published while .grad is None -- rather
+        than accumulated into; (None, False) when autograd must take it."""
+        g, fresh = weight.grad, False
+        if g is None:
+            g, fresh = getattr(weight, "_tsrl_flat_slot", None), True
         if (g is None or g.requires_grad or not g.is_cuda or g.dtype != weight.dtype or
-                not g.is_contiguous() or weight._backward_hooks or
+                g.shape != weight.shape or not g.is_contiguous() or weight._backward_hooks or
                 getattr(weight, "_post_accumulate_grad_hooks", None)):
-            return None
-        return g.view(O, C, H, W).permute(0, 2, 3, 1)
+            return None, False
+        return g, fresh
 
     @staticmethod
     def backward(ctx, gy):
@@ -248,11 +254,16 @@ class _FlattenLinear(torch.autograd.Function):
             return gx, gw, gb
         if ctx.needs_input_grad[1]:
             g_hwc = gy.t() @ xf
-            slot = _FlattenLinear._grad_slot(ctx.weight, O, C, H, W)
-            if slot is not None:
-                slot.add_(g_hwc.view(O, H, W, C))
-            else:
+            g, fresh = _FlattenLinear._grad_slot(ctx.weight, O, C, H, W)
+            if g is None:
                 gw = g_hwc.view(O, H, W, C).permute(0, 3, 1, 2).reshape(O, C * H * W)
+            else:
+                slot = g.view(O, C, H, W).permute(0, 2, 3, 1)
+                if fresh:
+                    slot.copy_(g_hwc.view(O, H, W, C))
+                    ctx.weight.grad = g  # the slot now holds this backward's gradient
+                else:
+                    slot.add_(g_hwc.view(O, H, W, C))
         if ctx.has_bias and ctx.needs_input_grad[2]:
             gb = sum_rows(gy) if gy.is_cuda else gy.sum(0)
         return gx, gw, gb

@@ -1,5 +1,6 @@
 #!/bin/bash
 # Round-6 A/B: eager Categorical minibatches hand autograd's gradients over (.grad = None before
+# (reused for the follow-up: the FC weight gradient written into its released flat slot)
 # backward, one multi-tensor copy into the flat bucket after: FlatAdam.release_grads /
 # gather_grads) vs the zero-filled bucket + per-parameter adds (variants/oldtree = the previous
 # commit's Python package, same libtsrl.so): the affected GPU tests, then config 5 twice interleaved.
