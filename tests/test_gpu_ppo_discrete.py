@@ -86,6 +86,43 @@ def test_cat_loss_vs_torch(dev, mode, kw, B, A):
                                atol=1e-6)
 
 
+
+def test_cat_loss_seed_paths(dev):
+    """_CatPPOLoss's backward under the learn path's constant unit seed (the kernel's
+    gradients handed over as they are, round 6) equals loss.backward()'s (x * 1.0 is x, bit
+    for bit), and any other seed still scales them (2.5 * loss)."""
+    from tianshou_amd import _C
+    from tianshou_amd.dist import DataParallel
+    from tianshou_amd.policy.ppo import _CatPPOLoss, _unit_seed
+    g = torch.Generator().manual_seed(11)
+    B, A, n = 96, 6, 137
+    x = torch.randn(B, A, generator=g)
+    value = torch.randn(B, generator=g)
+    act = torch.randint(0, A, (n,), generator=g)
+    logp_old, adv, ret = (torch.randn(n, generator=g) for _ in range(3))
+    v_s = ret + 0.3 * torch.randn(n, generator=g)
+    idx = torch.randperm(n, generator=g)[:B]
+    p = _C.PPOParams()
+    p.eps_clip, p.dual_clip, p.vf_coef, p.ent_coef, p.adv_eps, p.b_global = \
+        0.2, 0.0, 0.25, 0.01, 1e-8, B
+    p.value_clip, p.norm_adv = 1, 1
+    d = lambda t: t.to(dev).contiguous()  # noqa: E731
+    args = (d(act), d(logp_old), d(adv), d(ret), d(v_s), d(idx), p, DataParallel(), 0)
+    grads = []
+    for seed in ("ones", "unit", 2.5):
+        x_d, v_d = d(x).requires_grad_(True), d(value).requires_grad_(True)
+        loss, _ = _CatPPOLoss.apply(x_d, v_d, args)
+        if seed == "ones":
+            loss.backward()
+        elif seed == "unit":
+            loss.backward(_unit_seed(loss.device))
+        else:
+            (loss * seed).backward()
+        grads.append((x_d.grad.clone(), v_d.grad.clone()))
+    assert torch.equal(grads[0][0], grads[1][0]) and torch.equal(grads[0][1], grads[1][1])
+    torch.testing.assert_close(grads[2][0], 2.5 * grads[0][0], rtol=1e-6, atol=0)
+    torch.testing.assert_close(grads[2][1], 2.5 * grads[0][1], rtol=1e-6, atol=0)
+
 def _discrete_policy(z, tag, dev):
     from tianshou_amd.env import Discrete
     from tianshou_amd.policy import PPOPolicy
